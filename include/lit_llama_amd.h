@@ -1,0 +1,111 @@
+/* lit_llama_amd.h — C ABI of the MI355X (gfx950) quantized LLaMA decode path.
+ *
+ * Library: lit-llama-ja_amd/lit_llama/_lljamd.so (hipcc --offload-arch=gfx950).
+ * Conventions: every pointer is a device pointer (HBM) except where noted; bf16 tensors
+ * are raw 16-bit patterns; `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream
+ * on the Python side, or 0). Every entry point only enqueues work (graph-capturable: no
+ * allocation, no synchronisation) and returns 0 on success, a hipError_t, or
+ * LLJ_EINVAL (1000) for a shape/argument the kernels do not support. The library owns no
+ * memory; callers own every buffer.
+ *
+ * Reference = if001/lit-llama-ja @ 2025-02-05 (paths relative to its root).
+ */
+#ifndef LIT_LLAMA_AMD_H
+#define LIT_LLAMA_AMD_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LLJ_EINVAL 1000
+
+/* ---------------------------------------------------------------- int4 weight layout
+ * Replaces the `quant_weight` buffer contract of ColBlockQuantizedLinear
+ * (lit_llama/quantization.py:348-357, pack_weight 374-388): logical (N, K/2) uint8 stored
+ * column-major (= physical row-major (K/2, N)), low nibble = even k. The GEMV consumes the
+ * "W4P" tiling (1 KiB per 16 columns x 128 k). repack/unpack are exact inverses.
+ * N % 16 == 0, K % 128 == 0. */
+int llj_w4_repack(const void* qweight_ref, void* packed, int N, int K, void* stream);
+int llj_w4_unpack(const void* packed, void* qweight_ref, int N, int K, void* stream);
+
+/* sz[2n] = scales[n], sz[2n+1] = 128 + zeros[n] (fp32) from the module's (N, 1) `scales` /
+ * `zeros` buffers (quantization.py:358-367; gptq.int4 is tile_cols = -1, utils.py:181).
+ * dtype: 0 fp32, 1 bf16, 2 fp16. */
+int llj_w4_scale_zero(const void* scales, const void* zeros, int dtype, void* sz, int N, void* stream);
+
+/* ---------------------------------------------------------------- linear layers
+ * wfmt: 0 = int4 W4P (sz = (scale, 128+zero) pairs required), 1 = bf16 (N, K) row-major
+ * (torch.nn.Linear.weight), 2 = LLM.int8() CB (N, K) int8 with sz = SCB (N) fp32; for
+ * wfmt 2, `i8ws` is the statistics workspace llj_i8_stats filled for the whole activation
+ * and `i8_row0` the index of this call's first row in it (NULL / 0 otherwise).
+ * C[M, N] = A[M, K] . W^T (+ bias), bf16 in/out, fp32 (int8: int32) accumulation,
+ * M <= 16 rows per call (int8: <= 8).
+ * Replaces qlinear_4bit_weight / linear_kernel_4bit_weight (quantization.py:80-331),
+ * ColBlockQuantizedLinear.forward (quantization.py:411-421), bnb Linear8bitLt.forward
+ * (used by quantization.py:36-75) and, for wfmt 1, F.linear. */
+int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, const void* bias, void* C, int ldc,
+               int M, int N, int K, const void* i8ws, int i8_row0, void* stream);
+
+/* ---------------------------------------------------------------- fused decode-layer ops
+ * (Block.forward, lit_llama/model.py:162-175, split at its four Linear boundaries).
+ * norm_w == NULL means the input is used as is (no fused RMSNorm); int8 (wfmt 2) takes
+ * already-normalised input (its statistics are computed on it). */
+
+/* rms_1 + attn.c_attn + split q/k/v + apply_rope(q, k) + KV-cache write
+ * (model.py:171, 204-228, 312-329). x (B*T, C) rows m = b*T + t; q_out (B*T, C);
+ * kcache/vcache (B, n_head, S, hs) with token at absolute position p stored in slot p % S
+ * (ring form of the reference's roll-by-one sliding window, model.py:221-227);
+ * rope (block_size, hs/2, 2) fp32 (build_rope_cache, model.py:286-309); pos (T) int32.
+ * Handles rows [row0, row0 + rows) of the B*T rows; rows <= 8 (RMSNorm staged in LDS). */
+int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
+                      void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
+                      int C, int n_head, int S, int row0, int rows, const void* i8ws, void* stream);
+
+/* Causal attention of q (B*T, C) over the cache slots each query may see
+ * (F.scaled_dot_product_attention with the tril mask rows, model.py:101-104, 237):
+ * positions <= p, or all S slots once p >= S. y (B*T, C) bf16. head_size 64 or 128. */
+int llj_attention(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                  int n_head, int head_size, int S, void* stream);
+
+/* x[M, N] += A[M, K] . W^T (attn.c_proj / mlp.c_proj + residual add, model.py:172-173). */
+int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
+                     int N, int K, const void* i8ws, int i8_row0, void* stream);
+
+/* h[M, H] = silu(rms_2(x) . W1^T) * (rms_2(x) . W2^T)  (model.py:173, 258). M <= 8. */
+int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
+                    const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,
+                    void* stream);
+
+/* out[M, N] = RMSNorm(x) . W^T  (ln_f + lm_head, model.py:125-127). M <= 8. */
+int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
+                    void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, void* stream);
+
+/* ---------------------------------------------------------------- LLM.int8() */
+/* Bytes of the activation-statistics workspace for an (M, K) activation (host function). */
+size_t llj_i8_ws_bytes(int M, int K);
+/* Outlier columns (any row |A16| >= threshold) and per-row absmax of the other elements of
+ * A (M, K) bf16 into ws (bitsandbytes double_quant(A, threshold) as used by MatMul8bitLt). */
+int llj_i8_stats(const void* A, int lda, int M, int K, float threshold, void* ws, void* stream);
+/* CB = round(W16 * 127 / SCB), SCB = row absmax of W16 = W.half() (Linear8bitLt._quantize_weight,
+ * quantization.py:67-75). W (N, K) of dtype 0 fp32 / 1 bf16 / 2 fp16. */
+int llj_i8_quant_weight(const void* W, int dtype, void* CB, void* SCB, int N, int K, void* stream);
+
+/* ---------------------------------------------------------------- small ops */
+/* out[m] = wte[idx[m]] (model.py:110); if pos_inc != NULL, *pos_inc += 1 (device-side
+ * decode position, so a captured decode step advances itself). */
+int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, void* stream);
+
+/* Standalone RMSNorm (model.py:276-283) for rows the fused prologue does not take. */
+int llj_rmsnorm(const void* x, const void* w, float eps, void* y, int M, int C, void* stream);
+
+/* Greedy next token (generate.py:66-74 with top_k = 1): out_idx[m] = argmax logits[m, :V]
+ * (lowest index on ties). If tokens_out != NULL also tokens_out[m*tok_stride + *pos + 1]. */
+int llj_argmax(const void* logits, int ldl, int M, int V, int* out_idx, int* tokens_out, int tok_stride,
+               const int* pos, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LIT_LLAMA_AMD_H */

@@ -1,0 +1,70 @@
+// Shared device helpers for the lit-llama MI355X (gfx950) decode path.
+// Wave64 everywhere; MFMA 16x16x32 bf16 / 16x16x64 i8 operand maps per the CDNA4 guide:
+//   A: lane l holds A[row l&15][k = 8*(l>>4) + j], B: lane l holds B[k = 8*(l>>4) + j][col l&15]
+//   C/D: lane l, reg r holds C[row 4*(l>>4) + r][col l&15]
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace llj {
+
+typedef uint16_t bf16_t;  // raw bf16 bits in HBM
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(bf16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
+__device__ __forceinline__ float bflo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bfhi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+
+// fp32 -> bf16 round-to-nearest-even (lowers to v_cvt_pk_bf16_f32 on gfx950; keeps NaN)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  return __builtin_bit_cast(bf16_t, __float2bfloat16(f));
+}
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+
+// (x & m) | c in one VALU op (hipcc does not fuse literals into VOP3 on gfx9 encodings).
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m_sgpr, uint32_t c) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m_sgpr), "v"(c));
+  return r;
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+}  // namespace llj
+
+// Error convention for the C ABI: 0 = ok, otherwise a hipError_t or one of these.
+#define LLJ_EINVAL 1000
+#define LLJ_CHECK_LAUNCH()                         \
+  do {                                             \
+    hipError_t e__ = hipGetLastError();            \
+    if (e__ != hipSuccess) return (int)e__;        \
+  } while (0)
+#define LLJ_REQUIRE(c) \
+  do {                 \
+    if (!(c)) return LLJ_EINVAL; \
+  } while (0)

@@ -1,0 +1,597 @@
+// Weight-streaming skinny GEMM ("GEMV", M <= 16 rows per pass) for the LLaMA decode step on
+// gfx950, with the reference's per-layer elementwise work fused into prologue/epilogue.
+//
+// Replaces, for the decode path:
+//   reference lit_llama/quantization.py:282-331 (qlinear_4bit_weight / Triton
+//   linear_kernel_4bit_weight 80-280) and :411-421 (ColBlockQuantizedLinear.forward),
+//   :36-75 (Linear8bitLt = bitsandbytes LLM.int8() matmul), plus torch.nn.Linear (F.linear)
+//   for the bf16 model; fused with model.py:276-283 (RMSNorm), :204-228 (c_attn split,
+//   apply_rope, KV-cache write), :172-173 (residual adds) and :258 (silu(c_fc1) * c_fc2).
+//
+// Work decomposition: one workgroup (NW waves) owns one 16-column n-tile over the whole K;
+// its waves split K into 128-deep chunks round-robin and the partial sums are reduced in
+// LDS, so no cross-workgroup reduction exists. A chunk is 4 MFMA 16x16x32 bf16 steps (or 2
+// MFMA 16x16x64 i8 steps). The weight stream uses non-temporal loads, D chunks in flight.
+//
+// Weight formats (WF):
+//  * WF_W4 — int4 repacked "W4P" layout (w4pack.hip): per (n-tile, k-chunk) one contiguous
+//    1 KiB block; lane l's 16 bytes are the 32 codes of column 16*nt + (l&15) for
+//    k = 128*kc + 32*(l>>4) + [0,32), so one global_load_dwordx4 per wave fetches a fully
+//    coalesced 1 KiB and needs no LDS. Codes become bf16 (128 + q) with one v_and_or_b32
+//    (magic exponent) per pair; the 128 + zero offset is removed in the epilogue with the
+//    row sums of A, computed by an extra MFMA against a ones fragment:
+//      y[m,n] = s[n] * (sum_k A[m,k] (128 + q[k,n]) - (128 + z[n]) * sum_k A[m,k])
+//             = sum_k A[m,k] * (q[k,n] - z[n]) * s[n]          (get_weight semantics)
+//  * WF_BF16 — torch.nn.Linear weight (N, K) row-major bf16, read in place.
+//  * WF_I8 — LLM.int8(): CB (N, K) int8 row-quantized weight + SCB (N) fp32. A is quantized
+//    per row in the prologue (absmax over non-outlier elements, outlier columns zeroed,
+//    statistics from llj_i8_stats in int8.hip), int32 MFMA accumulation, dequant by
+//    SCA*SCB/127^2, plus the fp16 side product over the outlier columns.
+#include "common.h"
+
+namespace llj {
+
+enum : int { WF_W4 = 0, WF_BF16 = 1, WF_I8 = 2 };
+enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2 };
+enum : int { EP_STORE = 0, EP_RESID = 1, EP_QKV = 2, EP_SWIGLU = 3 };
+
+// int8 activation-statistics workspace written by llj_i8_stats (int8.hip)
+struct I8WsHeader {
+  int mtot, K, nsb, kb;
+};
+__host__ __device__ inline const float* i8_partial(const void* ws) {
+  return reinterpret_cast<const float*>(reinterpret_cast<const char*>(ws) + 16);
+}
+
+struct GemvParams {
+  const bf16_t* A;  // (M, K), row stride lda elements
+  int lda;
+  const bf16_t* norm_w;  // AM_NORM: RMSNorm scale (K)
+  float eps;
+  int M, N, K;
+  const void* W;   // WF_W4: W4P tiles; WF_BF16: (N, K) bf16; WF_I8: (N, K) int8
+  const void* W2;  // EP_SWIGLU: c_fc2
+  const float2* sz;   // WF_W4: per column (scale, 128 + zero); WF_I8: (const float*) SCB
+  const float2* sz2;
+  const bf16_t* bias;  // optional (N)
+  bf16_t* C;  // EP_STORE / EP_SWIGLU: out (M, ldc); EP_RESID: residual stream updated in place
+  int ldc;
+  // EP_QKV
+  bf16_t* q_out;   // (B*T, n_embd)
+  bf16_t* kcache;  // (B, n_head, S, hs)
+  bf16_t* vcache;
+  const float* rope;  // (block_size, hs/2, 2)
+  const int* pos;     // (T) absolute positions of the T rows of each sequence
+  int n_head, head_size, S, T;
+  int m0;  // global row index of local row 0 (QKV row chunks; int8 statistics rows)
+  const void* i8ws;
+};
+
+// ------------------------------------------------------------------------------------
+// Stage A rows [0, M) into LDS (row stride K + 8 elements); row M is all zeros (read by the
+// MFMA lanes of rows >= M). With NORM, rows are RMS-normalised with the reference's bf16
+// rounding points (model.py:281-283 evaluated on bf16 tensors).
+template <int NW, bool NORM>
+__device__ void stage_a(const GemvParams& p, bf16_t* As, int a_stride, float* red) {
+  const int tid = threadIdx.x;
+  constexpr int NT = NW * 64;
+  const int K = p.K, M = p.M;
+  const int nvec = K >> 3;
+  float ss[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) ss[m] = 0.f;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    if (m < M) {
+      const uint4* src = reinterpret_cast<const uint4*>(p.A + (size_t)m * p.lda);
+      uint4* dst = reinterpret_cast<uint4*>(As + (size_t)m * a_stride);
+      for (int v = tid; v < nvec; v += NT) {
+        uint4 x = src[v];
+        dst[v] = x;
+        if (NORM) {
+          uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float a = bflo(w[i]), b = bfhi(w[i]);
+            ss[m] += round_bf(a * a) + round_bf(b * b);
+          }
+        }
+      }
+    }
+  }
+  {
+    uint4* z = reinterpret_cast<uint4*>(As + (size_t)M * a_stride);
+    for (int v = tid; v < nvec; v += NT) z[v] = make_uint4(0, 0, 0, 0);
+  }
+  if (!NORM) return;
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    float s = wave_sum(ss[m]);
+    if (lane == 0) red[wave * 8 + m] = s;
+  }
+  __syncthreads();
+  if (tid < 8) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[w * 8 + tid];
+    // bf16: mean(x*x) -> +eps -> rsqrt, each rounded (torch bf16 ops)
+    float ms = round_bf(s / (float)K);
+    red[NW * 8 + tid] = round_bf(rsqrtf(round_bf(ms + p.eps)));
+  }
+  __syncthreads();
+  const uint4* g4 = reinterpret_cast<const uint4*>(p.norm_w);
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    if (m < M) {
+      const float r = red[NW * 8 + m];
+      uint4* row = reinterpret_cast<uint4*>(As + (size_t)m * a_stride);
+      for (int v = tid; v < nvec; v += NT) {
+        uint4 x = row[v], g = g4[v];
+        uint32_t xw[4] = {x.x, x.y, x.z, x.w}, gw[4] = {g.x, g.y, g.z, g.w}, o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float lo = round_bf(bflo(gw[i]) * round_bf(bflo(xw[i]) * r));
+          float hi = round_bf(bfhi(gw[i]) * round_bf(bfhi(xw[i]) * r));
+          o[i] = pack2bf(lo, hi);
+        }
+        row[v] = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+}
+
+// int8: quantize rows [0, M) of A into LDS int8 rows (stride K + 16 bytes) with the
+// per-row absmax SCA (non-outlier elements; from the llj_i8_stats partials) and the
+// outlier columns zeroed; row M is zeros. sca[] receives SCA per local row.
+template <int NW>
+__device__ void stage_i8(const GemvParams& p, int8_t* Aq, int q_stride, float* sca) {
+  const int tid = threadIdx.x;
+  constexpr int NT = NW * 64;
+  const int K = p.K, M = p.M;
+  const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
+  const float* part = i8_partial(p.i8ws);
+  const int* cnt = reinterpret_cast<const int*>(part + (size_t)h.nsb * h.mtot);
+  const int* list = cnt + h.nsb;
+  if (tid < M) {
+    float mx = 0.f;
+    for (int b = 0; b < h.nsb; ++b) mx = fmaxf(mx, part[(size_t)b * h.mtot + p.m0 + tid]);
+    sca[tid] = mx;
+  }
+  __syncthreads();
+  const int nvec = K >> 3;
+  for (int m = 0; m < M; ++m) {
+    const float s = sca[m];
+    const float inv = s > 0.f ? 127.f / s : 0.f;
+    const uint4* src = reinterpret_cast<const uint4*>(p.A + (size_t)m * p.lda);
+    uint2* dst = reinterpret_cast<uint2*>(Aq + (size_t)m * q_stride);
+    for (int v = tid; v < nvec; v += NT) {
+      uint4 x = src[v];
+      uint32_t w[4] = {x.x, x.y, x.z, x.w};
+      uint32_t o[2] = {0, 0};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float a = (float)(_Float16)bflo(w[i]), b = (float)(_Float16)bfhi(w[i]);
+        const int qa = (int)fminf(fmaxf(rintf(a * inv), -127.f), 127.f);
+        const int qb = (int)fminf(fmaxf(rintf(b * inv), -127.f), 127.f);
+        o[i >> 1] |= ((uint32_t)(qa & 0xFF) | ((uint32_t)(qb & 0xFF) << 8)) << (16 * (i & 1));
+      }
+      dst[v] = make_uint2(o[0], o[1]);
+    }
+  }
+  {
+    uint2* z = reinterpret_cast<uint2*>(Aq + (size_t)M * q_stride);
+    for (int v = tid; v < nvec; v += NT) z[v] = make_uint2(0, 0);
+  }
+  __syncthreads();
+  // zero the outlier columns (their contribution is the fp16 side product)
+  for (int b = 0; b < h.nsb; ++b) {
+    const int c = cnt[b];
+    for (int i = tid; i < c * M; i += NT) {
+      const int k = list[b * h.kb + i / M];
+      Aq[(size_t)(i % M) * q_stride + k] = 0;
+    }
+  }
+}
+
+__device__ __forceinline__ bf16x8 dequant_w4(uint32_t w, uint32_t msk, uint32_t mag) {
+  uint4 b = make_uint4(and_or(w, msk, mag), and_or(w >> 4, msk, mag), and_or(w >> 8, msk, mag),
+                       and_or(w >> 12, msk, mag));
+  return __builtin_bit_cast(bf16x8, b);
+}
+
+template <int WF>
+__device__ __forceinline__ int kofs(int t, int grp) {
+  // k offset inside a 128-deep chunk of the elements lane-group `grp` feeds at MFMA step t
+  return WF == WF_W4 ? 32 * grp + 8 * t : WF == WF_BF16 ? 32 * t + 8 * grp : 64 * t + 16 * grp;
+}
+
+// fp16 side product of LLM.int8() over the outlier columns: sum_k f16(A[m,k]) * f16(CB[n,k]*SCB[n]/127)
+__device__ float i8_side(const GemvParams& p, const int8_t* CB, float scb, int m, int n) {
+  const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
+  const float* part = i8_partial(p.i8ws);
+  const int* cnt = reinterpret_cast<const int*>(part + (size_t)h.nsb * h.mtot);
+  const int* list = cnt + h.nsb;
+  float s = 0.f;
+  for (int b = 0; b < h.nsb; ++b) {
+    const int c = cnt[b];
+    for (int i = 0; i < c; ++i) {
+      const int k = list[b * h.kb + i];
+      const float a = (float)(_Float16)bf2f(p.A[(size_t)m * p.lda + k]);
+      const float w = (float)(_Float16)((float)CB[(size_t)n * p.K + k] * (scb / 127.f));
+      s += a * w;
+    }
+  }
+  return s;
+}
+
+// Shared epilogue for one output element (m local row < M, n column) of value y (and y2).
+template <int EP>
+__device__ __forceinline__ void store_out(const GemvParams& p, int m, int n, float y, float y2) {
+  bf16_t* dst = p.C + (size_t)m * p.ldc + n;
+  if (EP == EP_STORE) {
+    *dst = f2bf(y);
+  } else if (EP == EP_RESID) {
+    *dst = f2bf(bf2f(*dst) + round_bf(y));  // x = x + h, both bf16 (model.py:172-173)
+  } else if (EP == EP_SWIGLU) {
+    const float a1 = round_bf(y), a2 = round_bf(y2);
+    const float sl = round_bf(a1 / (1.f + __expf(-a1)));  // F.silu in bf16
+    *dst = f2bf(sl * a2);
+  }
+}
+
+template <int WF, int AM, int EP, int NW, int D>
+__global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr bool DUAL = (EP == EP_SWIGLU);
+  constexpr bool I8 = (WF == WF_I8);
+  constexpr bool ALDS = I8 || (AM != AM_GLOBAL);
+  constexpr int WV = (WF == WF_W4) ? 1 : (WF == WF_BF16 ? 4 : 2);  // 16-B loads per lane per chunk per matrix
+  constexpr int NSTEP = I8 ? 2 : 4;
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform(threadIdx.x >> 6);
+  const int nt = blockIdx.x;
+  const int n0 = nt * 16;
+  const int K = p.K, M = p.M, KC = K >> 7;
+  const int row = lane & 15, grp = lane >> 4;
+  // LDS carve: A image | reduction scratch | sca
+  const int a_stride = I8 ? K + 16 : K + 8;  // elements (bytes for int8)
+  const size_t a_bytes = ALDS ? (((size_t)(M + 1) * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15) : 0;
+  float* red = reinterpret_cast<float*>(smem + a_bytes);
+  float* sca = red + NW * 64 * 12;
+
+  if constexpr (I8) {
+    stage_i8<NW>(p, reinterpret_cast<int8_t*>(smem), a_stride, sca);
+    __syncthreads();
+  } else if constexpr (ALDS) {
+    stage_a<NW, AM == AM_NORM>(p, reinterpret_cast<bf16_t*>(smem), a_stride, red);
+    __syncthreads();
+  }
+  const bool arow = row < M;
+  const unsigned char* abase;  // byte address of this lane's A row
+  if (ALDS) {
+    abase = smem + (size_t)(arow ? row : M) * a_stride * (I8 ? 1 : 2);
+  } else {
+    abase = reinterpret_cast<const unsigned char*>(p.A + (size_t)(arow ? row : 0) * p.lda);
+  }
+  constexpr int EB = I8 ? 1 : 2;  // A element bytes
+
+  const uint32_t msk = uniform(0x000F000F);
+  const uint32_t mag = 0x43004300u;
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
+  const u32x4 zero4 = {0, 0, 0, 0};
+
+  // weight stream pointers (lane-resolved), in 16-byte units
+  const u32x4* w1;
+  const u32x4* w2 = nullptr;
+  size_t wstep;  // 16-B units between consecutive chunks of this lane
+  int vstride;   // 16-B units between the WV loads of one chunk
+  if (WF == WF_W4) {
+    w1 = reinterpret_cast<const u32x4*>(p.W) + (size_t)nt * KC * 64 + lane;
+    if (DUAL) w2 = reinterpret_cast<const u32x4*>(p.W2) + (size_t)nt * KC * 64 + lane;
+    wstep = 64; vstride = 0;
+  } else if (WF == WF_BF16) {
+    const size_t off = (size_t)(n0 + row) * K + 8 * grp;  // elements
+    w1 = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.W) + off);
+    if (DUAL) w2 = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.W2) + off);
+    wstep = 16; vstride = 4;  // chunk = 256 B of a row; step t at +64 B
+  } else {
+    const size_t off = (size_t)(n0 + row) * K + 16 * grp;  // bytes
+    w1 = reinterpret_cast<const u32x4*>(reinterpret_cast<const int8_t*>(p.W) + off);
+    if (DUAL) w2 = reinterpret_cast<const u32x4*>(reinterpret_cast<const int8_t*>(p.W2) + off);
+    wstep = 8; vstride = 4;  // chunk = 128 B of a row; step t at +64 B
+  }
+
+  f32x4 acc = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, sacc = {0, 0, 0, 0};
+  i32x4 iacc = {0, 0, 0, 0}, iacc2 = {0, 0, 0, 0};
+  const int nmy = uniform((KC - wave + NW - 1) / NW);
+
+  if (nmy > 0) {
+    u32x4 r1[D][WV], r2[D][WV];
+    u32x4 ra[D][4];
+    auto load = [&](int d, int i) {
+      const int c = wave + NW * (i < nmy ? i : nmy - 1);
+#pragma unroll
+      for (int v = 0; v < WV; ++v) {
+        r1[d][v] = __builtin_nontemporal_load(w1 + (size_t)c * wstep + vstride * v);
+        if (DUAL) r2[d][v] = __builtin_nontemporal_load(w2 + (size_t)c * wstep + vstride * v);
+      }
+      if (!ALDS) {
+#pragma unroll
+        for (int t = 0; t < NSTEP; ++t)
+          ra[d][t] = arow ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : zero4;
+      }
+    };
+    auto compute = [&](int d, int i) {
+      const int c = wave + NW * i;
+#pragma unroll
+      for (int t = 0; t < NSTEP; ++t) {
+        const u32x4 av = ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
+        if constexpr (WF == WF_W4) {
+          const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+          acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
+          if (DUAL) acc2 = mfma_bf16(a, dequant_w4(r2[d][0][t], msk, mag), acc2);
+          sacc = mfma_bf16(a, ones, sacc);
+        } else if constexpr (WF == WF_BF16) {
+          const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+          acc = mfma_bf16(a, __builtin_bit_cast(bf16x8, r1[d][t]), acc);
+          if (DUAL) acc2 = mfma_bf16(a, __builtin_bit_cast(bf16x8, r2[d][t]), acc2);
+        } else {
+          const i32x4 a = __builtin_bit_cast(i32x4, av);
+          iacc = mfma_i8(a, __builtin_bit_cast(i32x4, r1[d][t]), iacc);
+          if (DUAL) iacc2 = mfma_i8(a, __builtin_bit_cast(i32x4, r2[d][t]), iacc2);
+        }
+      }
+    };
+#pragma unroll
+    for (int d = 0; d < D; ++d) load(d, d);
+    for (int i0 = 0; i0 < nmy; i0 += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        if (i0 + d < nmy) compute(d, i0 + d);
+        load(d, i0 + d + D);
+      }
+    }
+  }
+  // ---- reduce the NW partial tiles in LDS (each wave: 64 lanes x 12 words; int8 sums stay
+  // int32 — they exceed 2^24 at K = 11008, so they must not round-trip through fp32)
+  constexpr int NV = 12;
+  if (NW > 1) {
+    if constexpr (I8) {
+      int* mine = reinterpret_cast<int*>(red) + (size_t)(wave * 64 + lane) * NV;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        mine[r] = iacc[r];
+        mine[4 + r] = iacc2[r];
+      }
+    } else {
+      float* mine = red + (size_t)(wave * 64 + lane) * NV;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        mine[r] = acc[r];
+        mine[4 + r] = acc2[r];
+        mine[8 + r] = sacc[r];
+      }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      if constexpr (I8) {
+        const int* o = reinterpret_cast<const int*>(red) + (size_t)(w * 64 + lane) * NV;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          iacc[r] += o[r];
+          iacc2[r] += o[4 + r];
+        }
+      } else {
+        const float* o = red + (size_t)(w * 64 + lane) * NV;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc[r] += o[r];
+          acc2[r] += o[4 + r];
+          sacc[r] += o[8 + r];
+        }
+      }
+    }
+  }
+
+  // ---- epilogue (wave 0): lane holds C[m = 4*grp + r][n = n0 + row]
+  const int n = n0 + row;
+  float s1 = 1.f, o1 = 0.f, s2 = 1.f, o2 = 0.f;
+  if (WF == WF_W4) {
+    float2 a = p.sz[n];
+    s1 = a.x; o1 = a.y;
+    if (DUAL) { float2 b = p.sz2[n]; s2 = b.x; o2 = b.y; }
+  } else if (I8) {
+    s1 = reinterpret_cast<const float*>(p.sz)[n];
+    if (DUAL) s2 = reinterpret_cast<const float*>(p.sz2)[n];
+  }
+  const float bias = p.bias ? bf2f(p.bias[n]) : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = 4 * grp + r;
+    float y, y2 = 0.f;
+    if (WF == WF_W4) {
+      y = s1 * (acc[r] - o1 * sacc[r]);
+      if (DUAL) y2 = s2 * (acc2[r] - o2 * sacc[r]);
+    } else if (WF == WF_BF16) {
+      y = acc[r];
+      y2 = acc2[r];
+    } else {
+      // mm_dequant (fp16 out) + fp16 outlier product, then cast back (bnb MatMul8bitLt)
+      const float sa = m < M ? sca[m] : 0.f;
+      const float kq = 1.f / (127.f * 127.f);
+      y = (float)iacc[r] * (sa * s1 * kq);
+      if (DUAL) y2 = (float)iacc2[r] * (sa * s2 * kq);
+      if (m < M) {
+        y = (float)(_Float16)((float)(_Float16)y + i8_side(p, reinterpret_cast<const int8_t*>(p.W), s1, m, n));
+        if (DUAL) y2 = (float)(_Float16)((float)(_Float16)y2 + i8_side(p, reinterpret_cast<const int8_t*>(p.W2), s2, m, n));
+      }
+    }
+    y += bias;
+    if (EP == EP_QKV) {
+      // c_attn output rounded to bf16 (model.py:204), then RoPE in fp32 (model.py:318-329)
+      const float v = round_bf(y);
+      const float partner = __shfl_xor(v, 1, 64);
+      if (m < M) {
+        const int Cd = p.n_head * p.head_size;
+        const int region = n0 / Cd;  // 0 q, 1 k, 2 v (uniform per workgroup)
+        const int nc = n - region * Cd;
+        const int h = nc / p.head_size, dd = nc % p.head_size;
+        const int mg = p.m0 + m;
+        const int b = mg / p.T, t = mg % p.T;
+        const int ps = p.pos[t];
+        float out = v;
+        if (region < 2) {
+          const float* rc = p.rope + ((size_t)ps * (p.head_size >> 1) + (dd >> 1)) * 2;
+          const float c = rc[0], s = rc[1];
+          out = (dd & 1) ? (v * c + partner * s) : (v * c - partner * s);
+        }
+        const bf16_t ob = f2bf(out);
+        if (region == 0) {
+          p.q_out[(size_t)mg * Cd + nc] = ob;
+        } else {
+          const int slot = ps % p.S;
+          const size_t ci = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
+          (region == 1 ? p.kcache : p.vcache)[ci] = ob;
+        }
+      }
+    } else if (m < M) {
+      store_out<EP>(p, m, n, y, y2);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+constexpr int kNW = 4;
+constexpr int kD = 4;
+
+static inline size_t a_image_bytes(int wf, int am, int M, int K) {
+  if (wf == WF_I8) return (((size_t)(M + 1) * (K + 16)) + 15) & ~(size_t)15;
+  if (am == AM_GLOBAL) return 0;
+  return (((size_t)(M + 1) * (K + 8) * 2) + 15) & ~(size_t)15;
+}
+static inline size_t gemv_smem(int wf, int am, int M, int K) {
+  return a_image_bytes(wf, am, M, K) + (size_t)kNW * 64 * 12 * 4 + 8 * 4;
+}
+
+// the LDS A image must leave room for the reduction scratch: <= 96 KiB, M <= 8 rows
+static inline bool lds_fits(int wf, int M, int K) { return M <= 8 && a_image_bytes(wf, AM_LDS, M, K) <= 96 * 1024; }
+
+template <int WF, int AM, int EP>
+static int launch(const GemvParams& p, hipStream_t s) {
+  const size_t sm = gemv_smem(WF, AM, p.M, p.K);
+  auto kern = gemv_kernel<WF, AM, EP, kNW, kD>;
+  static bool attr_set = false;  // per instantiation; set before any graph capture
+  if (sm > 64 * 1024 && !attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(p.N / 16), dim3(kNW * 64), sm, s, p);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int EP>
+static int dispatch(int wf, int am, const GemvParams& p, hipStream_t s) {
+  if (wf == WF_I8) return launch<WF_I8, AM_LDS, EP>(p, s);
+  if (wf == WF_W4) {
+    if (am == AM_NORM) return launch<WF_W4, AM_NORM, EP>(p, s);
+    if (am == AM_LDS) return launch<WF_W4, AM_LDS, EP>(p, s);
+    return launch<WF_W4, AM_GLOBAL, EP>(p, s);
+  }
+  if (am == AM_NORM) return launch<WF_BF16, AM_NORM, EP>(p, s);
+  if (am == AM_LDS) return launch<WF_BF16, AM_LDS, EP>(p, s);
+  return launch<WF_BF16, AM_GLOBAL, EP>(p, s);
+}
+
+// A mode for a call: fused RMSNorm needs the LDS image; otherwise stage when it fits.
+static int pick_am(int wf, const GemvParams& p) {
+  if (wf == WF_I8) return (p.norm_w || !p.i8ws || !lds_fits(wf, p.M, p.K)) ? -1 : AM_LDS;
+  if (p.norm_w) return lds_fits(wf, p.M, p.K) ? AM_NORM : -1;
+  return lds_fits(wf, p.M, p.K) ? AM_LDS : AM_GLOBAL;
+}
+
+static int check_shape(int wf, const GemvParams& p) {
+  if (p.M < 1 || p.M > 16 || p.N % 16 || p.K % 128 || p.K < 128) return LLJ_EINVAL;
+  if (wf != WF_W4 && wf != WF_BF16 && wf != WF_I8) return LLJ_EINVAL;
+  if (wf != WF_BF16 && !p.sz) return LLJ_EINVAL;
+  return 0;
+}
+
+template <int EP>
+static int run(int wf, GemvParams& p, void* stream) {
+  if (int e = check_shape(wf, p)) return e;
+  if (EP == EP_SWIGLU && wf != WF_BF16 && !p.sz2) return LLJ_EINVAL;
+  const int am = pick_am(wf, p);
+  if (am < 0) return LLJ_EINVAL;
+  return dispatch<EP>(wf, am, p, (hipStream_t)stream);
+}
+
+}  // namespace llj
+
+using namespace llj;
+
+extern "C" {
+
+// C[M,N] = A[M,K] . W^T (+bias); bf16 in/out, fp32 accumulation, M <= 16 (int8: <= 8) per call.
+int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, const void* bias, void* C,
+               int ldc, int M, int N, int K, const void* i8ws, int i8_row0, void* stream) {
+  GemvParams p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K;
+  p.W = W; p.sz = (const float2*)sz; p.bias = (const bf16_t*)bias; p.C = (bf16_t*)C; p.ldc = ldc;
+  p.i8ws = i8ws; p.m0 = i8_row0;
+  return run<EP_STORE>(wfmt, p, stream);
+}
+
+// out[M,N] = RMSNorm(x)[M,K] . W^T  (ln_f + lm_head, model.py:125-127); norm_w NULL = no norm.
+int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
+                    void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, void* stream) {
+  GemvParams p{};
+  p.A = (const bf16_t*)x; p.lda = K; p.norm_w = (const bf16_t*)norm_w; p.eps = eps; p.M = M; p.N = N; p.K = K;
+  p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)out; p.ldc = ldo;
+  p.i8ws = i8ws; p.m0 = i8_row0;
+  return run<EP_STORE>(wfmt, p, stream);
+}
+
+// x[M,N] += A[M,K] . W^T, bf16 residual add (attn.c_proj / mlp.c_proj + model.py:172-173).
+int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
+                     int N, int K, const void* i8ws, int i8_row0, void* stream) {
+  GemvParams p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K;
+  p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)x; p.ldc = ldx;
+  p.i8ws = i8ws; p.m0 = i8_row0;
+  return run<EP_RESID>(wfmt, p, stream);
+}
+
+// h[M,H] = silu(RMSNorm(x) . W1^T) * (RMSNorm(x) . W2^T)  (rms_2 + model.py:258).
+int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
+                    const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,
+                    void* stream) {
+  GemvParams p{};
+  p.A = (const bf16_t*)x; p.lda = K; p.norm_w = (const bf16_t*)norm_w; p.eps = eps; p.M = M; p.N = H; p.K = K;
+  p.W = W1; p.W2 = W2; p.sz = (const float2*)sz1; p.sz2 = (const float2*)sz2; p.C = (bf16_t*)h; p.ldc = H;
+  p.i8ws = i8ws; p.m0 = i8_row0;
+  return run<EP_SWIGLU>(wfmt, p, stream);
+}
+
+// rms_1 + c_attn + split + RoPE(q,k) + KV-cache write at slot pos % S (model.py:171,204-228).
+// Rows m = b*T + t of x (B*T, C); this call handles rows [row0, row0 + rows), rows <= 8;
+// q_out (B*T, C); caches (B, n_head, S, hs).
+int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
+                      void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
+                      int C, int n_head, int S, int row0, int rows, const void* i8ws, void* stream) {
+  GemvParams p{};
+  if (row0 < 0 || rows < 1 || row0 + rows > B * T || n_head < 1 || C % n_head || S < 1) return LLJ_EINVAL;
+  p.A = (const bf16_t*)x + (size_t)row0 * C; p.lda = C; p.norm_w = (const bf16_t*)norm_w; p.eps = eps;
+  p.M = rows; p.m0 = row0; p.N = 3 * C; p.K = C;
+  p.W = W; p.sz = (const float2*)sz; p.q_out = (bf16_t*)q_out; p.kcache = (bf16_t*)kcache;
+  p.vcache = (bf16_t*)vcache; p.rope = rope; p.pos = pos; p.n_head = n_head; p.head_size = C / n_head;
+  p.S = S; p.T = T; p.i8ws = i8ws;
+  if (p.head_size & 1 || rows > 8) return LLJ_EINVAL;
+  return run<EP_QKV>(wfmt, p, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,222 @@
+// Decode-step ops around the weight-streaming GEMVs: token embedding, standalone RMSNorm
+// (prefill rows beyond the fused-LDS limit), causal attention over the KV cache, and the
+// greedy (top_k = 1) next-token selection.
+#include "common.h"
+
+namespace llj {
+
+// ---- embedding: out[m] = wte[idx[m]]  (reference model.py:110). Optionally bumps the
+// device-side decode position (*pos_inc += 1) so a captured decode step is self-advancing.
+__global__ void embedding_kernel(const int* __restrict__ idx, const uint4* __restrict__ wte, uint4* __restrict__ out,
+                                 int C8, int* pos_inc) {
+  const int m = blockIdx.x;
+  const size_t r = (size_t)idx[m];
+  for (int v = threadIdx.x; v < C8; v += blockDim.x) out[(size_t)m * C8 + v] = wte[r * C8 + v];
+  if (pos_inc && m == 0 && threadIdx.x == 0) *pos_inc += 1;
+}
+
+// ---- RMSNorm with the bf16 rounding points of model.py:281-283 on bf16 tensors.
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                      float eps, bf16_t* __restrict__ y, int C) {
+  __shared__ float red[4];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)m * C);
+  const uint4* g4 = reinterpret_cast<const uint4*>(w);
+  uint4* yr = reinterpret_cast<uint4*>(y + (size_t)m * C);
+  const int nvec = C >> 3;
+  float ss = 0.f;
+  for (int v = tid; v < nvec; v += 256) {
+    uint4 a = xr[v];
+    uint32_t aw[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ss += round_bf(bflo(aw[i]) * bflo(aw[i])) + round_bf(bfhi(aw[i]) * bfhi(aw[i]));
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float r = round_bf(rsqrtf(round_bf(round_bf(tot / (float)C) + eps)));
+  for (int v = tid; v < nvec; v += 256) {
+    uint4 a = xr[v], g = g4[v];
+    uint32_t aw[4] = {a.x, a.y, a.z, a.w}, gw[4] = {g.x, g.y, g.z, g.w}, o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      o[i] = pack2bf(round_bf(bflo(gw[i]) * round_bf(bflo(aw[i]) * r)), round_bf(bfhi(gw[i]) * round_bf(bfhi(aw[i]) * r)));
+    yr[v] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// ---- attention for query rows m = b*T + t against cache slots of sequence b.
+// Reference semantics (model.py:101-104, 218-237): query at absolute position p attends
+// the slots holding tokens <= p; once p >= S (sliding window after the roll) it attends
+// all S slots. Slots are a ring (token p lives at p % S): same key set as the reference's
+// roll-by-one, so the softmax is identical up to summation order.
+// 16 lanes per key (HS/16 dims each), 16 keys in flight per 256-thread block.
+template <int HS, int U>
+__global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+                                                        const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
+                                                        const int* __restrict__ pos, int T, int S, int nh,
+                                                        float scale_log2) {
+  constexpr int DPL = HS / 16;
+  __shared__ float s_m[16], s_l[16];
+  __shared__ float s_o[16][HS + 1];
+  const int h = blockIdx.x, m = blockIdx.y;
+  const int b = m / T, t = m % T;
+  const int ps = pos[t];
+  const int nvalid = ps < S ? ps + 1 : S;
+  const int sub = threadIdx.x & 15, kg = threadIdx.x >> 4;
+  const int C = nh * HS;
+  float qf[DPL];
+  {
+    const bf16_t* qp = q + (size_t)m * C + h * HS + sub * DPL;
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) qf[i] = bf2f(qp[i]) * scale_log2;
+  }
+  const size_t base = ((size_t)(b * nh + h) * S) * HS + sub * DPL;
+  const bf16_t* kb = kc + base;
+  const bf16_t* vb = vc + base;
+  float mx = -INFINITY, l = 0.f, o[DPL];
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) o[i] = 0.f;
+
+  for (int j0 = kg; j0 < nvalid; j0 += 16 * U) {
+    uint32_t kw[U][DPL / 2], vw[U][DPL / 2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + 16 * u < nvalid ? j0 + 16 * u : j0;
+      const uint32_t* kp = reinterpret_cast<const uint32_t*>(kb + (size_t)j * HS);
+      const uint32_t* vp = reinterpret_cast<const uint32_t*>(vb + (size_t)j * HS);
+      if constexpr (DPL == 8) {
+        uint4 a = *reinterpret_cast<const uint4*>(kp), c = *reinterpret_cast<const uint4*>(vp);
+        kw[u][0] = a.x; kw[u][1] = a.y; kw[u][2] = a.z; kw[u][3] = a.w;
+        vw[u][0] = c.x; vw[u][1] = c.y; vw[u][2] = c.z; vw[u][3] = c.w;
+      } else {
+        uint2 a = *reinterpret_cast<const uint2*>(kp), c = *reinterpret_cast<const uint2*>(vp);
+        kw[u][0] = a.x; kw[u][1] = a.y;
+        vw[u][0] = c.x; vw[u][1] = c.y;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < DPL / 2; ++i) s += qf[2 * i] * bflo(kw[u][i]) + qf[2 * i + 1] * bfhi(kw[u][i]);
+      s += __shfl_xor(s, 8, 64);
+      s += __shfl_xor(s, 4, 64);
+      s += __shfl_xor(s, 2, 64);
+      s += __shfl_xor(s, 1, 64);
+      if (j0 + 16 * u >= nvalid) continue;
+      const float mn = fmaxf(mx, s);
+      const float corr = exp2f(mx - mn);
+      const float pj = exp2f(s - mn);
+      l = l * corr + pj;
+#pragma unroll
+      for (int i = 0; i < DPL / 2; ++i) {
+        o[2 * i] = o[2 * i] * corr + pj * bflo(vw[u][i]);
+        o[2 * i + 1] = o[2 * i + 1] * corr + pj * bfhi(vw[u][i]);
+      }
+      mx = mn;
+    }
+  }
+  if (sub == 0) { s_m[kg] = mx; s_l[kg] = l; }
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) s_o[kg][sub * DPL + i] = o[i];
+  __syncthreads();
+  if (threadIdx.x < HS) {
+    const int d = threadIdx.x;
+    float M = -INFINITY;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) M = fmaxf(M, s_m[g]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const float f = s_m[g] == -INFINITY ? 0.f : exp2f(s_m[g] - M);
+      L += s_l[g] * f;
+      O += s_o[g][d] * f;
+    }
+    y[(size_t)m * C + h * HS + d] = f2bf(O / L);
+  }
+}
+
+// ---- greedy next token: argmax over bf16 logits (lowest index on ties). Reference
+// generate.py:66-74 with top_k = 1 (multinomial over the kept maximum).
+__global__ __launch_bounds__(1024) void argmax_kernel(const bf16_t* __restrict__ logits, int ldl, int V,
+                                                      int* __restrict__ out_idx, int* __restrict__ tokens_out,
+                                                      int tok_stride, const int* __restrict__ pos) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const bf16_t* lr = logits + (size_t)m * ldl;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int v = tid; v < V; v += 1024) {
+    const float x = bf2f(lr[v]);
+    if (x > best) { best = x; bi = v; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  if ((tid & 63) == 0) { sv[tid >> 6] = best; si[tid >> 6] = bi; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 16; ++w)
+      if (sv[w] > best || (sv[w] == best && si[w] < bi)) { best = sv[w]; bi = si[w]; }
+    if (bi == 0x7fffffff) bi = 0;  // all-NaN row
+    out_idx[m] = bi;
+    if (tokens_out) tokens_out[(size_t)m * tok_stride + pos[0] + 1] = bi;
+  }
+}
+
+}  // namespace llj
+
+using namespace llj;
+
+extern "C" {
+
+int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, void* stream) {
+  LLJ_REQUIRE(M > 0 && C % 8 == 0);
+  hipLaunchKernelGGL(embedding_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, idx, (const uint4*)wte,
+                     (uint4*)out, C / 8, pos_inc);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_rmsnorm(const void* x, const void* w, float eps, void* y, int M, int C, void* stream) {
+  LLJ_REQUIRE(M > 0 && C % 8 == 0);
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     (const bf16_t*)w, eps, (bf16_t*)y, C);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_attention(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                  int n_head, int head_size, int S, void* stream) {
+  LLJ_REQUIRE(B > 0 && T > 0 && n_head > 0 && S > 0);
+  const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
+  dim3 grid(n_head, B * T);
+  if (head_size == 128) {
+    hipLaunchKernelGGL((attention_kernel<128, 4>), grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)q,
+                       (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
+  } else if (head_size == 64) {
+    hipLaunchKernelGGL((attention_kernel<64, 4>), grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)q,
+                       (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
+  } else {
+    return LLJ_EINVAL;
+  }
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_argmax(const void* logits, int ldl, int M, int V, int* out_idx, int* tokens_out, int tok_stride,
+               const int* pos, void* stream) {
+  LLJ_REQUIRE(M > 0 && V > 0 && (!tokens_out || pos));
+  hipLaunchKernelGGL(argmax_kernel, dim3(M), dim3(1024), 0, (hipStream_t)stream, (const bf16_t*)logits, ldl, V,
+                     out_idx, tokens_out, tok_stride, pos);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

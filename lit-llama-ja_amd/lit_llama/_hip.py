@@ -1,0 +1,82 @@
+"""ctypes binding of the in-tree HIP library `_lljamd.so` (C ABI: include/lit_llama_amd.h).
+
+The library is the only compute path of this package: there is no CPU or eager-PyTorch
+fallback. If it is missing or the device is not a ROCm GPU, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+LIB_PATH = Path(__file__).resolve().parent / "_lljamd.so"
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+
+# name -> argtypes (every function returns int: 0 ok, hipError_t, or 1000 = EINVAL)
+SIGNATURES = {
+    "llj_w4_repack": [_P, _P, _I, _I, _P],
+    "llj_w4_unpack": [_P, _P, _I, _I, _P],
+    "llj_w4_scale_zero": [_P, _P, _I, _P, _I, _P],
+    "llj_linear": [_I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P],
+    "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P],
+    "llj_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "llj_linear_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P],
+    "llj_norm_swiglu": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P],
+    "llj_norm_linear": [_I, _P, _P, _F, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P],
+    "llj_i8_stats": [_P, _I, _I, _I, _F, _P, _P],
+    "llj_i8_quant_weight": [_P, _I, _P, _P, _I, _I, _P],
+    "llj_embedding": [_P, _P, _P, _I, _I, _P, _P],
+    "llj_rmsnorm": [_P, _P, _F, _P, _I, _I, _P],
+    "llj_argmax": [_P, _I, _I, _I, _P, _P, _I, _P, _P],
+}
+
+_lib = None
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise HipError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950). There is no fallback path.")
+        L = ctypes.CDLL(str(LIB_PATH))
+        for name, argt in SIGNATURES.items():
+            f = getattr(L, name)
+            f.argtypes = argt
+            f.restype = ctypes.c_int
+        L.llj_i8_ws_bytes.argtypes = [_I, _I]
+        L.llj_i8_ws_bytes.restype = ctypes.c_size_t
+        _lib = L
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        what = "unsupported shape/argument (EINVAL)" if rc == 1000 else f"hipError {rc}"
+        raise HipError(f"{name} failed: {what}")
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def require_device(t: torch.Tensor, what: str = "tensor") -> None:
+    if t.device.type != "cuda" or torch.version.hip is None:
+        raise HipError(
+            f"{what} is on {t.device}: this package runs only on a ROCm GPU (MI355X / gfx950); "
+            "it has no CPU path")
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,100 @@
+"""Decode session: the reference's token loop (generate.py:61-87) with the per-token work
+captured once into a HIP graph.
+
+One decode step = embedding of the current token (which also advances the device-side
+position), the n_layer fused blocks, ln_f + lm_head and the greedy argmax that writes the
+next token both into `cur` and into the output id buffer. Nothing in the step reads the
+host, so replaying the graph K times generates K tokens with no host round trip (the
+reference syncs per layer at model.py:221 and per token at generate.py:86).
+
+Batch B > 1 decodes B equal-length prompts together (each row equals an independent B=1
+run: tests/test_model_gpu.py); the reference's generate() is batch 1 only (generate.py:62).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _hip
+from .model import LLaMA, QKV_ROWS, _Work
+
+
+class DecodeSession:
+    def __init__(self, model: LLaMA, batch: int, max_seq_length: int, total_len: int, use_graph: bool = True):
+        cfg = model.config
+        assert max_seq_length <= cfg.block_size
+        self.model, self.B, self.S, self.total = model, batch, max_seq_length, total_len
+        dev = model.transformer.wte.weight.device
+        _hip.require_device(model.transformer.wte.weight, "model")
+        self.dev = dev
+        if batch > QKV_ROWS:
+            raise ValueError(f"decode batch {batch} > {QKV_ROWS} rows per fused launch")
+        self.cur = torch.zeros(batch, dtype=torch.int32, device=dev)
+        self.pos = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.tokens = torch.zeros(batch, total_len, dtype=torch.int32, device=dev)
+        self.logits = torch.empty(batch, cfg.padded_vocab_size, dtype=torch.bfloat16, device=dev)
+        self.use_graph = use_graph
+        self.graph = None
+        self.t_prompt = 0
+        self.steps_done = 0
+        self.specs = None
+        self.work = None
+
+    # -- prefill: eager (rows = B*T); fills the caches, picks the first new token
+    @torch.no_grad()
+    def prefill(self, prompts: torch.Tensor) -> None:
+        m = self.model
+        B, T = prompts.shape
+        assert B == self.B and T + 1 <= self.total
+        m.reset_cache()
+        m.kv_caches = m._alloc_kv(B, self.S, self.dev)
+        if m.rope_cache is None:
+            m.rope_cache = m.build_rope_cache(prompts)
+        pos = torch.arange(T, device=self.dev, dtype=torch.int32)
+        m._run(prompts.to(self.dev), pos, self.S, m.kv_caches, last_only_out=self.logits)
+        st = _hip.stream()
+        self.tokens[:, :T] = prompts.to(torch.int32)
+        self.pos.fill_(T - 1)
+        _hip.call("llj_argmax", self.logits.data_ptr(), self.logits.stride(0), B, m.config.padded_vocab_size,
+                  self.cur.data_ptr(), self.tokens.data_ptr(), self.total, self.pos.data_ptr(), st)
+        self.t_prompt = T
+        self.steps_done = 1
+        # decode-step operands (fixed for the session)
+        self.specs = m._layer_specs()
+        need_i8 = any(s[0] == 2 for layer in self.specs["layers"] for s in layer) or self.specs["head"][0] == 2
+        self.work = _Work(m.config, B, self.dev, need_i8)
+
+    def _step(self):
+        m, w, B = self.model, self.work, self.B
+        cfg = m.config
+        st = _hip.stream()
+        _hip.call("llj_embedding", self.cur.data_ptr(), m.transformer.wte.weight.data_ptr(), w.x.data_ptr(), B,
+                  cfg.n_embd, self.pos.data_ptr(), st)
+        m._blocks(w, self.specs, m.kv_caches, self.pos, B, 1, self.S, st)
+        m._head(w.x, B, self.specs, self.logits, st, w)
+        _hip.call("llj_argmax", self.logits.data_ptr(), self.logits.stride(0), B, cfg.padded_vocab_size,
+                  self.cur.data_ptr(), self.tokens.data_ptr(), self.total, self.pos.data_ptr(), st)
+
+    def capture(self):
+        if self.graph is not None or not self.use_graph:
+            return
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step()
+        self.graph = g
+
+    @torch.no_grad()
+    def decode(self, n: int) -> None:
+        """Generate n more tokens per row (positions t_prompt + steps_done ...)."""
+        assert self.t_prompt + self.steps_done + n <= self.total, "beyond the output buffer"
+        assert self.t_prompt + self.steps_done + n - 1 <= self.model.config.block_size, "beyond block_size"
+        if self.use_graph:
+            self.capture()
+            for _ in range(n):
+                self.graph.replay()
+        else:
+            for _ in range(n):
+                self._step()
+        self.steps_done += n
+
+    def output(self) -> torch.Tensor:
+        return self.tokens[:, :self.t_prompt + self.steps_done]

@@ -1,0 +1,477 @@
+"""LLaMA for the MI355X decode path: the reference's module tree and API (lit_llama/model.py),
+with LLaMA.forward executed by the fused gfx950 kernels of _lljamd.so.
+
+Same as the reference (if001/lit-llama-ja lit_llama/model.py): LLaMAConfig + llama_configs
+(23-56), parameter/buffer names and shapes (state_dict compatible), LLaMA.forward(idx,
+max_seq_length, input_pos) -> logits (59-128), lazily allocated per-layer KV caches
+(115-121), reset_cache, from_name, build_rope_cache / build_mask_cache, RMSNorm, apply_rope.
+
+Execution per Block (model.py:162-175) is four weight-streaming launches plus attention:
+  1. rms_1 + c_attn + RoPE(q, k) + KV write        (llj_norm_qkv_rope)
+  2. causal attention over the cache              (llj_attention)
+  3. c_proj + residual add                         (llj_linear_resid)
+  4. rms_2 + c_fc1 / c_fc2 + silu * mul            (llj_norm_swiglu)
+  5. mlp.c_proj + residual add                     (llj_linear_resid)
+and ln_f + lm_head (llj_norm_linear). The KV cache is a ring: the token at absolute
+position p is stored in slot p % S, which holds the same key set as the reference's
+roll-by-one sliding window (model.py:221-227); `kv_caches` therefore equals the reference's
+caches up to a rotation of the slot axis once more than S tokens were seen.
+
+The model must live on a ROCm GPU in bfloat16 (the reference's GPU precision, generate.py:121);
+there is no CPU path.
+"""
+from __future__ import annotations
+
+import math
+import types
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+from typing_extensions import Self
+
+from . import _hip
+from .utils import find_multiple
+
+MaskCache = torch.Tensor
+RoPECache = torch.Tensor
+KVCache = Tuple[torch.Tensor, torch.Tensor]
+
+
+@dataclass
+class LLaMAConfig:
+    block_size: int = 2048
+    vocab_size: int = 32000
+    padded_vocab_size: Optional[int] = None
+    n_layer: int = 32
+    n_head: int = 32
+    n_embd: int = 4096
+
+    def __post_init__(self):
+        if self.padded_vocab_size is None:
+            self.padded_vocab_size = find_multiple(self.vocab_size, 64)
+
+    @classmethod
+    def from_name(cls, name: str) -> Self:
+        return cls(**llama_configs[name])
+
+    def debug(self):
+        for k in ("block_size", "vocab_size", "padded_vocab_size", "n_layer", "n_head", "n_embd"):
+            print(f"{k}: ", getattr(self, k))
+
+
+llama_configs = {
+    "19M": dict(n_layer=6, n_head=8, n_embd=512, vocab_size=35000),
+    "49M": dict(n_layer=10, n_head=10, n_embd=640, vocab_size=35000),
+    "125M": dict(n_layer=12, n_head=10, n_embd=780, vocab_size=35000),
+    "7B": dict(n_layer=32, n_head=32, n_embd=4096),
+    "13B": dict(n_layer=40, n_head=40, n_embd=5120),
+    "30B": dict(n_layer=60, n_head=52, n_embd=6656),
+    "65B": dict(n_layer=80, n_head=64, n_embd=8192),
+}
+
+QKV_ROWS = 8    # fused-norm kernels stage <= 8 rows in LDS
+LIN_ROWS = 16   # plain linear kernels take <= 16 rows per launch
+I8_ROWS = 8     # int8 kernels quantize <= 8 rows in LDS
+
+
+def _wspec(lin: nn.Module):
+    """(wfmt, weight operand, scale operand) of a Linear for the HIP kernels."""
+    if hasattr(lin, "_wspec"):
+        return lin._wspec()
+    if isinstance(lin, nn.Linear):
+        w = lin.weight
+        _hip.require_device(w, "Linear.weight")
+        if w.dtype != torch.bfloat16 or not w.is_contiguous():
+            raise TypeError("dense Linear weights must be contiguous bfloat16 on the GPU "
+                            "(construct under EmptyInitOnDevice(dtype=torch.bfloat16) or call .to(torch.bfloat16))")
+        if lin.bias is not None:
+            raise NotImplementedError("biased dense Linear is not on the LLaMA path")
+        return 1, w, None
+    raise TypeError(f"unsupported Linear class {type(lin).__name__}")
+
+
+class _Work:
+    """Per-call scratch for M rows (allocated from torch's caching allocator)."""
+
+    def __init__(self, cfg: LLaMAConfig, M: int, device, need_i8: bool):
+        C, H = cfg.n_embd, MLP.hidden(cfg)
+        bf = torch.bfloat16
+        self.x = torch.empty(M, C, dtype=bf, device=device)
+        self.q = torch.empty(M, C, dtype=bf, device=device)
+        self.y = torch.empty(M, C, dtype=bf, device=device)
+        self.h = torch.empty(M, H, dtype=bf, device=device)
+        self.xn = torch.empty(M, C, dtype=bf, device=device) if need_i8 else None
+        if need_i8:
+            L = _hip.lib()
+            nb = max(L.llj_i8_ws_bytes(M, C), L.llj_i8_ws_bytes(M, H))
+            self.i8ws = torch.empty(nb, dtype=torch.uint8, device=device)
+        else:
+            self.i8ws = None
+
+
+class LLaMA(nn.Module):
+    def __init__(self, config: LLaMAConfig) -> None:
+        super().__init__()
+        assert config.padded_vocab_size is not None
+        self.config = config
+        self.lm_head = nn.Linear(config.n_embd, config.padded_vocab_size, bias=False)
+        self.transformer = nn.ModuleDict(
+            dict(
+                wte=nn.Embedding(config.padded_vocab_size, config.n_embd),
+                h=nn.ModuleList(Block(config) for _ in range(config.n_layer)),
+                ln_f=RMSNorm(config.n_embd),
+            )
+        )
+        self.rope_cache: Optional[RoPECache] = None
+        self.mask_cache: Optional[MaskCache] = None
+        self.kv_caches: List[KVCache] = []
+
+    def _init_weights(self, module: nn.Module) -> None:
+        """reference model.py:78-82"""
+        if isinstance(module, nn.Linear):
+            torch.nn.init.normal_(module.weight, mean=0.0, std=0.02 / math.sqrt(2 * self.config.n_layer))
+        elif isinstance(module, nn.Embedding):
+            torch.nn.init.normal_(module.weight, mean=0.0, std=0.02 / math.sqrt(2 * self.config.n_layer))
+
+    @classmethod
+    def from_name(cls, name: str) -> Self:
+        return cls(LLaMAConfig.from_name(name))
+
+    def build_rope_cache(self, idx: torch.Tensor) -> RoPECache:
+        return build_rope_cache(seq_len=self.config.block_size, n_elem=self.config.n_embd // self.config.n_head,
+                                dtype=idx.dtype, device=idx.device)
+
+    def build_mask_cache(self, idx: torch.Tensor) -> MaskCache:
+        ones = torch.ones((self.config.block_size, self.config.block_size), device=idx.device, dtype=torch.bool)
+        return torch.tril(ones).unsqueeze(0).unsqueeze(0)
+
+    def reset_cache(self) -> None:
+        """reference model.py:146-151"""
+        self.kv_caches.clear()
+
+    # ------------------------------------------------------------------ forward
+    @torch.no_grad()
+    def forward(self, idx: torch.Tensor, max_seq_length: Optional[int] = None,
+                input_pos: Optional[torch.Tensor] = None) -> torch.Tensor:
+        B, T = idx.size()
+        block_size = self.config.block_size
+        if max_seq_length is None:
+            max_seq_length = block_size
+        assert T <= max_seq_length, f"Cannot forward sequence of length {T}, max seq length is only {max_seq_length}"
+        assert max_seq_length <= block_size, f"Cannot attend to {max_seq_length}, block size is only {block_size}"
+        assert T <= block_size, f"Cannot forward sequence of length {T}, block size is only {block_size}"
+        _hip.require_device(idx, "idx")
+        self._check_dtype()
+        if self.rope_cache is None:
+            self.rope_cache = self.build_rope_cache(idx)
+        if input_pos is None:
+            # no-cache path (model.py:111-113): causal attention over the T tokens themselves,
+            # i.e. fresh caches of length T written at positions 0..T-1
+            pos = torch.arange(T, device=idx.device, dtype=torch.int32)
+            kv = self._alloc_kv(B, T, idx.device, n=1)
+            kv = kv * self.config.n_layer
+            return self._run(idx, pos, T, kv, all_rows=True)
+        pos = input_pos.to(device=idx.device, dtype=torch.int32)
+        assert pos.numel() == T, "input_pos must have one position per token"
+        if not self.kv_caches:
+            self.kv_caches = self._alloc_kv(B, max_seq_length, idx.device)
+        S = self.kv_caches[0][0].shape[2]
+        if S != max_seq_length or self.kv_caches[0][0].shape[0] != B:
+            raise ValueError(f"KV cache was allocated for batch {self.kv_caches[0][0].shape[0]} and "
+                             f"max_seq_length {S}; call reset_cache() first")
+        return self._run(idx, pos, S, self.kv_caches, all_rows=True)
+
+    def _alloc_kv(self, B, S, device, n=None):
+        hs = self.config.n_embd // self.config.n_head
+        shape = (B, self.config.n_head, S, hs)
+        return [(torch.zeros(shape, device=device, dtype=torch.bfloat16),
+                 torch.zeros(shape, device=device, dtype=torch.bfloat16))
+                for _ in range(self.config.n_layer if n is None else n)]
+
+    def _check_dtype(self):
+        wte = self.transformer.wte.weight
+        _hip.require_device(wte, "LLaMA parameters")
+        if wte.dtype != torch.bfloat16:
+            raise TypeError("the MI355X path computes in bfloat16: build the model under "
+                            "EmptyInitOnDevice(device='cuda', dtype=torch.bfloat16) or call model.to(torch.bfloat16)")
+
+    def _run(self, idx, pos, S, kv, all_rows=True, last_only_out=None):
+        """Embedding -> n_layer blocks -> ln_f -> lm_head for B*T rows; returns (B, T, V)
+        logits (or only the last position of each sequence into `last_only_out` (B, V))."""
+        cfg = self.config
+        B, T = idx.shape
+        M = B * T
+        dev = idx.device
+        specs = self._layer_specs()
+        need_i8 = any(s[0] == 2 for layer in specs["layers"] for s in layer) or specs["head"][0] == 2
+        w = _Work(cfg, M, dev, need_i8)
+        st = _hip.stream()
+        ids = idx.reshape(-1).to(torch.int32)
+        _hip.call("llj_embedding", ids.data_ptr(), self.transformer.wte.weight.data_ptr(), w.x.data_ptr(), M,
+                  cfg.n_embd, None, st)
+        self._blocks(w, specs, kv, pos, B, T, S, st)
+        V = cfg.padded_vocab_size
+        if last_only_out is not None:
+            rows = w.x.view(B, T, -1)[:, -1].contiguous()
+            self._head(rows, B, specs, last_only_out, st, w)
+            return last_only_out
+        logits = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
+        self._head(w.x, M, specs, logits, st, w)
+        return logits.view(B, T, V)
+
+    # -- weight operands, gathered once per call
+    def _layer_specs(self):
+        layers = []
+        for blk in self.transformer.h:
+            layers.append((_wspec(blk.attn.c_attn), _wspec(blk.attn.c_proj), _wspec(blk.mlp.c_fc1),
+                           _wspec(blk.mlp.c_fc2), _wspec(blk.mlp.c_proj)))
+        return {"layers": layers, "head": _wspec(self.lm_head)}
+
+    def _i8_prep(self, A, M, K, w, st):
+        _hip.call("llj_i8_stats", A.data_ptr(), A.stride(0), M, K, Linear8bitLtThreshold, w.i8ws.data_ptr(), st)
+
+    def _blocks(self, w, specs, kv, pos, B, T, S, st):
+        cfg = self.config
+        C, H, nh = cfg.n_embd, MLP.hidden(cfg), cfg.n_head
+        M = B * T
+        rope = self.rope_cache
+        P = _hip.ptr
+        for i, blk in enumerate(self.transformer.h):
+            (fa, wa, sa), (fp, wp, sp), (f1, w1, s1), (f2, w2, s2), (fd, wd, sd) = specs["layers"][i]
+            kc, vc = kv[i]
+            # 1. rms_1 + c_attn + rope + kv write
+            if fa == 2:
+                _hip.call("llj_rmsnorm", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps, w.xn.data_ptr(),
+                          M, C, st)
+                self._i8_prep(w.xn, M, C, w, st)
+                src, nw = w.xn, None
+            else:
+                src, nw = w.x, blk.rms_1.scale.data_ptr()
+            for r0 in range(0, M, QKV_ROWS):
+                r = min(QKV_ROWS, M - r0)
+                _hip.call("llj_norm_qkv_rope", fa, src.data_ptr(), nw, blk.rms_1.eps, wa.data_ptr(), P(sa),
+                          w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), B, T, C, nh,
+                          S, r0, r, P(w.i8ws), st)
+            # 2. attention
+            _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(), pos.data_ptr(),
+                      B, T, nh, C // nh, S, st)
+            # 3. c_proj + residual
+            self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st)
+            # 4. rms_2 + fc1/fc2 + silu*mul
+            if f1 != f2:
+                raise TypeError("c_fc1 and c_fc2 must share a weight format")
+            if f1 == 2:
+                _hip.call("llj_rmsnorm", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(),
+                          M, C, st)
+                self._i8_prep(w.xn, M, C, w, st)
+                src, nw, step = w.xn, None, I8_ROWS
+            else:
+                src, nw, step = w.x, blk.rms_2.scale.data_ptr(), QKV_ROWS
+            for r0 in range(0, M, step):
+                r = min(step, M - r0)
+                _hip.call("llj_norm_swiglu", f1, src[r0].data_ptr(), nw, blk.rms_2.eps, w1.data_ptr(), P(s1),
+                          w2.data_ptr(), P(s2), w.h[r0].data_ptr(), r, H, C, P(w.i8ws), r0, st)
+            # 5. mlp.c_proj + residual
+            self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st)
+
+    def _resid(self, f, A, W, sz, x, M, N, K, w, st):
+        if f == 2:
+            self._i8_prep(A, M, K, w, st)
+        step = I8_ROWS if f == 2 else LIN_ROWS
+        for r0 in range(0, M, step):
+            r = min(step, M - r0)
+            _hip.call("llj_linear_resid", f, A[r0].data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz),
+                      x[r0].data_ptr(), x.stride(0), r, N, K, _hip.ptr(w.i8ws), r0, st)
+
+    def _head(self, x, M, specs, out, st, w):
+        cfg = self.config
+        C, V = cfg.n_embd, cfg.padded_vocab_size
+        f, W, sz = specs["head"]
+        ln = self.transformer.ln_f
+        if f == 2:
+            xn = torch.empty_like(x)
+            _hip.call("llj_rmsnorm", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), M, C, st)
+            self._i8_prep(xn, M, C, w, st)
+            src, nw = xn, None
+        else:
+            src, nw = x, ln.scale.data_ptr()
+        for r0 in range(0, M, QKV_ROWS):
+            r = min(QKV_ROWS, M - r0)
+            _hip.call("llj_norm_linear", f, src[r0].data_ptr(), nw, ln.eps, W.data_ptr(), _hip.ptr(sz),
+                      out[r0].data_ptr(), out.stride(0), r, V, C, _hip.ptr(w.i8ws), r0, st)
+
+
+Linear8bitLtThreshold = 6.0  # reference quantization.py:45
+
+
+class Block(nn.Module):
+    """reference model.py:154-175 (module tree / parameter names). Its computation runs inside
+    LLaMA.forward; a standalone Block.forward is provided for the no-cache case."""
+
+    def __init__(self, config: LLaMAConfig) -> None:
+        super().__init__()
+        self.rms_1 = RMSNorm(config.n_embd)
+        self.attn = CausalSelfAttention(config)
+        self.rms_2 = RMSNorm(config.n_embd)
+        self.mlp = MLP(config)
+        self.config = config
+
+    def forward(self, x, rope, mask, max_seq_length, input_pos=None, kv_cache=None):
+        if input_pos is not None or kv_cache is not None:
+            raise NotImplementedError("Block.forward with a KV cache runs inside LLaMA.forward(idx, max_seq_length, "
+                                      "input_pos) on this path")
+        B, T, C = x.shape
+        _hip.require_device(x, "x")
+        cfg = self.config
+        model = _BlockHost(self, cfg)
+        return model.run(x, rope), None
+
+
+class _BlockHost:
+    """No-cache Block.forward: the same kernels as LLaMA.forward with positions 0..T-1 and
+    `rope` (rows 0..T-1 of the RoPE cache, as the reference passes it) as the table."""
+
+    def __init__(self, blk, cfg):
+        self.blk, self.cfg = blk, cfg
+
+    def run(self, x, rope):
+        blk, cfg = self.blk, self.cfg
+        B, T, C = x.shape
+        M = B * T
+        specs = {"layers": [(_wspec(blk.attn.c_attn), _wspec(blk.attn.c_proj), _wspec(blk.mlp.c_fc1),
+                             _wspec(blk.mlp.c_fc2), _wspec(blk.mlp.c_proj))]}
+        need_i8 = any(s[0] == 2 for s in specs["layers"][0])
+        w = _Work(cfg, M, x.device, need_i8)
+        w.x.copy_(x.reshape(M, C))
+        kv = [(torch.zeros(B, cfg.n_head, T, C // cfg.n_head, dtype=torch.bfloat16, device=x.device),
+               torch.zeros(B, cfg.n_head, T, C // cfg.n_head, dtype=torch.bfloat16, device=x.device))]
+        pos = torch.arange(T, device=x.device, dtype=torch.int32)
+        shim = _OneBlock(blk, rope.float().contiguous(), cfg)
+        LLaMA._blocks(shim, w, specs, kv, pos, B, T, T, _hip.stream())
+        return w.x.view(B, T, C).clone()
+
+
+class _OneBlock:
+    def __init__(self, blk, rope, cfg):
+        self.transformer = types.SimpleNamespace(h=[blk])
+        self.rope_cache = rope
+        self.config = cfg
+
+    def _i8_prep(self, A, M, K, w, st):
+        LLaMA._i8_prep(self, A, M, K, w, st)
+
+    def _resid(self, *a):
+        LLaMA._resid(self, *a)
+
+
+class CausalSelfAttention(nn.Module):
+    """reference model.py:178-190 (parameters); computed by LLaMA.forward / Block.forward."""
+
+    def __init__(self, config: LLaMAConfig) -> None:
+        super().__init__()
+        assert config.n_embd % config.n_head == 0
+        self.c_attn = nn.Linear(config.n_embd, 3 * config.n_embd, bias=False)
+        self.c_proj = nn.Linear(config.n_embd, config.n_embd, bias=False)
+        self.n_head = config.n_head
+        self.n_embd = config.n_embd
+        self.block_size = config.block_size
+
+
+class MLP(nn.Module):
+    """reference model.py:246-260"""
+
+    def __init__(self, config: LLaMAConfig) -> None:
+        super().__init__()
+        n_hidden = MLP.hidden(config)
+        self.c_fc1 = nn.Linear(config.n_embd, n_hidden, bias=False)
+        self.c_fc2 = nn.Linear(config.n_embd, n_hidden, bias=False)
+        self.c_proj = nn.Linear(n_hidden, config.n_embd, bias=False)
+
+    @staticmethod
+    def hidden(config) -> int:
+        return find_multiple(int(2 * (4 * config.n_embd) / 3), 256)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        _hip.require_device(x, "x")
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K).contiguous()
+        M = x2.shape[0]
+        H = self.c_fc1.out_features
+        (f1, w1, s1), (f2, w2, s2), (fd, wd, sd) = _wspec(self.c_fc1), _wspec(self.c_fc2), _wspec(self.c_proj)
+        if f1 != f2:
+            raise TypeError("c_fc1 and c_fc2 must share a weight format")
+        st = _hip.stream()
+        h = torch.empty(M, H, dtype=torch.bfloat16, device=x.device)
+        ws = None
+        L = _hip.lib()
+        if 2 in (f1, fd):
+            ws = torch.empty(max(L.llj_i8_ws_bytes(M, K), L.llj_i8_ws_bytes(M, H)), dtype=torch.uint8,
+                             device=x.device)
+        if f1 == 2:
+            _hip.call("llj_i8_stats", x2.data_ptr(), K, M, K, Linear8bitLtThreshold, ws.data_ptr(), st)
+        step = I8_ROWS if f1 == 2 else QKV_ROWS
+        for r0 in range(0, M, step):
+            r = min(step, M - r0)
+            _hip.call("llj_norm_swiglu", f1, x2[r0].data_ptr(), None, 0.0, w1.data_ptr(), _hip.ptr(s1), w2.data_ptr(),
+                      _hip.ptr(s2), h[r0].data_ptr(), r, H, K, _hip.ptr(ws), r0, st)
+        out = torch.empty(M, self.c_proj.out_features, dtype=torch.bfloat16, device=x.device)
+        if fd == 2:
+            _hip.call("llj_i8_stats", h.data_ptr(), H, M, H, Linear8bitLtThreshold, ws.data_ptr(), st)
+        step = I8_ROWS if fd == 2 else LIN_ROWS
+        for r0 in range(0, M, step):
+            r = min(step, M - r0)
+            _hip.call("llj_linear", fd, h[r0].data_ptr(), H, wd.data_ptr(), _hip.ptr(sd), None, out[r0].data_ptr(),
+                      out.stride(0), r, out.shape[1], H, _hip.ptr(ws), r0, st)
+        return out.view(*x.shape[:-1], out.shape[1])
+
+
+class RMSNorm(nn.Module):
+    """reference model.py:263-283: scale * x * rsqrt(mean(x*x) + eps), bf16 rounding points."""
+
+    def __init__(self, size: int, dim: int = -1, eps: float = 1e-5) -> None:
+        super().__init__()
+        self.scale = nn.Parameter(torch.ones(size))
+        self.eps = eps
+        self.dim = dim
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        _hip.require_device(x, "x")
+        if x.dtype != torch.bfloat16 or self.scale.dtype != torch.bfloat16 or self.dim not in (-1, x.dim() - 1):
+            raise TypeError("RMSNorm HIP path: bfloat16 input/scale over the last dim")
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C).contiguous()
+        y = torch.empty_like(x2)
+        _hip.call("llj_rmsnorm", x2.data_ptr(), self.scale.data_ptr(), self.eps, y.data_ptr(), x2.shape[0], C,
+                  _hip.stream())
+        return y.view_as(x)
+
+
+def build_rope_cache(seq_len: int, n_elem: int, dtype: torch.dtype, device: torch.device,
+                     base: int = 10000) -> RoPECache:
+    """reference model.py:286-309 (one-time table; (seq_len, n_elem/2, 2) [cos, sin])."""
+    theta = 1.0 / (base ** (torch.arange(0, n_elem, 2, dtype=dtype, device=device) / n_elem))
+    seq_idx = torch.arange(seq_len, dtype=dtype, device=device)
+    idx_theta = torch.outer(seq_idx, theta).float()
+    cache = torch.stack([torch.cos(idx_theta), torch.sin(idx_theta)], dim=-1)
+    if dtype in (torch.float16, torch.bfloat16, torch.int8):
+        cache = cache.half()
+    return cache
+
+
+def apply_rope(x: torch.Tensor, rope_cache: RoPECache) -> torch.Tensor:
+    """reference model.py:312-329. On this path RoPE is fused into the c_attn epilogue
+    (llj_norm_qkv_rope); this standalone form is the reference's definition."""
+    T = x.size(1)
+    rope_cache = rope_cache[:T]
+    xshaped = x.float().reshape(*x.shape[:-1], -1, 2)
+    rope_cache = rope_cache.view(1, xshaped.size(1), 1, xshaped.size(3), 2)
+    x_out2 = torch.stack(
+        [
+            xshaped[..., 0] * rope_cache[..., 0] - xshaped[..., 1] * rope_cache[..., 1],
+            xshaped[..., 1] * rope_cache[..., 0] + xshaped[..., 0] * rope_cache[..., 1],
+        ],
+        -1,
+    )
+    return x_out2.flatten(3).type_as(x)

@@ -1,0 +1,247 @@
+"""Quantized Linear replacements for the decode path, backed by the HIP library.
+
+Drop-in for reference lit_llama/quantization.py:
+  * ColBlockQuantizedLinear (338-421): same constructor, buffers and state_dict keys
+    (`quant_weight` (N, K*bits/8) uint8 column-major, `scales`, `zeros`, `bias`); forward
+    runs the gfx950 int4 GEMV on a repacked copy of `quant_weight` (W4P layout, see
+    csrc/w4pack.hip) kept as a non-persistent buffer and refreshed whenever the reference
+    buffers change.
+  * Linear8bitLt (36-75): nn.Linear-compatible constructor; the weight is re-quantized to
+    LLM.int8() row-wise int8 (CB, SCB) at construction and on load_state_dict; forward is
+    the int8 MFMA GEMV with the fp16 outlier-column side product (threshold 6.0).
+  * qlinear_4bit_weight (282-331): functional int4 linear on the reference buffers.
+There is no CPU path: forward on a non-ROCm device raises.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _hip
+
+_DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+ROWS_PER_CALL = 16  # llj_linear handles M <= 16 rows per launch
+
+
+def _linear_rows(wfmt: int, x2: torch.Tensor, W: torch.Tensor, sz, bias, out2: torch.Tensor, N: int, K: int):
+    s = _hip.stream()
+    M = x2.shape[0]
+    for r0 in range(0, M, ROWS_PER_CALL):
+        r = min(ROWS_PER_CALL, M - r0)
+        _hip.call("llj_linear", wfmt, x2[r0].data_ptr(), x2.stride(0), W.data_ptr(), _hip.ptr(sz), _hip.ptr(bias),
+                  out2[r0].data_ptr(), out2.stride(0), r, N, K, None, 0, s)
+
+
+def _as_rows(inp: torch.Tensor, K: int) -> torch.Tensor:
+    x2 = inp.reshape(-1, K)
+    if x2.stride(-1) != 1 or x2.stride(0) % 8:
+        x2 = x2.contiguous()
+    return x2
+
+
+# for correctness AND speed: the reference's class of the same name ("for correctness but
+# with terrible perf") with its forward on the gfx950 int4 kernel
+class ColBlockQuantizedLinear(torch.nn.Module):
+    def __init__(self, in_features, out_features, bias: bool, *, bits, tile_cols):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.tile_cols = tile_cols if tile_cols != -1 else self.in_features
+        self.bits = bits
+        self.entries_per_byte = 8 // bits
+        assert self.entries_per_byte > 0 and self.entries_per_byte * self.bits == 8
+        assert in_features % self.entries_per_byte == 0
+        self.register_buffer(
+            "quant_weight",
+            torch.empty((self.out_features, self.in_features // self.entries_per_byte), dtype=torch.uint8)
+            .t().contiguous().t(),
+        )
+        self.register_buffer(
+            "scales",
+            torch.empty((self.out_features, (self.in_features + self.tile_cols - 1) // self.tile_cols)),
+        )
+        self.register_buffer("zeros", torch.empty_like(self.scales))
+        assert isinstance(bias, bool)
+        if bias:
+            self.register_buffer("bias", torch.empty((self.out_features,)))
+        else:
+            self.register_buffer("bias", None)
+        # derived device-side operands of the HIP kernel (not part of the state_dict)
+        self.register_buffer("_w4p", None, persistent=False)
+        self.register_buffer("_sz", None, persistent=False)
+        self._key = None
+
+    # ---- reference buffer utilities (quantization.py:374-409) -------------------------
+    def pack_weight(self, weight):
+        """reference quantization.py:374-388 (the GPTQ producer's packing)."""
+        weight = weight.to(device=self.quant_weight.device, copy=True)
+        for j in range(self.scales.size(1)):
+            weight[:, j * self.tile_cols:(j + 1) * self.tile_cols] /= self.scales[:, j:j + 1]
+            weight[:, j * self.tile_cols:(j + 1) * self.tile_cols] += self.zeros[:, j:j + 1]
+        weight = weight.clamp_(min=0, max=2 ** self.bits - 1).to(dtype=torch.uint8)
+        self.quant_weight.zero_()
+        for nr in range(self.entries_per_byte):
+            self.quant_weight += weight[:, nr::self.entries_per_byte] << (nr * self.bits)
+
+    def get_weight(self, dtype=torch.float):
+        """reference quantization.py:390-409: the dequantized (N, K) weight."""
+        weight = torch.empty((self.out_features, self.in_features), device=self.quant_weight.device, dtype=dtype)
+        mask = (1 << self.bits) - 1
+        for nr in range(self.entries_per_byte):
+            weight[:, nr::self.entries_per_byte] = ((self.quant_weight >> (nr * self.bits)) & mask).float()
+        for j in range(self.scales.size(1)):
+            weight[:, j * self.tile_cols:(j + 1) * self.tile_cols] -= self.zeros[:, j:j + 1]
+            weight[:, j * self.tile_cols:(j + 1) * self.tile_cols] *= self.scales[:, j:j + 1]
+        return weight
+
+    # ---- HIP path ---------------------------------------------------------------------
+    def _supported(self) -> bool:
+        return self.bits == 4 and self.scales.shape[1] == 1 and self.out_features % 16 == 0 \
+            and self.in_features % 128 == 0
+
+    def _prepare(self):
+        """(Re)build the W4P copy and the fp32 (scale, 128 + zero) pairs when the reference
+        buffers changed (pointer or in-place version)."""
+        qw, sc, zr = self.quant_weight, self.scales, self.zeros
+        key = (qw.data_ptr(), qw._version, sc.data_ptr(), sc._version, zr.data_ptr(), zr._version, qw.device)
+        if key == self._key:
+            return
+        _hip.require_device(qw, "ColBlockQuantizedLinear.quant_weight")
+        if not self._supported():
+            raise NotImplementedError(
+                f"ColBlockQuantizedLinear(bits={self.bits}, groups={self.scales.shape[1]}, "
+                f"{self.in_features}->{self.out_features}) has no HIP kernel yet "
+                "(gptq.int4 with tile_cols=-1, N % 16 == 0, K % 128 == 0 is supported)")
+        N, K = self.out_features, self.in_features
+        s = _hip.stream()
+        ref = qw.t()  # physical (K/2, N) row-major when quant_weight keeps the reference strides
+        if not ref.is_contiguous():
+            ref = ref.contiguous()
+        if self._w4p is None or self._w4p.numel() != N * K // 2 or self._w4p.device != qw.device:
+            self._w4p = torch.empty(N * K // 2, dtype=torch.uint8, device=qw.device)
+            self._sz = torch.empty(N, 2, dtype=torch.float32, device=qw.device)
+        _hip.call("llj_w4_repack", ref.data_ptr(), self._w4p.data_ptr(), N, K, s)
+        sc1, zr1 = sc.reshape(N).contiguous(), zr.reshape(N).contiguous()
+        if sc1.dtype not in _DTYPE_CODE or zr1.dtype != sc1.dtype:
+            sc1, zr1 = sc1.float(), zr1.float()
+        _hip.call("llj_w4_scale_zero", sc1.data_ptr(), zr1.data_ptr(), _DTYPE_CODE[sc1.dtype], self._sz.data_ptr(),
+                  N, s)
+        self._key = key
+
+    def _wspec(self):
+        """(wfmt, weight operand, sz operand) for the fused model kernels."""
+        self._prepare()
+        return 0, self._w4p, self._sz
+
+    def forward(self, inp):
+        _hip.require_device(inp, "input")
+        if inp.dtype != torch.bfloat16:
+            raise TypeError(f"ColBlockQuantizedLinear HIP path computes in bfloat16, got {inp.dtype}")
+        self._prepare()
+        K, N = self.in_features, self.out_features
+        x2 = _as_rows(inp, K)
+        out = torch.empty((x2.shape[0], N), dtype=inp.dtype, device=inp.device)
+        bias = None if self.bias is None else self.bias.to(torch.bfloat16)
+        _linear_rows(0, x2, self._w4p, self._sz, bias, out, N, K)
+        return out.reshape(*inp.shape[:-1], N)
+
+
+def qlinear_4bit_weight(inp, weight, scales, zeros):
+    """Functional form of reference quantization.py:282-331 on the reference buffers
+    (`weight` = quant_weight (N, K/2), scales/zeros (N, 1))."""
+    N, K = weight.shape[0], weight.shape[1] * 2
+    lin = ColBlockQuantizedLinear(K, N, False, bits=4, tile_cols=-1).to(weight.device)
+    lin.quant_weight = weight
+    lin.scales = scales
+    lin.zeros = zeros
+    return lin(inp)
+
+
+def int8_linear(x: torch.Tensor, CB: torch.Tensor, SCB: torch.Tensor, bias, threshold: float = 6.0):
+    """LLM.int8() matmul of bf16 x (..., K) with the row-quantized (CB, SCB) weight."""
+    K = x.shape[-1]
+    N = CB.shape[0]
+    x2 = _as_rows(x, K)
+    M = x2.shape[0]
+    s = _hip.stream()
+    ws = torch.empty(_hip.lib().llj_i8_ws_bytes(M, K), dtype=torch.uint8, device=x.device)
+    _hip.call("llj_i8_stats", x2.data_ptr(), x2.stride(0), M, K, threshold, ws.data_ptr(), s)
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    for r0 in range(0, M, 8):
+        r = min(8, M - r0)
+        _hip.call("llj_linear", 2, x2[r0].data_ptr(), x2.stride(0), CB.data_ptr(), SCB.data_ptr(), _hip.ptr(bias),
+                  out[r0].data_ptr(), out.stride(0), r, N, K, ws.data_ptr(), r0, s)
+    return out.reshape(*x.shape[:-1], N)
+
+
+class Linear8bitLt(torch.nn.Module):
+    """LLM.int8() Linear (reference quantization.py:36-75 over bnb.nn.Linear8bitLt with
+    has_fp16_weights=False, threshold=6.0). `weight` holds the int8 row-quantized CB (N, K),
+    `SCB` the fp32 row absmax (N,). Loading a float `weight` re-quantizes it."""
+
+    threshold = 6.0
+
+    def __init__(self, in_features, out_features, bias=True, device=None, dtype=None):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        w = torch.empty((out_features, in_features), device=device, dtype=dtype)
+        torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+        self.weight = torch.nn.Parameter(w, requires_grad=False)
+        self.register_buffer("SCB", None)
+        if bias:
+            self.bias = torch.nn.Parameter(torch.zeros(out_features, device=device, dtype=dtype), requires_grad=False)
+        else:
+            self.register_parameter("bias", None)
+        # reference quantizes the initial weight right away (quantization.py:46-48); that
+        # needs the GPU, exactly like the reference's `.cuda()` there
+        if w.device.type == "cuda":
+            self._quantize_weight(w)
+
+    def _quantize_weight(self, weight: torch.Tensor) -> None:
+        """double_quant(W.half()) equivalent: CB = round(W16 * 127 / absmax_row), SCB = absmax_row."""
+        _hip.require_device(weight, "Linear8bitLt weight")
+        w = weight.contiguous()
+        if w.dtype not in _DTYPE_CODE:
+            w = w.float()
+        N, K = w.shape
+        cb = torch.empty((N, K), dtype=torch.int8, device=w.device)
+        scb = torch.empty((N,), dtype=torch.float32, device=w.device)
+        _hip.call("llj_i8_quant_weight", w.data_ptr(), _DTYPE_CODE[w.dtype], cb.data_ptr(), scb.data_ptr(), N, K,
+                  _hip.stream())
+        self.weight = torch.nn.Parameter(cb, requires_grad=False)
+        self.SCB = scb
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        key = prefix + "weight"
+        if key in state_dict:
+            w = state_dict[key]
+            scb_key = prefix + "SCB"
+            if w.dtype == torch.int8 and scb_key in state_dict:  # our own saved (CB, SCB) form
+                self.weight = torch.nn.Parameter(w.to(self.weight.device).contiguous(), requires_grad=False)
+                self.SCB = state_dict[scb_key].to(self.weight.device, torch.float32).contiguous()
+            else:
+                self._quantize_weight(w.to(self.weight.device))
+        bkey = prefix + "bias"
+        if self.bias is not None and bkey in state_dict:
+            with torch.no_grad():
+                self.bias.copy_(state_dict[bkey])
+        for k in (key, prefix + "SCB", bkey):
+            if k in missing_keys:
+                missing_keys.remove(k)
+
+    def _wspec(self):
+        if self.SCB is None:
+            self._quantize_weight(self.weight)
+        return 2, self.weight, self.SCB
+
+    def forward(self, x):
+        _hip.require_device(x, "input")
+        if x.dtype != torch.bfloat16:
+            raise TypeError(f"Linear8bitLt HIP path computes in bfloat16, got {x.dtype}")
+        if self.SCB is None:
+            self._quantize_weight(self.weight)
+        bias = None if self.bias is None else self.bias.to(torch.bfloat16)
+        return int8_linear(x, self.weight, self.SCB, bias, self.threshold)

@@ -1,0 +1,307 @@
+"""Kernel-level parity of the HIP library against the numpy oracle (GPU only).
+
+Every call goes through the C ABI (_lljamd.so via ctypes). Inputs are seeded; expected
+values come from oracle/llama_np.py (CPU restatement of the reference, pinned by
+tests/test_oracle_golden.py) or from the reference's own fixtures in tests/golden/.
+Tolerances: int/byte work is bit-exact; bf16 outputs within one bf16 rounding (see
+helpers.assert_bf16_close).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import llama_np as O
+from tests.helpers import assert_bf16_close, bf16, w4p_pack_np
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def T(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return t if dtype is None else t.to(dtype)
+
+
+def st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def call(hip, name, *args):
+    rc = getattr(hip, name)(*args)
+    assert rc == 0, f"{name} returned {rc}"
+
+
+def rand_w4(rng, N, K):
+    qw = rng.integers(0, 256, size=(N, K // 2), dtype=np.uint8)
+    scales = rng.uniform(0.5, 1.5, size=(N, 1)).astype(np.float32) * np.float32(0.02 / 7)
+    zeros = rng.integers(0, 16, size=(N, 1)).astype(np.float32)
+    return qw, scales, zeros
+
+
+def repack(hip, qw):
+    N, Kh = qw.shape
+    ref = T(qw.T.copy())  # physical (K/2, N) row-major = the reference's column-major buffer
+    out = torch.empty(N * Kh, dtype=torch.uint8, device=dev)
+    call(hip, "llj_w4_repack", ref.data_ptr(), out.data_ptr(), N, 2 * Kh, st())
+    return out
+
+
+def sz_of(hip, scales, zeros):
+    N = scales.shape[0]
+    sz = torch.empty(N, 2, dtype=torch.float32, device=dev)
+    sd, zd = T(scales), T(zeros)  # keep alive until the kernel ran (caching allocator reuse)
+    call(hip, "llj_w4_scale_zero", sd.data_ptr(), zd.data_ptr(), 0, sz.data_ptr(), N, st())
+    torch.cuda.synchronize()
+    return sz
+
+
+@pytest.mark.parametrize("N,K", [(16, 128), (160, 384), (48, 1024)])
+def test_w4_repack_layout_and_roundtrip(hip, N, K):
+    rng = np.random.default_rng(N + K)
+    qw = rng.integers(0, 256, size=(N, K // 2), dtype=np.uint8)
+    packed = repack(hip, qw)
+    np.testing.assert_array_equal(packed.cpu().numpy(), w4p_pack_np(qw))
+    back = torch.empty(K // 2, N, dtype=torch.uint8, device=dev)
+    call(hip, "llj_w4_unpack", packed.data_ptr(), back.data_ptr(), N, K, st())
+    np.testing.assert_array_equal(back.cpu().numpy().T, qw)
+
+
+def _linear(hip, wfmt, x, W, sz, N, K, bias=None):
+    M = x.shape[0]
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    call(hip, "llj_linear", wfmt, x.data_ptr(), x.stride(0), W.data_ptr(), None if sz is None else sz.data_ptr(),
+         None if bias is None else bias.data_ptr(), out.data_ptr(), N, M, N, K, None, 0, st())
+    torch.cuda.synchronize()
+    return out.float().cpu().numpy()
+
+
+def test_w4_linear_reference_fixture(hip, golden):
+    """The reference's own ColBlockQuantizedLinear buffers (N=160, K=384) and inputs."""
+    g = golden("colblock")
+    qw, sc, z = g["b4_qw"], g["b4_scales"], g["b4_zeros"]
+    N, K = qw.shape[0], qw.shape[1] * 2
+    Wp, sz = repack(hip, qw), sz_of(hip, sc, z)
+    for M in (1, 3, 8):
+        xb = bf16(g[f"b4_x{M}"])
+        got = _linear(hip, 0, T(xb, torch.bfloat16), Wp, sz, N, K)
+        assert_bf16_close(got, O.qlinear_4bit(xb, qw, sc, z), f"int4 M={M}")
+        # and against the reference's fp32 output on the unrounded input
+        assert_bf16_close(got, g[f"b4_y{M}"], f"int4 vs reference M={M}", rel=3e-2, abs_frac=1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 5, 8, 13, 16])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (256, 11008), (2000 * 16, 128)])
+def test_w4_linear_shapes(hip, M, N, K):
+    rng = np.random.default_rng(M * 7 + N + K)
+    qw, sc, z = rand_w4(rng, N, K)
+    x = bf16(rng.standard_normal((M, K)).astype(np.float32))
+    got = _linear(hip, 0, T(x, torch.bfloat16), repack(hip, qw), sz_of(hip, sc, z), N, K)
+    assert_bf16_close(got, O.qlinear_4bit(x, qw, sc, z), f"int4 M={M} N={N} K={K}")
+
+
+@pytest.mark.parametrize("M", [1, 4, 8, 16])
+@pytest.mark.parametrize("N,K", [(512, 4096), (64, 11008)])
+def test_bf16_linear(hip, M, N, K):
+    rng = np.random.default_rng(M + N)
+    W = bf16(rng.standard_normal((N, K)) / np.sqrt(K))
+    x = bf16(rng.standard_normal((M, K)))
+    bias = bf16(rng.standard_normal(N))
+    got = _linear(hip, 1, T(x, torch.bfloat16), T(W, torch.bfloat16), None, N, K, T(bias, torch.bfloat16))
+    assert_bf16_close(got, x @ W.T + bias, f"bf16 M={M}")
+
+
+@pytest.mark.parametrize("outliers", [False, True])
+@pytest.mark.parametrize("M", [1, 8])
+def test_int8_linear_vs_restatement(hip, M, outliers):
+    """LLM.int8() against the oracle's restatement (bitsandbytes absent: parity unpinned)."""
+    rng = np.random.default_rng(M + 100 * outliers)
+    N, K = 256, 4096
+    W = bf16(rng.standard_normal((N, K)) * 0.02)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    if outliers:
+        x[:, [17, 1000, 4000]] *= 25.0
+    x = bf16(x)
+    Wd = T(W, torch.bfloat16)
+    cb = torch.empty(N, K, dtype=torch.int8, device=dev)
+    scb = torch.empty(N, dtype=torch.float32, device=dev)
+    call(hip, "llj_i8_quant_weight", Wd.data_ptr(), 1, cb.data_ptr(), scb.data_ptr(), N, K, st())
+    cb_ref, scb_ref = O.int8_quantize_weight(W)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(cb.cpu().numpy(), cb_ref)
+    np.testing.assert_allclose(scb.cpu().numpy(), scb_ref, rtol=0, atol=0)
+    xd = T(x, torch.bfloat16)
+    ws = torch.empty(hip.llj_i8_ws_bytes(M, K), dtype=torch.uint8, device=dev)
+    call(hip, "llj_i8_stats", xd.data_ptr(), K, M, K, 6.0, ws.data_ptr(), st())
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    call(hip, "llj_linear", 2, xd.data_ptr(), K, cb.data_ptr(), scb.data_ptr(), None, out.data_ptr(), N, M, N, K,
+         ws.data_ptr(), 0, st())
+    torch.cuda.synchronize()
+    ref = O.int8_linear(x, cb_ref, scb_ref)
+    assert_bf16_close(out.float().cpu().numpy(), ref, f"int8 M={M} outliers={outliers}", rel=2e-2)
+
+
+@pytest.mark.parametrize("C", [256, 4096, 5120])
+def test_rmsnorm_kernel(hip, golden, C):
+    rng = np.random.default_rng(C)
+    x = bf16(rng.standard_normal((5, C)) * 3)
+    w = bf16(rng.uniform(0.5, 1.5, C))
+    xd, wd = T(x, torch.bfloat16), T(w, torch.bfloat16)
+    y = torch.empty_like(xd)
+    call(hip, "llj_rmsnorm", xd.data_ptr(), wd.data_ptr(), 1e-5, y.data_ptr(), 5, C, st())
+    torch.cuda.synchronize()
+    assert_bf16_close(y.float().cpu().numpy(), O.rmsnorm(x, w), f"rmsnorm C={C}")
+    if C in (256, 4096):  # the reference's own bf16 RMSNorm output
+        g = golden("ops")
+        xg = T(g[f"rms_x_{C}"].reshape(-1, C), torch.bfloat16)  # fixture input is fp32: bf16-rounded here
+        wg = T(g[f"rms_scale_{C}"], torch.bfloat16)
+        yg = torch.empty_like(xg)
+        call(hip, "llj_rmsnorm", xg.data_ptr(), wg.data_ptr(), 1e-5, yg.data_ptr(), xg.shape[0], C, st())
+        torch.cuda.synchronize()
+        ref = g[f"rms_ybf16_{C}"].reshape(-1, C)
+        diff = np.abs(yg.float().cpu().numpy() - ref)
+        ulp2 = np.abs(ref) * 2.0 ** -6  # <= 2 bf16 ulps (rounding points inside torch's bf16 mean differ)
+        assert (diff <= ulp2 + 1e-6).all(), f"max diff {diff.max()}"
+
+
+def _attn_oracle(q, kc, vc, pos, S, T_, nh, hs):
+    """numpy attention over the ring cache for rows m = b*T + t at positions pos[t]."""
+    M = q.shape[0]
+    y = np.zeros_like(q)
+    for m in range(M):
+        b, t = divmod(m, T_)
+        p = int(pos[t])
+        slots = np.arange(p + 1) if p < S else np.arange(S)
+        for h in range(nh):
+            qq = q[m, h * hs:(h + 1) * hs]
+            K = kc[b, h, slots]
+            V = vc[b, h, slots]
+            s = K @ qq / np.sqrt(hs)
+            e = np.exp(s - s.max())
+            y[m, h * hs:(h + 1) * hs] = (e / e.sum()) @ V
+    return y
+
+
+@pytest.mark.parametrize("hs,nh,B,T_,S,p0", [(128, 4, 1, 1, 144, 80), (128, 3, 8, 1, 144, 143), (64, 4, 2, 5, 16, 0),
+                                            (128, 2, 1, 1, 10, 37), (128, 2, 2, 1, 2048, 2000)])
+def test_attention(hip, hs, nh, B, T_, S, p0):
+    rng = np.random.default_rng(hs + S + p0)
+    C = nh * hs
+    kc = bf16(rng.standard_normal((B, nh, S, hs)))
+    vc = bf16(rng.standard_normal((B, nh, S, hs)))
+    q = bf16(rng.standard_normal((B * T_, C)) * 2)
+    pos = np.arange(p0, p0 + T_, dtype=np.int32)
+    y = torch.empty(B * T_, C, dtype=torch.bfloat16, device=dev)
+    qd, kd, vd, pd = T(q, torch.bfloat16), T(kc, torch.bfloat16), T(vc, torch.bfloat16), T(pos)
+    call(hip, "llj_attention", qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), y.data_ptr(), pd.data_ptr(), B, T_, nh,
+         hs, S, st())
+    torch.cuda.synchronize()
+    assert_bf16_close(y.float().cpu().numpy(), _attn_oracle(q, kc, vc, pos, S, T_, nh, hs), "attention")
+
+
+def test_argmax_and_advance(hip):
+    rng = np.random.default_rng(3)
+    V, M = 32000, 8
+    L = bf16(rng.standard_normal((M, V)))
+    L[2, 7] = L[2, 9] = 50.0  # exact tie: lowest index wins
+    Ld = T(L, torch.bfloat16)
+    out = torch.empty(M, dtype=torch.int32, device=dev)
+    toks = torch.zeros(M, 12, dtype=torch.int32, device=dev)
+    pos = torch.tensor([4], dtype=torch.int32, device=dev)
+    call(hip, "llj_argmax", Ld.data_ptr(), V, M, V, out.data_ptr(), toks.data_ptr(), 12, pos.data_ptr(), st())
+    torch.cuda.synchronize()
+    exp = L.argmax(-1)
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    np.testing.assert_array_equal(toks[:, 5].cpu().numpy(), exp)
+    assert int(out[2]) == 7
+
+
+def test_embedding_and_pos_inc(hip):
+    rng = np.random.default_rng(4)
+    wte = bf16(rng.standard_normal((1000, 256)))
+    idx = np.array([5, 999, 0], np.int32)
+    out = torch.empty(3, 256, dtype=torch.bfloat16, device=dev)
+    pos = torch.tensor([7], dtype=torch.int32, device=dev)
+    idd, wd = T(idx), T(wte, torch.bfloat16)
+    call(hip, "llj_embedding", idd.data_ptr(), wd.data_ptr(), out.data_ptr(), 3, 256, pos.data_ptr(), st())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.float().cpu().numpy(), wte[idx])
+    assert int(pos) == 8
+
+
+@pytest.mark.parametrize("wfmt", [0, 1])
+@pytest.mark.parametrize("B,T_", [(1, 1), (8, 1), (2, 5)])
+def test_fused_qkv_rope_kv(hip, wfmt, B, T_):
+    rng = np.random.default_rng(wfmt * 10 + B + T_)
+    nh, hs = 4, 64
+    C, S = nh * hs, 32
+    x = bf16(rng.standard_normal((B * T_, C)))
+    g = bf16(rng.uniform(0.5, 1.5, C))
+    rope = O.build_rope_cache(128, hs)
+    pos = np.arange(3, 3 + T_, dtype=np.int32)
+    if wfmt == 0:
+        qw, sc, z = rand_w4(rng, 3 * C, C)
+        Wref = O.colblock_get_weight(qw, sc, z, 4)
+        Wd, szd = repack(hip, qw), sz_of(hip, sc, z)
+    else:
+        Wref = bf16(rng.standard_normal((3 * C, C)) / np.sqrt(C))
+        Wd, szd = T(Wref, torch.bfloat16), None
+    q = torch.zeros(B * T_, C, dtype=torch.bfloat16, device=dev)
+    kc = torch.zeros(B, nh, S, hs, dtype=torch.bfloat16, device=dev)
+    vc = torch.zeros_like(kc)
+    M = B * T_
+    xd, gd, rd, pd = T(x, torch.bfloat16), T(g, torch.bfloat16), T(rope), T(pos)
+    for r0 in range(0, M, 8):
+        r = min(8, M - r0)
+        call(hip, "llj_norm_qkv_rope", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, Wd.data_ptr(),
+             None if szd is None else szd.data_ptr(), q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rd.data_ptr(),
+             pd.data_ptr(), B, T_, C, nh, S, r0, r, None, st())
+    torch.cuda.synchronize()
+    h = bf16(O.rmsnorm(x, g))
+    qkv = bf16(h @ Wref.T)
+    qe = O.apply_rope(qkv[:, :C].reshape(B, T_, nh, hs), rope[pos]).reshape(M, C)
+    ke = O.apply_rope(qkv[:, C:2 * C].reshape(B, T_, nh, hs), rope[pos])
+    ve = qkv[:, 2 * C:].reshape(B, T_, nh, hs)
+    assert_bf16_close(q.float().cpu().numpy(), qe, "q")
+    kcn, vcn = kc.float().cpu().numpy(), vc.float().cpu().numpy()
+    for t in range(T_):
+        assert_bf16_close(kcn[:, :, pos[t]], ke[:, t], "k cache")
+        assert_bf16_close(vcn[:, :, pos[t]], ve[:, t], "v cache")
+    untouched = np.ones(S, bool)
+    untouched[pos] = False
+    assert not kcn[:, :, untouched].any() and not vcn[:, :, untouched].any()
+
+
+@pytest.mark.parametrize("wfmt", [0, 1])
+def test_fused_swiglu_and_resid(hip, wfmt):
+    rng = np.random.default_rng(11 + wfmt)
+    M, C, H = 3, 256, 768
+    x = bf16(rng.standard_normal((M, C)))
+    g = bf16(rng.uniform(0.5, 1.5, C))
+
+    def mk(N, K):
+        if wfmt == 0:
+            qw, sc, z = rand_w4(rng, N, K)
+            return O.colblock_get_weight(qw, sc, z, 4), repack(hip, qw), sz_of(hip, sc, z)
+        W = bf16(rng.standard_normal((N, K)) / np.sqrt(K))
+        return W, T(W, torch.bfloat16), None
+
+    W1, W1d, s1 = mk(H, C)
+    W2, W2d, s2 = mk(H, C)
+    Wd_, Wdd, sd = mk(C, H)
+    h = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    xd, gd = T(x, torch.bfloat16), T(g, torch.bfloat16)
+    call(hip, "llj_norm_swiglu", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, W1d.data_ptr(), P(s1), W2d.data_ptr(),
+         P(s2), h.data_ptr(), M, H, C, None, 0, st())
+    xr = xd.clone()
+    call(hip, "llj_linear_resid", wfmt, h.data_ptr(), H, Wdd.data_ptr(), P(sd), xr.data_ptr(), C, M, C, H, None, 0,
+         st())
+    torch.cuda.synchronize()
+    hn = bf16(O.rmsnorm(x, g))
+    a1, a2 = bf16(hn @ W1.T), bf16(hn @ W2.T)
+    hexp = bf16(bf16(O.silu(a1)) * a2)
+    # a1, a2, silu(a1) and the product are each rounded to bf16 on the reference path
+    # (model.py:258 on bf16 tensors): a 1-ulp flip of a1 or a2 propagates, so allow 3%
+    assert_bf16_close(h.float().cpu().numpy(), hexp, "swiglu", rel=3e-2)
+    hg = h.float().cpu().numpy()
+    assert_bf16_close(xr.float().cpu().numpy(), x + bf16(hg @ Wd_.T), "resid")
