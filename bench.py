@@ -1,0 +1,352 @@
+"""Decode throughput of the MI355X quantized LLaMA path (BASELINE.json metric).
+
+Workload: LLaMA-7B with --quantize gptq.int4, synthetic weights of the
+exact shapes (random packed int4 codes, zeros = 8, scales ~ U(0.5, 1.5) * 0.02 / 7, bf16
+embeddings ~ N(0, 0.02)), batch 1, a 16-token random prompt, max_seq_length 144 (prompt +
+128 new tokens), greedy decoding. One "step" = one decode token for every sequence of the
+batch = one replay of the captured decode graph (embedding -> 32 fused blocks -> ln_f +
+lm_head -> argmax -> next-token/position update). `value` = decode tokens/s summed over
+ranks (B * K * world / max-over-ranks time of the K timed steps).
+
+Multi-GPU: replicas only (the path is not sharded; no collective on the data
+path). Every rank runs its own replica; the barrier and the max-over-ranks timing use
+torch.distributed (RCCL for GPUs). Launch: python -m torch.distributed.run --nproc-per-node N
+bench.py --gpus N.
+
+Also reported, on the same JSON line:
+  roofline      dominant kernel (rms_2 + c_fc1/c_fc2 int4 GEMV + silu*mul, 1 launch per
+                layer, 45.2 MB of algorithmic bytes at 7B) timed with HIP events on the
+                stream it runs on, vs the 8 TB/s HBM peak;
+  step_roofline algorithmic bytes of a whole decode step / step time;
+  cpu_baseline  the numpy port of the reference's CPU path (oracle/, dequantize-every-call
+                like ColBlockQuantizedLinear's fallback, quantization.py:420-421) timed on a
+                bounded sample (one decode token through a few layers, scaled to 32);
+  bs8           the same workload at batch 8 (aggregate tokens/s and its step roofline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "lit-llama-ja_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+# ----------------------------------------------------------------------------- distributed
+def dist_init():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1:
+        import torch.distributed as dist
+
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        dist.init_process_group(backend=backend)
+        return dist.get_rank(), ws, int(os.environ.get("LOCAL_RANK", "0"))
+    return 0, 1, 0
+
+
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def aggregate(local_seconds: float, local_tokens: int, ws: int, device=None):
+    """(max seconds over ranks, total tokens over ranks)."""
+    if ws == 1:
+        return local_seconds, local_tokens
+    import torch.distributed as dist
+
+    t = torch.tensor([local_seconds], dtype=torch.float64, device=device)
+    n = torch.tensor([float(local_tokens)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(n, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(n.item())
+
+
+# ----------------------------------------------------------------------------- model
+def build_model(name: str, mode: str, seed: int = 1234):
+    """LLaMA `name` under quantization `mode` with synthetic weights."""
+    from lit_llama import LLaMA
+    from lit_llama.utils import EmptyInitOnDevice
+
+    dev = torch.device("cuda")
+    with EmptyInitOnDevice(device=dev, dtype=torch.bfloat16, quantization_mode=mode):
+        model = LLaMA.from_name(name)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    with torch.no_grad():
+        for mod in model.modules():
+            if hasattr(mod, "quant_weight"):
+                mod.quant_weight.copy_(torch.randint(0, 256, mod.quant_weight.shape, device=dev, dtype=torch.uint8,
+                                                     generator=g))
+                mod.scales.copy_((torch.rand(mod.scales.shape, device=dev, generator=g) + 0.5) * (0.02 / 7))
+                mod.zeros.fill_(8.0)
+            elif isinstance(mod, torch.nn.Linear):
+                mod.weight.normal_(0.0, 0.02, generator=g)
+            elif isinstance(mod, torch.nn.Embedding):
+                mod.weight.normal_(0.0, 0.02, generator=g)
+        for blk in model.transformer.h:
+            blk.rms_1.scale.fill_(1.0)
+            blk.rms_2.scale.fill_(1.0)
+        model.transformer.ln_f.scale.fill_(1.0)
+    if mode == "llm.int8":  # quantize the random bf16 weights (Linear8bitLt._quantize_weight)
+        for mod in model.modules():
+            if hasattr(mod, "_quantize_weight"):
+                w = torch.empty((mod.out_features, mod.in_features), dtype=torch.bfloat16, device=dev)
+                w.normal_(0.0, 0.02, generator=g)
+                mod._quantize_weight(w)
+    return model.eval()
+
+
+def weight_bytes(model) -> int:
+    """Algorithmic weight bytes streamed per decode step (every Linear once; wte excluded:
+    only gathered rows count). int4: packed codes + (scale, zero) per row as stored on the
+    reference side (bf16 each)."""
+    total = 0
+    for mod in model.modules():
+        if hasattr(mod, "quant_weight"):
+            total += mod.quant_weight.numel() + 2 * mod.out_features * 2
+        elif hasattr(mod, "SCB"):
+            total += mod.weight.numel() + 4 * mod.out_features
+        elif isinstance(mod, torch.nn.Linear):
+            total += mod.weight.numel() * 2
+    return total
+
+
+def step_bytes(model, B: int, pos_mean: float) -> float:
+    """W + sum_b KV_read(p_b) + B*KV_write + B*C*2 (embedding row)."""
+    cfg = model.config
+    kv_per_tok = 2 * cfg.n_layer * cfg.n_embd * 2  # k and v, bf16, all layers
+    return weight_bytes(model) + B * kv_per_tok * (pos_mean + 1) + B * kv_per_tok + B * cfg.n_embd * 2
+
+
+# ----------------------------------------------------------------------------- timing
+def time_decode(model, B, prompt_len, S, warmup, steps, ws, seed=1234):
+    from lit_llama.engine import DecodeSession
+
+    cfg = model.config
+    total = prompt_len + 1 + warmup + steps
+    assert total <= cfg.block_size, "positions beyond block_size"
+    g = torch.Generator().manual_seed(seed)
+    prompts = torch.randint(3, cfg.vocab_size, (B, prompt_len), generator=g).cuda()
+    sess = DecodeSession(model, B, S, total)
+    sess.prefill(prompts)  # one-time work (int4 repack, kernel attributes) stays out of the timings
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sess.prefill(prompts)
+    torch.cuda.synchronize()
+    t_prefill = time.perf_counter() - t0
+    sess.capture()
+    if warmup:
+        sess.decode(warmup)
+    barrier(ws)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    sess.decode(steps)
+    ev1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    barrier(ws)
+    gpu_s = ev0.elapsed_time(ev1) / 1e3
+    pos_mean = prompt_len + warmup + (steps - 1) / 2.0
+    return dict(seconds=max(wall, gpu_s), gpu_seconds=gpu_s, wall_seconds=wall, t_prefill=t_prefill,
+                pos_mean=pos_mean, tokens=B * steps, session=sess)
+
+
+def time_dominant_kernel(model, B, iters=10):
+    """Average duration of the fused rms_2 + c_fc1/c_fc2 (+silu*mul) launch, one launch per
+    layer on that layer's weights (no cache reuse between consecutive launches: 32 x 45 MB),
+    measured with HIP events on the launch stream."""
+    from lit_llama import _hip
+    from lit_llama.model import MLP, _wspec
+
+    cfg = model.config
+    C, H = cfg.n_embd, MLP.hidden(cfg)
+    x = torch.randn(B, C, device="cuda").to(torch.bfloat16)
+    h = torch.empty(B, H, device="cuda", dtype=torch.bfloat16)
+    specs = []
+    for blk in model.transformer.h:
+        (f1, w1, s1), (f2, w2, s2) = _wspec(blk.mlp.c_fc1), _wspec(blk.mlp.c_fc2)
+        specs.append((f1, blk.rms_2, w1, s1, w2, s2))
+    st = _hip.stream()
+
+    def run_all():
+        for f1, rms, w1, s1, w2, s2 in specs:
+            _hip.call("llj_norm_swiglu", f1, x.data_ptr(), rms.scale.data_ptr(), rms.eps, w1.data_ptr(), _hip.ptr(s1),
+                      w2.data_ptr(), _hip.ptr(s2), h.data_ptr(), B, H, C, None, 0, st)
+
+    run_all()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(iters):
+        run_all()
+    ev1.record()
+    torch.cuda.synchronize()
+    avg_s = ev0.elapsed_time(ev1) / 1e3 / (iters * len(specs))
+    f1, _, w1, s1, w2, s2 = specs[0]
+    wbytes = 2 * (w1.numel() * w1.element_size()) + 2 * 2 * (H * 2)  # two matrices + (scale, zero) bf16
+    abytes = wbytes + B * C * 2 + B * H * 2 + C * 2  # + x row(s), h row(s), norm weight
+    return avg_s, abytes
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(model, budget_s: float = 20.0):
+    """The oracle's numpy port of the reference CPU decode path (dequantize every call),
+    one decode token at position 80 through n sampled layers + lm_head, scaled to the full
+    depth. Threads: numpy/BLAS limited to 16 (the box's CPU share)."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import llama_np as O
+
+    cfg = model.config
+    C, nh = cfg.n_embd, cfg.n_head
+    hs = C // nh
+    p = 80
+    rng = np.random.default_rng(0)
+
+    def lin_np(mod):
+        return (mod.quant_weight.cpu().numpy(), mod.scales.float().cpu().numpy(), mod.zeros.float().cpu().numpy())
+
+    def qlin(x, spec):  # ColBlockQuantizedLinear CPU fallback: get_weight + F.linear per call
+        W = O.colblock_get_weight(*spec, 4)
+        return x @ W.T
+
+    rope = O.build_rope_cache(cfg.block_size, hs)
+    threads = 16
+    with threadpool_limits(limits=threads):
+        layer_times = []
+        t_start = time.perf_counter()
+        x = rng.standard_normal((1, 1, C)).astype(np.float32) * 0.02
+        for li, blk in enumerate(model.transformer.h):
+            specs = [lin_np(m) for m in (blk.attn.c_attn, blk.attn.c_proj, blk.mlp.c_fc1, blk.mlp.c_fc2, blk.mlp.c_proj)]
+            kc = rng.standard_normal((1, nh, p + 1, hs)).astype(np.float32)
+            vc = rng.standard_normal((1, nh, p + 1, hs)).astype(np.float32)
+            t0 = time.perf_counter()
+            h = O.rmsnorm(x, np.ones(C, np.float32))
+            qkv = qlin(h, specs[0])
+            q = O.apply_rope(qkv[..., :C].reshape(1, 1, nh, hs), rope[p:p + 1]).transpose(0, 2, 1, 3)
+            k = O.apply_rope(qkv[..., C:2 * C].reshape(1, 1, nh, hs), rope[p:p + 1]).transpose(0, 2, 1, 3)
+            kc[:, :, p] = k[:, :, 0]
+            vc[:, :, p] = qkv[..., 2 * C:].reshape(1, nh, hs)
+            att = (q @ kc.transpose(0, 1, 3, 2)) / math.sqrt(hs)
+            att = np.exp(att - att.max(-1, keepdims=True))
+            att /= att.sum(-1, keepdims=True)
+            y = (att @ vc).transpose(0, 2, 1, 3).reshape(1, 1, C)
+            x = x + qlin(y, specs[1])
+            h = O.rmsnorm(x, np.ones(C, np.float32))
+            m = O.silu(qlin(h, specs[2])) * qlin(h, specs[3])
+            x = x + qlin(m, specs[4])
+            layer_times.append(time.perf_counter() - t0)
+            if time.perf_counter() - t_start > budget_s * 0.6 and len(layer_times) >= 1:
+                break
+        t0 = time.perf_counter()
+        qlin(O.rmsnorm(x, np.ones(C, np.float32)), lin_np(model.lm_head))
+        t_head = time.perf_counter() - t0
+    per_layer = float(np.mean(layer_times))
+    t_tok = per_layer * cfg.n_layer + t_head
+    return {"value": 1.0 / t_tok, "unit": "tokens/s", "cores": threads, "kind": "port",
+            "sample": f"1 decode token (bs=1, position {p}) through {len(layer_times)} of {cfg.n_layer} layers "
+                      f"({per_layer:.2f} s/layer) + lm_head ({t_head:.2f} s), scaled to {cfg.n_layer} layers; "
+                      "numpy port of the reference CPU path with per-call int4 dequantization"}
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="7B")
+    ap.add_argument("--quantize", default="gptq.int4", choices=["gptq.int4", "llm.int8", "none"])
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--prompt-len", type=int, default=16)
+    ap.add_argument("--max-seq-length", type=int, default=144)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-bs8", action="store_true")
+    args = ap.parse_args()
+
+    rank, ws, local_rank = dist_init()
+    if ws != args.gpus:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {ws}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    mode = None if args.quantize == "none" else args.quantize
+    model = build_model(args.model, mode)
+    S = args.max_seq_length
+
+    r = time_decode(model, args.batch, args.prompt_len, S, args.warmup, args.steps, ws)
+    t_max, tokens = aggregate(r["seconds"], r["tokens"], ws, dev)
+    value = tokens / t_max
+    ms_per_step = t_max / args.steps * 1e3
+    sb = step_bytes(model, args.batch, r["pos_mean"])
+    step_gbs = sb / (r["seconds"] / args.steps) / 1e9
+
+    k_s, k_bytes = time_dominant_kernel(model, args.batch)
+    k_gbs = k_bytes / k_s / 1e9
+
+    bs8 = None
+    if not args.no_bs8 and args.batch != 8:
+        del r["session"]
+        r8 = time_decode(model, 8, args.prompt_len, S, args.warmup, args.steps, ws)
+        t8, tok8 = aggregate(r8["seconds"], r8["tokens"], ws, dev)
+        sb8 = step_bytes(model, 8, r8["pos_mean"])
+        bs8 = {"value": tok8 / t8, "unit": "tokens/s", "ms_per_step": t8 / args.steps * 1e3,
+               "step_roofline_frac": sb8 / (r8["seconds"] / args.steps) / 1e9 / HBM_PEAK_GBS}
+        del r8["session"]
+
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and mode == "gptq.int4":
+        cpu = cpu_baseline(model)
+
+    if rank == 0:
+        name = {"gptq.int4": "gptq.int4", "llm.int8": "llm.int8", "none": "bf16"}[args.quantize]
+        line = {
+            "metric": f"decode tokens/sec LLaMA-{args.model} {name} bs={args.batch}, 1xMI355X per replica",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "weights": {"gptq.int4": "int4 (per-row scale/zero)", "llm.int8": "int8 (LLM.int8)",
+                        "none": "bf16"}[args.quantize],
+            "data": "synthetic (random weights of the exact shapes, random 16-token prompts)",
+            "config": {"workload": f"LLaMA-{args.model} --quantize {args.quantize} greedy decode, batch {args.batch}, "
+                                   f"prompt {args.prompt_len}, max_seq_length {S}",
+                       "batch_per_gpu": args.batch, "prompt_len": args.prompt_len, "max_seq_length": S,
+                       "parallelism": f"replicas x{ws} (no collective on the data path)"},
+            "roofline": {"bound": "hbm", "achieved": round(k_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(k_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "gemv_kernel<W4,NORM,SWIGLU> (rms_2 + c_fc1/c_fc2 + silu*mul)",
+                         "bytes_per_launch": k_bytes, "avg_launch_us": round(k_s * 1e6, 2)},
+            "step_roofline": {"bytes_per_step": sb, "achieved": round(step_gbs, 1), "frac": round(step_gbs / HBM_PEAK_GBS, 4)},
+            "reference_formula_tokens_per_s": round(r["tokens"] / (r["seconds"] + r["t_prefill"]), 2),
+            "cpu_baseline": cpu,
+            "bs8": bs8,
+        }
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
