@@ -51,7 +51,12 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
 /* ---------------------------------------------------------------- fused decode-layer ops
  * (Block.forward, lit_llama/model.py:162-175, split at its four Linear boundaries).
  * norm_w == NULL means the input is used as is (no fused RMSNorm); int8 (wfmt 2) takes
- * already-normalised input (its statistics are computed on it). */
+ * already-normalised input (its statistics are computed on it).
+ * RMSNorm row statistics (optional, decode path, <= 8 rows): fp64 partial sums of
+ * bf16(x^2) laid out [part][8 rows]. llj_embedding writes part 0 (whole rows);
+ * llj_linear_resid writes part n/16 for its 16-column tile n (N/16 parts); the norm-fused
+ * ops read `nstat_parts` parts (1 after the embedding, n_embd/16 after a residual GEMV)
+ * instead of re-reducing the row in every workgroup. NULL = off (row reduced in-kernel). */
 
 /* rms_1 + attn.c_attn + split q/k/v + apply_rope(q, k) + KV-cache write
  * (model.py:171, 204-228, 312-329). x (B*T, C) rows m = b*T + t; q_out (B*T, C);
@@ -61,7 +66,8 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
  * Handles rows [row0, row0 + rows) of the B*T rows; rows <= 8 (RMSNorm staged in LDS). */
 int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                       void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
-                      int C, int n_head, int S, int row0, int rows, const void* i8ws, void* stream);
+                      int C, int n_head, int S, int row0, int rows, const void* i8ws, const double* nstat_in,
+                      int nstat_parts, void* stream);
 
 /* Causal attention of q (B*T, C) over the cache slots each query may see
  * (F.scaled_dot_product_attention with the tril mask rows, model.py:101-104, 237):
@@ -71,16 +77,17 @@ int llj_attention(const void* q, const void* kcache, const void* vcache, void* y
 
 /* x[M, N] += A[M, K] . W^T (attn.c_proj / mlp.c_proj + residual add, model.py:172-173). */
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
-                     int N, int K, const void* i8ws, int i8_row0, void* stream);
+                     int N, int K, const void* i8ws, int i8_row0, double* nstat_out, void* stream);
 
 /* h[M, H] = silu(rms_2(x) . W1^T) * (rms_2(x) . W2^T)  (model.py:173, 258). M <= 8. */
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,
-                    void* stream);
+                    const double* nstat_in, int nstat_parts, void* stream);
 
 /* out[M, N] = RMSNorm(x) . W^T  (ln_f + lm_head, model.py:125-127). M <= 8. */
 int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
-                    void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, void* stream);
+                    void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const double* nstat_in,
+                    int nstat_parts, void* stream);
 
 /* ---------------------------------------------------------------- LLM.int8() */
 /* Bytes of the activation-statistics workspace for an (M, K) activation (host function). */
@@ -94,8 +101,10 @@ int llj_i8_quant_weight(const void* W, int dtype, void* CB, void* SCB, int N, in
 
 /* ---------------------------------------------------------------- small ops */
 /* out[m] = wte[idx[m]] (model.py:110); if pos_inc != NULL, *pos_inc += 1 (device-side
- * decode position, so a captured decode step advances itself). */
-int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, void* stream);
+ * decode position, so a captured decode step advances itself); nstat_out: per-row sum of
+ * bf16(x^2) (see "RMSNorm row statistics" above) or NULL. */
+int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, double* nstat_out,
+                  void* stream);
 
 /* Standalone RMSNorm (model.py:276-283) for rows the fused prologue does not take. */
 int llj_rmsnorm(const void* x, const void* w, float eps, void* y, int M, int C, void* stream);

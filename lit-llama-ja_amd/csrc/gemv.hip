@@ -65,18 +65,62 @@ struct GemvParams {
   int n_head, head_size, S, T;
   int m0;  // global row index of local row 0 (QKV row chunks; int8 statistics rows)
   const void* i8ws;
+  // RMSNorm row statistics, sum_k bf16(x[m,k]^2), produced once instead of re-reduced by
+  // every norm-fused workgroup: partial sums in fp64 laid out [part][8 rows] (M <= 8).
+  // EP_RESID writes one part per workgroup (its 16 columns, plain stores: no atomics, so
+  // no same-address contention and a deterministic order); AM_NORM sums nst_parts parts.
+  const double* nst_in;
+  int nst_parts;
+  double* nst_out;
 };
 
 // ------------------------------------------------------------------------------------
 // Stage A rows [0, M) into LDS (row stride K + 8 elements); row M is all zeros (read by the
 // MFMA lanes of rows >= M). With NORM, rows are RMS-normalised with the reference's bf16
 // rounding points (model.py:281-283 evaluated on bf16 tensors).
+__device__ __forceinline__ float rms_rstd(float sumsq_over_k, float eps) {
+  // bf16: mean(x*x) -> +eps -> rsqrt, each rounded (torch bf16 ops, model.py:281-282)
+  return round_bf(rsqrtf(round_bf(round_bf(sumsq_over_k) + eps)));
+}
+
+__device__ __forceinline__ uint4 norm8(uint4 x, uint4 g, float r) {
+  uint32_t xw[4] = {x.x, x.y, x.z, x.w}, gw[4] = {g.x, g.y, g.z, g.w}, o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float lo = round_bf(bflo(gw[i]) * round_bf(bflo(xw[i]) * r));
+    float hi = round_bf(bfhi(gw[i]) * round_bf(bfhi(xw[i]) * r));
+    o[i] = pack2bf(lo, hi);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 template <int NW, bool NORM>
 __device__ void stage_a(const GemvParams& p, bf16_t* As, int a_stride, float* red) {
   const int tid = threadIdx.x;
   constexpr int NT = NW * 64;
   const int K = p.K, M = p.M;
   const int nvec = K >> 3;
+  if (NORM && p.nst_in) {  // statistics precomputed by the producer: one pass
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int m = wave; m < M; m += NW) {
+      double s = 0.0;
+      for (int q = lane; q < p.nst_parts; q += 64) s += p.nst_in[q * 8 + m];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (lane == 0) red[m] = rms_rstd((float)(s / (double)K), p.eps);
+    }
+    __syncthreads();
+    const uint4* g4 = reinterpret_cast<const uint4*>(p.norm_w);
+    for (int m = 0; m < M; ++m) {
+      const float r = red[m];
+      const uint4* src = reinterpret_cast<const uint4*>(p.A + (size_t)m * p.lda);
+      uint4* dst = reinterpret_cast<uint4*>(As + (size_t)m * a_stride);
+      for (int v = tid; v < nvec; v += NT) dst[v] = norm8(src[v], g4[v], r);
+    }
+    uint4* z = reinterpret_cast<uint4*>(As + (size_t)M * a_stride);
+    for (int v = tid; v < nvec; v += NT) z[v] = make_uint4(0, 0, 0, 0);
+    return;
+  }
   float ss[8];
 #pragma unroll
   for (int m = 0; m < 8; ++m) ss[m] = 0.f;
@@ -115,9 +159,7 @@ __device__ void stage_a(const GemvParams& p, bf16_t* As, int a_stride, float* re
     float s = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) s += red[w * 8 + tid];
-    // bf16: mean(x*x) -> +eps -> rsqrt, each rounded (torch bf16 ops)
-    float ms = round_bf(s / (float)K);
-    red[NW * 8 + tid] = round_bf(rsqrtf(round_bf(ms + p.eps)));
+    red[NW * 8 + tid] = rms_rstd(s / (float)K, p.eps);
   }
   __syncthreads();
   const uint4* g4 = reinterpret_cast<const uint4*>(p.norm_w);
@@ -126,17 +168,7 @@ __device__ void stage_a(const GemvParams& p, bf16_t* As, int a_stride, float* re
     if (m < M) {
       const float r = red[NW * 8 + m];
       uint4* row = reinterpret_cast<uint4*>(As + (size_t)m * a_stride);
-      for (int v = tid; v < nvec; v += NT) {
-        uint4 x = row[v], g = g4[v];
-        uint32_t xw[4] = {x.x, x.y, x.z, x.w}, gw[4] = {g.x, g.y, g.z, g.w}, o[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float lo = round_bf(bflo(gw[i]) * round_bf(bflo(xw[i]) * r));
-          float hi = round_bf(bfhi(gw[i]) * round_bf(bfhi(xw[i]) * r));
-          o[i] = pack2bf(lo, hi);
-        }
-        row[v] = make_uint4(o[0], o[1], o[2], o[3]);
-      }
+      for (int v = tid; v < nvec; v += NT) row[v] = norm8(row[v], g4[v], r);
     }
   }
 }
@@ -254,19 +286,15 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   const int n0 = nt * 16;
   const int K = p.K, M = p.M, KC = K >> 7;
   const int row = lane & 15, grp = lane >> 4;
-  // LDS carve: A image | reduction scratch | sca
+  // LDS carve: [A image, aliased after the main loop by the NW x 64 x 12-word reduction
+  // scratch] [tail: 64 words for staging scratch / int8 SCA]
   const int a_stride = I8 ? K + 16 : K + 8;  // elements (bytes for int8)
   const size_t a_bytes = ALDS ? (((size_t)(M + 1) * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15) : 0;
-  float* red = reinterpret_cast<float*>(smem + a_bytes);
-  float* sca = red + NW * 64 * 12;
+  constexpr size_t kRedBytes = (size_t)NW * 64 * 12 * 4;
+  float* red = reinterpret_cast<float*>(smem);
+  float* tail = reinterpret_cast<float*>(smem + (a_bytes > kRedBytes ? a_bytes : kRedBytes));
+  float* sca = tail;
 
-  if constexpr (I8) {
-    stage_i8<NW>(p, reinterpret_cast<int8_t*>(smem), a_stride, sca);
-    __syncthreads();
-  } else if constexpr (ALDS) {
-    stage_a<NW, AM == AM_NORM>(p, reinterpret_cast<bf16_t*>(smem), a_stride, red);
-    __syncthreads();
-  }
   const bool arow = row < M;
   const unsigned char* abase;  // byte address of this lane's A row
   if (ALDS) {
@@ -306,45 +334,56 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   i32x4 iacc = {0, 0, 0, 0}, iacc2 = {0, 0, 0, 0};
   const int nmy = uniform((KC - wave + NW - 1) / NW);
 
+  u32x4 r1[D][WV], r2[D][WV];
+  u32x4 ra[D][4];
+  auto load = [&](int d, int i) {
+    const int c = wave + NW * (i < nmy ? i : nmy - 1);
+#pragma unroll
+    for (int v = 0; v < WV; ++v) {
+      r1[d][v] = __builtin_nontemporal_load(w1 + (size_t)c * wstep + vstride * v);
+      if (DUAL) r2[d][v] = __builtin_nontemporal_load(w2 + (size_t)c * wstep + vstride * v);
+    }
+    if (!ALDS) {
+#pragma unroll
+      for (int t = 0; t < NSTEP; ++t)
+        ra[d][t] = arow ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : zero4;
+    }
+  };
+  auto compute = [&](int d, int i) {
+    const int c = wave + NW * i;
+#pragma unroll
+    for (int t = 0; t < NSTEP; ++t) {
+      const u32x4 av = ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
+      if constexpr (WF == WF_W4) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+        acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
+        if (DUAL) acc2 = mfma_bf16(a, dequant_w4(r2[d][0][t], msk, mag), acc2);
+        sacc = mfma_bf16(a, ones, sacc);
+      } else if constexpr (WF == WF_BF16) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+        acc = mfma_bf16(a, __builtin_bit_cast(bf16x8, r1[d][t]), acc);
+        if (DUAL) acc2 = mfma_bf16(a, __builtin_bit_cast(bf16x8, r2[d][t]), acc2);
+      } else {
+        const i32x4 a = __builtin_bit_cast(i32x4, av);
+        iacc = mfma_i8(a, __builtin_bit_cast(i32x4, r1[d][t]), iacc);
+        if (DUAL) iacc2 = mfma_i8(a, __builtin_bit_cast(i32x4, r2[d][t]), iacc2);
+      }
+    }
+  };
+
+  // the weight stream starts before the A prologue so its HBM latency hides the staging
   if (nmy > 0) {
-    u32x4 r1[D][WV], r2[D][WV];
-    u32x4 ra[D][4];
-    auto load = [&](int d, int i) {
-      const int c = wave + NW * (i < nmy ? i : nmy - 1);
-#pragma unroll
-      for (int v = 0; v < WV; ++v) {
-        r1[d][v] = __builtin_nontemporal_load(w1 + (size_t)c * wstep + vstride * v);
-        if (DUAL) r2[d][v] = __builtin_nontemporal_load(w2 + (size_t)c * wstep + vstride * v);
-      }
-      if (!ALDS) {
-#pragma unroll
-        for (int t = 0; t < NSTEP; ++t)
-          ra[d][t] = arow ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : zero4;
-      }
-    };
-    auto compute = [&](int d, int i) {
-      const int c = wave + NW * i;
-#pragma unroll
-      for (int t = 0; t < NSTEP; ++t) {
-        const u32x4 av = ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
-        if constexpr (WF == WF_W4) {
-          const bf16x8 a = __builtin_bit_cast(bf16x8, av);
-          acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
-          if (DUAL) acc2 = mfma_bf16(a, dequant_w4(r2[d][0][t], msk, mag), acc2);
-          sacc = mfma_bf16(a, ones, sacc);
-        } else if constexpr (WF == WF_BF16) {
-          const bf16x8 a = __builtin_bit_cast(bf16x8, av);
-          acc = mfma_bf16(a, __builtin_bit_cast(bf16x8, r1[d][t]), acc);
-          if (DUAL) acc2 = mfma_bf16(a, __builtin_bit_cast(bf16x8, r2[d][t]), acc2);
-        } else {
-          const i32x4 a = __builtin_bit_cast(i32x4, av);
-          iacc = mfma_i8(a, __builtin_bit_cast(i32x4, r1[d][t]), iacc);
-          if (DUAL) iacc2 = mfma_i8(a, __builtin_bit_cast(i32x4, r2[d][t]), iacc2);
-        }
-      }
-    };
 #pragma unroll
     for (int d = 0; d < D; ++d) load(d, d);
+  }
+  if constexpr (I8) {
+    stage_i8<NW>(p, reinterpret_cast<int8_t*>(smem), a_stride, sca);
+    __syncthreads();
+  } else if constexpr (ALDS) {
+    stage_a<NW, AM == AM_NORM>(p, reinterpret_cast<bf16_t*>(smem), a_stride, tail);
+    __syncthreads();
+  }
+  if (nmy > 0) {
     for (int i0 = 0; i0 < nmy; i0 += D) {
 #pragma unroll
       for (int d = 0; d < D; ++d) {
@@ -357,6 +396,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   // int32 — they exceed 2^24 at K = 11008, so they must not round-trip through fp32)
   constexpr int NV = 12;
   if (NW > 1) {
+    if (ALDS) __syncthreads();  // every wave is done reading the A image it aliases
     if constexpr (I8) {
       int* mine = reinterpret_cast<int*>(red) + (size_t)(wave * 64 + lane) * NV;
 #pragma unroll
@@ -457,6 +497,23 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
           (region == 1 ? p.kcache : p.vcache)[ci] = ob;
         }
       }
+    } else if (EP == EP_RESID) {
+      // x = x + h in bf16 (model.py:172-173); optionally the partial sum_k bf16(x_new^2) of
+      // this workgroup's 16 columns for the next RMSNorm (part nt of nst_out)
+      float sq = 0.f;
+      if (m < M) {
+        bf16_t* dst = p.C + (size_t)m * p.ldc + n;
+        const float xn = round_bf(bf2f(*dst) + round_bf(y));
+        *dst = f2bf(xn);
+        sq = round_bf(xn * xn);
+      }
+      if (p.nst_out) {
+        sq += __shfl_xor(sq, 8, 64);
+        sq += __shfl_xor(sq, 4, 64);
+        sq += __shfl_xor(sq, 2, 64);
+        sq += __shfl_xor(sq, 1, 64);
+        if (row == 0 && m < M) p.nst_out[nt * 8 + m] = (double)sq;
+      }
     } else if (m < M) {
       store_out<EP>(p, m, n, y, y2);
     }
@@ -464,8 +521,14 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
 }
 
 // ------------------------------------------------------------------------------------
-constexpr int kNW = 4;
-constexpr int kD = 4;
+#ifndef LLJ_NW
+#define LLJ_NW 4  // waves per workgroup (K split across them)
+#endif
+#ifndef LLJ_D
+#define LLJ_D 4  // weight chunks in flight per wave
+#endif
+constexpr int kNW = LLJ_NW;
+constexpr int kD = LLJ_D;
 
 static inline size_t a_image_bytes(int wf, int am, int M, int K) {
   if (wf == WF_I8) return (((size_t)(M + 1) * (K + 16)) + 15) & ~(size_t)15;
@@ -473,7 +536,8 @@ static inline size_t a_image_bytes(int wf, int am, int M, int K) {
   return (((size_t)(M + 1) * (K + 8) * 2) + 15) & ~(size_t)15;
 }
 static inline size_t gemv_smem(int wf, int am, int M, int K) {
-  return a_image_bytes(wf, am, M, K) + (size_t)kNW * 64 * 12 * 4 + 8 * 4;
+  const size_t a = a_image_bytes(wf, am, M, K), red = (size_t)kNW * 64 * 12 * 4;
+  return (a > red ? a : red) + 64 * 4;
 }
 
 // the LDS A image must leave room for the reduction scratch: <= 96 KiB, M <= 8 rows
@@ -548,8 +612,12 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
 
 // out[M,N] = RMSNorm(x)[M,K] . W^T  (ln_f + lm_head, model.py:125-127); norm_w NULL = no norm.
 int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
-                    void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, void* stream) {
+                    void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const double* nstat_in,
+                    int nstat_parts, void* stream) {
   GemvParams p{};
+  if (nstat_in && (M > 8 || nstat_parts < 1)) return LLJ_EINVAL;
+  p.nst_in = nstat_in;
+  p.nst_parts = nstat_parts;
   p.A = (const bf16_t*)x; p.lda = K; p.norm_w = (const bf16_t*)norm_w; p.eps = eps; p.M = M; p.N = N; p.K = K;
   p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)out; p.ldc = ldo;
   p.i8ws = i8ws; p.m0 = i8_row0;
@@ -558,8 +626,10 @@ int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, cons
 
 // x[M,N] += A[M,K] . W^T, bf16 residual add (attn.c_proj / mlp.c_proj + model.py:172-173).
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
-                     int N, int K, const void* i8ws, int i8_row0, void* stream) {
+                     int N, int K, const void* i8ws, int i8_row0, double* nstat_out, void* stream) {
   GemvParams p{};
+  if (nstat_out && M > 8) return LLJ_EINVAL;
+  p.nst_out = nstat_out;
   p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K;
   p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)x; p.ldc = ldx;
   p.i8ws = i8ws; p.m0 = i8_row0;
@@ -569,8 +639,11 @@ int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void
 // h[M,H] = silu(RMSNorm(x) . W1^T) * (RMSNorm(x) . W2^T)  (rms_2 + model.py:258).
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,
-                    void* stream) {
+                    const double* nstat_in, int nstat_parts, void* stream) {
   GemvParams p{};
+  if (nstat_in && (M > 8 || nstat_parts < 1)) return LLJ_EINVAL;
+  p.nst_in = nstat_in;
+  p.nst_parts = nstat_parts;
   p.A = (const bf16_t*)x; p.lda = K; p.norm_w = (const bf16_t*)norm_w; p.eps = eps; p.M = M; p.N = H; p.K = K;
   p.W = W1; p.W2 = W2; p.sz = (const float2*)sz1; p.sz2 = (const float2*)sz2; p.C = (bf16_t*)h; p.ldc = H;
   p.i8ws = i8ws; p.m0 = i8_row0;
@@ -582,8 +655,12 @@ int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, cons
 // q_out (B*T, C); caches (B, n_head, S, hs).
 int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                       void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
-                      int C, int n_head, int S, int row0, int rows, const void* i8ws, void* stream) {
+                      int C, int n_head, int S, int row0, int rows, const void* i8ws, const double* nstat_in,
+                      int nstat_parts, void* stream) {
   GemvParams p{};
+  if (nstat_in && (row0 + rows > 8 || nstat_parts < 1)) return LLJ_EINVAL;
+  p.nst_in = nstat_in ? nstat_in + row0 : nullptr;
+  p.nst_parts = nstat_parts;
   if (row0 < 0 || rows < 1 || row0 + rows > B * T || n_head < 1 || C % n_head || S < 1) return LLJ_EINVAL;
   p.A = (const bf16_t*)x + (size_t)row0 * C; p.lda = C; p.norm_w = (const bf16_t*)norm_w; p.eps = eps;
   p.M = rows; p.m0 = row0; p.N = 3 * C; p.K = C;

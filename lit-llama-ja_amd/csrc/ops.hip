@@ -7,12 +7,26 @@ namespace llj {
 
 // ---- embedding: out[m] = wte[idx[m]]  (reference model.py:110). Optionally bumps the
 // device-side decode position (*pos_inc += 1) so a captured decode step is self-advancing.
-__global__ void embedding_kernel(const int* __restrict__ idx, const uint4* __restrict__ wte, uint4* __restrict__ out,
-                                 int C8, int* pos_inc) {
+__global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ idx, const uint4* __restrict__ wte,
+                                                        uint4* __restrict__ out, int C8, int* pos_inc, double* nstat) {
+  __shared__ float red[4];
   const int m = blockIdx.x;
   const size_t r = (size_t)idx[m];
-  for (int v = threadIdx.x; v < C8; v += blockDim.x) out[(size_t)m * C8 + v] = wte[r * C8 + v];
+  float ss = 0.f;
+  for (int v = threadIdx.x; v < C8; v += blockDim.x) {
+    const uint4 x = wte[r * C8 + v];
+    out[(size_t)m * C8 + v] = x;
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ss += round_bf(bflo(w[i]) * bflo(w[i])) + round_bf(bfhi(w[i]) * bfhi(w[i]));
+  }
   if (pos_inc && m == 0 && threadIdx.x == 0) *pos_inc += 1;
+  if (nstat) {  // sum_k bf16(x^2) of the row for the first RMSNorm (see gemv.hip nst_in)
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    if (threadIdx.x == 0) nstat[m] = (double)red[0] + (double)red[1] + (double)red[2] + (double)red[3];  // part 0
+  }
 }
 
 // ---- RMSNorm with the bf16 rounding points of model.py:281-283 on bf16 tensors.
@@ -176,10 +190,11 @@ using namespace llj;
 
 extern "C" {
 
-int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, void* stream) {
+int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, double* nstat_out,
+                  void* stream) {
   LLJ_REQUIRE(M > 0 && C % 8 == 0);
   hipLaunchKernelGGL(embedding_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, idx, (const uint4*)wte,
-                     (uint4*)out, C / 8, pos_inc);
+                     (uint4*)out, C / 8, pos_inc, nstat_out);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

@@ -30,7 +30,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = OUT.with_suffix(".so.tmp")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall",
-           "-Wno-unused-variable", "-Wno-unused-function", "-o", str(tmp)] + [str(s) for s in sources()]
+           "-Wno-unused-variable", "-Wno-unused-function", "-munsafe-fp-atomics", "-o", str(tmp)] + [str(s) for s in sources()]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

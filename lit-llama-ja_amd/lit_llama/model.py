@@ -93,7 +93,13 @@ def _wspec(lin: nn.Module):
 
 
 class _Work:
-    """Per-call scratch for M rows (allocated from torch's caching allocator)."""
+    """Per-call scratch for M rows (allocated from torch's caching allocator).
+
+    With M <= QKV_ROWS and no int8 Linear, RMSNorm row statistics flow between kernels
+    (`nst` = two fp64 [n_embd/16][8] partial-sum buffers, see include/lit_llama_amd.h "RMSNorm
+    row statistics"): the embedding / residual epilogues produce sum(bf16(x^2)) per row once,
+    instead of every norm-fused GEMV workgroup re-reducing the row. Buffer 0 feeds rms_1 /
+    ln_f (written by the embedding, then by mlp.c_proj), buffer 1 feeds rms_2 (attn.c_proj)."""
 
     def __init__(self, cfg: LLaMAConfig, M: int, device, need_i8: bool):
         C, H = cfg.n_embd, MLP.hidden(cfg)
@@ -109,6 +115,15 @@ class _Work:
             self.i8ws = torch.empty(nb, dtype=torch.uint8, device=device)
         else:
             self.i8ws = None
+        if M <= QKV_ROWS and not need_i8:
+            parts = max(1, C // 16)
+            self.nst = (torch.zeros(parts * 8, dtype=torch.float64, device=device),
+                        torch.zeros(parts * 8, dtype=torch.float64, device=device))
+        else:
+            self.nst = None
+
+    def nst_ptr(self, which: int):
+        return None if self.nst is None else self.nst[which].data_ptr()
 
 
 class LLaMA(nn.Module):
@@ -210,12 +225,15 @@ class LLaMA(nn.Module):
         st = _hip.stream()
         ids = idx.reshape(-1).to(torch.int32)
         _hip.call("llj_embedding", ids.data_ptr(), self.transformer.wte.weight.data_ptr(), w.x.data_ptr(), M,
-                  cfg.n_embd, None, st)
+                  cfg.n_embd, None, w.nst_ptr(0), st)
         self._blocks(w, specs, kv, pos, B, T, S, st)
         V = cfg.padded_vocab_size
         if last_only_out is not None:
-            rows = w.x.view(B, T, -1)[:, -1].contiguous()
-            self._head(rows, B, specs, last_only_out, st, w)
+            if T == 1:
+                self._head(w.x, B, specs, last_only_out, st, w)
+            else:
+                rows = w.x.view(B, T, -1)[:, -1].contiguous()
+                self._head(rows, B, specs, last_only_out, st, w, use_nst=False)
             return last_only_out
         logits = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
         self._head(w.x, M, specs, logits, st, w)
@@ -253,12 +271,12 @@ class LLaMA(nn.Module):
                 r = min(QKV_ROWS, M - r0)
                 _hip.call("llj_norm_qkv_rope", fa, src.data_ptr(), nw, blk.rms_1.eps, wa.data_ptr(), P(sa),
                           w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), B, T, C, nh,
-                          S, r0, r, P(w.i8ws), st)
+                          S, r0, r, P(w.i8ws), w.nst_ptr(0), 1 if i == 0 else C // 16, st)
             # 2. attention
             _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(), pos.data_ptr(),
                       B, T, nh, C // nh, S, st)
-            # 3. c_proj + residual
-            self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st)
+            # 3. c_proj + residual (+ rms_2 row statistics)
+            self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst_ptr(1))
             # 4. rms_2 + fc1/fc2 + silu*mul
             if f1 != f2:
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")
@@ -272,20 +290,22 @@ class LLaMA(nn.Module):
             for r0 in range(0, M, step):
                 r = min(step, M - r0)
                 _hip.call("llj_norm_swiglu", f1, src[r0].data_ptr(), nw, blk.rms_2.eps, w1.data_ptr(), P(s1),
-                          w2.data_ptr(), P(s2), w.h[r0].data_ptr(), r, H, C, P(w.i8ws), r0, st)
-            # 5. mlp.c_proj + residual
-            self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st)
+                          w2.data_ptr(), P(s2), w.h[r0].data_ptr(), r, H, C, P(w.i8ws), r0, w.nst_ptr(1),
+                          C // 16, st)
+            # 5. mlp.c_proj + residual (+ next rms_1 / ln_f row statistics)
+            self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st, w.nst_ptr(0))
 
-    def _resid(self, f, A, W, sz, x, M, N, K, w, st):
+    def _resid(self, f, A, W, sz, x, M, N, K, w, st, nst_out=None):
         if f == 2:
             self._i8_prep(A, M, K, w, st)
         step = I8_ROWS if f == 2 else LIN_ROWS
         for r0 in range(0, M, step):
             r = min(step, M - r0)
             _hip.call("llj_linear_resid", f, A[r0].data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz),
-                      x[r0].data_ptr(), x.stride(0), r, N, K, _hip.ptr(w.i8ws), r0, st)
+                      x[r0].data_ptr(), x.stride(0), r, N, K, _hip.ptr(w.i8ws), r0,
+                      nst_out, st)
 
-    def _head(self, x, M, specs, out, st, w):
+    def _head(self, x, M, specs, out, st, w, use_nst=True):
         cfg = self.config
         C, V = cfg.n_embd, cfg.padded_vocab_size
         f, W, sz = specs["head"]
@@ -299,8 +319,10 @@ class LLaMA(nn.Module):
             src, nw = x, ln.scale.data_ptr()
         for r0 in range(0, M, QKV_ROWS):
             r = min(QKV_ROWS, M - r0)
+            nin = w.nst_ptr(0) if use_nst else None
+            parts = 1 if cfg.n_layer == 0 else C // 16
             _hip.call("llj_norm_linear", f, src[r0].data_ptr(), nw, ln.eps, W.data_ptr(), _hip.ptr(sz),
-                      out[r0].data_ptr(), out.stride(0), r, V, C, _hip.ptr(w.i8ws), r0, st)
+                      out[r0].data_ptr(), out.stride(0), r, V, C, _hip.ptr(w.i8ws), r0, nin, parts, st)
 
 
 Linear8bitLtThreshold = 6.0  # reference quantization.py:45
@@ -415,7 +437,7 @@ class MLP(nn.Module):
         for r0 in range(0, M, step):
             r = min(step, M - r0)
             _hip.call("llj_norm_swiglu", f1, x2[r0].data_ptr(), None, 0.0, w1.data_ptr(), _hip.ptr(s1), w2.data_ptr(),
-                      _hip.ptr(s2), h[r0].data_ptr(), r, H, K, _hip.ptr(ws), r0, st)
+                      _hip.ptr(s2), h[r0].data_ptr(), r, H, K, _hip.ptr(ws), r0, None, 0, st)
         out = torch.empty(M, self.c_proj.out_features, dtype=torch.bfloat16, device=x.device)
         if fd == 2:
             _hip.call("llj_i8_stats", h.data_ptr(), H, M, H, Linear8bitLtThreshold, ws.data_ptr(), st)

@@ -222,10 +222,13 @@ def test_embedding_and_pos_inc(hip):
     out = torch.empty(3, 256, dtype=torch.bfloat16, device=dev)
     pos = torch.tensor([7], dtype=torch.int32, device=dev)
     idd, wd = T(idx), T(wte, torch.bfloat16)
-    call(hip, "llj_embedding", idd.data_ptr(), wd.data_ptr(), out.data_ptr(), 3, 256, pos.data_ptr(), st())
+    nst = torch.zeros(3, dtype=torch.float64, device=dev)
+    call(hip, "llj_embedding", idd.data_ptr(), wd.data_ptr(), out.data_ptr(), 3, 256, pos.data_ptr(), nst.data_ptr(),
+         st())
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.float().cpu().numpy(), wte[idx])
     assert int(pos) == 8
+    np.testing.assert_allclose(nst.cpu().numpy(), (bf16(wte[idx] ** 2)).sum(-1), rtol=1e-6)
 
 
 @pytest.mark.parametrize("wfmt", [0, 1])
@@ -254,7 +257,7 @@ def test_fused_qkv_rope_kv(hip, wfmt, B, T_):
         r = min(8, M - r0)
         call(hip, "llj_norm_qkv_rope", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, Wd.data_ptr(),
              None if szd is None else szd.data_ptr(), q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rd.data_ptr(),
-             pd.data_ptr(), B, T_, C, nh, S, r0, r, None, st())
+             pd.data_ptr(), B, T_, C, nh, S, r0, r, None, None, 0, st())
     torch.cuda.synchronize()
     h = bf16(O.rmsnorm(x, g))
     qkv = bf16(h @ Wref.T)
@@ -292,10 +295,10 @@ def test_fused_swiglu_and_resid(hip, wfmt):
     P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
     xd, gd = T(x, torch.bfloat16), T(g, torch.bfloat16)
     call(hip, "llj_norm_swiglu", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, W1d.data_ptr(), P(s1), W2d.data_ptr(),
-         P(s2), h.data_ptr(), M, H, C, None, 0, st())
+         P(s2), h.data_ptr(), M, H, C, None, 0, None, 0, st())
     xr = xd.clone()
     call(hip, "llj_linear_resid", wfmt, h.data_ptr(), H, Wdd.data_ptr(), P(sd), xr.data_ptr(), C, M, C, H, None, 0,
-         st())
+         None, st())
     torch.cuda.synchronize()
     hn = bf16(O.rmsnorm(x, g))
     a1, a2 = bf16(hn @ W1.T), bf16(hn @ W2.T)
