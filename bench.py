@@ -204,6 +204,23 @@ def time_dominant_kernel(model, B, iters=10):
     return avg_s, abytes
 
 
+def pmc_traffic(kernel_prefix: str = "llj::gemv_kernel<0, 2, 3"):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
+    (profiles/<round>_summary.json, written by tools/pmc_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command, gfx950
+    correction 2*FETCH+WRITE KiB). None when no summary is present."""
+    best = None
+    for p in sorted((REPO / "profiles").glob("r*_summary.json")):
+        try:
+            d = json.loads(p.read_text())
+        except (OSError, ValueError):
+            continue
+        for name, lp in d.get("dominant_loop", {}).items():
+            if name.startswith(kernel_prefix) and "hbm_bytes_per_dispatch" in lp:
+                best = (lp["hbm_bytes_per_dispatch"], p.name, lp.get("avg_us"))
+    return best
+
+
 # ----------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(model, budget_s: float = 20.0):
     """The oracle's numpy port of the reference CPU decode path (dequantize every call),
@@ -299,6 +316,7 @@ def main():
     k_s, k_bytes = time_dominant_kernel(model, args.batch)
     k_gbs = k_bytes / k_s / 1e9
 
+    pmc = pmc_traffic()
     bs8 = None
     if not args.no_bs8 and args.batch != 8:
         del r["session"]
@@ -335,7 +353,10 @@ def main():
                        "batch_per_gpu": args.batch, "prompt_len": args.prompt_len, "max_seq_length": S,
                        "parallelism": f"replicas x{ws} (no collective on the data path)"},
             "roofline": {"bound": "hbm", "achieved": round(k_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(k_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(k_gbs / HBM_PEAK_GBS, 4),
+                         "traffic": round(pmc[0]) if pmc and args.batch == 1 and mode == "gptq.int4" and args.model == "7B" else None,
+                         "traffic_source": (f"profiles/{pmc[1]} (PMC, rocprof avg {pmc[2]:.2f} us)"
+                                            if pmc and args.batch == 1 and mode == "gptq.int4" and args.model == "7B" else None),
                          "kernel": "gemv_kernel<W4,NORM,SWIGLU> (rms_2 + c_fc1/c_fc2 + silu*mul)",
                          "bytes_per_launch": k_bytes, "avg_launch_us": round(k_s * 1e6, 2)},
             "step_roofline": {"bytes_per_step": sb, "achieved": round(step_gbs, 1), "frac": round(step_gbs / HBM_PEAK_GBS, 4)},
