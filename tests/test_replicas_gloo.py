@@ -1,0 +1,57 @@
+"""bench.py's multi-GPU plumbing (replicas only) rehearsed on CPU with gloo,
+world_size 2: process-group init from the torchrun environment, the barrier, and the
+aggregate = (max seconds over ranks, sum of tokens over ranks) that `value` is built from."""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import torch
+import torch.multiprocessing as mp
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, ws, port, q):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(ws), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, str(REPO))
+    import bench
+
+    r, w, lr = bench.dist_init()
+    bench.barrier(w)
+    t, n = bench.aggregate(0.5 + rank, 100 * (rank + 1), w)
+    q.put((r, w, lr, t, n))
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+
+
+def test_replica_aggregate_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[:3] for r in res] == [(0, 2, 0), (1, 2, 1)]
+    for _, _, _, t, n in res:
+        assert t == 1.5 and n == 300  # max of (0.5, 1.5); 100 + 200 tokens
+
+
+def test_single_process_is_identity():
+    sys.path.insert(0, str(REPO))
+    import bench
+
+    assert bench.aggregate(2.0, 7, 1) == (2.0, 7)
+    assert not torch.distributed.is_initialized()
