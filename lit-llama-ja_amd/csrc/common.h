@@ -28,12 +28,11 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
 }
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
 
-// (x & m) | c in one VALU op (hipcc does not fuse literals into VOP3 on gfx9 encodings).
-__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m_sgpr, uint32_t c) {
-  uint32_t r;
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m_sgpr), "v"(c));
-  return r;
-}
+// (x & m) | c: the compiler selects one v_and_or_b32 when m is in an SGPR (pass it through
+// uniform()). Not inline asm: the hazard recognizer cannot see inside asm blocks, and an asm
+// VALU write to a VGPR an in-flight MFMA still reads as its B operand is a WAR hazard that
+// corrupted results when the writes were scheduled right after the MFMA.
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m_sgpr, uint32_t c) { return (x & m_sgpr) | c; }
 
 __device__ __forceinline__ f32x4 mfma_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);

@@ -272,7 +272,45 @@ __device__ __forceinline__ void store_out(const GemvParams& p, int m, int n, flo
   }
 }
 
-template <int WF, int AM, int EP, int NW, int D>
+#ifndef LLJ_TRACE
+#define LLJ_TRACE 0  // profiling only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
+#endif
+#if LLJ_TRACE
+__device__ unsigned long long g_trace[8192 * 6];
+#define LLJ_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < 8192) g_trace[blockIdx.x * 6 + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define LLJ_STAMP(k)
+#endif
+
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
+
+// Register-staged A prologue. Loads return to VGPRs in issue order, so the A-side loads
+// (RMSNorm partial statistics, activation rows, norm weights) and the epilogue operands are
+// issued BEFORE the weight prefetch: waiting for them then does not also wait for the
+// weight chunks' HBM latency, and the LDS image is written while the weights are in flight.
+// MB = row class of the instantiation (1: M == 1; 8: M <= 8); register budget per lane:
+//   XR 16-byte activation registers (MB 1: one row of K <= 8*XR*NT; MB 8: RS = 2 per row for
+//   M <= 8, K <= 16*NT, or RS = 4 for M <= 4), GR norm-weight registers, ST fp64 partials.
+template <int MB, bool NORM>
+struct APre {
+  static constexpr int XR = MB == 1 ? (NORM ? 4 : 8) : 16;
+  static constexpr int GR = NORM ? 4 : 1;
+  static constexpr int SM = MB == 1 ? 1 : 8;  // statistics rows interleaved over threads
+  static constexpr int ST = MB == 1 ? 2 : 8;  // partials per thread
+  u32x4 x[XR];
+  u32x4 g[GR];
+  double st[ST];
+};
+
+#ifndef LLJ_ABL
+#define LLJ_ABL 0  // ablation switches for profiling only (1 no A prologue, 2 no compute, 4 no epilogue)
+#endif
+
+template <int WF, int AM, int EP, int NW, int D, int MB>
 __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool DUAL = (EP == EP_SWIGLU);
@@ -287,7 +325,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   const int K = p.K, M = p.M, KC = K >> 7;
   const int row = lane & 15, grp = lane >> 4;
   // LDS carve: [A image, aliased after the main loop by the NW x 64 x 12-word reduction
-  // scratch] [tail: 64 words for staging scratch / int8 SCA]
+  // scratch] [tail: 128 words for staging scratch / int8 SCA]
   const int a_stride = I8 ? K + 16 : K + 8;  // elements (bytes for int8)
   const size_t a_bytes = ALDS ? (((size_t)(M + 1) * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15) : 0;
   constexpr size_t kRedBytes = (size_t)NW * 64 * 12 * 4;
@@ -304,8 +342,11 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   }
   constexpr int EB = I8 ? 1 : 2;  // A element bytes
 
-  const uint32_t msk = uniform(0x000F000F);
-  const uint32_t mag = 0x43004300u;
+  // mask in an SGPR and magic in a VGPR, hidden from constant folding (empty asm, no
+  // instruction) so that (w & msk) | mag selects one v_and_or_b32 (no literal in VOP3 on gfx9)
+  uint32_t msk = 0x000F000Fu, mag = 0x43004300u;
+  asm volatile("" : "+s"(msk));
+  asm volatile("" : "+v"(mag));
   const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
   const u32x4 zero4 = {0, 0, 0, 0};
 
@@ -337,7 +378,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   u32x4 r1[D][WV], r2[D][WV];
   u32x4 ra[D][4];
   auto load = [&](int d, int i) {
-    const int c = wave + NW * (i < nmy ? i : nmy - 1);
+    int c = wave + NW * (i < nmy ? i : nmy - 1);
+    c = c < 0 ? 0 : (c >= KC ? KC - 1 : c);  // always a valid chunk (loads past the end are unused)
 #pragma unroll
     for (int v = 0; v < WV; ++v) {
       r1[d][v] = __builtin_nontemporal_load(w1 + (size_t)c * wstep + vstride * v);
@@ -351,6 +393,11 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   };
   auto compute = [&](int d, int i) {
     const int c = wave + NW * i;
+    if constexpr ((LLJ_ABL & 2) != 0) {  // ablation: loads only
+      acc[0] += __builtin_bit_cast(float, (r1[d][0].x ^ r1[d][0].w) & 0x3FFu);
+      if (DUAL) acc2[0] += __builtin_bit_cast(float, (r2[d][0].x ^ r2[d][0].w) & 0x3FFu);
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < NSTEP; ++t) {
       const u32x4 av = ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
@@ -358,7 +405,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
         acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
         if (DUAL) acc2 = mfma_bf16(a, dequant_w4(r2[d][0][t], msk, mag), acc2);
-        sacc = mfma_bf16(a, ones, sacc);
+        if constexpr (!ALDS) sacc = mfma_bf16(a, ones, sacc);  // LDS paths: row sums from the prologue
       } else if constexpr (WF == WF_BF16) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
         acc = mfma_bf16(a, __builtin_bit_cast(bf16x8, r1[d][t]), acc);
@@ -371,18 +418,226 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
     }
   };
 
-  // the weight stream starts before the A prologue so its HBM latency hides the staging
-  if (nmy > 0) {
+  LLJ_STAMP(0);
+  // ---- epilogue operands, loaded first. Every prologue load is branch-free with a clamped
+  // (always valid) address and its validity applied where the value is used: a load under
+  // divergent control flow makes the compiler's wait before the first use a vmcnt(0), which
+  // would also wait for the weight prefetch issued after it.
+  const int n = n0 + row;
+  int e_ps[4] = {0, 0, 0, 0};
+  if constexpr (EP == EP_QKV) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) load(d, d);
+    for (int r = 0; r < 4; ++r) {
+      const int mm = 4 * grp + r < M ? 4 * grp + r : M - 1;
+      e_ps[r] = p.pos[(p.m0 + mm) % p.T];
+    }
   }
-  if constexpr (I8) {
+  float2 e_a = make_float2(1.f, 0.f), e_b = make_float2(1.f, 0.f);
+  if constexpr (WF == WF_W4) {
+    e_a = p.sz[n];
+    if (DUAL) e_b = p.sz2[n];
+  } else if constexpr (I8) {
+    e_a.x = reinterpret_cast<const float*>(p.sz)[n];
+    if (DUAL) e_b.x = reinterpret_cast<const float*>(p.sz2)[n];
+  }
+  const bf16_t e_braw = (p.bias ? p.bias : reinterpret_cast<const bf16_t*>(p.W))[n];
+  bf16_t e_xr[4] = {0, 0, 0, 0};
+  if constexpr (EP == EP_RESID) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int mm = 4 * grp + r < M ? 4 * grp + r : M - 1;
+      e_xr[r] = p.C[(size_t)mm * p.ldc + n];
+    }
+  }
+
+  // ---- A prologue, register form (see APre) or LDS-staged after the prefetch (rs == 0)
+  constexpr bool NORM = (AM == AM_NORM);
+  constexpr int NT = NW * 64;
+  using AP = APre<MB, NORM>;
+  const int tid = threadIdx.x;
+  const int nvec = K >> 3;
+  const int JA = (nvec + NT - 1) / NT;
+  int rs = 0;
+  if (ALDS && !I8 && (LLJ_ABL & 1) == 0 && M <= MB) {
+    const bool st_ok = !NORM || !p.nst_in || p.nst_parts <= AP::ST * (NT / AP::SM);
+    const bool g_ok = !NORM || JA <= AP::GR;
+    if (st_ok && g_ok) {
+      if (MB == 1) rs = JA <= 1 ? 1 : JA <= 2 ? 2 : JA <= 4 ? 4 : JA <= AP::XR ? AP::XR : 0;
+      else if (JA <= 2) rs = 2;
+      else if (JA <= 4 && M <= 4) rs = 4;
+    }
+  }
+  rs = uniform(rs);
+  AP ap;
+  const u32x4* g4 = reinterpret_cast<const u32x4*>(p.norm_w);
+  auto a_issue = [&](auto rsc) {
+    constexpr int RS = decltype(rsc)::value;
+    constexpr int MR = MB == 1 ? 1 : AP::XR / RS;
+    if (NORM && p.nst_in) {
+      const int m = tid % AP::SM;
+      const int mm = m < M ? m : M - 1;
+#pragma unroll
+      for (int i = 0; i < AP::ST; ++i) {
+        const int q = tid / AP::SM + (NT / AP::SM) * i;
+        ap.st[i] = p.nst_in[(q < p.nst_parts ? q : p.nst_parts - 1) * 8 + mm];
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const int v = tid + NT * j;
+        const int mm = m < M ? m : M - 1, vv = v < nvec ? v : nvec - 1;
+        ap.x[m * RS + j] = *reinterpret_cast<const u32x4*>(p.A + (size_t)mm * p.lda + 8 * vv);
+      }
+    if (NORM) {
+      constexpr int GJ = RS < AP::GR ? RS : AP::GR;
+#pragma unroll
+      for (int j = 0; j < GJ; ++j) {
+        const int v = tid + NT * j;
+        ap.g[j] = g4[v < nvec ? v : nvec - 1];
+      }
+    }
+  };
+  auto a_finish = [&](auto rsc) {
+    constexpr int RS = decltype(rsc)::value;
+    constexpr int MR = MB == 1 ? 1 : AP::XR / RS;
+    if (NORM) {
+      double* redd = reinterpret_cast<double*>(tail + 32);  // [wave][8] fp64
+      float* redf = tail + 32;                              // [wave][8] fp32
+      if (p.nst_in) {
+        double sd = 0.0;
+        const bool mok = tid % AP::SM < M;
+#pragma unroll
+        for (int i = 0; i < AP::ST; ++i) {
+          const int q = tid / AP::SM + (NT / AP::SM) * i;
+          sd += (mok && q < p.nst_parts) ? ap.st[i] : 0.0;
+        }
+#pragma unroll
+        for (int o = 32; o >= AP::SM; o >>= 1) sd += __shfl_xor(sd, o, 64);
+        if (lane < AP::SM) redd[wave * 8 + lane] = sd;
+        __syncthreads();
+        if (tid < M) {
+          double t = 0.0;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) t += redd[w * 8 + tid];
+          tail[tid] = rms_rstd((float)(t / (double)K), p.eps);
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          float ss = 0.f;
+#pragma unroll
+          for (int j = 0; j < RS; ++j) {
+            const u32x4 xv = (m < M && tid + NT * j < nvec) ? ap.x[m * RS + j] : zero4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float a = bflo(xv[i]), b = bfhi(xv[i]);
+              ss += round_bf(a * a) + round_bf(b * b);
+            }
+          }
+          ss = wave_sum(ss);
+          if (lane == 0) redf[wave * 8 + m] = ss;
+        }
+        __syncthreads();
+        if (tid < M) {
+          float sf = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) sf += redf[w * 8 + tid];
+          tail[tid] = rms_rstd(sf / (float)K, p.eps);
+        }
+      }
+      __syncthreads();
+    }
+    bf16_t* As = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      float rsum = 0.f;
+      if (m < M) {
+        const float r = NORM ? tail[m] : 1.f;
+#pragma unroll
+        for (int j = 0; j < RS; ++j) {
+          const int v = tid + NT * j;
+          if (v < nvec) {
+            u32x4 o = ap.x[m * RS + j];
+            if (NORM) {
+              const uint4 nv = norm8(__builtin_bit_cast(uint4, o), __builtin_bit_cast(uint4, ap.g[j < AP::GR ? j : 0]), r);
+              o = __builtin_bit_cast(u32x4, nv);
+            }
+            *reinterpret_cast<u32x4*>(As + (size_t)m * a_stride + 8 * v) = o;
+            if (WF == WF_W4) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) rsum += bflo(o[i]) + bfhi(o[i]);
+            }
+          }
+        }
+      }
+      if (WF == WF_W4 && m < M) {
+        rsum = wave_sum(rsum);
+        if (lane == 0) tail[96 + wave * 8 + m] = rsum;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      const int v = tid + NT * j;
+      if (v < nvec) *reinterpret_cast<u32x4*>(As + (size_t)M * a_stride + 8 * v) = zero4;
+    }
+    __syncthreads();
+  };
+  if constexpr (MB == 1) {
+    if (rs == 1) a_issue(IC<1>{});
+    else if (rs == 2) a_issue(IC<2>{});
+    else if (rs == 4) a_issue(IC<4>{});
+    else if (rs == AP::XR) a_issue(IC<AP::XR>{});
+  } else {
+    if (rs == 2) a_issue(IC<2>{});
+    else if (rs == 4) a_issue(IC<4>{});
+  }
+
+  // the weight stream starts before any A wait so its HBM latency hides the staging
+#pragma unroll
+  for (int d = 0; d < D; ++d) load(d, d);
+  LLJ_STAMP(1);
+  float2 e_cs[4];
+  if constexpr (EP == EP_QKV) {  // RoPE rows of the rows' positions (needs e_ps: waits for it only)
+    const int Cd = p.n_head * p.head_size;
+    const int dd = (n - (n0 / Cd) * Cd) % p.head_size;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      e_cs[r] = *reinterpret_cast<const float2*>(p.rope + ((size_t)e_ps[r] * (p.head_size >> 1) + (dd >> 1)) * 2);
+  }
+  if constexpr ((LLJ_ABL & 1) != 0) {  // ablation: no A prologue (garbage A)
+  } else if constexpr (I8) {
     stage_i8<NW>(p, reinterpret_cast<int8_t*>(smem), a_stride, sca);
     __syncthreads();
   } else if constexpr (ALDS) {
-    stage_a<NW, AM == AM_NORM>(p, reinterpret_cast<bf16_t*>(smem), a_stride, tail);
-    __syncthreads();
+    if (rs == 0) {
+      stage_a<NW, AM == AM_NORM>(p, reinterpret_cast<bf16_t*>(smem), a_stride, tail);
+      __syncthreads();
+      if constexpr (WF == WF_W4) {  // row sums of the staged rows (offset removal, see header)
+        const bf16_t* As = reinterpret_cast<const bf16_t*>(smem);
+        for (int m = 0; m < M; ++m) {
+          float rsum = 0.f;
+          for (int v = tid; v < nvec; v += NT) {
+            const u32x4 o = *reinterpret_cast<const u32x4*>(As + (size_t)m * a_stride + 8 * v);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rsum += bflo(o[i]) + bfhi(o[i]);
+          }
+          rsum = wave_sum(rsum);
+          if (lane == 0) tail[96 + wave * 8 + m] = rsum;
+        }
+      }
+    } else if constexpr (MB == 1) {
+      if (rs == 1) a_finish(IC<1>{});
+      else if (rs == 2) a_finish(IC<2>{});
+      else if (rs == 4) a_finish(IC<4>{});
+      else a_finish(IC<AP::XR>{});
+    } else {
+      if (rs == 2) a_finish(IC<2>{});
+      else a_finish(IC<4>{});
+    }
   }
+  LLJ_STAMP(2);
   if (nmy > 0) {
     for (int i0 = 0; i0 < nmy; i0 += D) {
 #pragma unroll
@@ -392,6 +647,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
       }
     }
   }
+  LLJ_STAMP(3);
   // ---- reduce the NW partial tiles in LDS (each wave: 64 lanes x 12 words; int8 sums stay
   // int32 — they exceed 2^24 at K = 11008, so they must not round-trip through fp32)
   constexpr int NV = 12;
@@ -436,25 +692,29 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
     }
   }
 
+  LLJ_STAMP(4);
   // ---- epilogue (wave 0): lane holds C[m = 4*grp + r][n = n0 + row]
-  const int n = n0 + row;
-  float s1 = 1.f, o1 = 0.f, s2 = 1.f, o2 = 0.f;
-  if (WF == WF_W4) {
-    float2 a = p.sz[n];
-    s1 = a.x; o1 = a.y;
-    if (DUAL) { float2 b = p.sz2[n]; s2 = b.x; o2 = b.y; }
-  } else if (I8) {
-    s1 = reinterpret_cast<const float*>(p.sz)[n];
-    if (DUAL) s2 = reinterpret_cast<const float*>(p.sz2)[n];
+  if constexpr ((LLJ_ABL & 4) != 0) {  // ablation: minimal epilogue
+    if (acc[0] == 1234.5f && row < M) p.C[n] = f2bf(acc[1] + acc2[2]);
+    return;
   }
-  const float bias = p.bias ? bf2f(p.bias[n]) : 0.f;
+  const float s1 = e_a.x, o1 = e_a.y, s2 = e_b.x, o2 = e_b.y;
+  const float bias = p.bias ? bf2f(e_braw) : 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int m = 4 * grp + r;
     float y, y2 = 0.f;
     if (WF == WF_W4) {
-      y = s1 * (acc[r] - o1 * sacc[r]);
-      if (DUAL) y2 = s2 * (acc2[r] - o2 * sacc[r]);
+      float sa = sacc[r];
+      if constexpr (ALDS) {
+        sa = 0.f;
+        if (m < M) {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) sa += tail[96 + w * 8 + m];
+        }
+      }
+      y = s1 * (acc[r] - o1 * sa);
+      if (DUAL) y2 = s2 * (acc2[r] - o2 * sa);
     } else if (WF == WF_BF16) {
       y = acc[r];
       y2 = acc2[r];
@@ -480,12 +740,11 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
         const int nc = n - region * Cd;
         const int h = nc / p.head_size, dd = nc % p.head_size;
         const int mg = p.m0 + m;
-        const int b = mg / p.T, t = mg % p.T;
-        const int ps = p.pos[t];
+        const int b = mg / p.T;
+        const int ps = e_ps[r];
         float out = v;
         if (region < 2) {
-          const float* rc = p.rope + ((size_t)ps * (p.head_size >> 1) + (dd >> 1)) * 2;
-          const float c = rc[0], s = rc[1];
+          const float c = e_cs[r].x, s = e_cs[r].y;
           out = (dd & 1) ? (v * c + partner * s) : (v * c - partner * s);
         }
         const bf16_t ob = f2bf(out);
@@ -503,7 +762,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
       float sq = 0.f;
       if (m < M) {
         bf16_t* dst = p.C + (size_t)m * p.ldc + n;
-        const float xn = round_bf(bf2f(*dst) + round_bf(y));
+        const float xn = round_bf(bf2f(e_xr[r]) + round_bf(y));
         *dst = f2bf(xn);
         sq = round_bf(xn * xn);
       }
@@ -518,6 +777,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
       store_out<EP>(p, m, n, y, y2);
     }
   }
+  LLJ_STAMP(5);
 }
 
 // ------------------------------------------------------------------------------------
@@ -537,16 +797,16 @@ static inline size_t a_image_bytes(int wf, int am, int M, int K) {
 }
 static inline size_t gemv_smem(int wf, int am, int M, int K) {
   const size_t a = a_image_bytes(wf, am, M, K), red = (size_t)kNW * 64 * 12 * 4;
-  return (a > red ? a : red) + 64 * 4;
+  return (a > red ? a : red) + 128 * 4;
 }
 
 // the LDS A image must leave room for the reduction scratch: <= 96 KiB, M <= 8 rows
 static inline bool lds_fits(int wf, int M, int K) { return M <= 8 && a_image_bytes(wf, AM_LDS, M, K) <= 96 * 1024; }
 
-template <int WF, int AM, int EP>
-static int launch(const GemvParams& p, hipStream_t s) {
+template <int WF, int AM, int EP, int MB>
+static int launch_mb(const GemvParams& p, hipStream_t s) {
   const size_t sm = gemv_smem(WF, AM, p.M, p.K);
-  auto kern = gemv_kernel<WF, AM, EP, kNW, kD>;
+  auto kern = gemv_kernel<WF, AM, EP, kNW, kD, MB>;
   static bool attr_set = false;  // per instantiation; set before any graph capture
   if (sm > 64 * 1024 && !attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -556,6 +816,13 @@ static int launch(const GemvParams& p, hipStream_t s) {
   hipLaunchKernelGGL(kern, dim3(p.N / 16), dim3(kNW * 64), sm, s, p);
   LLJ_CHECK_LAUNCH();
   return 0;
+}
+
+template <int WF, int AM, int EP>
+static int launch(const GemvParams& p, hipStream_t s) {
+  // the register-staged prologue has an M == 1 class (bs = 1 decode) and an M <= 8 class
+  if (WF != WF_I8 && AM != AM_GLOBAL && p.M == 1) return launch_mb<WF, AM, EP, 1>(p, s);
+  return launch_mb<WF, AM, EP, 8>(p, s);
 }
 
 template <int EP>
@@ -599,6 +866,11 @@ static int run(int wf, GemvParams& p, void* stream) {
 using namespace llj;
 
 extern "C" {
+#if LLJ_TRACE
+int llj_trace_copy(void* host_dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(llj::g_trace), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 // C[M,N] = A[M,K] . W^T (+bias); bf16 in/out, fp32 accumulation, M <= 16 (int8: <= 8) per call.
 int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, const void* bias, void* C,
