@@ -735,12 +735,14 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
       const float v = round_bf(y);
       const float partner = __shfl_xor(v, 1, 64);
       if (m < M) {
+        // head_size is a power of two (64 / 128, checked on the host): shifts, no divisions
         const int Cd = p.n_head * p.head_size;
-        const int region = n0 / Cd;  // 0 q, 1 k, 2 v (uniform per workgroup)
+        const int hs_sh = uniform(31 - __builtin_clz(p.head_size));
+        const int region = uniform(n0 / Cd);  // 0 q, 1 k, 2 v (uniform per workgroup)
         const int nc = n - region * Cd;
-        const int h = nc / p.head_size, dd = nc % p.head_size;
+        const int h = nc >> hs_sh, dd = nc & (p.head_size - 1);
         const int mg = p.m0 + m;
-        const int b = mg / p.T;
+        const int b = p.T == 1 ? mg : mg / p.T;
         const int ps = e_ps[r];
         float out = v;
         if (region < 2) {
@@ -751,7 +753,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
         if (region == 0) {
           p.q_out[(size_t)mg * Cd + nc] = ob;
         } else {
-          const int slot = ps % p.S;
+          const int slot = ps < p.S ? ps : ps % p.S;
           const size_t ci = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
           (region == 1 ? p.kcache : p.vcache)[ci] = ob;
         }
@@ -939,7 +941,7 @@ int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, co
   p.W = W; p.sz = (const float2*)sz; p.q_out = (bf16_t*)q_out; p.kcache = (bf16_t*)kcache;
   p.vcache = (bf16_t*)vcache; p.rope = rope; p.pos = pos; p.n_head = n_head; p.head_size = C / n_head;
   p.S = S; p.T = T; p.i8ws = i8ws;
-  if (p.head_size & 1 || rows > 8) return LLJ_EINVAL;
+  if (p.head_size < 2 || (p.head_size & (p.head_size - 1)) || rows > 8) return LLJ_EINVAL;  // power of two
   return run<EP_QKV>(wfmt, p, stream);
 }
 

@@ -65,39 +65,58 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__
 // the slots holding tokens <= p; once p >= S (sliding window after the roll) it attends
 // all S slots. Slots are a ring (token p lives at p % S): same key set as the reference's
 // roll-by-one, so the softmax is identical up to summation order.
-// 16 lanes per key (HS/16 dims each), 16 keys in flight per 256-thread block.
-template <int HS, int U>
-__global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+// 16 lanes per key (HS/16 dims each); NG = NTH/16 key groups, U keys per group per pass, so
+// one pass has NG*U keys in flight (1024 threads, U = 4: 256 keys — a decode context up to
+// 256 positions is one round of loads). Per-group online softmax, combined through LDS.
+#ifndef LLJ_ATT_NTH
+#define LLJ_ATT_NTH 512  // threads per (row, head) block
+#endif
+#ifndef LLJ_ATT_U
+#define LLJ_ATT_U 4  // keys per 16-lane group per pass
+#endif
+template <int HS, int U, int NTH>
+__global__ __launch_bounds__(NTH) void attention_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                         const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                         const int* __restrict__ pos, int T, int S, int nh,
                                                         float scale_log2) {
   constexpr int DPL = HS / 16;
-  __shared__ float s_m[16], s_l[16];
-  __shared__ float s_o[16][HS + 1];
+  constexpr int NG = NTH / 16;
+  __shared__ float s_m[NG], s_l[NG];
+  __shared__ float s_o[NG][HS + 1];
   const int h = blockIdx.x, m = blockIdx.y;
   const int b = m / T, t = m % T;
   const int ps = pos[t];
   const int nvalid = ps < S ? ps + 1 : S;
   const int sub = threadIdx.x & 15, kg = threadIdx.x >> 4;
   const int C = nh * HS;
-  float qf[DPL];
-  {
-    const bf16_t* qp = q + (size_t)m * C + h * HS + sub * DPL;
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) qf[i] = bf2f(qp[i]) * scale_log2;
-  }
   const size_t base = ((size_t)(b * nh + h) * S) * HS + sub * DPL;
   const bf16_t* kb = kc + base;
   const bf16_t* vb = vc + base;
+  float qf[DPL];
+  {
+    const bf16_t* qp = q + (size_t)m * C + h * HS + sub * DPL;
+    if constexpr (DPL == 8) {
+      const uint4 a = *reinterpret_cast<const uint4*>(qp);
+      const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        qf[2 * i] = bflo(w[i]) * scale_log2;
+        qf[2 * i + 1] = bfhi(w[i]) * scale_log2;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < DPL; ++i) qf[i] = bf2f(qp[i]) * scale_log2;
+    }
+  }
   float mx = -INFINITY, l = 0.f, o[DPL];
 #pragma unroll
   for (int i = 0; i < DPL; ++i) o[i] = 0.f;
 
-  for (int j0 = kg; j0 < nvalid; j0 += 16 * U) {
+  for (int j0 = kg; j0 < nvalid; j0 += NG * U) {
     uint32_t kw[U][DPL / 2], vw[U][DPL / 2];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = j0 + 16 * u < nvalid ? j0 + 16 * u : j0;
+    for (int u = 0; u < U; ++u) {  // every load of the pass first (clamped: always valid rows)
+      const int j = j0 + NG * u < nvalid ? j0 + NG * u : j0;
       const uint32_t* kp = reinterpret_cast<const uint32_t*>(kb + (size_t)j * HS);
       const uint32_t* vp = reinterpret_cast<const uint32_t*>(vb + (size_t)j * HS);
       if constexpr (DPL == 8) {
@@ -119,7 +138,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
       s += __shfl_xor(s, 4, 64);
       s += __shfl_xor(s, 2, 64);
       s += __shfl_xor(s, 1, 64);
-      if (j0 + 16 * u >= nvalid) continue;
+      if (j0 + NG * u >= nvalid) continue;
       const float mn = fmaxf(mx, s);
       const float corr = exp2f(mx - mn);
       const float pj = exp2f(s - mn);
@@ -136,17 +155,31 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
 #pragma unroll
   for (int i = 0; i < DPL; ++i) s_o[kg][sub * DPL + i] = o[i];
   __syncthreads();
-  if (threadIdx.x < HS) {
-    const int d = threadIdx.x;
+  // combine the NG groups: HS output dims x (NTH / HS) partial sums over the groups
+  constexpr int PARTS = NTH / HS;
+  __shared__ float s_po[PARTS][HS], s_pl[PARTS];
+  {
+    const int d = threadIdx.x % HS, part = threadIdx.x / HS;
     float M = -INFINITY;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) M = fmaxf(M, s_m[g]);
+#pragma unroll 8
+    for (int g = 0; g < NG; ++g) M = fmaxf(M, s_m[g]);
     float L = 0.f, O = 0.f;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
+    for (int g = part; g < NG; g += PARTS) {
       const float f = s_m[g] == -INFINITY ? 0.f : exp2f(s_m[g] - M);
       L += s_l[g] * f;
       O += s_o[g][d] * f;
+    }
+    s_po[part][d] = O;
+    if (d == 0) s_pl[part] = L;
+  }
+  __syncthreads();
+  if (threadIdx.x < HS) {
+    const int d = threadIdx.x;
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int pp = 0; pp < PARTS; ++pp) {
+      L += s_pl[pp];
+      O += s_po[pp][d];
     }
     y[(size_t)m * C + h * HS + d] = f2bf(O / L);
   }
@@ -163,9 +196,35 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const bf16_t* __restrict__
   const bf16_t* lr = logits + (size_t)m * ldl;
   float best = -INFINITY;
   int bi = 0x7fffffff;
-  for (int v = tid; v < V; v += 1024) {
-    const float x = bf2f(lr[v]);
-    if (x > best) { best = x; bi = v; }
+  auto take = [&](float x, int v) {
+    if (x > best || (x == best && v < bi)) { best = x; bi = v; }
+  };
+  if ((V & 7) == 0 && (ldl & 7) == 0 && (reinterpret_cast<uintptr_t>(lr) & 15) == 0) {
+    // 16-byte loads, 4 in flight per thread before any compare (V <= 32768 in one round)
+    const uint4* l4 = reinterpret_cast<const uint4*>(lr);
+    const int nv = V >> 3;
+    for (int v0 = tid; v0 < nv; v0 += 4 * 1024) {
+      uint4 r[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int v = v0 + 1024 * u;
+        r[u] = l4[v < nv ? v : v0];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int v = v0 + 1024 * u;
+        if (v < nv) {
+          const uint32_t w[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            take(bflo(w[i]), 8 * v + 2 * i);
+            take(bfhi(w[i]), 8 * v + 2 * i + 1);
+          }
+        }
+      }
+    }
+  } else {
+    for (int v = tid; v < V; v += 1024) take(bf2f(lr[v]), v);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -213,10 +272,10 @@ int llj_attention(const void* q, const void* kcache, const void* vcache, void* y
   const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
   dim3 grid(n_head, B * T);
   if (head_size == 128) {
-    hipLaunchKernelGGL((attention_kernel<128, 4>), grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)q,
+    hipLaunchKernelGGL((attention_kernel<128, LLJ_ATT_U, LLJ_ATT_NTH>), grid, dim3(LLJ_ATT_NTH), 0, (hipStream_t)stream, (const bf16_t*)q,
                        (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
   } else if (head_size == 64) {
-    hipLaunchKernelGGL((attention_kernel<64, 4>), grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)q,
+    hipLaunchKernelGGL((attention_kernel<64, LLJ_ATT_U, LLJ_ATT_NTH>), grid, dim3(LLJ_ATT_NTH), 0, (hipStream_t)stream, (const bf16_t*)q,
                        (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
   } else {
     return LLJ_EINVAL;
