@@ -89,6 +89,40 @@ int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, cons
                     void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const double* nstat_in,
                     int nstat_parts, void* stream);
 
+/* ---------------------------------------------------------------- one decode layer, one launch
+ * Block.forward (model.py:162-175) for a decode step (T = 1, M = B <= 8 rows) with int4 W4P
+ * (wfmt 0) or bf16 (wfmt 1) linears: rms_1 + c_attn + RoPE + KV write -> attention -> c_proj +
+ * residual -> rms_2 + c_fc1/c_fc2 + silu*mul -> mlp.c_proj + residual. Same math and results
+ * as the five entry points above; when the shapes allow, all five run in ONE launch whose
+ * consumer workgroups start streaming their weights before their producer op has finished
+ * (completion counters, sc1 write-through hand-offs), otherwise as separate launches.
+ * counters: 128 words the caller zeroes before every call; err: set non-zero if a
+ * dependency wait timed out (never expected; a diagnostic, results then invalid). */
+typedef struct llj_layer {
+  int wfmt, M, C, H, n_head, S;
+  void* x;                       /* (M, C) residual stream, updated in place */
+  const void* rms1;
+  const void* rms2;
+  float eps;
+  const void* w_qkv;  const void* sz_qkv;
+  const void* w_proj; const void* sz_proj;
+  const void* w_fc1;  const void* sz_fc1;
+  const void* w_fc2;  const void* sz_fc2;
+  const void* w_down; const void* sz_down;
+  void* q;                       /* (M, C) scratch */
+  void* kcache; void* vcache;    /* (M, n_head, S, C/n_head), ring slot pos % S */
+  const float* rope;
+  const int* pos;                /* device position of the decode token */
+  void* y;                       /* (M, C) attention output scratch */
+  void* h;                       /* (M, H) MLP hidden scratch */
+  const double* nst_in; int nst_in_parts;  /* RMSNorm statistics of x for rms_1 (or NULL) */
+  double* nst_mid;               /* written by c_proj, read by rms_2: C/16 parts x 8 rows */
+  double* nst_out;               /* written by mlp.c_proj for the next layer's rms_1 */
+  unsigned* counters;
+  unsigned* err;
+} llj_layer;
+int llj_decode_layer(const llj_layer* layer, void* stream);
+
 /* ---------------------------------------------------------------- LLM.int8() */
 /* Bytes of the activation-statistics workspace for an (M, K) activation (host function). */
 size_t llj_i8_ws_bytes(int M, int K);

@@ -9,6 +9,17 @@
 
 namespace llj {
 
+#ifndef LLJ_TRACE
+#define LLJ_TRACE 0  // profiling only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
+#endif
+#if LLJ_TRACE
+static __device__ unsigned long long g_trace[8192 * 6];  // per translation unit
+#define LLJ_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < 8192) g_trace[blockIdx.x * 6 + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define LLJ_STAMP(k)
+#endif
+
 typedef uint16_t bf16_t;  // raw bf16 bits in HBM
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

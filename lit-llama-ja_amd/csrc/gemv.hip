@@ -27,7 +27,12 @@
 //    per row in the prologue (absmax over non-outlier elements, outlier columns zeroed,
 //    statistics from llj_i8_stats in int8.hip), int32 MFMA accumulation, dequant by
 //    SCA*SCB/127^2, plus the fp16 side product over the outlier columns.
+#include <algorithm>
+
 #include "common.h"
+#include "chain.h"
+#include "attention.h"
+#include "lit_llama_amd.h"
 
 namespace llj {
 
@@ -75,8 +80,8 @@ struct GemvParams {
 };
 
 // ------------------------------------------------------------------------------------
-// Stage A rows [0, M) into LDS (row stride K + 8 elements); row M is all zeros (read by the
-// MFMA lanes of rows >= M). With NORM, rows are RMS-normalised with the reference's bf16
+// Stage A rows [0, M) into LDS (row stride K + 8 elements; MFMA lanes of rows >= M use zero
+// registers instead of reading LDS). With NORM, rows are RMS-normalised with the reference's bf16
 // rounding points (model.py:281-283 evaluated on bf16 tensors).
 __device__ __forceinline__ float rms_rstd(float sumsq_over_k, float eps) {
   // bf16: mean(x*x) -> +eps -> rsqrt, each rounded (torch bf16 ops, model.py:281-282)
@@ -117,8 +122,6 @@ __device__ void stage_a(const GemvParams& p, bf16_t* As, int a_stride, float* re
       uint4* dst = reinterpret_cast<uint4*>(As + (size_t)m * a_stride);
       for (int v = tid; v < nvec; v += NT) dst[v] = norm8(src[v], g4[v], r);
     }
-    uint4* z = reinterpret_cast<uint4*>(As + (size_t)M * a_stride);
-    for (int v = tid; v < nvec; v += NT) z[v] = make_uint4(0, 0, 0, 0);
     return;
   }
   float ss[8];
@@ -142,10 +145,6 @@ __device__ void stage_a(const GemvParams& p, bf16_t* As, int a_stride, float* re
         }
       }
     }
-  }
-  {
-    uint4* z = reinterpret_cast<uint4*>(As + (size_t)M * a_stride);
-    for (int v = tid; v < nvec; v += NT) z[v] = make_uint4(0, 0, 0, 0);
   }
   if (!NORM) return;
   const int lane = tid & 63, wave = tid >> 6;
@@ -175,7 +174,7 @@ __device__ void stage_a(const GemvParams& p, bf16_t* As, int a_stride, float* re
 
 // int8: quantize rows [0, M) of A into LDS int8 rows (stride K + 16 bytes) with the
 // per-row absmax SCA (non-outlier elements; from the llj_i8_stats partials) and the
-// outlier columns zeroed; row M is zeros. sca[] receives SCA per local row.
+// outlier columns zeroed. sca[] receives SCA per local row.
 template <int NW>
 __device__ void stage_i8(const GemvParams& p, int8_t* Aq, int q_stride, float* sca) {
   const int tid = threadIdx.x;
@@ -210,10 +209,6 @@ __device__ void stage_i8(const GemvParams& p, int8_t* Aq, int q_stride, float* s
       }
       dst[v] = make_uint2(o[0], o[1]);
     }
-  }
-  {
-    uint2* z = reinterpret_cast<uint2*>(Aq + (size_t)M * q_stride);
-    for (int v = tid; v < nvec; v += NT) z[v] = make_uint2(0, 0);
   }
   __syncthreads();
   // zero the outlier columns (their contribution is the fp16 side product)
@@ -257,30 +252,20 @@ __device__ float i8_side(const GemvParams& p, const int8_t* CB, float scb, int m
   return s;
 }
 
-// Shared epilogue for one output element (m local row < M, n column) of value y (and y2).
+// Output value of one element for the plain / SwiGLU epilogues (SwiGLU: model.py:258 in bf16).
 template <int EP>
-__device__ __forceinline__ void store_out(const GemvParams& p, int m, int n, float y, float y2) {
-  bf16_t* dst = p.C + (size_t)m * p.ldc + n;
-  if (EP == EP_STORE) {
-    *dst = f2bf(y);
-  } else if (EP == EP_RESID) {
-    *dst = f2bf(bf2f(*dst) + round_bf(y));  // x = x + h, both bf16 (model.py:172-173)
-  } else if (EP == EP_SWIGLU) {
+__device__ __forceinline__ float out_value(float y, float y2) {
+  if (EP == EP_SWIGLU) {
     const float a1 = round_bf(y), a2 = round_bf(y2);
     const float sl = round_bf(a1 / (1.f + __expf(-a1)));  // F.silu in bf16
-    *dst = f2bf(sl * a2);
+    return sl * a2;
   }
+  return y;
 }
 
-#ifndef LLJ_TRACE
-#define LLJ_TRACE 0  // profiling only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
-#endif
-#if LLJ_TRACE
-__device__ unsigned long long g_trace[8192 * 6];
-#define LLJ_STAMP(k) \
-  if (threadIdx.x == 0 && blockIdx.x < 8192) g_trace[blockIdx.x * 6 + (k)] = __builtin_amdgcn_s_memrealtime()
-#else
-#define LLJ_STAMP(k)
+
+#ifndef LLJ_CH_PLAIN_A
+#define LLJ_CH_PLAIN_A 0  // experiment only: chained consumers read A with plain loads
 #endif
 
 template <int V>
@@ -310,9 +295,9 @@ struct APre {
 #define LLJ_ABL 0  // ablation switches for profiling only (1 no A prologue, 2 no compute, 4 no epilogue)
 #endif
 
-template <int WF, int AM, int EP, int NW, int D, int MB>
-__global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+template <int WF, int AM, int EP, int NW, int D, int MB, bool CH>
+__device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, unsigned char* smem,
+                                          const ChainCtl& cc) {
   constexpr bool DUAL = (EP == EP_SWIGLU);
   constexpr bool I8 = (WF == WF_I8);
   constexpr bool ALDS = I8 || (AM != AM_GLOBAL);
@@ -320,14 +305,13 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   constexpr int NSTEP = I8 ? 2 : 4;
   const int lane = threadIdx.x & 63;
   const int wave = uniform(threadIdx.x >> 6);
-  const int nt = blockIdx.x;
   const int n0 = nt * 16;
   const int K = p.K, M = p.M, KC = K >> 7;
   const int row = lane & 15, grp = lane >> 4;
   // LDS carve: [A image, aliased after the main loop by the NW x 64 x 12-word reduction
   // scratch] [tail: 128 words for staging scratch / int8 SCA]
   const int a_stride = I8 ? K + 16 : K + 8;  // elements (bytes for int8)
-  const size_t a_bytes = ALDS ? (((size_t)(M + 1) * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15) : 0;
+  const size_t a_bytes = ALDS ? (((size_t)M * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15) : 0;
   constexpr size_t kRedBytes = (size_t)NW * 64 * 12 * 4;
   float* red = reinterpret_cast<float*>(smem);
   float* tail = reinterpret_cast<float*>(smem + (a_bytes > kRedBytes ? a_bytes : kRedBytes));
@@ -336,7 +320,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   const bool arow = row < M;
   const unsigned char* abase;  // byte address of this lane's A row
   if (ALDS) {
-    abase = smem + (size_t)(arow ? row : M) * a_stride * (I8 ? 1 : 2);
+    abase = smem + (size_t)(arow ? row : 0) * a_stride * (I8 ? 1 : 2);  // rows >= M read as zeros
   } else {
     abase = reinterpret_cast<const unsigned char*>(p.A + (size_t)(arow ? row : 0) * p.lda);
   }
@@ -400,7 +384,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
     }
 #pragma unroll
     for (int t = 0; t < NSTEP; ++t) {
-      const u32x4 av = ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
+      const u32x4 av = ALDS ? (arow ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : zero4)
+                            : ra[d][t];
       if constexpr (WF == WF_W4) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
         acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
@@ -425,30 +410,42 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   // would also wait for the weight prefetch issued after it.
   const int n = n0 + row;
   int e_ps[4] = {0, 0, 0, 0};
-  if constexpr (EP == EP_QKV) {
+  auto issue_pos = [&]() {
+    if constexpr (EP == EP_QKV) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int mm = 4 * grp + r < M ? 4 * grp + r : M - 1;
-      e_ps[r] = p.pos[(p.m0 + mm) % p.T];
+      for (int r = 0; r < 4; ++r) {
+        const int mm = 4 * grp + r < M ? 4 * grp + r : M - 1;
+        e_ps[r] = p.pos[(p.m0 + mm) % p.T];
+      }
     }
-  }
+  };
   float2 e_a = make_float2(1.f, 0.f), e_b = make_float2(1.f, 0.f);
-  if constexpr (WF == WF_W4) {
-    e_a = p.sz[n];
-    if (DUAL) e_b = p.sz2[n];
-  } else if constexpr (I8) {
-    e_a.x = reinterpret_cast<const float*>(p.sz)[n];
-    if (DUAL) e_b.x = reinterpret_cast<const float*>(p.sz2)[n];
-  }
-  const bf16_t e_braw = (p.bias ? p.bias : reinterpret_cast<const bf16_t*>(p.W))[n];
-  bf16_t e_xr[4] = {0, 0, 0, 0};
-  if constexpr (EP == EP_RESID) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int mm = 4 * grp + r < M ? 4 * grp + r : M - 1;
-      e_xr[r] = p.C[(size_t)mm * p.ldc + n];
+  bf16_t e_braw = 0;
+  auto issue_const = [&]() {  // weights-side epilogue operands (never written in a launch)
+    if constexpr (WF == WF_W4) {
+      e_a = p.sz[n];
+      if (DUAL) e_b = p.sz2[n];
+    } else if constexpr (I8) {
+      e_a.x = reinterpret_cast<const float*>(p.sz)[n];
+      if (DUAL) e_b.x = reinterpret_cast<const float*>(p.sz2)[n];
     }
-  }
+    e_braw = (p.bias ? p.bias : reinterpret_cast<const bf16_t*>(p.W))[n];
+  };
+  bf16_t e_xr[4] = {0, 0, 0, 0};
+  auto issue_xr = [&]() {  // residual stream values this workgroup updates
+    if constexpr (EP == EP_RESID) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mm = 4 * grp + r < M ? 4 * grp + r : M - 1;
+        if constexpr (CH) {
+          const uint32_t w = ld4_sc1(p.C, (unsigned)(((size_t)mm * p.ldc + (n & ~1)) * 2));
+          e_xr[r] = (bf16_t)((n & 1) ? (w >> 16) : (w & 0xFFFFu));
+        } else {
+          e_xr[r] = p.C[(size_t)mm * p.ldc + n];
+        }
+      }
+    }
+  };
 
   // ---- A prologue, register form (see APre) or LDS-staged after the prefetch (rs == 0)
   constexpr bool NORM = (AM == AM_NORM);
@@ -479,7 +476,9 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
 #pragma unroll
       for (int i = 0; i < AP::ST; ++i) {
         const int q = tid / AP::SM + (NT / AP::SM) * i;
-        ap.st[i] = p.nst_in[(q < p.nst_parts ? q : p.nst_parts - 1) * 8 + mm];
+        const int si = (q < p.nst_parts ? q : p.nst_parts - 1) * 8 + mm;
+        if constexpr (CH && !LLJ_CH_PLAIN_A) ap.st[i] = ld8d_sc1(p.nst_in, (unsigned)si * 8u);
+        else ap.st[i] = p.nst_in[si];
       }
     }
 #pragma unroll
@@ -488,7 +487,9 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
       for (int j = 0; j < RS; ++j) {
         const int v = tid + NT * j;
         const int mm = m < M ? m : M - 1, vv = v < nvec ? v : nvec - 1;
-        ap.x[m * RS + j] = *reinterpret_cast<const u32x4*>(p.A + (size_t)mm * p.lda + 8 * vv);
+        const size_t eo = (size_t)mm * p.lda + 8 * vv;
+        if constexpr (CH && !LLJ_CH_PLAIN_A) ap.x[m * RS + j] = ld16_sc1(p.A, (unsigned)(eo * 2));
+        else ap.x[m * RS + j] = *reinterpret_cast<const u32x4*>(p.A + eo);
       }
     if (NORM) {
       constexpr int GJ = RS < AP::GR ? RS : AP::GR;
@@ -577,26 +578,40 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
         if (lane == 0) tail[96 + wave * 8 + m] = rsum;
       }
     }
-#pragma unroll
-    for (int j = 0; j < RS; ++j) {
-      const int v = tid + NT * j;
-      if (v < nvec) *reinterpret_cast<u32x4*>(As + (size_t)M * a_stride + 8 * v) = zero4;
-    }
     __syncthreads();
   };
-  if constexpr (MB == 1) {
-    if (rs == 1) a_issue(IC<1>{});
-    else if (rs == 2) a_issue(IC<2>{});
-    else if (rs == 4) a_issue(IC<4>{});
-    else if (rs == AP::XR) a_issue(IC<AP::XR>{});
-  } else {
-    if (rs == 2) a_issue(IC<2>{});
-    else if (rs == 4) a_issue(IC<4>{});
-  }
+  auto a_issue_any = [&]() {
+    if constexpr (MB == 1) {
+      if (rs == 1) a_issue(IC<1>{});
+      else if (rs == 2) a_issue(IC<2>{});
+      else if (rs == 4) a_issue(IC<4>{});
+      else if (rs == AP::XR) a_issue(IC<AP::XR>{});
+    } else {
+      if (rs == 2) a_issue(IC<2>{});
+      else if (rs == 4) a_issue(IC<4>{});
+    }
+  };
 
-  // the weight stream starts before any A wait so its HBM latency hides the staging
+  if constexpr (!CH) {
+    // standalone launch: every input is final, so the A-side loads go first (a wait for
+    // them then never waits for the weight chunks issued after them)
+    issue_pos();
+    issue_const();
+    issue_xr();
+    a_issue_any();
 #pragma unroll
-  for (int d = 0; d < D; ++d) load(d, d);
+    for (int d = 0; d < D; ++d) load(d, d);  // the weight stream starts before any A wait
+  } else {
+    // chained: the weight stream needs no producer, so it starts first; then wait for the
+    // producer op and read its results (sc1)
+    issue_const();
+#pragma unroll
+    for (int d = 0; d < D; ++d) load(d, d);
+    chain_wait(cc);
+    issue_pos();
+    issue_xr();
+    a_issue_any();
+  }
   LLJ_STAMP(1);
   float2 e_cs[4];
   if constexpr (EP == EP_QKV) {  // RoPE rows of the rows' positions (needs e_ps: waits for it only)
@@ -749,37 +764,66 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
           const float c = e_cs[r].x, s = e_cs[r].y;
           out = (dd & 1) ? (v * c + partner * s) : (v * c - partner * s);
         }
-        const bf16_t ob = f2bf(out);
-        if (region == 0) {
-          p.q_out[(size_t)mg * Cd + nc] = ob;
-        } else {
-          const int slot = ps < p.S ? ps : ps % p.S;
-          const size_t ci = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
-          (region == 1 ? p.kcache : p.vcache)[ci] = ob;
+        const uint32_t ob = (uint32_t)f2bf(out);
+        const uint32_t pr = __shfl_xor(ob, 1, 64);  // columns (dd, dd + 1) leave as one 4-byte store
+        if (!(dd & 1)) {
+          bf16_t* dst;
+          size_t ei;
+          if (region == 0) {
+            dst = p.q_out;
+            ei = (size_t)mg * Cd + nc;
+          } else {
+            const int slot = ps < p.S ? ps : ps % p.S;
+            dst = region == 1 ? p.kcache : p.vcache;
+            ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
+          }
+          if constexpr (CH) st4_sc1(dst, (unsigned)(ei * 2), ob | (pr << 16));
+          else *reinterpret_cast<uint32_t*>(dst + ei) = ob | (pr << 16);
         }
       }
     } else if (EP == EP_RESID) {
       // x = x + h in bf16 (model.py:172-173); optionally the partial sum_k bf16(x_new^2) of
       // this workgroup's 16 columns for the next RMSNorm (part nt of nst_out)
+      const float xn = round_bf(bf2f(e_xr[r]) + round_bf(y));
+      const uint32_t xb = (uint32_t)f2bf(xn);
+      const uint32_t pr = __shfl_xor(xb, 1, 64);
       float sq = 0.f;
       if (m < M) {
-        bf16_t* dst = p.C + (size_t)m * p.ldc + n;
-        const float xn = round_bf(bf2f(e_xr[r]) + round_bf(y));
-        *dst = f2bf(xn);
         sq = round_bf(xn * xn);
+        if (!(row & 1)) {
+          const size_t ei = (size_t)m * p.ldc + n;
+          if constexpr (CH) st4_sc1(p.C, (unsigned)(ei * 2), xb | (pr << 16));
+          else *reinterpret_cast<uint32_t*>(p.C + ei) = xb | (pr << 16);
+        }
       }
       if (p.nst_out) {
         sq += __shfl_xor(sq, 8, 64);
         sq += __shfl_xor(sq, 4, 64);
         sq += __shfl_xor(sq, 2, 64);
         sq += __shfl_xor(sq, 1, 64);
-        if (row == 0 && m < M) p.nst_out[nt * 8 + m] = (double)sq;
+        if (row == 0 && m < M) {
+          if constexpr (CH) st8d_sc1(p.nst_out, (unsigned)(nt * 8 + m) * 8u, (double)sq);
+          else p.nst_out[nt * 8 + m] = (double)sq;
+        }
       }
-    } else if (m < M) {
-      store_out<EP>(p, m, n, y, y2);
+    } else {
+      const uint32_t ob = (uint32_t)f2bf(out_value<EP>(y, y2));
+      const uint32_t pr = __shfl_xor(ob, 1, 64);
+      if (m < M && !(row & 1)) {
+        const size_t ei = (size_t)m * p.ldc + n;
+        if constexpr (CH) st4_sc1(p.C, (unsigned)(ei * 2), ob | (pr << 16));
+        else *reinterpret_cast<uint32_t*>(p.C + ei) = ob | (pr << 16);
+      }
     }
   }
+  if constexpr (CH) chain_signal(cc);
   LLJ_STAMP(5);
+}
+
+template <int WF, int AM, int EP, int NW, int D, int MB>
+__global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  gemv_body<WF, AM, EP, NW, D, MB, false>(p, blockIdx.x, smem, ChainCtl{});
 }
 
 // ------------------------------------------------------------------------------------
@@ -793,9 +837,9 @@ constexpr int kNW = LLJ_NW;
 constexpr int kD = LLJ_D;
 
 static inline size_t a_image_bytes(int wf, int am, int M, int K) {
-  if (wf == WF_I8) return (((size_t)(M + 1) * (K + 16)) + 15) & ~(size_t)15;
+  if (wf == WF_I8) return (((size_t)M * (K + 16)) + 15) & ~(size_t)15;
   if (am == AM_GLOBAL) return 0;
-  return (((size_t)(M + 1) * (K + 8) * 2) + 15) & ~(size_t)15;
+  return (((size_t)M * (K + 8) * 2) + 15) & ~(size_t)15;
 }
 static inline size_t gemv_smem(int wf, int am, int M, int K) {
   const size_t a = a_image_bytes(wf, am, M, K), red = (size_t)kNW * 64 * 12 * 4;
@@ -851,6 +895,7 @@ static int check_shape(int wf, const GemvParams& p) {
   if (p.M < 1 || p.M > 16 || p.N % 16 || p.K % 128 || p.K < 128) return LLJ_EINVAL;
   if (wf != WF_W4 && wf != WF_BF16 && wf != WF_I8) return LLJ_EINVAL;
   if (wf != WF_BF16 && !p.sz) return LLJ_EINVAL;
+  if (p.C && (p.ldc & 1)) return LLJ_EINVAL;  // epilogues store column pairs as 4-byte words
   return 0;
 }
 
@@ -861,6 +906,88 @@ static int run(int wf, GemvParams& p, void* stream) {
   const int am = pick_am(wf, p);
   if (am < 0) return LLJ_EINVAL;
   return dispatch<EP>(wf, am, p, (hipStream_t)stream);
+}
+
+// ------------------------------------------------------------------------------------
+// One decode layer as ONE launch (llj_decode_layer): the grid holds, in order,
+//   [QKV 3C/16] [attention n_head*M] [c_proj C/16] [fc1/fc2 H/16] [mlp.c_proj C/16]
+// workgroups. Each op's workgroups start their weight stream, then wait for the previous
+// op's completion counter (chain.h); a workgroup only waits for lower-numbered ones, which
+// the in-order dispatch has already placed, so the chain cannot deadlock.
+struct LayerChain {
+  GemvParams qkv, cproj, fc12, down;
+  const bf16_t* q;
+  const bf16_t* kc;
+  const bf16_t* vc;
+  bf16_t* y;
+  const int* pos;
+  int S, nh;
+  float sl2;
+  int b_att, b_cproj, b_fc12, b_down, n_qkv, n_att, n_cproj, n_fc12;
+  int has_down;
+  unsigned* ctr;  // [4 ops][kCtrWords] (chain.h)
+  unsigned* err;
+};
+
+constexpr int kAttU = 8;  // attention keys per group per pass in the chained launch (256 threads)
+
+template <int WF, int MB, int HS>
+__global__ __launch_bounds__(256) void layer_chain_kernel(LayerChain c) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int bid = blockIdx.x;
+  unsigned* const k0 = c.ctr;  // counter blocks: QKV, attention, c_proj, fc1/fc2
+  unsigned* const k1 = c.ctr + kCtrWords;
+  unsigned* const k2 = c.ctr + 2 * kCtrWords;
+  unsigned* const k3 = c.ctr + 3 * kCtrWords;
+  if (bid < c.b_att) {
+    gemv_body<WF, AM_NORM, EP_QKV, kNW, kD, MB, true>(c.qkv, bid, smem,
+                                                      ChainCtl{nullptr, 0, k0, c.n_qkv, c.err, bid});
+  } else if (bid < c.b_cproj) {
+    const int local = bid - c.b_att;
+    attention_body<HS, kAttU, 256, true>(c.q, c.kc, c.vc, c.y, c.pos, 1, c.S, c.nh, c.sl2, local % c.nh, local / c.nh,
+                                         reinterpret_cast<float*>(smem),
+                                         ChainCtl{k0, c.n_qkv, k1, c.n_att, c.err, local});
+  } else if (bid < c.b_fc12) {
+    const int local = bid - c.b_cproj;
+    gemv_body<WF, AM_LDS, EP_RESID, kNW, kD, MB, true>(c.cproj, local, smem,
+                                                       ChainCtl{k1, c.n_att, k2, c.n_cproj, c.err, local});
+  } else if (!c.has_down || bid < c.b_down) {
+    const int local = bid - c.b_fc12;
+    gemv_body<WF, AM_NORM, EP_SWIGLU, kNW, kD, MB, true>(c.fc12, local, smem,
+                                                         ChainCtl{k2, c.n_cproj, c.has_down ? k3 : nullptr,
+                                                                  c.n_fc12, c.err, local});
+  } else {
+    const int local = bid - c.b_down;
+    gemv_body<WF, AM_LDS, EP_RESID, kNW, kD, MB, true>(c.down, local, smem,
+                                                       ChainCtl{k3, c.n_fc12, nullptr, 0, c.err, local});
+  }
+}
+
+// Does the register-staged prologue (the only one the chained path reads sc1) take this op?
+static bool chain_prologue_ok(int am, int M, int K, int nst_parts) {
+  const int MB = M == 1 ? 1 : 8;
+  const bool norm = am == AM_NORM;
+  const int NT = kNW * 64, JA = (K / 8 + NT - 1) / NT;
+  const int XR = MB == 1 ? (norm ? 4 : 8) : 16, GR = norm ? 4 : 1, SM = MB == 1 ? 1 : 8, ST = MB == 1 ? 2 : 8;
+  if (M > 8) return false;
+  if (norm && nst_parts > 0 && nst_parts > ST * (NT / SM)) return false;
+  if (norm && JA > GR) return false;
+  if (MB == 1) return JA <= XR;
+  return JA <= 2 || (JA <= 4 && M <= 4);
+}
+
+template <int WF, int MB, int HS>
+static int launch_chain(const LayerChain& c, size_t lds, int grid, hipStream_t s) {
+  auto kern = layer_chain_kernel<WF, MB, HS>;
+  static bool attr_set = false;
+  if (lds > 64 * 1024 && !attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, c);
+  LLJ_CHECK_LAUNCH();
+  return 0;
 }
 
 }  // namespace llj
@@ -943,6 +1070,73 @@ int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, co
   p.S = S; p.T = T; p.i8ws = i8ws;
   if (p.head_size < 2 || (p.head_size & (p.head_size - 1)) || rows > 8) return LLJ_EINVAL;  // power of two
   return run<EP_QKV>(wfmt, p, stream);
+}
+
+int llj_decode_layer(const llj_layer* L, void* stream) {
+  if (!L) return LLJ_EINVAL;
+  const int M = L->M, C = L->C, H = L->H, nh = L->n_head, wf = L->wfmt;
+  if (M < 1 || M > 8 || nh < 1 || C % nh || (wf != WF_W4 && wf != WF_BF16) || !L->counters || !L->err)
+    return LLJ_EINVAL;
+  const int hs = C / nh;
+  const int parts = C / 16;
+  const bool chain = chain_prologue_ok(AM_NORM, M, C, parts) && chain_prologue_ok(AM_LDS, M, C, 0) &&
+                     (hs == 64 || hs == 128) && (M > 1 || chain_prologue_ok(AM_LDS, M, H, 0));
+  hipStream_t st = (hipStream_t)stream;
+  if (!chain) {  // the same five ops as separate launches
+    int e;
+    if ((e = llj_norm_qkv_rope(wf, L->x, L->rms1, L->eps, L->w_qkv, L->sz_qkv, L->q, L->kcache, L->vcache, L->rope,
+                               L->pos, M, 1, C, nh, L->S, 0, M, nullptr, L->nst_in, L->nst_in_parts, stream)))
+      return e;
+    if ((e = llj_attention(L->q, L->kcache, L->vcache, L->y, L->pos, M, 1, nh, hs, L->S, stream))) return e;
+    if ((e = llj_linear_resid(wf, L->y, C, L->w_proj, L->sz_proj, L->x, C, M, C, C, nullptr, 0, L->nst_mid, stream)))
+      return e;
+    if ((e = llj_norm_swiglu(wf, L->x, L->rms2, L->eps, L->w_fc1, L->sz_fc1, L->w_fc2, L->sz_fc2, L->h, M, H, C,
+                             nullptr, 0, L->nst_mid, parts, stream)))
+      return e;
+    return llj_linear_resid(wf, L->h, H, L->w_down, L->sz_down, L->x, C, M, C, H, nullptr, 0, L->nst_out, stream);
+  }
+  LayerChain c{};
+  GemvParams& q = c.qkv;
+  q.A = (const bf16_t*)L->x; q.lda = C; q.norm_w = (const bf16_t*)L->rms1; q.eps = L->eps;
+  q.M = M; q.m0 = 0; q.N = 3 * C; q.K = C; q.W = L->w_qkv; q.sz = (const float2*)L->sz_qkv;
+  q.q_out = (bf16_t*)L->q; q.kcache = (bf16_t*)L->kcache; q.vcache = (bf16_t*)L->vcache; q.rope = L->rope;
+  q.pos = L->pos; q.n_head = nh; q.head_size = hs; q.S = L->S; q.T = 1;
+  q.nst_in = L->nst_in; q.nst_parts = L->nst_in_parts;
+  GemvParams& pr = c.cproj;
+  pr.A = (const bf16_t*)L->y; pr.lda = C; pr.M = M; pr.N = C; pr.K = C; pr.W = L->w_proj;
+  pr.sz = (const float2*)L->sz_proj; pr.C = (bf16_t*)L->x; pr.ldc = C; pr.nst_out = L->nst_mid;
+  GemvParams& f = c.fc12;
+  f.A = (const bf16_t*)L->x; f.lda = C; f.norm_w = (const bf16_t*)L->rms2; f.eps = L->eps; f.M = M; f.N = H;
+  f.K = C; f.W = L->w_fc1; f.W2 = L->w_fc2; f.sz = (const float2*)L->sz_fc1; f.sz2 = (const float2*)L->sz_fc2;
+  f.C = (bf16_t*)L->h; f.ldc = H; f.nst_in = L->nst_mid; f.nst_parts = parts;
+  GemvParams& d = c.down;
+  d.A = (const bf16_t*)L->h; d.lda = H; d.M = M; d.N = C; d.K = H; d.W = L->w_down;
+  d.sz = (const float2*)L->sz_down; d.C = (bf16_t*)L->x; d.ldc = C; d.nst_out = L->nst_out;
+  for (const GemvParams* g : {&c.qkv, &c.cproj, &c.fc12, &c.down})
+    if (check_shape(wf, *g)) return LLJ_EINVAL;
+  if (!L->nst_mid || (L->nst_in && L->nst_in_parts < 1)) return LLJ_EINVAL;
+  c.q = (const bf16_t*)L->q; c.kc = (const bf16_t*)L->kcache; c.vc = (const bf16_t*)L->vcache;
+  c.y = (bf16_t*)L->y; c.pos = L->pos; c.S = L->S; c.nh = nh; c.sl2 = 1.4426950408889634f / sqrtf((float)hs);
+  c.n_qkv = 3 * C / 16; c.n_att = nh * M; c.n_cproj = C / 16; c.n_fc12 = H / 16;
+  c.b_att = c.n_qkv; c.b_cproj = c.b_att + c.n_att; c.b_fc12 = c.b_cproj + c.n_cproj; c.b_down = c.b_fc12 + c.n_fc12;
+  c.has_down = M == 1;  // M > 1: the (M, H) A image does not fit the LDS; separate launch below
+  c.ctr = L->counters; c.err = L->err;
+  const int grid = c.b_down + (c.has_down ? C / 16 : 0);
+  size_t lds = gemv_smem(wf, AM_NORM, M, C);
+  lds = std::max(lds, gemv_smem(wf, AM_LDS, M, C));
+  if (c.has_down) lds = std::max(lds, gemv_smem(wf, AM_LDS, M, H));
+  lds = std::max(lds, (size_t)(hs == 128 ? attention_lds_floats<128, 256>() : attention_lds_floats<64, 256>()) * 4);
+  if (lds > 160 * 1024) return LLJ_EINVAL;
+  int e;
+  if (wf == WF_W4) {
+    if (M == 1) e = hs == 128 ? launch_chain<WF_W4, 1, 128>(c, lds, grid, st) : launch_chain<WF_W4, 1, 64>(c, lds, grid, st);
+    else e = hs == 128 ? launch_chain<WF_W4, 8, 128>(c, lds, grid, st) : launch_chain<WF_W4, 8, 64>(c, lds, grid, st);
+  } else {
+    if (M == 1) e = hs == 128 ? launch_chain<WF_BF16, 1, 128>(c, lds, grid, st) : launch_chain<WF_BF16, 1, 64>(c, lds, grid, st);
+    else e = hs == 128 ? launch_chain<WF_BF16, 8, 128>(c, lds, grid, st) : launch_chain<WF_BF16, 8, 64>(c, lds, grid, st);
+  }
+  if (e || c.has_down) return e;
+  return llj_linear_resid(wf, L->h, H, L->w_down, L->sz_down, L->x, C, M, C, H, nullptr, 0, L->nst_out, stream);
 }
 
 }  // extern "C"

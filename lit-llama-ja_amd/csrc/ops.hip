@@ -2,6 +2,7 @@
 // (prefill rows beyond the fused-LDS limit), causal attention over the KV cache, and the
 // greedy (top_k = 1) next-token selection.
 #include "common.h"
+#include "attention.h"
 
 namespace llj {
 
@@ -60,129 +61,21 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__
   }
 }
 
-// ---- attention for query rows m = b*T + t against cache slots of sequence b.
-// Reference semantics (model.py:101-104, 218-237): query at absolute position p attends
-// the slots holding tokens <= p; once p >= S (sliding window after the roll) it attends
-// all S slots. Slots are a ring (token p lives at p % S): same key set as the reference's
-// roll-by-one, so the softmax is identical up to summation order.
-// 16 lanes per key (HS/16 dims each); NG = NTH/16 key groups, U keys per group per pass, so
-// one pass has NG*U keys in flight (1024 threads, U = 4: 256 keys — a decode context up to
-// 256 positions is one round of loads). Per-group online softmax, combined through LDS.
+// ---- attention (attention.h): one block per (head, query row)
 #ifndef LLJ_ATT_NTH
-#define LLJ_ATT_NTH 512  // threads per (row, head) block
+#define LLJ_ATT_NTH 256  // threads per (row, head) block (= the chained layer launch, same sums)
 #endif
 #ifndef LLJ_ATT_U
-#define LLJ_ATT_U 4  // keys per 16-lane group per pass
+#define LLJ_ATT_U 8  // keys per 16-lane group per pass (= kAttU in gemv.hip)
 #endif
 template <int HS, int U, int NTH>
 __global__ __launch_bounds__(NTH) void attention_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                         const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                         const int* __restrict__ pos, int T, int S, int nh,
                                                         float scale_log2) {
-  constexpr int DPL = HS / 16;
-  constexpr int NG = NTH / 16;
-  __shared__ float s_m[NG], s_l[NG];
-  __shared__ float s_o[NG][HS + 1];
-  const int h = blockIdx.x, m = blockIdx.y;
-  const int b = m / T, t = m % T;
-  const int ps = pos[t];
-  const int nvalid = ps < S ? ps + 1 : S;
-  const int sub = threadIdx.x & 15, kg = threadIdx.x >> 4;
-  const int C = nh * HS;
-  const size_t base = ((size_t)(b * nh + h) * S) * HS + sub * DPL;
-  const bf16_t* kb = kc + base;
-  const bf16_t* vb = vc + base;
-  float qf[DPL];
-  {
-    const bf16_t* qp = q + (size_t)m * C + h * HS + sub * DPL;
-    if constexpr (DPL == 8) {
-      const uint4 a = *reinterpret_cast<const uint4*>(qp);
-      const uint32_t w[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        qf[2 * i] = bflo(w[i]) * scale_log2;
-        qf[2 * i + 1] = bfhi(w[i]) * scale_log2;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < DPL; ++i) qf[i] = bf2f(qp[i]) * scale_log2;
-    }
-  }
-  float mx = -INFINITY, l = 0.f, o[DPL];
-#pragma unroll
-  for (int i = 0; i < DPL; ++i) o[i] = 0.f;
-
-  for (int j0 = kg; j0 < nvalid; j0 += NG * U) {
-    uint32_t kw[U][DPL / 2], vw[U][DPL / 2];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {  // every load of the pass first (clamped: always valid rows)
-      const int j = j0 + NG * u < nvalid ? j0 + NG * u : j0;
-      const uint32_t* kp = reinterpret_cast<const uint32_t*>(kb + (size_t)j * HS);
-      const uint32_t* vp = reinterpret_cast<const uint32_t*>(vb + (size_t)j * HS);
-      if constexpr (DPL == 8) {
-        uint4 a = *reinterpret_cast<const uint4*>(kp), c = *reinterpret_cast<const uint4*>(vp);
-        kw[u][0] = a.x; kw[u][1] = a.y; kw[u][2] = a.z; kw[u][3] = a.w;
-        vw[u][0] = c.x; vw[u][1] = c.y; vw[u][2] = c.z; vw[u][3] = c.w;
-      } else {
-        uint2 a = *reinterpret_cast<const uint2*>(kp), c = *reinterpret_cast<const uint2*>(vp);
-        kw[u][0] = a.x; kw[u][1] = a.y;
-        vw[u][0] = c.x; vw[u][1] = c.y;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < DPL / 2; ++i) s += qf[2 * i] * bflo(kw[u][i]) + qf[2 * i + 1] * bfhi(kw[u][i]);
-      s += __shfl_xor(s, 8, 64);
-      s += __shfl_xor(s, 4, 64);
-      s += __shfl_xor(s, 2, 64);
-      s += __shfl_xor(s, 1, 64);
-      if (j0 + NG * u >= nvalid) continue;
-      const float mn = fmaxf(mx, s);
-      const float corr = exp2f(mx - mn);
-      const float pj = exp2f(s - mn);
-      l = l * corr + pj;
-#pragma unroll
-      for (int i = 0; i < DPL / 2; ++i) {
-        o[2 * i] = o[2 * i] * corr + pj * bflo(vw[u][i]);
-        o[2 * i + 1] = o[2 * i + 1] * corr + pj * bfhi(vw[u][i]);
-      }
-      mx = mn;
-    }
-  }
-  if (sub == 0) { s_m[kg] = mx; s_l[kg] = l; }
-#pragma unroll
-  for (int i = 0; i < DPL; ++i) s_o[kg][sub * DPL + i] = o[i];
-  __syncthreads();
-  // combine the NG groups: HS output dims x (NTH / HS) partial sums over the groups
-  constexpr int PARTS = NTH / HS;
-  __shared__ float s_po[PARTS][HS], s_pl[PARTS];
-  {
-    const int d = threadIdx.x % HS, part = threadIdx.x / HS;
-    float M = -INFINITY;
-#pragma unroll 8
-    for (int g = 0; g < NG; ++g) M = fmaxf(M, s_m[g]);
-    float L = 0.f, O = 0.f;
-    for (int g = part; g < NG; g += PARTS) {
-      const float f = s_m[g] == -INFINITY ? 0.f : exp2f(s_m[g] - M);
-      L += s_l[g] * f;
-      O += s_o[g][d] * f;
-    }
-    s_po[part][d] = O;
-    if (d == 0) s_pl[part] = L;
-  }
-  __syncthreads();
-  if (threadIdx.x < HS) {
-    const int d = threadIdx.x;
-    float L = 0.f, O = 0.f;
-#pragma unroll
-    for (int pp = 0; pp < PARTS; ++pp) {
-      L += s_pl[pp];
-      O += s_po[pp][d];
-    }
-    y[(size_t)m * C + h * HS + d] = f2bf(O / L);
-  }
+  __shared__ float lds[attention_lds_floats<HS, NTH>()];
+  attention_body<HS, U, NTH, false>(q, kc, vc, y, pos, T, S, nh, scale_log2, blockIdx.x, blockIdx.y, lds,
+                                    ChainCtl{});
 }
 
 // ---- greedy next token: argmax over bf16 logits (lowest index on ties). Reference

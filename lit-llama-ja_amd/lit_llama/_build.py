@@ -9,6 +9,7 @@ from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
 CSRC = PKG.parent / "csrc"
+INCLUDE = PKG.parent.parent / "include"  # the public C ABI header (llj_layer)
 OUT = PKG / "_lljamd.so"
 ARCH = os.environ.get("LLJ_OFFLOAD_ARCH", "gfx950")
 
@@ -21,7 +22,7 @@ def needs_build() -> bool:
     if not OUT.exists():
         return True
     t = OUT.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in list(CSRC.glob("*")))
+    return any(p.stat().st_mtime > t for p in list(CSRC.glob("*")) + [INCLUDE / "lit_llama_amd.h"])
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
@@ -30,7 +31,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = OUT.with_suffix(".so.tmp")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall",
-           "-Wno-unused-variable", "-Wno-unused-function", "-munsafe-fp-atomics", "-o", str(tmp)] + [str(s) for s in sources()]
+           "-Wno-unused-variable", "-Wno-unused-function", "-munsafe-fp-atomics", f"-I{INCLUDE}", "-o", str(tmp)] + [str(s) for s in sources()]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

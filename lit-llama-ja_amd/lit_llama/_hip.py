@@ -17,6 +17,17 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
 
+
+class LlLayer(ctypes.Structure):
+    """`llj_layer` of include/lit_llama_amd.h (one decode layer, llj_decode_layer)."""
+    _fields_ = [(n, _I) for n in ("wfmt", "M", "C", "H", "n_head", "S")] + [
+        ("x", _P), ("rms1", _P), ("rms2", _P), ("eps", _F),
+        ("w_qkv", _P), ("sz_qkv", _P), ("w_proj", _P), ("sz_proj", _P), ("w_fc1", _P), ("sz_fc1", _P),
+        ("w_fc2", _P), ("sz_fc2", _P), ("w_down", _P), ("sz_down", _P),
+        ("q", _P), ("kcache", _P), ("vcache", _P), ("rope", _P), ("pos", _P), ("y", _P), ("h", _P),
+        ("nst_in", _P), ("nst_in_parts", _I), ("nst_mid", _P), ("nst_out", _P), ("counters", _P), ("err", _P)]
+
+
 # name -> argtypes (every function returns int: 0 ok, hipError_t, or 1000 = EINVAL)
 SIGNATURES = {
     "llj_w4_repack": [_P, _P, _I, _I, _P],
@@ -33,6 +44,7 @@ SIGNATURES = {
     "llj_embedding": [_P, _P, _P, _I, _I, _P, _P, _P],
     "llj_rmsnorm": [_P, _P, _F, _P, _I, _I, _P],
     "llj_argmax": [_P, _I, _I, _I, _P, _P, _I, _P, _P],
+    "llj_decode_layer": [_P, _P],
 }
 
 _lib = None

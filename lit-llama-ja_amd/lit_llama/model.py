@@ -22,6 +22,8 @@ there is no CPU path.
 """
 from __future__ import annotations
 
+import ctypes
+
 import math
 import types
 from dataclasses import dataclass
@@ -74,6 +76,11 @@ llama_configs = {
 QKV_ROWS = 8    # fused-norm kernels stage <= 8 rows in LDS
 LIN_ROWS = 16   # plain linear kernels take <= 16 rows per launch
 I8_ROWS = 8     # int8 kernels quantize <= 8 rows in LDS
+# decode steps (T = 1) can run each layer as ONE chained launch (llj_decode_layer) instead of
+# five. Same results (tests compare them bitwise), but measured 3x SLOWER at 7B: the sc1
+# write-through stores each producer must drain before signalling take 6-10 us to be
+# acknowledged while the weight stream saturates the fabric. Off by default.
+CHAIN_LAYERS = False
 
 
 def _wspec(lin: nn.Module):
@@ -121,6 +128,10 @@ class _Work:
                         torch.zeros(parts * 8, dtype=torch.float64, device=device))
         else:
             self.nst = None
+        # llj_decode_layer (one launch per decode layer): 128 completion-counter words per layer,
+        # zeroed once per step, and a timeout flag
+        self.ctr = torch.zeros(cfg.n_layer * 128, dtype=torch.int32, device=device)
+        self.err = torch.zeros(4, dtype=torch.int32, device=device)
 
     def nst_ptr(self, which: int):
         return None if self.nst is None else self.nst[which].data_ptr()
@@ -256,9 +267,22 @@ class LLaMA(nn.Module):
         M = B * T
         rope = self.rope_cache
         P = _hip.ptr
+        chained = T == 1 and M <= QKV_ROWS and w.nst is not None and CHAIN_LAYERS
+        if chained:
+            w.ctr.zero_()
         for i, blk in enumerate(self.transformer.h):
             (fa, wa, sa), (fp, wp, sp), (f1, w1, s1), (f2, w2, s2), (fd, wd, sd) = specs["layers"][i]
             kc, vc = kv[i]
+            if chained and fa == fp == f1 == f2 == fd and fa in (0, 1):
+                # the five ops of this layer in one launch (include/lit_llama_amd.h llj_decode_layer)
+                L = _hip.LlLayer(fa, M, C, H, nh, S, w.x.data_ptr(), blk.rms_1.scale.data_ptr(),
+                                 blk.rms_2.scale.data_ptr(), blk.rms_1.eps, wa.data_ptr(), P(sa), wp.data_ptr(),
+                                 P(sp), w1.data_ptr(), P(s1), w2.data_ptr(), P(s2), wd.data_ptr(), P(sd),
+                                 w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(),
+                                 w.y.data_ptr(), w.h.data_ptr(), w.nst_ptr(0), 1 if i == 0 else C // 16,
+                                 w.nst_ptr(1), w.nst_ptr(0), w.ctr[128 * i].data_ptr(), w.err.data_ptr())
+                _hip.call("llj_decode_layer", ctypes.addressof(L), st)
+                continue
             # 1. rms_1 + c_attn + rope + kv write
             if fa == 2:
                 _hip.call("llj_rmsnorm", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps, w.xn.data_ptr(),

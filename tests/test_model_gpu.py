@@ -252,3 +252,55 @@ def test_bf16_vs_int4_module_forward_paths(golden):
     x = torch.from_numpy(bf16(g["b4_x8"])).cuda().to(torch.bfloat16)
     y = qlinear_4bit_weight(x, qw, sc, zr).float().cpu().numpy()
     np.testing.assert_allclose(y, g["b4_ytriton8"] if "b4_ytriton8" in g else g["b4_y8"], rtol=3e-2, atol=3e-2)
+
+
+def _random_int4_model(n_embd, n_head, n_layer=2, vocab=2048, seed=0, mode="gptq.int4"):
+    """Random-weight model of the given shape (bench.py's synthetic init)."""
+    from lit_llama import LLaMA, LLaMAConfig
+    from lit_llama.utils import EmptyInitOnDevice
+
+    dev = torch.device("cuda")
+    with EmptyInitOnDevice(device=dev, dtype=torch.bfloat16, quantization_mode=mode):
+        m = LLaMA(LLaMAConfig(block_size=128, vocab_size=vocab, n_layer=n_layer, n_head=n_head, n_embd=n_embd))
+    g = torch.Generator(device=dev).manual_seed(seed)
+    with torch.no_grad():
+        for mod in m.modules():
+            if hasattr(mod, "quant_weight"):
+                mod.quant_weight.copy_(torch.randint(0, 256, mod.quant_weight.shape, device=dev, dtype=torch.uint8,
+                                                     generator=g))
+                mod.scales.copy_((torch.rand(mod.scales.shape, device=dev, generator=g) + 0.5) * (0.5 / 7))
+                mod.zeros.copy_(torch.randint(6, 10, mod.zeros.shape, device=dev, generator=g).to(mod.zeros.dtype))
+            elif isinstance(mod, torch.nn.Linear):
+                mod.weight.normal_(0.0, 1.0 / mod.in_features ** 0.5, generator=g)
+            elif isinstance(mod, torch.nn.Embedding):
+                mod.weight.normal_(0.0, 1.0, generator=g)
+        for blk in m.transformer.h:
+            blk.rms_1.scale.uniform_(0.5, 1.5, generator=g)
+            blk.rms_2.scale.uniform_(0.5, 1.5, generator=g)
+    return m.eval()
+
+
+@pytest.mark.parametrize("mode", ["gptq.int4", None])
+@pytest.mark.parametrize("n_embd,n_head,B", [(256, 4, 1), (256, 4, 3), (1024, 8, 1), (1024, 8, 5)])
+def test_chained_layer_equals_five_launches(mode, n_embd, n_head, B):
+    """llj_decode_layer (one launch per layer, consumer workgroups overlapping their producers)
+    computes exactly what the five separate launches compute: tokens and logits bitwise."""
+    from lit_llama import model as MD
+    from lit_llama.engine import DecodeSession
+
+    m = _random_int4_model(n_embd, n_head, mode=mode, seed=n_embd + B)
+    prompt = torch.randint(3, 2048, (B, 6), generator=torch.Generator().manual_seed(B)).cuda()
+    outs = []
+    try:
+        for chain in (False, True):
+            MD.CHAIN_LAYERS = chain
+            s = DecodeSession(m, B, 64, 40)
+            s.prefill(prompt)
+            s.decode(24)
+            torch.cuda.synchronize()
+            assert int(s.work.err.sum()) == 0, "a chained dependency wait timed out"
+            outs.append((s.output().cpu().numpy(), s.logits.float().cpu().numpy()))
+    finally:
+        MD.CHAIN_LAYERS = False
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
