@@ -46,7 +46,7 @@ int llj_w4_scale_zero(const void* scales, const void* zeros, int dtype, void* sz
  * ColBlockQuantizedLinear.forward (quantization.py:411-421), bnb Linear8bitLt.forward
  * (used by quantization.py:36-75) and, for wfmt 1, F.linear. */
 int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, const void* bias, void* C, int ldc,
-               int M, int N, int K, const void* i8ws, int i8_row0, void* stream);
+               int M, int N, int K, const void* i8ws, int i8_row0, const float* rowsum, void* stream);
 
 /* ---------------------------------------------------------------- fused decode-layer ops
  * (Block.forward, lit_llama/model.py:162-175, split at its four Linear boundaries).
@@ -56,7 +56,10 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
  * bf16(x^2) laid out [part][8 rows]. llj_embedding writes part 0 (whole rows);
  * llj_linear_resid writes part n/16 for its 16-column tile n (N/16 parts); the norm-fused
  * ops read `nstat_parts` parts (1 after the embedding, n_embd/16 after a residual GEMV)
- * instead of re-reducing the row in every workgroup. NULL = off (row reduced in-kernel). */
+ * instead of re-reducing the row in every workgroup. NULL = off (row reduced in-kernel).
+ * rowsum (int4 only, optional): fp32 sum over k of each row of A exactly as the MFMA reads it
+ * (i.e. after the RMSNorm when norm_w is given), from llj_rmsnorm_rows; used for the int4
+ * offset term instead of a per-workgroup reduction. NULL = reduced in-kernel. */
 
 /* rms_1 + attn.c_attn + split q/k/v + apply_rope(q, k) + KV-cache write
  * (model.py:171, 204-228, 312-329). x (B*T, C) rows m = b*T + t; q_out (B*T, C);
@@ -67,7 +70,7 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
 int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                       void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
                       int C, int n_head, int S, int row0, int rows, const void* i8ws, const double* nstat_in,
-                      int nstat_parts, void* stream);
+                      int nstat_parts, const float* rowsum, void* stream);
 
 /* Causal attention of q (B*T, C) over the cache slots each query may see
  * (F.scaled_dot_product_attention with the tril mask rows, model.py:101-104, 237):
@@ -82,12 +85,12 @@ int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void
 /* h[M, H] = silu(rms_2(x) . W1^T) * (rms_2(x) . W2^T)  (model.py:173, 258). M <= 8. */
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,
-                    const double* nstat_in, int nstat_parts, void* stream);
+                    const double* nstat_in, int nstat_parts, const float* rowsum, void* stream);
 
 /* out[M, N] = RMSNorm(x) . W^T  (ln_f + lm_head, model.py:125-127). M <= 8. */
 int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                     void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const double* nstat_in,
-                    int nstat_parts, void* stream);
+                    int nstat_parts, const float* rowsum, void* stream);
 
 /* ---------------------------------------------------------------- one decode layer, one launch
  * Block.forward (model.py:162-175) for a decode step (T = 1, M = B <= 8 rows) with int4 W4P
@@ -142,6 +145,9 @@ int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int*
 
 /* Standalone RMSNorm (model.py:276-283) for rows the fused prologue does not take. */
 int llj_rmsnorm(const void* x, const void* w, float eps, void* y, int M, int C, void* stream);
+/* The same, plus rowsum[m] = fp32 sum of the normalized bf16 row (the int4 GEMVs' offset
+ * term): batched rows (M >= 2) are normalized once here instead of in every GEMV workgroup. */
+int llj_rmsnorm_rows(const void* x, const void* w, float eps, void* y, float* rowsum, int M, int C, void* stream);
 
 /* Greedy next token (generate.py:66-74 with top_k = 1): out_idx[m] = argmax logits[m, :V]
  * (lowest index on ties). If tokens_out != NULL also tokens_out[m*tok_stride + *pos + 1]. */

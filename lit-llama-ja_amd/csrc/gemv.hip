@@ -77,6 +77,9 @@ struct GemvParams {
   const double* nst_in;
   int nst_parts;
   double* nst_out;
+  // int4: sum_k A[m,k] of this call's rows as the MFMA sees them (pre-normalized rows,
+  // llj_rmsnorm_rows); nullptr = computed in the prologue
+  const float* rowsum;
 };
 
 // ------------------------------------------------------------------------------------
@@ -390,7 +393,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
         acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
         if (DUAL) acc2 = mfma_bf16(a, dequant_w4(r2[d][0][t], msk, mag), acc2);
-        if constexpr (!ALDS) sacc = mfma_bf16(a, ones, sacc);  // LDS paths: row sums from the prologue
+        if (!ALDS && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);  // else: row sums from the prologue / caller
       } else if constexpr (WF == WF_BF16) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
         acc = mfma_bf16(a, __builtin_bit_cast(bf16x8, r1[d][t]), acc);
@@ -566,14 +569,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
               o = __builtin_bit_cast(u32x4, nv);
             }
             *reinterpret_cast<u32x4*>(As + (size_t)m * a_stride + 8 * v) = o;
-            if (WF == WF_W4) {
+            if (WF == WF_W4 && !p.rowsum) {
 #pragma unroll
               for (int i = 0; i < 4; ++i) rsum += bflo(o[i]) + bfhi(o[i]);
             }
           }
         }
       }
-      if (WF == WF_W4 && m < M) {
+      if (WF == WF_W4 && m < M && !p.rowsum) {
         rsum = wave_sum(rsum);
         if (lane == 0) tail[96 + wave * 8 + m] = rsum;
       }
@@ -629,7 +632,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     if (rs == 0) {
       stage_a<NW, AM == AM_NORM>(p, reinterpret_cast<bf16_t*>(smem), a_stride, tail);
       __syncthreads();
-      if constexpr (WF == WF_W4) {  // row sums of the staged rows (offset removal, see header)
+      if (WF == WF_W4 && !p.rowsum) {  // row sums of the staged rows (offset removal, see header)
         const bf16_t* As = reinterpret_cast<const bf16_t*>(smem);
         for (int m = 0; m < M; ++m) {
           float rsum = 0.f;
@@ -721,7 +724,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     float y, y2 = 0.f;
     if (WF == WF_W4) {
       float sa = sacc[r];
-      if constexpr (ALDS) {
+      if (p.rowsum) {
+        sa = m < M ? p.rowsum[m] : 0.f;
+      } else if constexpr (ALDS) {
         sa = 0.f;
         if (m < M) {
 #pragma unroll
@@ -1003,8 +1008,9 @@ int llj_trace_copy(void* host_dst, size_t bytes) {
 
 // C[M,N] = A[M,K] . W^T (+bias); bf16 in/out, fp32 accumulation, M <= 16 (int8: <= 8) per call.
 int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, const void* bias, void* C,
-               int ldc, int M, int N, int K, const void* i8ws, int i8_row0, void* stream) {
+               int ldc, int M, int N, int K, const void* i8ws, int i8_row0, const float* rowsum, void* stream) {
   GemvParams p{};
+  p.rowsum = rowsum;
   p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K;
   p.W = W; p.sz = (const float2*)sz; p.bias = (const bf16_t*)bias; p.C = (bf16_t*)C; p.ldc = ldc;
   p.i8ws = i8ws; p.m0 = i8_row0;
@@ -1014,8 +1020,9 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
 // out[M,N] = RMSNorm(x)[M,K] . W^T  (ln_f + lm_head, model.py:125-127); norm_w NULL = no norm.
 int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                     void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const double* nstat_in,
-                    int nstat_parts, void* stream) {
+                    int nstat_parts, const float* rowsum, void* stream) {
   GemvParams p{};
+  p.rowsum = rowsum;
   if (nstat_in && (M > 8 || nstat_parts < 1)) return LLJ_EINVAL;
   p.nst_in = nstat_in;
   p.nst_parts = nstat_parts;
@@ -1040,8 +1047,9 @@ int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void
 // h[M,H] = silu(RMSNorm(x) . W1^T) * (RMSNorm(x) . W2^T)  (rms_2 + model.py:258).
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,
-                    const double* nstat_in, int nstat_parts, void* stream) {
+                    const double* nstat_in, int nstat_parts, const float* rowsum, void* stream) {
   GemvParams p{};
+  p.rowsum = rowsum;
   if (nstat_in && (M > 8 || nstat_parts < 1)) return LLJ_EINVAL;
   p.nst_in = nstat_in;
   p.nst_parts = nstat_parts;
@@ -1057,8 +1065,9 @@ int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, cons
 int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                       void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
                       int C, int n_head, int S, int row0, int rows, const void* i8ws, const double* nstat_in,
-                      int nstat_parts, void* stream) {
+                      int nstat_parts, const float* rowsum, void* stream) {
   GemvParams p{};
+  p.rowsum = rowsum ? rowsum + row0 : nullptr;
   if (nstat_in && (row0 + rows > 8 || nstat_parts < 1)) return LLJ_EINVAL;
   p.nst_in = nstat_in ? nstat_in + row0 : nullptr;
   p.nst_parts = nstat_parts;
@@ -1085,13 +1094,13 @@ int llj_decode_layer(const llj_layer* L, void* stream) {
   if (!chain) {  // the same five ops as separate launches
     int e;
     if ((e = llj_norm_qkv_rope(wf, L->x, L->rms1, L->eps, L->w_qkv, L->sz_qkv, L->q, L->kcache, L->vcache, L->rope,
-                               L->pos, M, 1, C, nh, L->S, 0, M, nullptr, L->nst_in, L->nst_in_parts, stream)))
+                               L->pos, M, 1, C, nh, L->S, 0, M, nullptr, L->nst_in, L->nst_in_parts, nullptr, stream)))
       return e;
     if ((e = llj_attention(L->q, L->kcache, L->vcache, L->y, L->pos, M, 1, nh, hs, L->S, stream))) return e;
     if ((e = llj_linear_resid(wf, L->y, C, L->w_proj, L->sz_proj, L->x, C, M, C, C, nullptr, 0, L->nst_mid, stream)))
       return e;
     if ((e = llj_norm_swiglu(wf, L->x, L->rms2, L->eps, L->w_fc1, L->sz_fc1, L->w_fc2, L->sz_fc2, L->h, M, H, C,
-                             nullptr, 0, L->nst_mid, parts, stream)))
+                             nullptr, 0, L->nst_mid, parts, nullptr, stream)))
       return e;
     return llj_linear_resid(wf, L->h, H, L->w_down, L->sz_down, L->x, C, M, C, H, nullptr, 0, L->nst_out, stream);
   }

@@ -3,6 +3,7 @@
 // greedy (top_k = 1) next-token selection.
 #include "common.h"
 #include "attention.h"
+#include "lit_llama_amd.h"
 
 namespace llj {
 
@@ -32,7 +33,8 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ 
 
 // ---- RMSNorm with the bf16 rounding points of model.py:281-283 on bf16 tensors.
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-                                                      float eps, bf16_t* __restrict__ y, int C) {
+                                                      float eps, bf16_t* __restrict__ y, int C,
+                                                      float* __restrict__ rowsum) {
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x;
   const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)m * C);
@@ -51,13 +53,23 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__
   __syncthreads();
   const float tot = red[0] + red[1] + red[2] + red[3];
   const float r = round_bf(rsqrtf(round_bf(round_bf(tot / (float)C) + eps)));
+  float rsum = 0.f;
   for (int v = tid; v < nvec; v += 256) {
     uint4 a = xr[v], g = g4[v];
     uint32_t aw[4] = {a.x, a.y, a.z, a.w}, gw[4] = {g.x, g.y, g.z, g.w}, o[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
       o[i] = pack2bf(round_bf(bflo(gw[i]) * round_bf(bflo(aw[i]) * r)), round_bf(bfhi(gw[i]) * round_bf(bfhi(aw[i]) * r)));
+      rsum += bflo(o[i]) + bfhi(o[i]);
+    }
     yr[v] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  if (rowsum) {  // sum of the normalized bf16 row: the int4 GEMV's offset term (gemv.hip header)
+    __syncthreads();
+    rsum = wave_sum(rsum);
+    if ((tid & 63) == 0) red[tid >> 6] = rsum;
+    __syncthreads();
+    if (tid == 0) rowsum[m] = red[0] + red[1] + red[2] + red[3];
   }
 }
 
@@ -152,9 +164,13 @@ int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int*
 }
 
 int llj_rmsnorm(const void* x, const void* w, float eps, void* y, int M, int C, void* stream) {
+  return llj_rmsnorm_rows(x, w, eps, y, nullptr, M, C, stream);
+}
+
+int llj_rmsnorm_rows(const void* x, const void* w, float eps, void* y, float* rowsum, int M, int C, void* stream) {
   LLJ_REQUIRE(M > 0 && C % 8 == 0);
   hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                     (const bf16_t*)w, eps, (bf16_t*)y, C);
+                     (const bf16_t*)w, eps, (bf16_t*)y, C, rowsum);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

@@ -33,16 +33,17 @@ SIGNATURES = {
     "llj_w4_repack": [_P, _P, _I, _I, _P],
     "llj_w4_unpack": [_P, _P, _I, _I, _P],
     "llj_w4_scale_zero": [_P, _P, _I, _P, _I, _P],
-    "llj_linear": [_I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P],
-    "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P],
+    "llj_linear": [_I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
+    "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P],
     "llj_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_linear_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
-    "llj_norm_swiglu": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _I, _P],
-    "llj_norm_linear": [_I, _P, _P, _F, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _I, _P],
+    "llj_norm_swiglu": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P],
+    "llj_norm_linear": [_I, _P, _P, _F, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P],
     "llj_i8_stats": [_P, _I, _I, _I, _F, _P, _P],
     "llj_i8_quant_weight": [_P, _I, _P, _P, _I, _I, _P],
     "llj_embedding": [_P, _P, _P, _I, _I, _P, _P, _P],
     "llj_rmsnorm": [_P, _P, _F, _P, _I, _I, _P],
+    "llj_rmsnorm_rows": [_P, _P, _F, _P, _P, _I, _I, _P],
     "llj_argmax": [_P, _I, _I, _I, _P, _P, _I, _P, _P],
     "llj_decode_layer": [_P, _P],
 }

@@ -115,14 +115,18 @@ class _Work:
         self.q = torch.empty(M, C, dtype=bf, device=device)
         self.y = torch.empty(M, C, dtype=bf, device=device)
         self.h = torch.empty(M, H, dtype=bf, device=device)
-        self.xn = torch.empty(M, C, dtype=bf, device=device) if need_i8 else None
+        # batched rows (M >= 2): each RMSNorm runs once (llj_rmsnorm_rows -> xn, rs = fp32 row
+        # sums for the int4 offset term) instead of inside every norm-fused GEMV workgroup
+        self.pre = M >= 2 and not need_i8
+        self.xn = torch.empty(M, C, dtype=bf, device=device) if (need_i8 or self.pre) else None
+        self.rs = torch.empty(M, dtype=torch.float32, device=device) if self.pre else None
         if need_i8:
             L = _hip.lib()
             nb = max(L.llj_i8_ws_bytes(M, C), L.llj_i8_ws_bytes(M, H))
             self.i8ws = torch.empty(nb, dtype=torch.uint8, device=device)
         else:
             self.i8ws = None
-        if M <= QKV_ROWS and not need_i8:
+        if M == 1 and not need_i8:
             parts = max(1, C // 16)
             self.nst = (torch.zeros(parts * 8, dtype=torch.float64, device=device),
                         torch.zeros(parts * 8, dtype=torch.float64, device=device))
@@ -284,10 +288,16 @@ class LLaMA(nn.Module):
                 _hip.call("llj_decode_layer", ctypes.addressof(L), st)
                 continue
             # 1. rms_1 + c_attn + rope + kv write
+            rs = None
             if fa == 2:
                 _hip.call("llj_rmsnorm", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps, w.xn.data_ptr(),
                           M, C, st)
                 self._i8_prep(w.xn, M, C, w, st)
+                src, nw = w.xn, None
+            elif w.pre:
+                rs = w.rs if fa == 0 else None
+                _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
+                          w.xn.data_ptr(), P(rs), M, C, st)
                 src, nw = w.xn, None
             else:
                 src, nw = w.x, blk.rms_1.scale.data_ptr()
@@ -295,7 +305,7 @@ class LLaMA(nn.Module):
                 r = min(QKV_ROWS, M - r0)
                 _hip.call("llj_norm_qkv_rope", fa, src.data_ptr(), nw, blk.rms_1.eps, wa.data_ptr(), P(sa),
                           w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), B, T, C, nh,
-                          S, r0, r, P(w.i8ws), w.nst_ptr(0), 1 if i == 0 else C // 16, st)
+                          S, r0, r, P(w.i8ws), w.nst_ptr(0), 1 if i == 0 else C // 16, P(rs), st)
             # 2. attention
             _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(), pos.data_ptr(),
                       B, T, nh, C // nh, S, st)
@@ -304,18 +314,24 @@ class LLaMA(nn.Module):
             # 4. rms_2 + fc1/fc2 + silu*mul
             if f1 != f2:
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")
+            rs = None
             if f1 == 2:
                 _hip.call("llj_rmsnorm", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(),
                           M, C, st)
                 self._i8_prep(w.xn, M, C, w, st)
                 src, nw, step = w.xn, None, I8_ROWS
+            elif w.pre:
+                rs = w.rs if f1 == 0 else None
+                _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
+                          w.xn.data_ptr(), P(rs), M, C, st)
+                src, nw, step = w.xn, None, QKV_ROWS
             else:
                 src, nw, step = w.x, blk.rms_2.scale.data_ptr(), QKV_ROWS
             for r0 in range(0, M, step):
                 r = min(step, M - r0)
                 _hip.call("llj_norm_swiglu", f1, src[r0].data_ptr(), nw, blk.rms_2.eps, w1.data_ptr(), P(s1),
                           w2.data_ptr(), P(s2), w.h[r0].data_ptr(), r, H, C, P(w.i8ws), r0, w.nst_ptr(1),
-                          C // 16, st)
+                          C // 16, None if rs is None else rs[r0].data_ptr(), st)
             # 5. mlp.c_proj + residual (+ next rms_1 / ln_f row statistics)
             self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st, w.nst_ptr(0))
 
@@ -334,11 +350,18 @@ class LLaMA(nn.Module):
         C, V = cfg.n_embd, cfg.padded_vocab_size
         f, W, sz = specs["head"]
         ln = self.transformer.ln_f
+        rs = None
         if f == 2:
             xn = torch.empty_like(x)
             _hip.call("llj_rmsnorm", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), M, C, st)
             self._i8_prep(xn, M, C, w, st)
             src, nw = xn, None
+        elif M >= 2:  # batched rows: normalize once (see _Work.pre)
+            xn = torch.empty_like(x)
+            rs = torch.empty(M, dtype=torch.float32, device=x.device) if f == 0 else None
+            _hip.call("llj_rmsnorm_rows", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), _hip.ptr(rs), M,
+                      C, st)
+            src, nw, use_nst = xn, None, False
         else:
             src, nw = x, ln.scale.data_ptr()
         for r0 in range(0, M, QKV_ROWS):
@@ -346,7 +369,8 @@ class LLaMA(nn.Module):
             nin = w.nst_ptr(0) if use_nst else None
             parts = 1 if cfg.n_layer == 0 else C // 16
             _hip.call("llj_norm_linear", f, src[r0].data_ptr(), nw, ln.eps, W.data_ptr(), _hip.ptr(sz),
-                      out[r0].data_ptr(), out.stride(0), r, V, C, _hip.ptr(w.i8ws), r0, nin, parts, st)
+                      out[r0].data_ptr(), out.stride(0), r, V, C, _hip.ptr(w.i8ws), r0, nin, parts,
+                      None if rs is None else rs[r0].data_ptr(), st)
 
 
 Linear8bitLtThreshold = 6.0  # reference quantization.py:45
@@ -461,7 +485,7 @@ class MLP(nn.Module):
         for r0 in range(0, M, step):
             r = min(step, M - r0)
             _hip.call("llj_norm_swiglu", f1, x2[r0].data_ptr(), None, 0.0, w1.data_ptr(), _hip.ptr(s1), w2.data_ptr(),
-                      _hip.ptr(s2), h[r0].data_ptr(), r, H, K, _hip.ptr(ws), r0, None, 0, st)
+                      _hip.ptr(s2), h[r0].data_ptr(), r, H, K, _hip.ptr(ws), r0, None, 0, None, st)
         out = torch.empty(M, self.c_proj.out_features, dtype=torch.bfloat16, device=x.device)
         if fd == 2:
             _hip.call("llj_i8_stats", h.data_ptr(), H, M, H, Linear8bitLtThreshold, ws.data_ptr(), st)
@@ -469,7 +493,7 @@ class MLP(nn.Module):
         for r0 in range(0, M, step):
             r = min(step, M - r0)
             _hip.call("llj_linear", fd, h[r0].data_ptr(), H, wd.data_ptr(), _hip.ptr(sd), None, out[r0].data_ptr(),
-                      out.stride(0), r, out.shape[1], H, _hip.ptr(ws), r0, st)
+                      out.stride(0), r, out.shape[1], H, _hip.ptr(ws), r0, None, st)
         return out.view(*x.shape[:-1], out.shape[1])
 
 

@@ -30,7 +30,7 @@ def _linear_rows(wfmt: int, x2: torch.Tensor, W: torch.Tensor, sz, bias, out2: t
     for r0 in range(0, M, ROWS_PER_CALL):
         r = min(ROWS_PER_CALL, M - r0)
         _hip.call("llj_linear", wfmt, x2[r0].data_ptr(), x2.stride(0), W.data_ptr(), _hip.ptr(sz), _hip.ptr(bias),
-                  out2[r0].data_ptr(), out2.stride(0), r, N, K, None, 0, s)
+                  out2[r0].data_ptr(), out2.stride(0), r, N, K, None, 0, None, s)
 
 
 def _as_rows(inp: torch.Tensor, K: int) -> torch.Tensor:
@@ -171,7 +171,7 @@ def int8_linear(x: torch.Tensor, CB: torch.Tensor, SCB: torch.Tensor, bias, thre
     for r0 in range(0, M, 8):
         r = min(8, M - r0)
         _hip.call("llj_linear", 2, x2[r0].data_ptr(), x2.stride(0), CB.data_ptr(), SCB.data_ptr(), _hip.ptr(bias),
-                  out[r0].data_ptr(), out.stride(0), r, N, K, ws.data_ptr(), r0, s)
+                  out[r0].data_ptr(), out.stride(0), r, N, K, ws.data_ptr(), r0, None, s)
     return out.reshape(*x.shape[:-1], N)
 
 

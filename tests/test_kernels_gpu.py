@@ -70,7 +70,7 @@ def _linear(hip, wfmt, x, W, sz, N, K, bias=None):
     M = x.shape[0]
     out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     call(hip, "llj_linear", wfmt, x.data_ptr(), x.stride(0), W.data_ptr(), None if sz is None else sz.data_ptr(),
-         None if bias is None else bias.data_ptr(), out.data_ptr(), N, M, N, K, None, 0, st())
+         None if bias is None else bias.data_ptr(), out.data_ptr(), N, M, N, K, None, 0, None, st())
     torch.cuda.synchronize()
     return out.float().cpu().numpy()
 
@@ -134,7 +134,7 @@ def test_int8_linear_vs_restatement(hip, M, outliers):
     call(hip, "llj_i8_stats", xd.data_ptr(), K, M, K, 6.0, ws.data_ptr(), st())
     out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     call(hip, "llj_linear", 2, xd.data_ptr(), K, cb.data_ptr(), scb.data_ptr(), None, out.data_ptr(), N, M, N, K,
-         ws.data_ptr(), 0, st())
+         ws.data_ptr(), 0, None, st())
     torch.cuda.synchronize()
     ref = O.int8_linear(x, cb_ref, scb_ref)
     assert_bf16_close(out.float().cpu().numpy(), ref, f"int8 M={M} outliers={outliers}", rel=2e-2)
@@ -257,7 +257,7 @@ def test_fused_qkv_rope_kv(hip, wfmt, B, T_):
         r = min(8, M - r0)
         call(hip, "llj_norm_qkv_rope", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, Wd.data_ptr(),
              None if szd is None else szd.data_ptr(), q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rd.data_ptr(),
-             pd.data_ptr(), B, T_, C, nh, S, r0, r, None, None, 0, st())
+             pd.data_ptr(), B, T_, C, nh, S, r0, r, None, None, 0, None, st())
     torch.cuda.synchronize()
     h = bf16(O.rmsnorm(x, g))
     qkv = bf16(h @ Wref.T)
@@ -295,7 +295,7 @@ def test_fused_swiglu_and_resid(hip, wfmt):
     P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
     xd, gd = T(x, torch.bfloat16), T(g, torch.bfloat16)
     call(hip, "llj_norm_swiglu", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, W1d.data_ptr(), P(s1), W2d.data_ptr(),
-         P(s2), h.data_ptr(), M, H, C, None, 0, None, 0, st())
+         P(s2), h.data_ptr(), M, H, C, None, 0, None, 0, None, st())
     xr = xd.clone()
     call(hip, "llj_linear_resid", wfmt, h.data_ptr(), H, Wdd.data_ptr(), P(sd), xr.data_ptr(), C, M, C, H, None, 0,
          None, st())
@@ -308,3 +308,32 @@ def test_fused_swiglu_and_resid(hip, wfmt):
     assert_bf16_close(h.float().cpu().numpy(), hexp, "swiglu", rel=3e-2)
     hg = h.float().cpu().numpy()
     assert_bf16_close(xr.float().cpu().numpy(), x + bf16(hg @ Wd_.T), "resid")
+
+
+def test_rmsnorm_rows_rowsum_and_int4_rowsum_operand(hip, golden):
+    """llj_rmsnorm_rows: same normalized rows as llj_rmsnorm plus fp32 row sums; an int4 GEMV
+    fed those sums (rowsum operand) equals the one that reduces them in-kernel."""
+    rng = np.random.default_rng(5)
+    M, C, N = 5, 512, 256
+    x = T(bf16(rng.standard_normal((M, C))), torch.bfloat16)
+    g = T(bf16(rng.uniform(0.5, 1.5, C)), torch.bfloat16)
+    y1 = torch.empty_like(x)
+    y2 = torch.empty_like(x)
+    rs = torch.empty(M, dtype=torch.float32, device=dev)
+    call(hip, "llj_rmsnorm", x.data_ptr(), g.data_ptr(), 1e-5, y1.data_ptr(), M, C, st())
+    call(hip, "llj_rmsnorm_rows", x.data_ptr(), g.data_ptr(), 1e-5, y2.data_ptr(), rs.data_ptr(), M, C, st())
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    np.testing.assert_allclose(rs.cpu().numpy(), y2.float().sum(1).cpu().numpy(), rtol=1e-5, atol=1e-3)
+    qw, sc, z = rand_w4(rng, N, C)
+    Wd, szd = repack(hip, qw), sz_of(hip, sc, z)
+    outs = []
+    for r in (None, rs):
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        call(hip, "llj_linear", 0, y2.data_ptr(), C, Wd.data_ptr(), szd.data_ptr(), None, out.data_ptr(), N, M, N, C,
+             None, 0, None if r is None else r.data_ptr(), st())
+        outs.append(out)
+    torch.cuda.synchronize()
+    ref = bf16(y2.float().cpu().numpy() @ O.colblock_get_weight(qw, sc, z, 4).T)
+    for o in outs:
+        assert_bf16_close(o.float().cpu().numpy(), ref, "int4 with/without rowsum")

@@ -93,6 +93,8 @@ def trace_phases(path):
             att = [x for x in cur if "attention" in x["Kernel_Name"]]
             if att and len(cur) > 20:
                 steps[int(att[0]["Grid_Size_Y"])].append(cur)
+            elif len(cur) > 20:  # chained layers (no standalone attention): batch from the argmax grid
+                steps[int(r["Grid_Size_X"]) // 1024].append(cur)
             cur = []
     phases = {}
     for bsz, st in steps.items():
