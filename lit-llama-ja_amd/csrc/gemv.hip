@@ -31,6 +31,7 @@
 
 #include "common.h"
 #include "chain.h"
+#include "i8ws.h"
 #include "attention.h"
 #include "lit_llama_amd.h"
 
@@ -40,13 +41,7 @@ enum : int { WF_W4 = 0, WF_BF16 = 1, WF_I8 = 2 };
 enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2 };
 enum : int { EP_STORE = 0, EP_RESID = 1, EP_QKV = 2, EP_SWIGLU = 3 };
 
-// int8 activation-statistics workspace written by llj_i8_stats (int8.hip)
-struct I8WsHeader {
-  int mtot, K, nsb, kb;
-};
-__host__ __device__ inline const float* i8_partial(const void* ws) {
-  return reinterpret_cast<const float*>(reinterpret_cast<const char*>(ws) + 16);
-}
+// int8 activation workspace written by llj_i8_stats (int8.hip): i8ws.h
 
 struct GemvParams {
   const bf16_t* A;  // (M, K), row stride lda elements
@@ -175,52 +170,21 @@ __device__ void stage_a(const GemvParams& p, bf16_t* As, int a_stride, float* re
   }
 }
 
-// int8: quantize rows [0, M) of A into LDS int8 rows (stride K + 16 bytes) with the
-// per-row absmax SCA (non-outlier elements; from the llj_i8_stats partials) and the
-// outlier columns zeroed. sca[] receives SCA per local row.
+// int8: copy rows [0, M) of the activation quantized once by llj_i8_stats (outlier columns
+// already 0) into LDS int8 rows (stride K + 16 bytes); sca[] receives SCA per local row.
 template <int NW>
 __device__ void stage_i8(const GemvParams& p, int8_t* Aq, int q_stride, float* sca) {
   const int tid = threadIdx.x;
   constexpr int NT = NW * 64;
   const int K = p.K, M = p.M;
   const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
-  const float* part = i8_partial(p.i8ws);
-  const int* cnt = reinterpret_cast<const int*>(part + (size_t)h.nsb * h.mtot);
-  const int* list = cnt + h.nsb;
-  if (tid < M) {
-    float mx = 0.f;
-    for (int b = 0; b < h.nsb; ++b) mx = fmaxf(mx, part[(size_t)b * h.mtot + p.m0 + tid]);
-    sca[tid] = mx;
-  }
-  __syncthreads();
-  const int nvec = K >> 3;
+  const I8Layout L = i8_layout(p.i8ws, h.mtot, h.K);
+  if (tid < M) sca[tid] = L.sca[p.m0 + tid];
+  const int nv = K >> 4;
   for (int m = 0; m < M; ++m) {
-    const float s = sca[m];
-    const float inv = s > 0.f ? 127.f / s : 0.f;
-    const uint4* src = reinterpret_cast<const uint4*>(p.A + (size_t)m * p.lda);
-    uint2* dst = reinterpret_cast<uint2*>(Aq + (size_t)m * q_stride);
-    for (int v = tid; v < nvec; v += NT) {
-      uint4 x = src[v];
-      uint32_t w[4] = {x.x, x.y, x.z, x.w};
-      uint32_t o[2] = {0, 0};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float a = (float)(_Float16)bflo(w[i]), b = (float)(_Float16)bfhi(w[i]);
-        const int qa = (int)fminf(fmaxf(rintf(a * inv), -127.f), 127.f);
-        const int qb = (int)fminf(fmaxf(rintf(b * inv), -127.f), 127.f);
-        o[i >> 1] |= ((uint32_t)(qa & 0xFF) | ((uint32_t)(qb & 0xFF) << 8)) << (16 * (i & 1));
-      }
-      dst[v] = make_uint2(o[0], o[1]);
-    }
-  }
-  __syncthreads();
-  // zero the outlier columns (their contribution is the fp16 side product)
-  for (int b = 0; b < h.nsb; ++b) {
-    const int c = cnt[b];
-    for (int i = tid; i < c * M; i += NT) {
-      const int k = list[b * h.kb + i / M];
-      Aq[(size_t)(i % M) * q_stride + k] = 0;
-    }
+    const uint4* src = reinterpret_cast<const uint4*>(L.aq + (size_t)(p.m0 + m) * K);
+    uint4* dst = reinterpret_cast<uint4*>(Aq + (size_t)m * q_stride);
+    for (int v = tid; v < nv; v += NT) dst[v] = src[v];
   }
 }
 
@@ -236,23 +200,67 @@ __device__ __forceinline__ int kofs(int t, int grp) {
   return WF == WF_W4 ? 32 * grp + 8 * t : WF == WF_BF16 ? 32 * t + 8 * grp : 64 * t + 16 * grp;
 }
 
-// fp16 side product of LLM.int8() over the outlier columns: sum_k f16(A[m,k]) * f16(CB[n,k]*SCB[n]/127)
-__device__ float i8_side(const GemvParams& p, const int8_t* CB, float scb, int m, int n) {
+// fp16 side product of LLM.int8() over the outlier columns, for this workgroup's 16 columns
+// and M <= 8 rows: side[m][n] = sum_k f16(A[m,k]) * f16(CB[n,k] * SCB[n] / 127). The outlier
+// columns are taken in chunks of kSideChunk: their indices and f16(A) values are staged in LDS
+// (`stage`, free A-image space) once per workgroup, then thread t (column t % 16, every
+// (NW*4)-th outlier of the chunk) accumulates; the four lanes of a wave sharing a column are
+// combined by shuffles and the per-wave partials land in part[NW][8][16]. Ends with a barrier.
+constexpr int kSideChunk = 256;
+template <int NW>
+__device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float* SCB, int n0, float* part,
+                             unsigned char* stage) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nl = tid & 15, g = tid >> 4;
+  constexpr int NG = NW * 4, NT = NW * 64;
   const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
-  const float* part = i8_partial(p.i8ws);
-  const int* cnt = reinterpret_cast<const int*>(part + (size_t)h.nsb * h.mtot);
-  const int* list = cnt + h.nsb;
-  float s = 0.f;
-  for (int b = 0; b < h.nsb; ++b) {
-    const int c = cnt[b];
-    for (int i = 0; i < c; ++i) {
-      const int k = list[b * h.kb + i];
-      const float a = (float)(_Float16)bf2f(p.A[(size_t)m * p.lda + k]);
-      const float w = (float)(_Float16)((float)CB[(size_t)n * p.K + k] * (scb / 127.f));
-      s += a * w;
+  const I8Layout L = i8_layout(p.i8ws, h.mtot, h.K);
+  int* s_pre = reinterpret_cast<int*>(stage);           // [kNSB + 1] prefix of the block counts
+  int* s_k = s_pre + 64;                                // [kSideChunk] column indices
+  float* s_a = reinterpret_cast<float*>(s_k + kSideChunk);  // [8][kSideChunk] f16(A) values
+  const int n = n0 + nl, M = p.M;
+  const float scb = SCB[n] / 127.f;
+  if (tid < 64) {  // prefix sum of the per-block outlier counts (kNSB <= 64)
+    int c = tid < h.nsb ? L.cnt[tid] : 0;
+    int x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
     }
+    s_pre[tid + 1] = x;
+    if (tid == 0) s_pre[0] = 0;
   }
-  return s;
+  __syncthreads();
+  const int total = s_pre[h.nsb];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < total; c0 += kSideChunk) {
+    const int len = min(kSideChunk, total - c0);
+    for (int i = tid; i < len; i += NT) {
+      const int fi = c0 + i;
+      int b = 0;
+      while (b + 1 < h.nsb && s_pre[b + 1] <= fi) ++b;  // blocks are few (kNSB)
+      const int k = L.list[b * h.kb + (fi - s_pre[b])];
+      s_k[i] = k;
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+        s_a[m * kSideChunk + i] = m < M ? (float)(_Float16)bf2f(p.A[(size_t)m * p.lda + k]) : 0.f;
+    }
+    __syncthreads();
+    for (int i = g; i < len; i += NG) {
+      const float w = (float)(_Float16)((float)CB[(size_t)n * p.K + s_k[i]] * scb);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) acc[m] += s_a[m * kSideChunk + i] * w;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    acc[m] += __shfl_xor(acc[m], 16, 64);
+    acc[m] += __shfl_xor(acc[m], 32, 64);
+    if (lane < 16) part[(wave * 8 + m) * 16 + nl] = acc[m];
+  }
+  __syncthreads();
 }
 
 // Output value of one element for the plain / SwiGLU epilogues (SwiGLU: model.py:258 in bf16).
@@ -316,8 +324,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   const int a_stride = I8 ? K + 16 : K + 8;  // elements (bytes for int8)
   const size_t a_bytes = ALDS ? (((size_t)M * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15) : 0;
   constexpr size_t kRedBytes = (size_t)NW * 64 * 12 * 4;
+  constexpr size_t kScratch = kRedBytes + (I8 ? (size_t)2 * NW * 8 * 16 * 4 : 0);  // + int8 side partials
   float* red = reinterpret_cast<float*>(smem);
-  float* tail = reinterpret_cast<float*>(smem + (a_bytes > kRedBytes ? a_bytes : kRedBytes));
+  float* tail = reinterpret_cast<float*>(smem + (a_bytes > kScratch ? a_bytes : kScratch));
   float* sca = tail;
 
   const bool arow = row < M;
@@ -669,8 +678,17 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   // ---- reduce the NW partial tiles in LDS (each wave: 64 lanes x 12 words; int8 sums stay
   // int32 — they exceed 2^24 at K = 11008, so they must not round-trip through fp32)
   constexpr int NV = 12;
+  // int8 side products in the LDS beyond the reduction scratch (the A image is no longer read)
+  float* side = reinterpret_cast<float*>(smem + kRedBytes);
   if (NW > 1) {
     if (ALDS) __syncthreads();  // every wave is done reading the A image it aliases
+    if constexpr (I8) {
+      i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W), reinterpret_cast<const float*>(p.sz), n0, side,
+                       smem);
+      if (DUAL)
+        i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W2), reinterpret_cast<const float*>(p.sz2), n0,
+                         side + NW * 8 * 16, smem);
+    }
     if constexpr (I8) {
       int* mine = reinterpret_cast<int*>(red) + (size_t)(wave * 64 + lane) * NV;
 #pragma unroll
@@ -745,8 +763,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
       y = (float)iacc[r] * (sa * s1 * kq);
       if (DUAL) y2 = (float)iacc2[r] * (sa * s2 * kq);
       if (m < M) {
-        y = (float)(_Float16)((float)(_Float16)y + i8_side(p, reinterpret_cast<const int8_t*>(p.W), s1, m, n));
-        if (DUAL) y2 = (float)(_Float16)((float)(_Float16)y2 + i8_side(p, reinterpret_cast<const int8_t*>(p.W2), s2, m, n));
+        float sd = 0.f, sd2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          sd += side[(w * 8 + m) * 16 + row];
+          if (DUAL) sd2 += side[NW * 128 + (w * 8 + m) * 16 + row];
+        }
+        y = (float)(_Float16)((float)(_Float16)y + sd);
+        if (DUAL) y2 = (float)(_Float16)((float)(_Float16)y2 + sd2);
       }
     }
     y += bias;
@@ -847,7 +871,9 @@ static inline size_t a_image_bytes(int wf, int am, int M, int K) {
   return (((size_t)M * (K + 8) * 2) + 15) & ~(size_t)15;
 }
 static inline size_t gemv_smem(int wf, int am, int M, int K) {
-  const size_t a = a_image_bytes(wf, am, M, K), red = (size_t)kNW * 64 * 12 * 4;
+  const size_t a = a_image_bytes(wf, am, M, K);
+  // int8: the side-product partials (2 matrices x NW x 8 rows x 16 columns) follow the scratch
+  const size_t red = (size_t)kNW * 64 * 12 * 4 + (wf == WF_I8 ? (size_t)2 * kNW * 8 * 16 * 4 : 0);
   return (a > red ? a : red) + 128 * 4;
 }
 

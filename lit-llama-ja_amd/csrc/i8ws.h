@@ -1,0 +1,61 @@
+// LLM.int8() activation workspace (filled by llj_i8_stats, read by the int8 GEMV).
+//
+//   [0, 16)        header {mtot, K, nsb, kb}
+//   part[nsb][M]   fp32 per-(k-block, row) absmax of the non-outlier elements
+//   cnt[nsb]       outlier columns found in each k-block
+//   list[nsb][kb]  their column indices (ascending within a block)
+//   sca[M]         SCA[m] = max over the k-blocks of part
+//   flag[K]        1 for an outlier column
+//   aq[M][K]       the activation quantized once: round(A16 * 127 / SCA), outlier columns 0
+// Quantizing once here (instead of in every GEMV workgroup) is what keeps the batched int8
+// GEMV weight-streaming.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace llj {
+
+constexpr int kNSB = 32;  // statistics blocks (k-ranges)
+
+struct I8WsHeader {
+  int mtot, K, nsb, kb;
+};
+
+__host__ __device__ inline int i8_kb(int K) { return ((K + kNSB - 1) / kNSB + 15) & ~15; }
+
+__host__ __device__ inline size_t i8_align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// byte offsets of the arrays (the layout above)
+struct I8Offsets {
+  size_t part, cnt, list, sca, flag, aq, total;
+};
+__host__ __device__ inline I8Offsets i8_offsets(int M, int K) {
+  I8Offsets o;
+  o.part = 16;
+  o.cnt = o.part + sizeof(float) * (size_t)kNSB * M;
+  o.list = o.cnt + sizeof(int) * kNSB;
+  o.sca = o.list + sizeof(int) * (size_t)kNSB * i8_kb(K);
+  o.flag = i8_align16(o.sca + sizeof(float) * (size_t)M);
+  o.aq = i8_align16(o.flag + (size_t)K);
+  o.total = o.aq + (size_t)M * K;
+  return o;
+}
+
+struct I8Layout {
+  float* part;
+  int* cnt;
+  int* list;
+  float* sca;
+  uint8_t* flag;  // flag[k] = 1 for an outlier column
+  int8_t* aq;
+};
+
+__host__ __device__ inline I8Layout i8_layout(const void* ws, int M, int K) {
+  char* b = const_cast<char*>(reinterpret_cast<const char*>(ws));
+  const I8Offsets o = i8_offsets(M, K);
+  return I8Layout{reinterpret_cast<float*>(b + o.part), reinterpret_cast<int*>(b + o.cnt),
+                  reinterpret_cast<int*>(b + o.list), reinterpret_cast<float*>(b + o.sca),
+                  reinterpret_cast<uint8_t*>(b + o.flag), reinterpret_cast<int8_t*>(b + o.aq)};
+}
+
+}  // namespace llj

@@ -8,27 +8,20 @@
 //   activation:  A16 = A.half(); outlier columns = {k : any row |A16[m,k]| >= threshold};
 //                SCA[m] = max over the row's elements with |A16| < threshold
 #include "common.h"
+#include "i8ws.h"
 
 namespace llj {
 
-constexpr int kNSB = 32;  // statistics blocks (k-ranges)
-
-struct I8Ws {
-  int mtot, K, nsb, kb;
-};
-
-static inline int i8_kb(int K) { return ((K + kNSB - 1) / kNSB + 15) & ~15; }
-
 __device__ __forceinline__ float to_f16f(float x) { return (float)(_Float16)x; }
 
+// Pass 1, one block per k-range: outlier columns (any row |A16| >= thr) as flags and an
+// ascending list, and per-row absmax of the other elements.
 __global__ __launch_bounds__(256) void i8_stats_kernel(const bf16_t* __restrict__ A, int lda, int M, int K,
                                                        float thr, char* __restrict__ ws, int kb) {
   __shared__ int flag[1024];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float* part = reinterpret_cast<float*>(ws + 16);
-  int* cnt = reinterpret_cast<int*>(part + (size_t)kNSB * M);
-  int* list = cnt + kNSB;
-  if (b == 0 && tid == 0) *reinterpret_cast<I8Ws*>(ws) = I8Ws{M, K, kNSB, kb};
+  const I8Layout L = i8_layout(ws, M, K);
+  if (b == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb};
   const int k0 = b * kb;
   const int k1 = min(K, k0 + kb);
   for (int i = tid; i < kb; i += 256) flag[i] = 0;
@@ -41,14 +34,59 @@ __global__ __launch_bounds__(256) void i8_stats_kernel(const bf16_t* __restrict_
       else mx = fmaxf(mx, a);
     }
     mx = wave_max(mx);
-    if (lane == 0) part[(size_t)b * M + m] = mx;
+    if (lane == 0) L.part[(size_t)b * M + m] = mx;
   }
   __syncthreads();
-  if (tid == 0) {
+  for (int k = k0 + tid; k < k1; k += 256) L.flag[k] = (uint8_t)flag[k - k0];
+  if (wave == 0) {  // compact the flags into the list, 64 columns per ballot
     int c = 0;
-    for (int i = 0; i < k1 - k0; ++i)
-      if (flag[i]) list[b * kb + c++] = k0 + i;
-    cnt[b] = c;
+    for (int i0 = 0; i0 < k1 - k0; i0 += 64) {
+      const bool f = i0 + lane < k1 - k0 && flag[i0 + lane];
+      const unsigned long long bal = __ballot(f);
+      if (f) L.list[b * kb + c + __popcll(bal & ((1ull << lane) - 1ull))] = k0 + i0 + lane;
+      c += __popcll(bal);
+    }
+    if (lane == 0) L.cnt[b] = c;
+  }
+}
+
+// Pass 2, one block per row: SCA = max over the k-blocks, then the row quantized once:
+// q = round(A16 * 127 / SCA) clamped to +-127, outlier columns 0 (their contribution is the
+// fp16 side product).
+__global__ __launch_bounds__(256) void i8_quant_act_kernel(const bf16_t* __restrict__ A, int lda, int M, int K,
+                                                           char* __restrict__ ws) {
+  __shared__ float s_sca;
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const I8Layout L = i8_layout(ws, M, K);
+  if (tid < 64) {
+    float mx = tid < kNSB ? L.part[(size_t)tid * M + m] : 0.f;
+    mx = wave_max(mx);
+    if (tid == 0) {
+      s_sca = mx;
+      L.sca[m] = mx;
+    }
+  }
+  __syncthreads();
+  const float s = s_sca;
+  const float inv = s > 0.f ? 127.f / s : 0.f;
+  const bf16_t* ar = A + (size_t)m * lda;
+  int8_t* qr = L.aq + (size_t)m * K;
+  for (int v = tid; v < K / 8; v += 256) {
+    const uint4 x = *reinterpret_cast<const uint4*>(ar + 8 * v);
+    const uint2 fl = *reinterpret_cast<const uint2*>(L.flag + 8 * v);
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    const uint32_t fw[2] = {fl.x, fl.y};
+    uint32_t o[2] = {0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float a = to_f16f(bflo(w[i])), bb = to_f16f(bfhi(w[i]));
+      int qa = (int)fminf(fmaxf(rintf(a * inv), -127.f), 127.f);
+      int qb = (int)fminf(fmaxf(rintf(bb * inv), -127.f), 127.f);
+      if ((fw[i >> 1] >> (16 * (i & 1))) & 0xFF) qa = 0;
+      if ((fw[i >> 1] >> (16 * (i & 1) + 8)) & 0xFF) qb = 0;
+      o[i >> 1] |= ((uint32_t)(qa & 0xFF) | ((uint32_t)(qb & 0xFF) << 8)) << (16 * (i & 1));
+    }
+    *reinterpret_cast<uint2*>(qr + 8 * v) = make_uint2(o[0], o[1]);
   }
 }
 
@@ -81,14 +119,15 @@ using namespace llj;
 extern "C" {
 
 // Bytes of the statistics workspace for an (M, K) activation.
-size_t llj_i8_ws_bytes(int M, int K) {
-  return 16 + sizeof(float) * (size_t)kNSB * M + sizeof(int) * kNSB + sizeof(int) * (size_t)kNSB * i8_kb(K);
-}
+size_t llj_i8_ws_bytes(int M, int K) { return i8_offsets(M, K).total; }
 
 int llj_i8_stats(const void* A, int lda, int M, int K, float threshold, void* ws, void* stream) {
-  LLJ_REQUIRE(M > 0 && K > 0 && i8_kb(K) <= 1024);
+  LLJ_REQUIRE(M > 0 && K > 0 && K % 16 == 0 && lda % 8 == 0 && i8_kb(K) <= 1024);
   hipLaunchKernelGGL(i8_stats_kernel, dim3(kNSB), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)A, lda, M, K,
                      threshold, (char*)ws, i8_kb(K));
+  LLJ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(i8_quant_act_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)A, lda, M, K,
+                     (char*)ws);
   LLJ_CHECK_LAUNCH();
   return 0;
 }
