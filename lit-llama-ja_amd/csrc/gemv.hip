@@ -870,27 +870,33 @@ static inline size_t a_image_bytes(int wf, int am, int M, int K) {
   if (am == AM_GLOBAL) return 0;
   return (((size_t)M * (K + 8) * 2) + 15) & ~(size_t)15;
 }
-static inline size_t gemv_smem(int wf, int am, int M, int K) {
+static inline size_t gemv_smem(int wf, int am, int M, int K, int nw = kNW) {
   const size_t a = a_image_bytes(wf, am, M, K);
   // int8: the side-product partials (2 matrices x NW x 8 rows x 16 columns) follow the scratch
-  const size_t red = (size_t)kNW * 64 * 12 * 4 + (wf == WF_I8 ? (size_t)2 * kNW * 8 * 16 * 4 : 0);
+  const size_t red = (size_t)nw * 64 * 12 * 4 + (wf == WF_I8 ? (size_t)2 * nw * 8 * 16 * 4 : 0);
   return (a > red ? a : red) + 128 * 4;
 }
 
 // the LDS A image must leave room for the reduction scratch: <= 96 KiB, M <= 8 rows
 static inline bool lds_fits(int wf, int M, int K) { return M <= 8 && a_image_bytes(wf, AM_LDS, M, K) <= 96 * 1024; }
 
+// waves per workgroup: the global-A form (rows whose A image does not fit the LDS) keeps twice
+// as many waves, each with fewer chunks, for more A-fragment loads in flight
+template <int AM>
+constexpr int nw_of() { return AM == AM_GLOBAL ? 2 * kNW : kNW; }
+
 template <int WF, int AM, int EP, int MB>
 static int launch_mb(const GemvParams& p, hipStream_t s) {
-  const size_t sm = gemv_smem(WF, AM, p.M, p.K);
-  auto kern = gemv_kernel<WF, AM, EP, kNW, kD, MB>;
+  constexpr int NW = nw_of<AM>();
+  const size_t sm = gemv_smem(WF, AM, p.M, p.K, NW);
+  auto kern = gemv_kernel<WF, AM, EP, NW, kD, MB>;
   static bool attr_set = false;  // per instantiation; set before any graph capture
   if (sm > 64 * 1024 && !attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(p.N / 16), dim3(kNW * 64), sm, s, p);
+  hipLaunchKernelGGL(kern, dim3(p.N / 16), dim3(NW * 64), sm, s, p);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

@@ -31,22 +31,48 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ 
   }
 }
 
-// ---- RMSNorm with the bf16 rounding points of model.py:281-283 on bf16 tensors.
+// ---- RMSNorm with the bf16 rounding points of model.py:281-283 on bf16 tensors. One block
+// per row; rows up to 8192 wide are loaded once into registers (x and the scale together,
+// before any use), so the kernel is one memory round trip.
+__device__ __forceinline__ uint32_t norm_pair(uint32_t a, uint32_t g, float r) {
+  return pack2bf(round_bf(bflo(g) * round_bf(bflo(a) * r)), round_bf(bfhi(g) * round_bf(bfhi(a) * r)));
+}
+
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                       float eps, bf16_t* __restrict__ y, int C,
                                                       float* __restrict__ rowsum) {
-  __shared__ float red[4];
+  constexpr int MAXV = 4;  // 16-byte vectors per thread held in registers
+  __shared__ float red[8];
   const int m = blockIdx.x, tid = threadIdx.x;
   const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)m * C);
   const uint4* g4 = reinterpret_cast<const uint4*>(w);
   uint4* yr = reinterpret_cast<uint4*>(y + (size_t)m * C);
   const int nvec = C >> 3;
+  const bool regs = nvec <= MAXV * 256;
+  uint4 xa[MAXV], ga[MAXV];
   float ss = 0.f;
-  for (int v = tid; v < nvec; v += 256) {
-    uint4 a = xr[v];
-    uint32_t aw[4] = {a.x, a.y, a.z, a.w};
+  if (regs) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ss += round_bf(bflo(aw[i]) * bflo(aw[i])) + round_bf(bfhi(aw[i]) * bfhi(aw[i]));
+    for (int j = 0; j < MAXV; ++j) {
+      const int v = tid + 256 * j, vv = v < nvec ? v : 0;
+      xa[j] = xr[vv];
+      ga[j] = g4[vv];
+    }
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      if (tid + 256 * j < nvec) {
+        const uint32_t aw[4] = {xa[j].x, xa[j].y, xa[j].z, xa[j].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ss += round_bf(bflo(aw[i]) * bflo(aw[i])) + round_bf(bfhi(aw[i]) * bfhi(aw[i]));
+      }
+    }
+  } else {
+    for (int v = tid; v < nvec; v += 256) {
+      const uint4 a = xr[v];
+      const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ss += round_bf(bflo(aw[i]) * bflo(aw[i])) + round_bf(bfhi(aw[i]) * bfhi(aw[i]));
+    }
   }
   ss = wave_sum(ss);
   if ((tid & 63) == 0) red[tid >> 6] = ss;
@@ -54,22 +80,24 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__
   const float tot = red[0] + red[1] + red[2] + red[3];
   const float r = round_bf(rsqrtf(round_bf(round_bf(tot / (float)C) + eps)));
   float rsum = 0.f;
-  for (int v = tid; v < nvec; v += 256) {
-    uint4 a = xr[v], g = g4[v];
-    uint32_t aw[4] = {a.x, a.y, a.z, a.w}, gw[4] = {g.x, g.y, g.z, g.w}, o[4];
+  auto emit = [&](int v, uint4 a, uint4 g) {
+    const uint32_t o0 = norm_pair(a.x, g.x, r), o1 = norm_pair(a.y, g.y, r), o2 = norm_pair(a.z, g.z, r),
+                   o3 = norm_pair(a.w, g.w, r);
+    rsum += bflo(o0) + bfhi(o0) + bflo(o1) + bfhi(o1) + bflo(o2) + bfhi(o2) + bflo(o3) + bfhi(o3);
+    yr[v] = make_uint4(o0, o1, o2, o3);
+  };
+  if (regs) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      o[i] = pack2bf(round_bf(bflo(gw[i]) * round_bf(bflo(aw[i]) * r)), round_bf(bfhi(gw[i]) * round_bf(bfhi(aw[i]) * r)));
-      rsum += bflo(o[i]) + bfhi(o[i]);
-    }
-    yr[v] = make_uint4(o[0], o[1], o[2], o[3]);
+    for (int j = 0; j < MAXV; ++j)
+      if (tid + 256 * j < nvec) emit(tid + 256 * j, xa[j], ga[j]);
+  } else {
+    for (int v = tid; v < nvec; v += 256) emit(v, xr[v], g4[v]);
   }
   if (rowsum) {  // sum of the normalized bf16 row: the int4 GEMV's offset term (gemv.hip header)
-    __syncthreads();
     rsum = wave_sum(rsum);
-    if ((tid & 63) == 0) red[tid >> 6] = rsum;
+    if ((tid & 63) == 0) red[4 + (tid >> 6)] = rsum;
     __syncthreads();
-    if (tid == 0) rowsum[m] = red[0] + red[1] + red[2] + red[3];
+    if (tid == 0) rowsum[m] = red[4] + red[5] + red[6] + red[7];
   }
 }
 
