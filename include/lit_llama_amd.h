@@ -82,6 +82,16 @@ int llj_attention(const void* q, const void* kcache, const void* vcache, void* y
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
                      int N, int K, const void* i8ws, int i8_row0, double* nstat_out, void* stream);
 
+/* The same, then the next RMSNorm of the updated rows (rms_2 after c_proj, the next layer's
+ * rms_1 / ln_f after mlp.c_proj; model.py:173, 171, 125): xn[M, N] = RMSNorm(x) with scale
+ * norm_w, rowsum[m] = fp32 sum of the normalized row (or NULL). Computed once, by the last
+ * workgroup to finish (agent release/acquire + the completion `counter`, one word the caller
+ * zeroes once; the kernel leaves it 0). M <= 8, wfmt 0 or 1. Batched decode (M >= 2) uses it
+ * instead of a separate llj_rmsnorm_rows launch. */
+int llj_linear_resid_norm(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
+                          int N, int K, const void* norm_w, float eps, void* xn, float* rowsum, unsigned* counter,
+                          void* stream);
+
 /* h[M, H] = silu(rms_2(x) . W1^T) * (rms_2(x) . W2^T)  (model.py:173, 258). M <= 8. */
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,

@@ -75,6 +75,14 @@ struct GemvParams {
   // int4: sum_k A[m,k] of this call's rows as the MFMA sees them (pre-normalized rows,
   // llj_rmsnorm_rows); nullptr = computed in the prologue
   const float* rowsum;
+  // EP_RESID: RMSNorm of the updated residual rows, computed once by the LAST workgroup to
+  // finish (completion counter nn_ctr; it resets the counter): xn = RMSNorm(x) with scale
+  // nn_w / eps nn_eps, nn_rs[m] = fp32 sum of the normalized bf16 row. nullptr = off.
+  const bf16_t* nn_w;
+  float nn_eps;
+  bf16_t* nn_out;
+  float* nn_rs;
+  unsigned* nn_ctr;
 };
 
 // ------------------------------------------------------------------------------------
@@ -301,6 +309,91 @@ struct APre {
   u32x4 g[GR];
   double st[ST];
 };
+
+// Last-arriver RMSNorm after a residual GEMV (GemvParams::nn_*): every workgroup stores its x
+// columns write-through (sc1), drains them and counts itself done; the one whose add returns
+// nwg - 1 reads the rows back with sc1 loads (chain.h protocol) and normalizes them with the bf16
+// rounding points of model.py:281-283 (as rmsnorm_kernel), so the consumer GEMVs read a
+// finished xn instead of a separate norm launch. `red` = LDS scratch (>= 64 floats). All
+// waves of the workgroup call it (wave 0 after its epilogue stores).
+template <int NW>
+__device__ void resid_norm_tail(const GemvParams& p, float* red, bool storing_wave) {
+  constexpr int NT = NW * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = p.M, C = p.N;
+  int* flag = reinterpret_cast<int*>(red + 64);
+  if (storing_wave) {  // x columns were stored sc1 (write-through): drain, then count done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(p.nn_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, 0, 64);
+    if (lane == 0) *flag = old + 1 == gridDim.x ? 1 : 0;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  // the last workgroup: sum_k bf16(x^2) per row
+  const int nvec = C >> 3;
+  float ss[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int v = tid; v < nvec; v += NT) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      if (m < M) {
+        const u32x4 a = ld16_sc1(p.C, (unsigned)(((size_t)m * p.ldc + 8 * v) * 2));  // other workgroups' x
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          ss[m] += round_bf(bflo(a[i]) * bflo(a[i])) + round_bf(bfhi(a[i]) * bfhi(a[i]));
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const float t = wave_sum(ss[m]);
+    if (lane == 0) red[wave * 8 + m] = t;
+  }
+  __syncthreads();
+  float r[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += red[w * 8 + m];
+    r[m] = round_bf(rsqrtf(round_bf(round_bf(t / (float)C) + p.nn_eps)));
+  }
+  __syncthreads();
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const uint4* g4 = reinterpret_cast<const uint4*>(p.nn_w);
+  for (int v = tid; v < nvec; v += NT) {
+    const uint4 g = g4[v];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      if (m < M) {
+        const u32x4 a = ld16_sc1(p.C, (unsigned)(((size_t)m * p.ldc + 8 * v) * 2));
+        uint32_t o[4];
+        const uint32_t aw[4] = {a[0], a[1], a[2], a[3]}, gw[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          o[i] = pack2bf(round_bf(bflo(gw[i]) * round_bf(bflo(aw[i]) * r[m])),
+                         round_bf(bfhi(gw[i]) * round_bf(bfhi(aw[i]) * r[m])));
+          rs[m] += bflo(o[i]) + bfhi(o[i]);
+        }
+        *reinterpret_cast<uint4*>(p.nn_out + (size_t)m * C + 8 * v) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const float t = wave_sum(rs[m]);
+    if (lane == 0) red[wave * 8 + m] = t;
+  }
+  __syncthreads();
+  if (tid < M && p.nn_rs) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += red[w * 8 + tid];
+    p.nn_rs[tid] = t;
+  }
+  if (tid == 0) *p.nn_ctr = 0u;  // ready for the next launch (kernel boundaries order it)
+}
 
 #ifndef LLJ_ABL
 #define LLJ_ABL 0  // ablation switches for profiling only (1 no A prologue, 2 no compute, 4 no epilogue)
@@ -706,7 +799,11 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
       }
     }
     __syncthreads();
-    if (wave != 0) return;
+    if (wave != 0) {
+      if constexpr (EP == EP_RESID)
+        if (p.nn_ctr) resid_norm_tail<NW>(p, red, false);
+      return;
+    }
 #pragma unroll
     for (int w = 1; w < NW; ++w) {
       if constexpr (I8) {
@@ -821,7 +918,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
         sq = round_bf(xn * xn);
         if (!(row & 1)) {
           const size_t ei = (size_t)m * p.ldc + n;
-          if constexpr (CH) st4_sc1(p.C, (unsigned)(ei * 2), xb | (pr << 16));
+          if (CH || p.nn_ctr) st4_sc1(p.C, (unsigned)(ei * 2), xb | (pr << 16));  // read by another workgroup
           else *reinterpret_cast<uint32_t*>(p.C + ei) = xb | (pr << 16);
         }
       }
@@ -846,6 +943,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     }
   }
   if constexpr (CH) chain_signal(cc);
+  if constexpr (EP == EP_RESID)
+    if (p.nn_ctr) resid_norm_tail<NW>(p, red, true);
   LLJ_STAMP(5);
 }
 
@@ -1065,6 +1164,16 @@ int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, cons
 }
 
 // x[M,N] += A[M,K] . W^T, bf16 residual add (attn.c_proj / mlp.c_proj + model.py:172-173).
+int llj_linear_resid_norm(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
+                          int N, int K, const void* norm_w, float eps, void* xn, float* rowsum, unsigned* counter,
+                          void* stream) {
+  GemvParams p{};
+  if (M > 8 || !norm_w || !xn || !counter || N % 8) return LLJ_EINVAL;
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K;
+  p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)x; p.ldc = ldx;
+  p.nn_w = (const bf16_t*)norm_w; p.nn_eps = eps; p.nn_out = (bf16_t*)xn; p.nn_rs = rowsum; p.nn_ctr = counter;
+  return run<EP_RESID>(wfmt, p, stream);
+}
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
                      int N, int K, const void* i8ws, int i8_row0, double* nstat_out, void* stream) {
   GemvParams p{};

@@ -81,6 +81,11 @@ I8_ROWS = 8     # int8 kernels quantize <= 8 rows in LDS
 # write-through stores each producer must drain before signalling take 6-10 us to be
 # acknowledged while the weight stream saturates the fabric. Off by default.
 CHAIN_LAYERS = False
+# batched rows: fold each RMSNorm into the residual GEMV before it (llj_linear_resid_norm, the
+# last workgroup normalizes) instead of a separate llj_rmsnorm_rows launch. Correct (tested)
+# but measured slower at 7B bs=8 (3.0 vs 2.2 ms/step): the write-through x stores every
+# workgroup must drain, plus the last workgroup's serial pass, cost more than the launch.
+FUSE_RESID_NORM = False
 
 
 def _wspec(lin: nn.Module):
@@ -120,6 +125,11 @@ class _Work:
         self.pre = M >= 2 and not need_i8
         self.xn = torch.empty(M, C, dtype=bf, device=device) if (need_i8 or self.pre) else None
         self.rs = torch.empty(M, dtype=torch.float32, device=device) if self.pre else None
+        # completion counter of llj_linear_resid_norm (M <= 8): the residual GEMV's last
+        # workgroup writes the next RMSNorm into xn / rs (kernel leaves it 0)
+        self.nctr = (torch.zeros(4, dtype=torch.int32, device=device)
+                     if FUSE_RESID_NORM and self.pre and M <= 8 else None)
+        self.xn_ready = False  # xn / rs hold the norm the next op needs (set by a fused resid)
         if need_i8:
             L = _hip.lib()
             nb = max(L.llj_i8_ws_bytes(M, C), L.llj_i8_ws_bytes(M, H))
@@ -271,6 +281,7 @@ class LLaMA(nn.Module):
         M = B * T
         rope = self.rope_cache
         P = _hip.ptr
+        w.xn_ready = False  # the embedding (or caller) just wrote a fresh x
         chained = T == 1 and M <= QKV_ROWS and w.nst is not None and CHAIN_LAYERS
         if chained:
             w.ctr.zero_()
@@ -296,8 +307,9 @@ class LLaMA(nn.Module):
                 src, nw = w.xn, None
             elif w.pre:
                 rs = w.rs if fa == 0 else None
-                _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
-                          w.xn.data_ptr(), P(rs), M, C, st)
+                if not w.xn_ready:
+                    _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
+                              w.xn.data_ptr(), P(rs), M, C, st)
                 src, nw = w.xn, None
             else:
                 src, nw = w.x, blk.rms_1.scale.data_ptr()
@@ -309,8 +321,15 @@ class LLaMA(nn.Module):
             # 2. attention
             _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(), pos.data_ptr(),
                       B, T, nh, C // nh, S, st)
-            # 3. c_proj + residual (+ rms_2 row statistics)
-            self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst_ptr(1))
+            # 3. c_proj + residual (+ rms_2 row statistics, or rms_2 itself for batched rows)
+            w.xn_ready = False
+            if w.nctr is not None and fp in (0, 1) and f1 in (0, 1):
+                _hip.call("llj_linear_resid_norm", fp, w.y.data_ptr(), C, wp.data_ptr(), P(sp), w.x.data_ptr(), C, M,
+                          C, C, blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(), w.rs.data_ptr(),
+                          w.nctr.data_ptr(), st)
+                w.xn_ready = True
+            else:
+                self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst_ptr(1))
             # 4. rms_2 + fc1/fc2 + silu*mul
             if f1 != f2:
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")
@@ -322,8 +341,9 @@ class LLaMA(nn.Module):
                 src, nw, step = w.xn, None, I8_ROWS
             elif w.pre:
                 rs = w.rs if f1 == 0 else None
-                _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
-                          w.xn.data_ptr(), P(rs), M, C, st)
+                if not w.xn_ready:
+                    _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
+                              w.xn.data_ptr(), P(rs), M, C, st)
                 src, nw, step = w.xn, None, QKV_ROWS
             else:
                 src, nw, step = w.x, blk.rms_2.scale.data_ptr(), QKV_ROWS
@@ -332,8 +352,18 @@ class LLaMA(nn.Module):
                 _hip.call("llj_norm_swiglu", f1, src[r0].data_ptr(), nw, blk.rms_2.eps, w1.data_ptr(), P(s1),
                           w2.data_ptr(), P(s2), w.h[r0].data_ptr(), r, H, C, P(w.i8ws), r0, w.nst_ptr(1),
                           C // 16, None if rs is None else rs[r0].data_ptr(), st)
-            # 5. mlp.c_proj + residual (+ next rms_1 / ln_f row statistics)
-            self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st, w.nst_ptr(0))
+            # 5. mlp.c_proj + residual (+ next rms_1 / ln_f row statistics, or that norm itself)
+            last = i + 1 == len(self.transformer.h)
+            nxt_norm = self.transformer.ln_f if last else self.transformer.h[i + 1].rms_1
+            nxt_fmt = specs["head"][0] if last else specs["layers"][i + 1][0][0]
+            w.xn_ready = False
+            if w.nctr is not None and fd in (0, 1) and nxt_fmt in (0, 1):
+                _hip.call("llj_linear_resid_norm", fd, w.h.data_ptr(), H, wd.data_ptr(), P(sd), w.x.data_ptr(), C, M,
+                          C, H, nxt_norm.scale.data_ptr(), nxt_norm.eps, w.xn.data_ptr(), w.rs.data_ptr(),
+                          w.nctr.data_ptr(), st)
+                w.xn_ready = True
+            else:
+                self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st, w.nst_ptr(0))
 
     def _resid(self, f, A, W, sz, x, M, N, K, w, st, nst_out=None):
         if f == 2:
@@ -355,6 +385,9 @@ class LLaMA(nn.Module):
             xn = torch.empty_like(x)
             _hip.call("llj_rmsnorm", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), M, C, st)
             self._i8_prep(xn, M, C, w, st)
+            src, nw = xn, None
+        elif M >= 2 and w.xn_ready and x is w.x:  # ln_f already applied by the last mlp.c_proj
+            xn, rs, use_nst = w.xn, (w.rs if f == 0 else None), False
             src, nw = xn, None
         elif M >= 2:  # batched rows: normalize once (see _Work.pre)
             xn = torch.empty_like(x)

@@ -337,3 +337,40 @@ def test_rmsnorm_rows_rowsum_and_int4_rowsum_operand(hip, golden):
     ref = bf16(y2.float().cpu().numpy() @ O.colblock_get_weight(qw, sc, z, 4).T)
     for o in outs:
         assert_bf16_close(o.float().cpu().numpy(), ref, "int4 with/without rowsum")
+
+
+@pytest.mark.parametrize("wfmt", [0, 1])
+@pytest.mark.parametrize("M", [2, 8])
+def test_linear_resid_norm_equals_resid_then_rmsnorm(hip, wfmt, M):
+    """llj_linear_resid_norm (the last workgroup normalizes the updated rows) == llj_linear_resid
+    followed by llj_rmsnorm_rows; repeated calls reuse the self-resetting counter."""
+    rng = np.random.default_rng(40 + M + wfmt)
+    N, K = 512, 1024
+    if wfmt == 0:
+        qw, sc, z = rand_w4(rng, N, K)
+        Wd, szd = repack(hip, qw), sz_of(hip, sc, z)
+    else:
+        Wd, szd = T(bf16(rng.standard_normal((N, K)) / np.sqrt(K)), torch.bfloat16), None
+    A = T(bf16(rng.standard_normal((M, K))), torch.bfloat16)
+    x0 = T(bf16(rng.standard_normal((M, N))), torch.bfloat16)
+    g = T(bf16(rng.uniform(0.5, 1.5, N)), torch.bfloat16)
+    ctr = torch.zeros(4, dtype=torch.int32, device=dev)
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    for rep in range(3):
+        xa, xb = x0.clone(), x0.clone()
+        xn_a, xn_b = torch.empty(M, N, dtype=torch.bfloat16, device=dev), torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        rs_a, rs_b = torch.empty(M, device=dev), torch.empty(M, device=dev)
+        call(hip, "llj_linear_resid", wfmt, A.data_ptr(), K, Wd.data_ptr(), P(szd), xa.data_ptr(), N, M, N, K, None, 0,
+             None, st())
+        call(hip, "llj_rmsnorm_rows", xa.data_ptr(), g.data_ptr(), 1e-5, xn_a.data_ptr(), rs_a.data_ptr(), M, N, st())
+        call(hip, "llj_linear_resid_norm", wfmt, A.data_ptr(), K, Wd.data_ptr(), P(szd), xb.data_ptr(), N, M, N, K,
+             g.data_ptr(), 1e-5, xn_b.data_ptr(), rs_b.data_ptr(), ctr.data_ptr(), st())
+        torch.cuda.synchronize()
+        assert torch.equal(xa, xb)
+        d = (xn_a.float() - xn_b.float()).abs()
+        # same rounding points; only the fp32 order of the sum of squares differs, which can
+        # flip the bf16 rstd of a row in rare cases (then every element of that row moves 1 ulp)
+        assert float(d.max()) <= 2e-2 * float(xn_a.float().abs().max())
+        assert int((d > 0).sum()) <= N * 1 + 0 or torch.equal(xn_a, xn_b)
+        np.testing.assert_allclose(rs_b.cpu().numpy(), rs_a.cpu().numpy(), rtol=1e-4, atol=1e-2)
+        assert int(ctr.sum()) == 0
