@@ -295,6 +295,8 @@ def main():
     ap.add_argument("--max-seq-length", type=int, default=144)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bs8", action="store_true")
+    ap.add_argument("--only-dominant", action="store_true",
+                    help="profiling aid: only the dominant-kernel loop (for the PMC traffic passes)")
     args = ap.parse_args()
 
     rank, ws, local_rank = dist_init()
@@ -306,6 +308,10 @@ def main():
     model = build_model(args.model, mode)
     S = args.max_seq_length
 
+    if args.only_dominant:
+        k_s, k_bytes = time_dominant_kernel(model, args.batch)
+        print(json.dumps({"dominant_avg_us": round(k_s * 1e6, 2), "bytes_per_launch": k_bytes}), flush=True)
+        return
     r = time_decode(model, args.batch, args.prompt_len, S, args.warmup, args.steps, ws)
     t_max, tokens = aggregate(r["seconds"], r["tokens"], ws, dev)
     value = tokens / t_max
