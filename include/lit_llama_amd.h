@@ -35,9 +35,19 @@ int llj_w4_unpack(const void* packed, void* qweight_ref, int N, int K, void* str
  * dtype: 0 fp32, 1 bf16, 2 fp16. */
 int llj_w4_scale_zero(const void* scales, const void* zeros, int dtype, void* sz, int N, void* stream);
 
+/* ---------------------------------------------------------------- int8 (gptq.int8) weight layout
+ * ColBlockQuantizedLinear(bits=8, tile_cols=-1) (quantization.py:338-409, utils.py:182-184):
+ * `quant_weight` is the logical (N, K) uint8 tensor stored column-major (= physical row-major
+ * (K, N)), one code per byte. The GEMV consumes "W8P": per 16 columns x 128 k, the W4P tile of
+ * the low nibbles followed by the W4P tile of the high nibbles (2 KiB). `packed` holds N*K
+ * bytes. sz[2n] = scales[n], sz[2n+1] = 2176 + zeros[n] (the W8P magic offset). */
+int llj_w8_repack(const void* qweight_ref, void* packed, int N, int K, void* stream);
+int llj_w8_scale_zero(const void* scales, const void* zeros, int dtype, void* sz, int N, void* stream);
+
 /* ---------------------------------------------------------------- linear layers
  * wfmt: 0 = int4 W4P (sz = (scale, 128+zero) pairs required), 1 = bf16 (N, K) row-major
- * (torch.nn.Linear.weight), 2 = LLM.int8() CB (N, K) int8 with sz = SCB (N) fp32; for
+ * (torch.nn.Linear.weight), 2 = LLM.int8() CB (N, K) int8 with sz = SCB (N) fp32,
+ * 3 = gptq.int8 W8P (sz = (scale, 2176+zero) pairs, llj_w8_scale_zero); for
  * wfmt 2, `i8ws` is the statistics workspace llj_i8_stats filled for the whole activation
  * and `i8_row0` the index of this call's first row in it (NULL / 0 otherwise).
  * C[M, N] = A[M, K] . W^T (+ bias), bf16 in/out, fp32 (int8: int32) accumulation,
@@ -104,7 +114,7 @@ int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, cons
 
 /* ---------------------------------------------------------------- one decode layer, one launch
  * Block.forward (model.py:162-175) for a decode step (T = 1, M = B <= 8 rows) with int4 W4P
- * (wfmt 0) or bf16 (wfmt 1) linears: rms_1 + c_attn + RoPE + KV write -> attention -> c_proj +
+ * (wfmt 0), bf16 (wfmt 1) or int8 W8P (wfmt 3, always as separate launches) linears: rms_1 + c_attn + RoPE + KV write -> attention -> c_proj +
  * residual -> rms_2 + c_fc1/c_fc2 + silu*mul -> mlp.c_proj + residual. Same math and results
  * as the five entry points above; when the shapes allow, all five run in ONE launch whose
  * consumer workgroups start streaming their weights before their producer op has finished

@@ -22,6 +22,12 @@
 //    row sums of A, computed by an extra MFMA against a ones fragment:
 //      y[m,n] = s[n] * (sum_k A[m,k] (128 + q[k,n]) - (128 + z[n]) * sum_k A[m,k])
 //             = sum_k A[m,k] * (q[k,n] - z[n]) * s[n]          (get_weight semantics)
+//  * WF_W8 — gptq.int8 (ColBlock bits=8): the 8-bit codes as two int4 planes in the W4P
+//    layout, per (n-tile, k-chunk) 2 KiB = [low nibbles 1 KiB][high nibbles 1 KiB]. The low
+//    nibble dequantizes to bf16 128 + lo (exponent 0x43), the high one to 2048 + 16 hi
+//    (exponent 0x45, same v_and_or_b32), both into ONE accumulator:
+//      sum_k A (128 + lo) + A (2048 + 16 hi) = sum_k A q + 2176 sum_k A,
+//    so y = s * (acc - (2176 + z) * sum_k A), the W4 epilogue with offset 2176.
 //  * WF_BF16 — torch.nn.Linear weight (N, K) row-major bf16, read in place.
 //  * WF_I8 — LLM.int8(): CB (N, K) int8 row-quantized weight + SCB (N) fp32. A is quantized
 //    per row in the prologue (absmax over non-outlier elements, outlier columns zeroed,
@@ -37,7 +43,7 @@
 
 namespace llj {
 
-enum : int { WF_W4 = 0, WF_BF16 = 1, WF_I8 = 2 };
+enum : int { WF_W4 = 0, WF_BF16 = 1, WF_I8 = 2, WF_W8 = 3 };
 enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2 };
 enum : int { EP_STORE = 0, EP_RESID = 1, EP_QKV = 2, EP_SWIGLU = 3 };
 
@@ -49,9 +55,9 @@ struct GemvParams {
   const bf16_t* norm_w;  // AM_NORM: RMSNorm scale (K)
   float eps;
   int M, N, K;
-  const void* W;   // WF_W4: W4P tiles; WF_BF16: (N, K) bf16; WF_I8: (N, K) int8
+  const void* W;   // WF_W4: W4P tiles; WF_W8: W8P tiles; WF_BF16: (N, K) bf16; WF_I8: (N, K) int8
   const void* W2;  // EP_SWIGLU: c_fc2
-  const float2* sz;   // WF_W4: per column (scale, 128 + zero); WF_I8: (const float*) SCB
+  const float2* sz;   // WF_W4 / WF_W8: per column (scale, 128 / 2176 + zero); WF_I8: (const float*) SCB
   const float2* sz2;
   const bf16_t* bias;  // optional (N)
   bf16_t* C;  // EP_STORE / EP_SWIGLU: out (M, ldc); EP_RESID: residual stream updated in place
@@ -86,8 +92,8 @@ struct GemvParams {
 };
 
 // ------------------------------------------------------------------------------------
-// Stage A rows [0, M) into LDS (row stride K + 8 elements; MFMA lanes of rows >= M use zero
-// registers instead of reading LDS). With NORM, rows are RMS-normalised with the reference's bf16
+// Stage A rows [0, M) into LDS (row stride K + 8 elements; MFMA lanes of rows >= M read row 0
+// and their output rows are discarded). With NORM, rows are RMS-normalised with the reference's bf16
 // rounding points (model.py:281-283 evaluated on bf16 tensors).
 __device__ __forceinline__ float rms_rstd(float sumsq_over_k, float eps) {
   // bf16: mean(x*x) -> +eps -> rsqrt, each rounded (torch bf16 ops, model.py:281-282)
@@ -205,7 +211,7 @@ __device__ __forceinline__ bf16x8 dequant_w4(uint32_t w, uint32_t msk, uint32_t 
 template <int WF>
 __device__ __forceinline__ int kofs(int t, int grp) {
   // k offset inside a 128-deep chunk of the elements lane-group `grp` feeds at MFMA step t
-  return WF == WF_W4 ? 32 * grp + 8 * t : WF == WF_BF16 ? 32 * t + 8 * grp : 64 * t + 16 * grp;
+  return (WF == WF_W4 || WF == WF_W8) ? 32 * grp + 8 * t : WF == WF_BF16 ? 32 * t + 8 * grp : 64 * t + 16 * grp;
 }
 
 // fp16 side product of LLM.int8() over the outlier columns, for this workgroup's 16 columns
@@ -404,6 +410,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
                                           const ChainCtl& cc) {
   constexpr bool DUAL = (EP == EP_SWIGLU);
   constexpr bool I8 = (WF == WF_I8);
+  constexpr bool W4L = (WF == WF_W4 || WF == WF_W8);  // nibble-coded: offset removed with row sums
   constexpr bool ALDS = I8 || (AM != AM_GLOBAL);
   constexpr int WV = (WF == WF_W4) ? 1 : (WF == WF_BF16 ? 4 : 2);  // 16-B loads per lane per chunk per matrix
   constexpr int NSTEP = I8 ? 2 : 4;
@@ -425,7 +432,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   const bool arow = row < M;
   const unsigned char* abase;  // byte address of this lane's A row
   if (ALDS) {
-    abase = smem + (size_t)(arow ? row : 0) * a_stride * (I8 ? 1 : 2);  // rows >= M read as zeros
+    abase = smem + (size_t)(arow ? row : 0) * a_stride * (I8 ? 1 : 2);  // rows >= M read row 0 (outputs discarded)
   } else {
     abase = reinterpret_cast<const unsigned char*>(p.A + (size_t)(arow ? row : 0) * p.lda);
   }
@@ -433,9 +440,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
 
   // mask in an SGPR and magic in a VGPR, hidden from constant folding (empty asm, no
   // instruction) so that (w & msk) | mag selects one v_and_or_b32 (no literal in VOP3 on gfx9)
-  uint32_t msk = 0x000F000Fu, mag = 0x43004300u;
+  uint32_t msk = 0x000F000Fu, mag = 0x43004300u, mag_hi = 0x45004500u;  // mag_hi: WF_W8 high nibbles, 2048 + 16 hi
   asm volatile("" : "+s"(msk));
   asm volatile("" : "+v"(mag));
+  if constexpr (WF == WF_W8) asm volatile("" : "+v"(mag_hi));
   const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
   const u32x4 zero4 = {0, 0, 0, 0};
 
@@ -448,6 +456,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     w1 = reinterpret_cast<const u32x4*>(p.W) + (size_t)nt * KC * 64 + lane;
     if (DUAL) w2 = reinterpret_cast<const u32x4*>(p.W2) + (size_t)nt * KC * 64 + lane;
     wstep = 64; vstride = 0;
+  } else if (WF == WF_W8) {  // 2 KiB per (tile, chunk): low plane, then high plane
+    w1 = reinterpret_cast<const u32x4*>(p.W) + (size_t)nt * KC * 128 + lane;
+    if (DUAL) w2 = reinterpret_cast<const u32x4*>(p.W2) + (size_t)nt * KC * 128 + lane;
+    wstep = 128; vstride = 64;
   } else if (WF == WF_BF16) {
     const size_t off = (size_t)(n0 + row) * K + 8 * grp;  // elements
     w1 = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.W) + off);
@@ -477,7 +489,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     if (!ALDS) {
 #pragma unroll
       for (int t = 0; t < NSTEP; ++t)
-        ra[d][t] = arow ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : zero4;
+        ra[d][t] = *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp)));  // rows >= M: row 0
     }
   };
   auto compute = [&](int d, int i) {
@@ -489,13 +501,23 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     }
 #pragma unroll
     for (int t = 0; t < NSTEP; ++t) {
-      const u32x4 av = ALDS ? (arow ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : zero4)
-                            : ra[d][t];
+      // LDS lanes of rows >= M read row 0 (abase clamped): their output rows are never stored, and
+      // an unconditional read keeps the hot loop free of divergent LDS accesses
+      const u32x4 av = ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
       if constexpr (WF == WF_W4) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
         acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
         if (DUAL) acc2 = mfma_bf16(a, dequant_w4(r2[d][0][t], msk, mag), acc2);
         if (!ALDS && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);  // else: row sums from the prologue / caller
+      } else if constexpr (WF == WF_W8) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+        acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
+        acc = mfma_bf16(a, dequant_w4(r1[d][1][t], msk, mag_hi), acc);
+        if (DUAL) {
+          acc2 = mfma_bf16(a, dequant_w4(r2[d][0][t], msk, mag), acc2);
+          acc2 = mfma_bf16(a, dequant_w4(r2[d][1][t], msk, mag_hi), acc2);
+        }
+        if (!ALDS && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);
       } else if constexpr (WF == WF_BF16) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
         acc = mfma_bf16(a, __builtin_bit_cast(bf16x8, r1[d][t]), acc);
@@ -526,10 +548,16 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   };
   float2 e_a = make_float2(1.f, 0.f), e_b = make_float2(1.f, 0.f);
   bf16_t e_braw = 0;
+  float e_rs[4] = {0.f, 0.f, 0.f, 0.f};  // caller's row sums (p.rowsum) of rows 4*grp + r
   auto issue_const = [&]() {  // weights-side epilogue operands (never written in a launch)
-    if constexpr (WF == WF_W4) {
+    if constexpr (W4L) {
       e_a = p.sz[n];
       if (DUAL) e_b = p.sz2[n];
+      // an epilogue load under divergent control flow would put a vmcnt(0) between the
+      // row stores (stores count in vmcnt): read the row sums here, from a valid address
+      const float* rsp = p.rowsum ? p.rowsum : reinterpret_cast<const float*>(p.sz);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) e_rs[r] = rsp[4 * grp + r < M ? 4 * grp + r : M - 1];
     } else if constexpr (I8) {
       e_a.x = reinterpret_cast<const float*>(p.sz)[n];
       if (DUAL) e_b.x = reinterpret_cast<const float*>(p.sz2)[n];
@@ -671,14 +699,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
               o = __builtin_bit_cast(u32x4, nv);
             }
             *reinterpret_cast<u32x4*>(As + (size_t)m * a_stride + 8 * v) = o;
-            if (WF == WF_W4 && !p.rowsum) {
+            if (W4L && !p.rowsum) {
 #pragma unroll
               for (int i = 0; i < 4; ++i) rsum += bflo(o[i]) + bfhi(o[i]);
             }
           }
         }
       }
-      if (WF == WF_W4 && m < M && !p.rowsum) {
+      if (W4L && m < M && !p.rowsum) {
         rsum = wave_sum(rsum);
         if (lane == 0) tail[96 + wave * 8 + m] = rsum;
       }
@@ -734,7 +762,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     if (rs == 0) {
       stage_a<NW, AM == AM_NORM>(p, reinterpret_cast<bf16_t*>(smem), a_stride, tail);
       __syncthreads();
-      if (WF == WF_W4 && !p.rowsum) {  // row sums of the staged rows (offset removal, see header)
+      if (W4L && !p.rowsum) {  // row sums of the staged rows (offset removal, see header)
         const bf16_t* As = reinterpret_cast<const bf16_t*>(smem);
         for (int m = 0; m < M; ++m) {
           float rsum = 0.f;
@@ -758,15 +786,25 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     }
   }
   LLJ_STAMP(2);
-  if (nmy > 0) {
-    for (int i0 = 0; i0 < nmy; i0 += D) {
+  // chunk i lives in buffer i % D; after computing it the buffer is refilled with chunk i + D.
+  // The steady loop runs while every refill is a real chunk; the peeled tail (< 2D chunks)
+  // issues no loads past the last chunk, so nothing is in flight when the epilogue waits.
+  int i0 = 0;
+  for (; i0 + 2 * D <= nmy; i0 += D) {
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
-        if (i0 + d < nmy) compute(d, i0 + d);
-        load(d, i0 + d + D);
-      }
+    for (int d = 0; d < D; ++d) {
+      compute(d, i0 + d);
+      load(d, i0 + d + D);
     }
   }
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    if (i0 + d < nmy) compute(d, i0 + d);
+    if (i0 + d + D < nmy) load(d, i0 + d + D);
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (i0 + D + d < nmy) compute(d, i0 + D + d);
   LLJ_STAMP(3);
   // ---- reduce the NW partial tiles in LDS (each wave: 64 lanes x 12 words; int8 sums stay
   // int32 — they exceed 2^24 at K = 11008, so they must not round-trip through fp32)
@@ -837,10 +875,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   for (int r = 0; r < 4; ++r) {
     const int m = 4 * grp + r;
     float y, y2 = 0.f;
-    if (WF == WF_W4) {
+    if (W4L) {
       float sa = sacc[r];
       if (p.rowsum) {
-        sa = m < M ? p.rowsum[m] : 0.f;
+        sa = e_rs[r];  // rows >= M hold a clamped copy; their outputs are not stored
       } else if constexpr (ALDS) {
         sa = 0.f;
         if (m < M) {
@@ -1015,6 +1053,11 @@ static int dispatch(int wf, int am, const GemvParams& p, hipStream_t s) {
     if (am == AM_LDS) return launch<WF_W4, AM_LDS, EP>(p, s);
     return launch<WF_W4, AM_GLOBAL, EP>(p, s);
   }
+  if (wf == WF_W8) {
+    if (am == AM_NORM) return launch<WF_W8, AM_NORM, EP>(p, s);
+    if (am == AM_LDS) return launch<WF_W8, AM_LDS, EP>(p, s);
+    return launch<WF_W8, AM_GLOBAL, EP>(p, s);
+  }
   if (am == AM_NORM) return launch<WF_BF16, AM_NORM, EP>(p, s);
   if (am == AM_LDS) return launch<WF_BF16, AM_LDS, EP>(p, s);
   return launch<WF_BF16, AM_GLOBAL, EP>(p, s);
@@ -1029,7 +1072,7 @@ static int pick_am(int wf, const GemvParams& p) {
 
 static int check_shape(int wf, const GemvParams& p) {
   if (p.M < 1 || p.M > 16 || p.N % 16 || p.K % 128 || p.K < 128) return LLJ_EINVAL;
-  if (wf != WF_W4 && wf != WF_BF16 && wf != WF_I8) return LLJ_EINVAL;
+  if (wf != WF_W4 && wf != WF_BF16 && wf != WF_I8 && wf != WF_W8) return LLJ_EINVAL;
   if (wf != WF_BF16 && !p.sz) return LLJ_EINVAL;
   if (p.C && (p.ldc & 1)) return LLJ_EINVAL;  // epilogues store column pairs as 4-byte words
   return 0;
@@ -1225,11 +1268,12 @@ int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, co
 int llj_decode_layer(const llj_layer* L, void* stream) {
   if (!L) return LLJ_EINVAL;
   const int M = L->M, C = L->C, H = L->H, nh = L->n_head, wf = L->wfmt;
-  if (M < 1 || M > 8 || nh < 1 || C % nh || (wf != WF_W4 && wf != WF_BF16) || !L->counters || !L->err)
+  if (M < 1 || M > 8 || nh < 1 || C % nh || (wf != WF_W4 && wf != WF_BF16 && wf != WF_W8) || !L->counters ||
+      !L->err)
     return LLJ_EINVAL;
   const int hs = C / nh;
   const int parts = C / 16;
-  const bool chain = chain_prologue_ok(AM_NORM, M, C, parts) && chain_prologue_ok(AM_LDS, M, C, 0) &&
+  const bool chain = wf != WF_W8 && chain_prologue_ok(AM_NORM, M, C, parts) && chain_prologue_ok(AM_LDS, M, C, 0) &&
                      (hs == 64 || hs == 128) && (M > 1 || chain_prologue_ok(AM_LDS, M, H, 0));
   hipStream_t st = (hipStream_t)stream;
   if (!chain) {  // the same five ops as separate launches

@@ -11,6 +11,11 @@
 // 16 nt + (l & 15) for k = 128 kc + 32 (l >> 4) + 8 t + j, j = 0..7, with code j at bit
 // 4 (j >> 1) + 16 (j & 1) so that ((dword >> 4 i) & 0x000F000F) is the (j = 2i, 2i+1) pair.
 // Both conversions are exact inverses (tested bit-for-bit).
+//
+// W8P (gptq.int8, ColBlock bits=8): the reference buffer is the logical (N, K) uint8 tensor
+// stored column-major = physically row-major (K, N), one code per byte. Tile (nt, kc) is 2 KiB
+// at (nt * K/128 + kc) * 2048: the W4P tile of the low nibbles, then the W4P tile of the high
+// nibbles (gemv.hip WF_W8 streams both with one 16-B load each per lane).
 #include "common.h"
 
 namespace llj {
@@ -39,6 +44,28 @@ __global__ void w4_repack_kernel(const uint8_t* __restrict__ ref, uint32_t* __re
   }
 }
 
+__global__ void w8_repack_kernel(const uint8_t* __restrict__ ref, uint32_t* __restrict__ out, int N, int K) {
+  const size_t total = (size_t)N * K / 4;  // dwords (two nibble planes)
+  const int KC = K >> 7;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int t = (int)(i & 3);
+    const int l = (int)((i >> 2) & 63);
+    const int hi = (int)((i >> 8) & 1);
+    const size_t tile = i >> 9;
+    const int kc = (int)(tile % KC);
+    const int nt = (int)(tile / KC);
+    const int n = nt * 16 + (l & 15);
+    const int k0 = kc * 128 + 32 * (l >> 4) + 8 * t;
+    uint32_t d = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t b = ref[(size_t)(k0 + j) * N + n];
+      d |= (hi ? b >> 4 : b & 0xF) << w4p_bit(j);
+    }
+    out[i] = d;
+  }
+}
+
 __global__ void w4_unpack_kernel(const uint32_t* __restrict__ in, uint8_t* __restrict__ ref, int N, int K) {
   const size_t total = (size_t)N * K / 2;  // bytes of the reference buffer
   const int KC = K >> 7;
@@ -53,9 +80,10 @@ __global__ void w4_unpack_kernel(const uint32_t* __restrict__ in, uint8_t* __res
   }
 }
 
-// sz[n] = (scale[n], 128 + zero[n]) in fp32 from the module's scale/zero buffers (any of
-// fp32 / bf16 / fp16, given by dtype code 0/1/2; one group per row: tile_cols = -1).
-__global__ void w4_sz_kernel(const void* scales, const void* zeros, int dtype, float2* sz, int N) {
+// sz[n] = (scale[n], off + zero[n]) in fp32 from the module's scale/zero buffers (any of
+// fp32 / bf16 / fp16, given by dtype code 0/1/2; one group per row: tile_cols = -1); off is the
+// magic-exponent offset of the format (W4P 128, W8P 128 + 2048).
+__global__ void w4_sz_kernel(const void* scales, const void* zeros, int dtype, float2* sz, int N, float off) {
   int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   float s, z;
@@ -66,7 +94,7 @@ __global__ void w4_sz_kernel(const void* scales, const void* zeros, int dtype, f
   } else {
     s = (float)((const _Float16*)scales)[n]; z = (float)((const _Float16*)zeros)[n];
   }
-  sz[n] = make_float2(s, 128.f + z);
+  sz[n] = make_float2(s, off + z);
 }
 
 }  // namespace llj
@@ -98,7 +126,25 @@ int llj_w4_unpack(const void* packed, void* qweight_ref, int N, int K, void* str
 int llj_w4_scale_zero(const void* scales, const void* zeros, int dtype, void* sz, int N, void* stream) {
   LLJ_REQUIRE(N > 0 && dtype >= 0 && dtype <= 2);
   hipLaunchKernelGGL(w4_sz_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, scales, zeros, dtype,
-                     (float2*)sz, N);
+                     (float2*)sz, N, 128.f);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_w8_repack(const void* qweight_ref, void* packed, int N, int K, void* stream) {
+  LLJ_REQUIRE(N > 0 && K > 0 && N % 16 == 0 && K % 128 == 0);
+  const size_t total = (size_t)N * K / 4;
+  int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  hipLaunchKernelGGL(w8_repack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)qweight_ref,
+                     (uint32_t*)packed, N, K);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_w8_scale_zero(const void* scales, const void* zeros, int dtype, void* sz, int N, void* stream) {
+  LLJ_REQUIRE(N > 0 && dtype >= 0 && dtype <= 2);
+  hipLaunchKernelGGL(w4_sz_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, scales, zeros, dtype,
+                     (float2*)sz, N, 2176.f);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

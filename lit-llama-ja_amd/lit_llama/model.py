@@ -88,6 +88,10 @@ CHAIN_LAYERS = False
 FUSE_RESID_NORM = False
 
 
+# weight formats whose kernels remove the nibble offset with the row sums of A (W4P, W8P)
+_ROWSUM_FMTS = (0, 3)
+
+
 def _wspec(lin: nn.Module):
     """(wfmt, weight operand, scale operand) of a Linear for the HIP kernels."""
     if hasattr(lin, "_wspec"):
@@ -306,7 +310,7 @@ class LLaMA(nn.Module):
                 self._i8_prep(w.xn, M, C, w, st)
                 src, nw = w.xn, None
             elif w.pre:
-                rs = w.rs if fa == 0 else None
+                rs = w.rs if fa in _ROWSUM_FMTS else None
                 if not w.xn_ready:
                     _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
                               w.xn.data_ptr(), P(rs), M, C, st)
@@ -340,7 +344,7 @@ class LLaMA(nn.Module):
                 self._i8_prep(w.xn, M, C, w, st)
                 src, nw, step = w.xn, None, I8_ROWS
             elif w.pre:
-                rs = w.rs if f1 == 0 else None
+                rs = w.rs if f1 in _ROWSUM_FMTS else None
                 if not w.xn_ready:
                     _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
                               w.xn.data_ptr(), P(rs), M, C, st)
@@ -387,11 +391,11 @@ class LLaMA(nn.Module):
             self._i8_prep(xn, M, C, w, st)
             src, nw = xn, None
         elif M >= 2 and w.xn_ready and x is w.x:  # ln_f already applied by the last mlp.c_proj
-            xn, rs, use_nst = w.xn, (w.rs if f == 0 else None), False
+            xn, rs, use_nst = w.xn, (w.rs if f in _ROWSUM_FMTS else None), False
             src, nw = xn, None
         elif M >= 2:  # batched rows: normalize once (see _Work.pre)
             xn = torch.empty_like(x)
-            rs = torch.empty(M, dtype=torch.float32, device=x.device) if f == 0 else None
+            rs = torch.empty(M, dtype=torch.float32, device=x.device) if f in _ROWSUM_FMTS else None
             _hip.call("llj_rmsnorm_rows", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), _hip.ptr(rs), M,
                       C, st)
             src, nw, use_nst = xn, None, False

@@ -3,9 +3,12 @@
 Drop-in for reference lit_llama/quantization.py:
   * ColBlockQuantizedLinear (338-421): same constructor, buffers and state_dict keys
     (`quant_weight` (N, K*bits/8) uint8 column-major, `scales`, `zeros`, `bias`); forward
-    runs the gfx950 int4 GEMV on a repacked copy of `quant_weight` (W4P layout, see
-    csrc/w4pack.hip) kept as a non-persistent buffer and refreshed whenever the reference
-    buffers change.
+    runs the gfx950 GEMV on a repacked copy of `quant_weight` (bits=4: W4P layout, bits=8:
+    W8P = two nibble planes in W4P tiles; csrc/w4pack.hip) kept as a non-persistent buffer
+    and refreshed whenever the reference buffers change. The reference computes bits=8 (and
+    any non-Triton case) as F.linear(inp, get_weight(inp.dtype)) (409-421), i.e. with weights
+    rounded to bf16((q - z) * s); the kernel applies s to the exact integer sum instead
+    (difference <= 1 bf16 ulp per weight, covered by the tests' tolerance).
   * Linear8bitLt (36-75): nn.Linear-compatible constructor; the weight is re-quantized to
     LLM.int8() row-wise int8 (CB, SCB) at construction and on load_state_dict; forward is
     the int8 MFMA GEMV with the fp16 outlier-column side product (threshold 6.0).
@@ -97,7 +100,7 @@ class ColBlockQuantizedLinear(torch.nn.Module):
 
     # ---- HIP path ---------------------------------------------------------------------
     def _supported(self) -> bool:
-        return self.bits == 4 and self.scales.shape[1] == 1 and self.out_features % 16 == 0 \
+        return self.bits in (4, 8) and self.scales.shape[1] == 1 and self.out_features % 16 == 0 \
             and self.in_features % 128 == 0
 
     def _prepare(self):
@@ -112,27 +115,34 @@ class ColBlockQuantizedLinear(torch.nn.Module):
             raise NotImplementedError(
                 f"ColBlockQuantizedLinear(bits={self.bits}, groups={self.scales.shape[1]}, "
                 f"{self.in_features}->{self.out_features}) has no HIP kernel yet "
-                "(gptq.int4 with tile_cols=-1, N % 16 == 0, K % 128 == 0 is supported)")
+                "(gptq.int4 / gptq.int8 with tile_cols=-1, N % 16 == 0, K % 128 == 0 is supported)")
         N, K = self.out_features, self.in_features
         s = _hip.stream()
-        ref = qw.t()  # physical (K/2, N) row-major when quant_weight keeps the reference strides
+        ref = qw.t()  # physical (K*bits/8, N) row-major when quant_weight keeps the reference strides
         if not ref.is_contiguous():
             ref = ref.contiguous()
-        if self._w4p is None or self._w4p.numel() != N * K // 2 or self._w4p.device != qw.device:
-            self._w4p = torch.empty(N * K // 2, dtype=torch.uint8, device=qw.device)
+        nbytes = N * K * self.bits // 8
+        if self._w4p is None or self._w4p.numel() != nbytes or self._w4p.device != qw.device:
+            self._w4p = torch.empty(nbytes, dtype=torch.uint8, device=qw.device)
             self._sz = torch.empty(N, 2, dtype=torch.float32, device=qw.device)
-        _hip.call("llj_w4_repack", ref.data_ptr(), self._w4p.data_ptr(), N, K, s)
+        _hip.call("llj_w4_repack" if self.bits == 4 else "llj_w8_repack", ref.data_ptr(), self._w4p.data_ptr(),
+                  N, K, s)
         sc1, zr1 = sc.reshape(N).contiguous(), zr.reshape(N).contiguous()
         if sc1.dtype not in _DTYPE_CODE or zr1.dtype != sc1.dtype:
             sc1, zr1 = sc1.float(), zr1.float()
-        _hip.call("llj_w4_scale_zero", sc1.data_ptr(), zr1.data_ptr(), _DTYPE_CODE[sc1.dtype], self._sz.data_ptr(),
-                  N, s)
+        _hip.call("llj_w4_scale_zero" if self.bits == 4 else "llj_w8_scale_zero", sc1.data_ptr(), zr1.data_ptr(),
+                  _DTYPE_CODE[sc1.dtype], self._sz.data_ptr(), N, s)
         self._key = key
 
     def _wspec(self):
         """(wfmt, weight operand, sz operand) for the fused model kernels."""
         self._prepare()
-        return 0, self._w4p, self._sz
+        return self.wfmt, self._w4p, self._sz
+
+    @property
+    def wfmt(self) -> int:
+        """C-ABI weight format: 0 = W4P (bits=4), 3 = W8P (bits=8)."""
+        return 0 if self.bits == 4 else 3
 
     def forward(self, inp):
         _hip.require_device(inp, "input")
@@ -143,7 +153,7 @@ class ColBlockQuantizedLinear(torch.nn.Module):
         x2 = _as_rows(inp, K)
         out = torch.empty((x2.shape[0], N), dtype=inp.dtype, device=inp.device)
         bias = None if self.bias is None else self.bias.to(torch.bfloat16)
-        _linear_rows(0, x2, self._w4p, self._sz, bias, out, N, K)
+        _linear_rows(self.wfmt, x2, self._w4p, self._sz, bias, out, N, K)
         return out.reshape(*inp.shape[:-1], N)
 
 

@@ -19,6 +19,20 @@ def w4p_pack_np(qw_logical: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(d).reshape(-1).view(np.uint8)
 
 
+def w8p_pack_np(qw_logical: np.ndarray) -> np.ndarray:
+    """Host restatement of the W8P layout (csrc/w4pack.hip) from the reference's logical (N, K)
+    int8-code byte array (ColBlock bits=8): per (16-column tile, 128-k chunk) the W4P tile of
+    the low nibbles, then the W4P tile of the high nibbles. Returns uint8 (N*K,)."""
+    N, K = qw_logical.shape
+
+    def as_w4_logical(nib):  # (N, K) nibbles -> the (N, K/2) int4 byte array of the same codes
+        return (nib[:, 0::2] | (nib[:, 1::2] << 4)).astype(np.uint8)
+
+    lo = w4p_pack_np(as_w4_logical(qw_logical & 0xF)).reshape(-1, 1024)
+    hi = w4p_pack_np(as_w4_logical(qw_logical >> 4)).reshape(-1, 1024)
+    return np.ascontiguousarray(np.stack([lo, hi], 1)).reshape(-1)
+
+
 def bf16(x):
     return O.bf16_round(np.asarray(x, np.float32))
 

@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from oracle import llama_np as O
-from tests.helpers import assert_bf16_close, bf16, w4p_pack_np
+from tests.helpers import assert_bf16_close, bf16, w4p_pack_np, w8p_pack_np
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
@@ -46,13 +46,42 @@ def repack(hip, qw):
     return out
 
 
-def sz_of(hip, scales, zeros):
+def sz_of(hip, scales, zeros, bits=4):
     N = scales.shape[0]
     sz = torch.empty(N, 2, dtype=torch.float32, device=dev)
     sd, zd = T(scales), T(zeros)  # keep alive until the kernel ran (caching allocator reuse)
-    call(hip, "llj_w4_scale_zero", sd.data_ptr(), zd.data_ptr(), 0, sz.data_ptr(), N, st())
+    call(hip, "llj_w4_scale_zero" if bits == 4 else "llj_w8_scale_zero", sd.data_ptr(), zd.data_ptr(), 0,
+         sz.data_ptr(), N, st())
     torch.cuda.synchronize()
     return sz
+
+
+def rand_w8(rng, N, K):
+    qw = rng.integers(0, 256, size=(N, K), dtype=np.uint8)
+    scales = rng.uniform(0.5, 1.5, size=(N, 1)).astype(np.float32) * np.float32(0.02 / 127)
+    zeros = rng.integers(0, 256, size=(N, 1)).astype(np.float32)
+    return qw, scales, zeros
+
+
+def repack8(hip, qw):
+    N, K = qw.shape
+    ref = T(qw.T.copy())  # physical (K, N) row-major = the reference's column-major bits=8 buffer
+    out = torch.empty(N * K, dtype=torch.uint8, device=dev)
+    call(hip, "llj_w8_repack", ref.data_ptr(), out.data_ptr(), N, K, st())
+    torch.cuda.synchronize()
+    return out
+
+
+def quant_operands(hip, rng, wfmt, N, K):
+    """(reference fp32 weight (N, K), device weight operand, device sz) for wfmt 0 / 1 / 3."""
+    if wfmt == 0:
+        qw, sc, z = rand_w4(rng, N, K)
+        return O.colblock_get_weight(qw, sc, z, 4), repack(hip, qw), sz_of(hip, sc, z)
+    if wfmt == 3:
+        qw, sc, z = rand_w8(rng, N, K)
+        return O.colblock_get_weight(qw, sc, z, 8), repack8(hip, qw), sz_of(hip, sc, z, 8)
+    W = bf16(rng.standard_normal((N, K)) / np.sqrt(K))
+    return W, T(W, torch.bfloat16), None
 
 
 @pytest.mark.parametrize("N,K", [(16, 128), (160, 384), (48, 1024)])
@@ -97,6 +126,40 @@ def test_w4_linear_shapes(hip, M, N, K):
     x = bf16(rng.standard_normal((M, K)).astype(np.float32))
     got = _linear(hip, 0, T(x, torch.bfloat16), repack(hip, qw), sz_of(hip, sc, z), N, K)
     assert_bf16_close(got, O.qlinear_4bit(x, qw, sc, z), f"int4 M={M} N={N} K={K}")
+
+
+@pytest.mark.parametrize("N,K", [(16, 128), (160, 384), (48, 1024)])
+def test_w8_repack_layout(hip, N, K):
+    rng = np.random.default_rng(3 * N + K)
+    qw = rng.integers(0, 256, size=(N, K), dtype=np.uint8)
+    np.testing.assert_array_equal(repack8(hip, qw).cpu().numpy(), w8p_pack_np(qw))
+
+
+def test_w8_linear_reference_fixture(hip, golden):
+    """gptq.int8: the reference's ColBlockQuantizedLinear(bits=8) buffers (N=160, K=384), its fp32
+    forward on the same inputs, and its bf16 path (get_weight(bf16) + F.linear, quantization.py
+    419-421, the reference's only bits=8 forward)."""
+    g = golden("colblock")
+    qw, sc, z = g["b8_qw"], g["b8_scales"], g["b8_zeros"]
+    N, K = qw.shape
+    Wp, sz = repack8(hip, qw), sz_of(hip, sc, z, 8)
+    Wd = O.colblock_get_weight(qw, sc, z, 8)
+    for M in (1, 3, 8):
+        xb = bf16(g[f"b8_x{M}"])
+        got = _linear(hip, 3, T(xb, torch.bfloat16), Wp, sz, N, K)
+        assert_bf16_close(got, xb @ Wd.T, f"int8 M={M}")
+        assert_bf16_close(got, g[f"b8_y{M}"], f"int8 vs reference fp32 M={M}", rel=3e-2, abs_frac=1e-2)
+        assert_bf16_close(got, g[f"b8_ybf16_{M}"], f"int8 vs reference bf16 M={M}", rel=3e-2, abs_frac=1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 8, 16])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (256, 11008)])
+def test_w8_linear_shapes(hip, M, N, K):
+    rng = np.random.default_rng(M * 5 + N + K)
+    Wref, Wd, sz = quant_operands(hip, rng, 3, N, K)
+    x = bf16(rng.standard_normal((M, K)).astype(np.float32))
+    got = _linear(hip, 3, T(x, torch.bfloat16), Wd, sz, N, K)
+    assert_bf16_close(got, x @ Wref.T, f"int8 (gptq) M={M} N={N} K={K}")
 
 
 @pytest.mark.parametrize("M", [1, 4, 8, 16])
@@ -231,7 +294,7 @@ def test_embedding_and_pos_inc(hip):
     np.testing.assert_allclose(nst.cpu().numpy(), (bf16(wte[idx] ** 2)).sum(-1), rtol=1e-6)
 
 
-@pytest.mark.parametrize("wfmt", [0, 1])
+@pytest.mark.parametrize("wfmt", [0, 1, 3])
 @pytest.mark.parametrize("B,T_", [(1, 1), (8, 1), (2, 5)])
 def test_fused_qkv_rope_kv(hip, wfmt, B, T_):
     rng = np.random.default_rng(wfmt * 10 + B + T_)
@@ -241,13 +304,7 @@ def test_fused_qkv_rope_kv(hip, wfmt, B, T_):
     g = bf16(rng.uniform(0.5, 1.5, C))
     rope = O.build_rope_cache(128, hs)
     pos = np.arange(3, 3 + T_, dtype=np.int32)
-    if wfmt == 0:
-        qw, sc, z = rand_w4(rng, 3 * C, C)
-        Wref = O.colblock_get_weight(qw, sc, z, 4)
-        Wd, szd = repack(hip, qw), sz_of(hip, sc, z)
-    else:
-        Wref = bf16(rng.standard_normal((3 * C, C)) / np.sqrt(C))
-        Wd, szd = T(Wref, torch.bfloat16), None
+    Wref, Wd, szd = quant_operands(hip, rng, wfmt, 3 * C, C)
     q = torch.zeros(B * T_, C, dtype=torch.bfloat16, device=dev)
     kc = torch.zeros(B, nh, S, hs, dtype=torch.bfloat16, device=dev)
     vc = torch.zeros_like(kc)
@@ -274,7 +331,7 @@ def test_fused_qkv_rope_kv(hip, wfmt, B, T_):
     assert not kcn[:, :, untouched].any() and not vcn[:, :, untouched].any()
 
 
-@pytest.mark.parametrize("wfmt", [0, 1])
+@pytest.mark.parametrize("wfmt", [0, 1, 3])
 def test_fused_swiglu_and_resid(hip, wfmt):
     rng = np.random.default_rng(11 + wfmt)
     M, C, H = 3, 256, 768
@@ -282,11 +339,7 @@ def test_fused_swiglu_and_resid(hip, wfmt):
     g = bf16(rng.uniform(0.5, 1.5, C))
 
     def mk(N, K):
-        if wfmt == 0:
-            qw, sc, z = rand_w4(rng, N, K)
-            return O.colblock_get_weight(qw, sc, z, 4), repack(hip, qw), sz_of(hip, sc, z)
-        W = bf16(rng.standard_normal((N, K)) / np.sqrt(K))
-        return W, T(W, torch.bfloat16), None
+        return quant_operands(hip, rng, wfmt, N, K)
 
     W1, W1d, s1 = mk(H, C)
     W2, W2d, s2 = mk(H, C)

@@ -241,6 +241,41 @@ def test_int8_model_vs_restatement():
     assert rel < 3e-2, rel
 
 
+def test_gptq_int8_model_vs_oracle():
+    """gptq.int8 (ColBlockQuantizedLinear bits=8, tile_cols=-1) through quantization(): every
+    Linear packed with the reference's pack_weight semantics (8-bit min/max per row), logits and
+    margin-guarded greedy ids against the oracle running get_weight on the same buffers (the
+    reference's bits=8 forward, quantization.py:419-421)."""
+    cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=2048)
+    p = make_params(cfg, 31)
+    packed, lin = {}, {}
+    for k, v in p.items():
+        if not k.endswith(".weight") or "wte" in k or "rms" in k or "ln_f" in k:
+            continue
+        w = v.astype(np.float32)
+        xmin, xmax = np.minimum(w.min(1), 0), np.maximum(w.max(1), 0)
+        sc = bf16(((xmax - xmin) / 255).astype(np.float32)[:, None])  # the module's scales buffer is bf16
+        z = np.round(-xmin[:, None] / sc).astype(np.float32)
+        q = np.clip(np.round(w / sc) + z, 0, 255)
+        qw = O.colblock_pack(sc * (q - z), sc, z, 8)
+        name = k[:-7]
+        packed.update({name + ".quant_weight": qw, name + ".scales": sc, name + ".zeros": z})
+        lin[name] = O.LinearSpec("colblock", qw=qw, scales=sc, zeros=z, bits=8)
+    m = build(cfg, p, mode="gptq.int8", packed=packed)
+    from lit_llama.quantization import ColBlockQuantizedLinear
+
+    assert isinstance(m.lm_head, ColBlockQuantizedLinear) and m.lm_head.bits == 8
+    prompt = np.random.default_rng(9).integers(3, 2048, 8).astype(np.int32)
+    orc = O.OracleLLaMA(cfg, {k: bf16(v) for k, v in p.items()}, linears=lin, act_bf16=True)
+    oids, olog = O.generate_greedy(orc, prompt, 12, return_logits=True)
+    ids = gen(m, prompt, 12)
+    top = np.sort(olog, -1)[:, ::-1][:, :2]
+    assert guarded(ids, oids, top, len(prompt), tol=0.3) >= 8
+    out = m(torch.from_numpy(prompt[None].astype(np.int64)).cuda()).float().cpu().numpy()[0, -1]
+    rel = np.linalg.norm(out - olog[0]) / np.linalg.norm(olog[0])
+    assert rel < 3e-2, rel
+
+
 def test_bf16_vs_int4_module_forward_paths(golden):
     """ColBlockQuantizedLinear.forward, qlinear_4bit_weight and the fused model path agree."""
     from lit_llama.quantization import qlinear_4bit_weight
