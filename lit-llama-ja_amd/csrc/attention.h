@@ -107,10 +107,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
       float s = 0.f;
 #pragma unroll
       for (int i = 0; i < DPL / 2; ++i) s += qf[2 * i] * bflo(kw[u][i]) + qf[2 * i + 1] * bfhi(kw[u][i]);
-      s += __shfl_xor(s, 8, 64);
-      s += __shfl_xor(s, 4, 64);
-      s += __shfl_xor(s, 2, 64);
-      s += __shfl_xor(s, 1, 64);
+      s = row16_sum(s);  // the 16 lanes of this key
       if (j0 + NG * u >= nvalid) continue;
       const float mn = fmaxf(mx, s);
       const float corr = exp2f(mx - mn);
@@ -156,7 +153,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
       O += s_po[pp * HS + d];
     }
     const uint32_t ob = (uint32_t)f2bf(O / L);
-    const uint32_t pr = __shfl_xor(ob, 1, 64);
+    const uint32_t pr = lane_xor1(ob);
     if (!(d & 1)) {
       const size_t eo = (size_t)m * C + h * HS + d;
       if constexpr (CH) st4_sc1(y, (unsigned)(eo * 2), ob | (pr << 16));

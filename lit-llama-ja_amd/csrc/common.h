@@ -65,6 +65,32 @@ __device__ __forceinline__ float wave_max(float v) {
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Cross-lane moves inside a DPP row (16 lanes) as one VALU op each, instead of __shfl_xor's
+// ds_bpermute (an LDS round trip plus a wait).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __builtin_bit_cast(float, dpp_u32<CTRL>(__builtin_bit_cast(uint32_t, v)));
+}
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppRowMirror = 0x140;  // lane i <- 15 - i
+constexpr int kDppHalfMirror = 0x141; // lane i <- 7 - i within each half row
+__device__ __forceinline__ uint32_t lane_xor1(uint32_t v) { return dpp_u32<kDppXor1>(v); }
+__device__ __forceinline__ float lane_xor1(float v) { return dpp_f32<kDppXor1>(v); }
+// Sum over the 16 lanes of a row; every step pairs lanes symmetrically, so all 16 lanes end
+// with the bitwise-same total (as an xor butterfly would).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f32<kDppHalfMirror>(v);
+  v += dpp_f32<kDppRowMirror>(v);
+  v += dpp_f32<kDppXor1>(v);
+  v += dpp_f32<kDppXor2>(v);
+  return v;
+}
+
 }  // namespace llj
 
 // Error convention for the C ABI: 0 = ok, otherwise a hipError_t or one of these.

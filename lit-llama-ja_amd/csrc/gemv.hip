@@ -873,6 +873,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   const float bias = p.bias ? bf2f(e_braw) : 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
+    if (r >= M) break;  // m = 4 grp + r >= r: no lane of the wave has a row left (uniform)
     const int m = 4 * grp + r;
     float y, y2 = 0.f;
     if (W4L) {
@@ -912,7 +913,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     if (EP == EP_QKV) {
       // c_attn output rounded to bf16 (model.py:204), then RoPE in fp32 (model.py:318-329)
       const float v = round_bf(y);
-      const float partner = __shfl_xor(v, 1, 64);
+      const float partner = lane_xor1(v);
       if (m < M) {
         // head_size is a power of two (64 / 128, checked on the host): shifts, no divisions
         const int Cd = p.n_head * p.head_size;
@@ -929,7 +930,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
           out = (dd & 1) ? (v * c + partner * s) : (v * c - partner * s);
         }
         const uint32_t ob = (uint32_t)f2bf(out);
-        const uint32_t pr = __shfl_xor(ob, 1, 64);  // columns (dd, dd + 1) leave as one 4-byte store
+        const uint32_t pr = lane_xor1(ob);  // columns (dd, dd + 1) leave as one 4-byte store
         if (!(dd & 1)) {
           bf16_t* dst;
           size_t ei;
@@ -950,7 +951,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
       // this workgroup's 16 columns for the next RMSNorm (part nt of nst_out)
       const float xn = round_bf(bf2f(e_xr[r]) + round_bf(y));
       const uint32_t xb = (uint32_t)f2bf(xn);
-      const uint32_t pr = __shfl_xor(xb, 1, 64);
+      const uint32_t pr = lane_xor1(xb);
       float sq = 0.f;
       if (m < M) {
         sq = round_bf(xn * xn);
@@ -961,10 +962,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
         }
       }
       if (p.nst_out) {
-        sq += __shfl_xor(sq, 8, 64);
-        sq += __shfl_xor(sq, 4, 64);
-        sq += __shfl_xor(sq, 2, 64);
-        sq += __shfl_xor(sq, 1, 64);
+        sq = row16_sum(sq);
         if (row == 0 && m < M) {
           if constexpr (CH) st8d_sc1(p.nst_out, (unsigned)(nt * 8 + m) * 8u, (double)sq);
           else p.nst_out[nt * 8 + m] = (double)sq;
@@ -972,7 +970,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
       }
     } else {
       const uint32_t ob = (uint32_t)f2bf(out_value<EP>(y, y2));
-      const uint32_t pr = __shfl_xor(ob, 1, 64);
+      const uint32_t pr = lane_xor1(ob);
       if (m < M && !(row & 1)) {
         const size_t ei = (size_t)m * p.ldc + n;
         if constexpr (CH) st4_sc1(p.C, (unsigned)(ei * 2), ob | (pr << 16));
