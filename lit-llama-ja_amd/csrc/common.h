@@ -13,9 +13,16 @@ namespace llj {
 #define LLJ_TRACE 0  // profiling only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
 #endif
 #if LLJ_TRACE
-static __device__ unsigned long long g_trace[8192 * 6];  // per translation unit
-#define LLJ_STAMP(k) \
-  if (threadIdx.x == 0 && blockIdx.x < 8192) g_trace[blockIdx.x * 6 + (k)] = __builtin_amdgcn_s_memrealtime()
+// [workgroup][8]: 6 phase stamps, then HW_ID (CU / SE of the workgroup) and XCC_ID at stamp 0
+static __device__ unsigned long long g_trace[8192 * 8];  // per translation unit
+#define LLJ_STAMP(k)                                                                             \
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {                                                   \
+    g_trace[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                            \
+    if ((k) == 0) {                                                                              \
+      g_trace[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  /* HW_ID */   \
+      g_trace[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 20); /* XCC_ID */  \
+    }                                                                                            \
+  }
 #else
 #define LLJ_STAMP(k)
 #endif

@@ -997,6 +997,18 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
 #ifndef LLJ_D
 #define LLJ_D 4  // weight chunks in flight per wave
 #endif
+#ifndef LLJ_D1
+#define LLJ_D1 LLJ_D  // chunks in flight per wave for the single-matrix ops (QKV, c_proj, down, head)
+#endif
+// The residual ops have only N / 16 = C / 16 workgroups (256 at 7B, one per CU); with a long K
+// (mlp.c_proj, K = n_hidden) twice the waves keep twice the weight chunks in flight per CU
+// (measured 7B bs=1: 8.8 -> 8.2 us; c_proj with K = C gains nothing and keeps 4 waves).
+#ifndef LLJ_NWR
+#define LLJ_NWR 8  // waves per workgroup of a residual op with K >= LLJ_NWR_KMIN
+#endif
+#ifndef LLJ_NWR_KMIN
+#define LLJ_NWR_KMIN 8192
+#endif
 constexpr int kNW = LLJ_NW;
 constexpr int kD = LLJ_D;
 
@@ -1019,12 +1031,13 @@ static inline bool lds_fits(int wf, int M, int K) { return M <= 8 && a_image_byt
 // as many waves, each with fewer chunks, for more A-fragment loads in flight
 template <int AM>
 constexpr int nw_of() { return AM == AM_GLOBAL ? 2 * kNW : kNW; }
+template <int EP>
+constexpr int d_of() { return EP == EP_SWIGLU ? kD : LLJ_D1; }
 
-template <int WF, int AM, int EP, int MB>
+template <int WF, int AM, int EP, int MB, int NW = nw_of<AM>()>
 static int launch_mb(const GemvParams& p, hipStream_t s) {
-  constexpr int NW = nw_of<AM>();
   const size_t sm = gemv_smem(WF, AM, p.M, p.K, NW);
-  auto kern = gemv_kernel<WF, AM, EP, NW, kD, MB>;
+  auto kern = gemv_kernel<WF, AM, EP, NW, d_of<EP>(), MB>;
   static bool attr_set = false;  // per instantiation; set before any graph capture
   if (sm > 64 * 1024 && !attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1039,6 +1052,12 @@ static int launch_mb(const GemvParams& p, hipStream_t s) {
 template <int WF, int AM, int EP>
 static int launch(const GemvParams& p, hipStream_t s) {
   // the register-staged prologue has an M == 1 class (bs = 1 decode) and an M <= 8 class
+  if constexpr (EP == EP_RESID && AM != AM_GLOBAL && LLJ_NWR != kNW) {
+    if (p.K >= LLJ_NWR_KMIN) {  // residual ops: 256 workgroups, more waves each
+      if (WF != WF_I8 && p.M == 1) return launch_mb<WF, AM, EP, 1, LLJ_NWR>(p, s);
+      return launch_mb<WF, AM, EP, 8, LLJ_NWR>(p, s);
+    }
+  }
   if (WF != WF_I8 && AM != AM_GLOBAL && p.M == 1) return launch_mb<WF, AM, EP, 1>(p, s);
   return launch_mb<WF, AM, EP, 8>(p, s);
 }
@@ -1311,7 +1330,9 @@ int llj_decode_layer(const llj_layer* L, void* stream) {
   c.y = (bf16_t*)L->y; c.pos = L->pos; c.S = L->S; c.nh = nh; c.sl2 = 1.4426950408889634f / sqrtf((float)hs);
   c.n_qkv = 3 * C / 16; c.n_att = nh * M; c.n_cproj = C / 16; c.n_fc12 = H / 16;
   c.b_att = c.n_qkv; c.b_cproj = c.b_att + c.n_att; c.b_fc12 = c.b_cproj + c.n_cproj; c.b_down = c.b_fc12 + c.n_fc12;
-  c.has_down = M == 1;  // M > 1: the (M, H) A image does not fit the LDS; separate launch below
+  // M > 1: the (M, H) A image does not fit the LDS; a long-K down op runs with LLJ_NWR waves (not
+  // the chain's 4): both as the separate launch below, so results stay those of the five launches
+  c.has_down = M == 1 && !(LLJ_NWR != kNW && H >= LLJ_NWR_KMIN);
   c.ctr = L->counters; c.err = L->err;
   const int grid = c.b_down + (c.has_down ? C / 16 : 0);
   size_t lds = gemv_smem(wf, AM_NORM, M, C);
