@@ -89,8 +89,10 @@ def build_model(name: str, mode: str, seed: int = 1234):
             if hasattr(mod, "quant_weight"):
                 mod.quant_weight.copy_(torch.randint(0, 256, mod.quant_weight.shape, device=dev, dtype=torch.uint8,
                                                      generator=g))
-                mod.scales.copy_((torch.rand(mod.scales.shape, device=dev, generator=g) + 0.5) * (0.02 / 7))
-                mod.zeros.fill_(8.0)
+                # scales U(0.5, 1.5) * 0.02 / 7, zeros 8; gptq.int8 the same at 8 bits
+                half = 2 ** (mod.bits - 1)  # 8 / 128
+                mod.scales.copy_((torch.rand(mod.scales.shape, device=dev, generator=g) + 0.5) * (0.02 / (half - 1)))
+                mod.zeros.fill_(float(half))
             elif isinstance(mod, torch.nn.Linear):
                 mod.weight.normal_(0.0, 0.02, generator=g)
             elif isinstance(mod, torch.nn.Embedding):

@@ -4,6 +4,7 @@
   C2  LLaMA-7B gptq.int4, bs=1 and bs=8
   C3  LLaMA-7B llm.int8, bs=8
   C4  LLaMA-13B gptq.int4, bs=1 (one replica; the driver runs the 8-replica scan)
+  X-gptq.int8  LLaMA-7B gptq.int8 (ColBlock bits=8), bs=1 (not a BASELINE config; informational)
 
 Synthetic weights of the exact shapes (bench.build_model), 16-token random prompts,
 max_seq_length 144, greedy; value = decode tokens/s, step_roofline = algorithmic bytes of a
@@ -27,7 +28,8 @@ sys.path.insert(0, str(REPO))
 import bench  # noqa: E402
 
 CONFIGS = [("C1", "7B", "none", 1), ("C2", "7B", "gptq.int4", 1), ("C2-bs8", "7B", "gptq.int4", 8),
-           ("C3", "7B", "llm.int8", 8), ("C4", "13B", "gptq.int4", 1)]
+           ("C3", "7B", "llm.int8", 8), ("C4", "13B", "gptq.int4", 1),
+           ("X-gptq.int8", "7B", "gptq.int8", 1)]  # extra: the reference's third --quantize mode
 
 
 def main():
