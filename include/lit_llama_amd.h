@@ -88,6 +88,16 @@ int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, co
 int llj_attention(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
                   int n_head, int head_size, int S, void* stream);
 
+/* y = attention (as llj_attention, T = 1 decode rows, M = B <= 8) and then
+ * x[M, C] += y . W_proj^T (as llj_linear_resid, attn.c_proj + residual, model.py:172,239-242),
+ * in ONE launch: the c_proj workgroups load their weights while the attention runs and wait
+ * for it on a completion counter. counters: 32 words the caller zeroes before every call;
+ * err: set non-zero if the wait timed out (never expected). wfmt 0, 1 or 3. Bitwise equal
+ * to llj_attention + llj_linear_resid. */
+int llj_attn_resid(int wfmt, const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int M,
+                   int n_head, int S, const void* W, const void* sz, void* x, int C, double* nstat_out,
+                   unsigned* counters, unsigned* err, void* stream);
+
 /* x[M, N] += A[M, K] . W^T (attn.c_proj / mlp.c_proj + residual add, model.py:172-173). */
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
                      int N, int K, const void* i8ws, int i8_row0, double* nstat_out, void* stream);

@@ -23,7 +23,8 @@ constexpr int attention_lds_floats() {
 
 // CH: chained launch — wait for the QKV op, then read q and the cache with sc1 loads and
 // store y with sc1 stores (chain.h protocol).
-template <int HS, int U, int NTH, bool CH>
+// SIG: signal a consumer op of the same launch (sc1 y stores, drain, count done); CH implies it.
+template <int HS, int U, int NTH, bool CH, bool SIG = CH>
 __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                const int* __restrict__ pos, int T, int S, int nh, float scale_log2,
@@ -156,11 +157,11 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
     const uint32_t pr = lane_xor1(ob);
     if (!(d & 1)) {
       const size_t eo = (size_t)m * C + h * HS + d;
-      if constexpr (CH) st4_sc1(y, (unsigned)(eo * 2), ob | (pr << 16));
+      if constexpr (SIG) st4_sc1(y, (unsigned)(eo * 2), ob | (pr << 16));
       else *reinterpret_cast<uint32_t*>(y + eo) = ob | (pr << 16);
     }
   }
-  if constexpr (CH) {
+  if constexpr (SIG) {
     // every storing wave drains; the workgroup counts done once all have (LDS barrier)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

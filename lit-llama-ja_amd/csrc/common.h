@@ -23,8 +23,14 @@ static __device__ unsigned long long g_trace[8192 * 8];  // per translation unit
       g_trace[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 20); /* XCC_ID */  \
     }                                                                                            \
   }
+// per translation unit: extern "C" llj_trace_copy_<tu>(host_dst, bytes)
+#define LLJ_TRACE_EXPORT(tu)                                                                     \
+  int llj_trace_copy_##tu(void* host_dst, size_t bytes) {                                        \
+    return (int)hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(llj::g_trace), bytes, 0, hipMemcpyDeviceToHost); \
+  }
 #else
 #define LLJ_STAMP(k)
+#define LLJ_TRACE_EXPORT(tu)
 #endif
 
 typedef uint16_t bf16_t;  // raw bf16 bits in HBM

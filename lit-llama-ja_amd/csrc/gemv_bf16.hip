@@ -1,0 +1,10 @@
+// Instantiations of the GEMV kernels for weight format WF_BF16 (gemv_impl.h).
+#include "gemv_impl.h"
+
+namespace llj {
+int gemv_launch_bf16(int am, int ep, const GemvParams& p, hipStream_t s) { return launch_fmt<WF_BF16>(am, ep, p, s); }
+}  // namespace llj
+
+extern "C" {
+LLJ_TRACE_EXPORT(bf16)
+}

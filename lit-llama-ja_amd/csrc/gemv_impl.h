@@ -1,0 +1,1113 @@
+// Weight-streaming skinny GEMM ("GEMV", M <= 16 rows per pass) for the LLaMA decode step on
+// gfx950, with the reference's per-layer elementwise work fused into prologue/epilogue.
+//
+// Replaces, for the decode path:
+//   reference lit_llama/quantization.py:282-331 (qlinear_4bit_weight / Triton
+//   linear_kernel_4bit_weight 80-280) and :411-421 (ColBlockQuantizedLinear.forward),
+//   :36-75 (Linear8bitLt = bitsandbytes LLM.int8() matmul), plus torch.nn.Linear (F.linear)
+//   for the bf16 model; fused with model.py:276-283 (RMSNorm), :204-228 (c_attn split,
+//   apply_rope, KV-cache write), :172-173 (residual adds) and :258 (silu(c_fc1) * c_fc2).
+//
+// Work decomposition: one workgroup (NW waves) owns one 16-column n-tile over the whole K;
+// its waves split K into 128-deep chunks round-robin and the partial sums are reduced in
+// LDS, so no cross-workgroup reduction exists. A chunk is 4 MFMA 16x16x32 bf16 steps (or 2
+// MFMA 16x16x64 i8 steps). The weight stream uses non-temporal loads, D chunks in flight.
+//
+// Weight formats (WF):
+//  * WF_W4 — int4 repacked "W4P" layout (w4pack.hip): per (n-tile, k-chunk) one contiguous
+//    1 KiB block; lane l's 16 bytes are the 32 codes of column 16*nt + (l&15) for
+//    k = 128*kc + 32*(l>>4) + [0,32), so one global_load_dwordx4 per wave fetches a fully
+//    coalesced 1 KiB and needs no LDS. Codes become bf16 (128 + q) with one v_and_or_b32
+//    (magic exponent) per pair; the 128 + zero offset is removed in the epilogue with the
+//    row sums of A, computed by an extra MFMA against a ones fragment:
+//      y[m,n] = s[n] * (sum_k A[m,k] (128 + q[k,n]) - (128 + z[n]) * sum_k A[m,k])
+//             = sum_k A[m,k] * (q[k,n] - z[n]) * s[n]          (get_weight semantics)
+//  * WF_W8 — gptq.int8 (ColBlock bits=8): the 8-bit codes as two int4 planes in the W4P
+//    layout, per (n-tile, k-chunk) 2 KiB = [low nibbles 1 KiB][high nibbles 1 KiB]. The low
+//    nibble dequantizes to bf16 128 + lo (exponent 0x43), the high one to 2048 + 16 hi
+//    (exponent 0x45, same v_and_or_b32), both into ONE accumulator:
+//      sum_k A (128 + lo) + A (2048 + 16 hi) = sum_k A q + 2176 sum_k A,
+//    so y = s * (acc - (2176 + z) * sum_k A), the W4 epilogue with offset 2176.
+//  * WF_BF16 — torch.nn.Linear weight (N, K) row-major bf16, read in place.
+//  * WF_I8 — LLM.int8(): CB (N, K) int8 row-quantized weight + SCB (N) fp32. A is quantized
+//    per row in the prologue (absmax over non-outlier elements, outlier columns zeroed,
+//    statistics from llj_i8_stats in int8.hip), int32 MFMA accumulation, dequant by
+//    SCA*SCB/127^2, plus the fp16 side product over the outlier columns.
+#pragma once
+#include <algorithm>
+
+#include "common.h"
+#include "chain.h"
+#include "i8ws.h"
+#include "attention.h"
+#include "lit_llama_amd.h"
+
+namespace llj {
+
+enum : int { WF_W4 = 0, WF_BF16 = 1, WF_I8 = 2, WF_W8 = 3 };
+enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2 };
+enum : int { EP_STORE = 0, EP_RESID = 1, EP_QKV = 2, EP_SWIGLU = 3 };
+
+// int8 activation workspace written by llj_i8_stats (int8.hip): i8ws.h
+
+struct GemvParams {
+  const bf16_t* A;  // (M, K), row stride lda elements
+  int lda;
+  const bf16_t* norm_w;  // AM_NORM: RMSNorm scale (K)
+  float eps;
+  int M, N, K;
+  const void* W;   // WF_W4: W4P tiles; WF_W8: W8P tiles; WF_BF16: (N, K) bf16; WF_I8: (N, K) int8
+  const void* W2;  // EP_SWIGLU: c_fc2
+  const float2* sz;   // WF_W4 / WF_W8: per column (scale, 128 / 2176 + zero); WF_I8: (const float*) SCB
+  const float2* sz2;
+  const bf16_t* bias;  // optional (N)
+  bf16_t* C;  // EP_STORE / EP_SWIGLU: out (M, ldc); EP_RESID: residual stream updated in place
+  int ldc;
+  // EP_QKV
+  bf16_t* q_out;   // (B*T, n_embd)
+  bf16_t* kcache;  // (B, n_head, S, hs)
+  bf16_t* vcache;
+  const float* rope;  // (block_size, hs/2, 2)
+  const int* pos;     // (T) absolute positions of the T rows of each sequence
+  int n_head, head_size, S, T;
+  int m0;  // global row index of local row 0 (QKV row chunks; int8 statistics rows)
+  const void* i8ws;
+  // RMSNorm row statistics, sum_k bf16(x[m,k]^2), produced once instead of re-reduced by
+  // every norm-fused workgroup: partial sums in fp64 laid out [part][8 rows] (M <= 8).
+  // EP_RESID writes one part per workgroup (its 16 columns, plain stores: no atomics, so
+  // no same-address contention and a deterministic order); AM_NORM sums nst_parts parts.
+  const double* nst_in;
+  int nst_parts;
+  double* nst_out;
+  // int4: sum_k A[m,k] of this call's rows as the MFMA sees them (pre-normalized rows,
+  // llj_rmsnorm_rows); nullptr = computed in the prologue
+  const float* rowsum;
+  // EP_RESID: RMSNorm of the updated residual rows, computed once by the LAST workgroup to
+  // finish (completion counter nn_ctr; it resets the counter): xn = RMSNorm(x) with scale
+  // nn_w / eps nn_eps, nn_rs[m] = fp32 sum of the normalized bf16 row. nullptr = off.
+  const bf16_t* nn_w;
+  float nn_eps;
+  bf16_t* nn_out;
+  float* nn_rs;
+  unsigned* nn_ctr;
+};
+
+// ------------------------------------------------------------------------------------
+// Stage A rows [0, M) into LDS (row stride K + 8 elements; MFMA lanes of rows >= M read row 0
+// and their output rows are discarded). With NORM, rows are RMS-normalised with the reference's bf16
+// rounding points (model.py:281-283 evaluated on bf16 tensors).
+__device__ __forceinline__ float rms_rstd(float sumsq_over_k, float eps) {
+  // bf16: mean(x*x) -> +eps -> rsqrt, each rounded (torch bf16 ops, model.py:281-282)
+  return round_bf(rsqrtf(round_bf(round_bf(sumsq_over_k) + eps)));
+}
+
+__device__ __forceinline__ uint4 norm8(uint4 x, uint4 g, float r) {
+  uint32_t xw[4] = {x.x, x.y, x.z, x.w}, gw[4] = {g.x, g.y, g.z, g.w}, o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float lo = round_bf(bflo(gw[i]) * round_bf(bflo(xw[i]) * r));
+    float hi = round_bf(bfhi(gw[i]) * round_bf(bfhi(xw[i]) * r));
+    o[i] = pack2bf(lo, hi);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+template <int NW, bool NORM>
+__device__ void stage_a(const GemvParams& p, bf16_t* As, int a_stride, float* red) {
+  const int tid = threadIdx.x;
+  constexpr int NT = NW * 64;
+  const int K = p.K, M = p.M;
+  const int nvec = K >> 3;
+  if (NORM && p.nst_in) {  // statistics precomputed by the producer: one pass
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int m = wave; m < M; m += NW) {
+      double s = 0.0;
+      for (int q = lane; q < p.nst_parts; q += 64) s += p.nst_in[q * 8 + m];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (lane == 0) red[m] = rms_rstd((float)(s / (double)K), p.eps);
+    }
+    __syncthreads();
+    const uint4* g4 = reinterpret_cast<const uint4*>(p.norm_w);
+    for (int m = 0; m < M; ++m) {
+      const float r = red[m];
+      const uint4* src = reinterpret_cast<const uint4*>(p.A + (size_t)m * p.lda);
+      uint4* dst = reinterpret_cast<uint4*>(As + (size_t)m * a_stride);
+      for (int v = tid; v < nvec; v += NT) dst[v] = norm8(src[v], g4[v], r);
+    }
+    return;
+  }
+  float ss[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) ss[m] = 0.f;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    if (m < M) {
+      const uint4* src = reinterpret_cast<const uint4*>(p.A + (size_t)m * p.lda);
+      uint4* dst = reinterpret_cast<uint4*>(As + (size_t)m * a_stride);
+      for (int v = tid; v < nvec; v += NT) {
+        uint4 x = src[v];
+        dst[v] = x;
+        if (NORM) {
+          uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float a = bflo(w[i]), b = bfhi(w[i]);
+            ss[m] += round_bf(a * a) + round_bf(b * b);
+          }
+        }
+      }
+    }
+  }
+  if (!NORM) return;
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    float s = wave_sum(ss[m]);
+    if (lane == 0) red[wave * 8 + m] = s;
+  }
+  __syncthreads();
+  if (tid < 8) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[w * 8 + tid];
+    red[NW * 8 + tid] = rms_rstd(s / (float)K, p.eps);
+  }
+  __syncthreads();
+  const uint4* g4 = reinterpret_cast<const uint4*>(p.norm_w);
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    if (m < M) {
+      const float r = red[NW * 8 + m];
+      uint4* row = reinterpret_cast<uint4*>(As + (size_t)m * a_stride);
+      for (int v = tid; v < nvec; v += NT) row[v] = norm8(row[v], g4[v], r);
+    }
+  }
+}
+
+// int8: copy rows [0, M) of the activation quantized once by llj_i8_stats (outlier columns
+// already 0) into LDS int8 rows (stride K + 16 bytes); sca[] receives SCA per local row.
+template <int NW>
+__device__ void stage_i8(const GemvParams& p, int8_t* Aq, int q_stride, float* sca) {
+  const int tid = threadIdx.x;
+  constexpr int NT = NW * 64;
+  const int K = p.K, M = p.M;
+  const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
+  const I8Layout L = i8_layout(p.i8ws, h.mtot, h.K);
+  if (tid < M) sca[tid] = L.sca[p.m0 + tid];
+  const int nv = K >> 4;
+  for (int m = 0; m < M; ++m) {
+    const uint4* src = reinterpret_cast<const uint4*>(L.aq + (size_t)(p.m0 + m) * K);
+    uint4* dst = reinterpret_cast<uint4*>(Aq + (size_t)m * q_stride);
+    for (int v = tid; v < nv; v += NT) dst[v] = src[v];
+  }
+}
+
+__device__ __forceinline__ bf16x8 dequant_w4(uint32_t w, uint32_t msk, uint32_t mag) {
+  uint4 b = make_uint4(and_or(w, msk, mag), and_or(w >> 4, msk, mag), and_or(w >> 8, msk, mag),
+                       and_or(w >> 12, msk, mag));
+  return __builtin_bit_cast(bf16x8, b);
+}
+
+template <int WF>
+__device__ __forceinline__ int kofs(int t, int grp) {
+  // k offset inside a 128-deep chunk of the elements lane-group `grp` feeds at MFMA step t
+  return (WF == WF_W4 || WF == WF_W8) ? 32 * grp + 8 * t : WF == WF_BF16 ? 32 * t + 8 * grp : 64 * t + 16 * grp;
+}
+
+// fp16 side product of LLM.int8() over the outlier columns, for this workgroup's 16 columns
+// and M <= 8 rows: side[m][n] = sum_k f16(A[m,k]) * f16(CB[n,k] * SCB[n] / 127). The outlier
+// columns are taken in chunks of kSideChunk: their indices and f16(A) values are staged in LDS
+// (`stage`, free A-image space) once per workgroup, then thread t (column t % 16, every
+// (NW*4)-th outlier of the chunk) accumulates; the four lanes of a wave sharing a column are
+// combined by shuffles and the per-wave partials land in part[NW][8][16]. Ends with a barrier.
+constexpr int kSideChunk = 256;
+template <int NW>
+__device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float* SCB, int n0, float* part,
+                             unsigned char* stage) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nl = tid & 15, g = tid >> 4;
+  constexpr int NG = NW * 4, NT = NW * 64;
+  const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
+  const I8Layout L = i8_layout(p.i8ws, h.mtot, h.K);
+  int* s_pre = reinterpret_cast<int*>(stage);           // [kNSB + 1] prefix of the block counts
+  int* s_k = s_pre + 64;                                // [kSideChunk] column indices
+  float* s_a = reinterpret_cast<float*>(s_k + kSideChunk);  // [8][kSideChunk] f16(A) values
+  const int n = n0 + nl, M = p.M;
+  const float scb = SCB[n] / 127.f;
+  if (tid < 64) {  // prefix sum of the per-block outlier counts (kNSB <= 64)
+    int c = tid < h.nsb ? L.cnt[tid] : 0;
+    int x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    s_pre[tid + 1] = x;
+    if (tid == 0) s_pre[0] = 0;
+  }
+  __syncthreads();
+  const int total = s_pre[h.nsb];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < total; c0 += kSideChunk) {
+    const int len = min(kSideChunk, total - c0);
+    for (int i = tid; i < len; i += NT) {
+      const int fi = c0 + i;
+      int b = 0;
+      while (b + 1 < h.nsb && s_pre[b + 1] <= fi) ++b;  // blocks are few (kNSB)
+      const int k = L.list[b * h.kb + (fi - s_pre[b])];
+      s_k[i] = k;
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+        s_a[m * kSideChunk + i] = m < M ? (float)(_Float16)bf2f(p.A[(size_t)m * p.lda + k]) : 0.f;
+    }
+    __syncthreads();
+    for (int i = g; i < len; i += NG) {
+      const float w = (float)(_Float16)((float)CB[(size_t)n * p.K + s_k[i]] * scb);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) acc[m] += s_a[m * kSideChunk + i] * w;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    acc[m] += __shfl_xor(acc[m], 16, 64);
+    acc[m] += __shfl_xor(acc[m], 32, 64);
+    if (lane < 16) part[(wave * 8 + m) * 16 + nl] = acc[m];
+  }
+  __syncthreads();
+}
+
+// Output value of one element for the plain / SwiGLU epilogues (SwiGLU: model.py:258 in bf16).
+template <int EP>
+__device__ __forceinline__ float out_value(float y, float y2) {
+  if (EP == EP_SWIGLU) {
+    const float a1 = round_bf(y), a2 = round_bf(y2);
+    const float sl = round_bf(a1 / (1.f + __expf(-a1)));  // F.silu in bf16
+    return sl * a2;
+  }
+  return y;
+}
+
+
+#ifndef LLJ_CH_PLAIN_A
+#define LLJ_CH_PLAIN_A 0  // experiment only: chained consumers read A with plain loads
+#endif
+
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
+
+// Register-staged A prologue. Loads return to VGPRs in issue order, so the A-side loads
+// (RMSNorm partial statistics, activation rows, norm weights) and the epilogue operands are
+// issued BEFORE the weight prefetch: waiting for them then does not also wait for the
+// weight chunks' HBM latency, and the LDS image is written while the weights are in flight.
+// MB = row class of the instantiation (1: M == 1; 8: M <= 8); register budget per lane:
+//   XR 16-byte activation registers (MB 1: one row of K <= 8*XR*NT; MB 8: RS = 2 per row for
+//   M <= 8, K <= 16*NT, or RS = 4 for M <= 4), GR norm-weight registers, ST fp64 partials.
+template <int MB, bool NORM>
+struct APre {
+  static constexpr int XR = MB == 1 ? (NORM ? 4 : 8) : 16;
+  static constexpr int GR = NORM ? 4 : 1;
+  static constexpr int SM = MB == 1 ? 1 : 8;  // statistics rows interleaved over threads
+  static constexpr int ST = MB == 1 ? 2 : 8;  // partials per thread
+  u32x4 x[XR];
+  u32x4 g[GR];
+  double st[ST];
+};
+
+// Last-arriver RMSNorm after a residual GEMV (GemvParams::nn_*): every workgroup stores its x
+// columns write-through (sc1), drains them and counts itself done; the one whose add returns
+// nwg - 1 reads the rows back with sc1 loads (chain.h protocol) and normalizes them with the bf16
+// rounding points of model.py:281-283 (as rmsnorm_kernel), so the consumer GEMVs read a
+// finished xn instead of a separate norm launch. `red` = LDS scratch (>= 64 floats). All
+// waves of the workgroup call it (wave 0 after its epilogue stores).
+template <int NW>
+__device__ void resid_norm_tail(const GemvParams& p, float* red, bool storing_wave) {
+  constexpr int NT = NW * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = p.M, C = p.N;
+  int* flag = reinterpret_cast<int*>(red + 64);
+  if (storing_wave) {  // x columns were stored sc1 (write-through): drain, then count done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(p.nn_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, 0, 64);
+    if (lane == 0) *flag = old + 1 == gridDim.x ? 1 : 0;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  // the last workgroup: sum_k bf16(x^2) per row
+  const int nvec = C >> 3;
+  float ss[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int v = tid; v < nvec; v += NT) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      if (m < M) {
+        const u32x4 a = ld16_sc1(p.C, (unsigned)(((size_t)m * p.ldc + 8 * v) * 2));  // other workgroups' x
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          ss[m] += round_bf(bflo(a[i]) * bflo(a[i])) + round_bf(bfhi(a[i]) * bfhi(a[i]));
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const float t = wave_sum(ss[m]);
+    if (lane == 0) red[wave * 8 + m] = t;
+  }
+  __syncthreads();
+  float r[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += red[w * 8 + m];
+    r[m] = round_bf(rsqrtf(round_bf(round_bf(t / (float)C) + p.nn_eps)));
+  }
+  __syncthreads();
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const uint4* g4 = reinterpret_cast<const uint4*>(p.nn_w);
+  for (int v = tid; v < nvec; v += NT) {
+    const uint4 g = g4[v];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      if (m < M) {
+        const u32x4 a = ld16_sc1(p.C, (unsigned)(((size_t)m * p.ldc + 8 * v) * 2));
+        uint32_t o[4];
+        const uint32_t aw[4] = {a[0], a[1], a[2], a[3]}, gw[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          o[i] = pack2bf(round_bf(bflo(gw[i]) * round_bf(bflo(aw[i]) * r[m])),
+                         round_bf(bfhi(gw[i]) * round_bf(bfhi(aw[i]) * r[m])));
+          rs[m] += bflo(o[i]) + bfhi(o[i]);
+        }
+        *reinterpret_cast<uint4*>(p.nn_out + (size_t)m * C + 8 * v) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const float t = wave_sum(rs[m]);
+    if (lane == 0) red[wave * 8 + m] = t;
+  }
+  __syncthreads();
+  if (tid < M && p.nn_rs) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += red[w * 8 + tid];
+    p.nn_rs[tid] = t;
+  }
+  if (tid == 0) *p.nn_ctr = 0u;  // ready for the next launch (kernel boundaries order it)
+}
+
+#ifndef LLJ_ABL
+#define LLJ_ABL 0  // ablation switches for profiling only (1 no A prologue, 2 no compute, 4 no epilogue)
+#endif
+
+template <int WF, int AM, int EP, int NW, int D, int MB, bool CH>
+__device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, unsigned char* smem,
+                                          const ChainCtl& cc) {
+  constexpr bool DUAL = (EP == EP_SWIGLU);
+  constexpr bool I8 = (WF == WF_I8);
+  constexpr bool W4L = (WF == WF_W4 || WF == WF_W8);  // nibble-coded: offset removed with row sums
+  constexpr bool ALDS = I8 || (AM != AM_GLOBAL);
+  constexpr int WV = (WF == WF_W4) ? 1 : (WF == WF_BF16 ? 4 : 2);  // 16-B loads per lane per chunk per matrix
+  constexpr int NSTEP = I8 ? 2 : 4;
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform(threadIdx.x >> 6);
+  const int n0 = nt * 16;
+  const int K = p.K, M = p.M, KC = K >> 7;
+  const int row = lane & 15, grp = lane >> 4;
+  // LDS carve: [A image, aliased after the main loop by the NW x 64 x 12-word reduction
+  // scratch] [tail: 128 words for staging scratch / int8 SCA]
+  const int a_stride = I8 ? K + 16 : K + 8;  // elements (bytes for int8)
+  const size_t a_bytes = ALDS ? (((size_t)M * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15) : 0;
+  constexpr size_t kRedBytes = (size_t)NW * 64 * 12 * 4;
+  constexpr size_t kScratch = kRedBytes + (I8 ? (size_t)2 * NW * 8 * 16 * 4 : 0);  // + int8 side partials
+  float* red = reinterpret_cast<float*>(smem);
+  float* tail = reinterpret_cast<float*>(smem + (a_bytes > kScratch ? a_bytes : kScratch));
+  float* sca = tail;
+
+  const bool arow = row < M;
+  const unsigned char* abase;  // byte address of this lane's A row
+  if (ALDS) {
+    abase = smem + (size_t)(arow ? row : 0) * a_stride * (I8 ? 1 : 2);  // rows >= M read row 0 (outputs discarded)
+  } else {
+    abase = reinterpret_cast<const unsigned char*>(p.A + (size_t)(arow ? row : 0) * p.lda);
+  }
+  constexpr int EB = I8 ? 1 : 2;  // A element bytes
+
+  // mask in an SGPR and magic in a VGPR, hidden from constant folding (empty asm, no
+  // instruction) so that (w & msk) | mag selects one v_and_or_b32 (no literal in VOP3 on gfx9)
+  uint32_t msk = 0x000F000Fu, mag = 0x43004300u, mag_hi = 0x45004500u;  // mag_hi: WF_W8 high nibbles, 2048 + 16 hi
+  asm volatile("" : "+s"(msk));
+  asm volatile("" : "+v"(mag));
+  if constexpr (WF == WF_W8) asm volatile("" : "+v"(mag_hi));
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
+  const u32x4 zero4 = {0, 0, 0, 0};
+
+  // weight stream pointers (lane-resolved), in 16-byte units
+  const u32x4* w1;
+  const u32x4* w2 = nullptr;
+  size_t wstep;  // 16-B units between consecutive chunks of this lane
+  int vstride;   // 16-B units between the WV loads of one chunk
+  if (WF == WF_W4) {
+    w1 = reinterpret_cast<const u32x4*>(p.W) + (size_t)nt * KC * 64 + lane;
+    if (DUAL) w2 = reinterpret_cast<const u32x4*>(p.W2) + (size_t)nt * KC * 64 + lane;
+    wstep = 64; vstride = 0;
+  } else if (WF == WF_W8) {  // 2 KiB per (tile, chunk): low plane, then high plane
+    w1 = reinterpret_cast<const u32x4*>(p.W) + (size_t)nt * KC * 128 + lane;
+    if (DUAL) w2 = reinterpret_cast<const u32x4*>(p.W2) + (size_t)nt * KC * 128 + lane;
+    wstep = 128; vstride = 64;
+  } else if (WF == WF_BF16) {
+    const size_t off = (size_t)(n0 + row) * K + 8 * grp;  // elements
+    w1 = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.W) + off);
+    if (DUAL) w2 = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.W2) + off);
+    wstep = 16; vstride = 4;  // chunk = 256 B of a row; step t at +64 B
+  } else {
+    const size_t off = (size_t)(n0 + row) * K + 16 * grp;  // bytes
+    w1 = reinterpret_cast<const u32x4*>(reinterpret_cast<const int8_t*>(p.W) + off);
+    if (DUAL) w2 = reinterpret_cast<const u32x4*>(reinterpret_cast<const int8_t*>(p.W2) + off);
+    wstep = 8; vstride = 4;  // chunk = 128 B of a row; step t at +64 B
+  }
+
+  f32x4 acc = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, sacc = {0, 0, 0, 0};
+  i32x4 iacc = {0, 0, 0, 0}, iacc2 = {0, 0, 0, 0};
+  const int nmy = uniform((KC - wave + NW - 1) / NW);
+
+  u32x4 r1[D][WV], r2[D][WV];
+  u32x4 ra[D][4];
+  auto load = [&](int d, int i) {
+    int c = wave + NW * (i < nmy ? i : nmy - 1);
+    c = c < 0 ? 0 : (c >= KC ? KC - 1 : c);  // always a valid chunk (loads past the end are unused)
+#pragma unroll
+    for (int v = 0; v < WV; ++v) {
+      r1[d][v] = __builtin_nontemporal_load(w1 + (size_t)c * wstep + vstride * v);
+      if (DUAL) r2[d][v] = __builtin_nontemporal_load(w2 + (size_t)c * wstep + vstride * v);
+    }
+    if (!ALDS) {
+#pragma unroll
+      for (int t = 0; t < NSTEP; ++t)
+        ra[d][t] = *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp)));  // rows >= M: row 0
+    }
+  };
+  auto compute = [&](int d, int i) {
+    const int c = wave + NW * i;
+    if constexpr ((LLJ_ABL & 2) != 0) {  // ablation: loads only
+      acc[0] += __builtin_bit_cast(float, (r1[d][0].x ^ r1[d][0].w) & 0x3FFu);
+      if (DUAL) acc2[0] += __builtin_bit_cast(float, (r2[d][0].x ^ r2[d][0].w) & 0x3FFu);
+      return;
+    }
+#pragma unroll
+    for (int t = 0; t < NSTEP; ++t) {
+      // LDS lanes of rows >= M read row 0 (abase clamped): their output rows are never stored, and
+      // an unconditional read keeps the hot loop free of divergent LDS accesses
+      const u32x4 av = ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
+      if constexpr (WF == WF_W4) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+        acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
+        if (DUAL) acc2 = mfma_bf16(a, dequant_w4(r2[d][0][t], msk, mag), acc2);
+        if (!ALDS && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);  // else: row sums from the prologue / caller
+      } else if constexpr (WF == WF_W8) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+        acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
+        acc = mfma_bf16(a, dequant_w4(r1[d][1][t], msk, mag_hi), acc);
+        if (DUAL) {
+          acc2 = mfma_bf16(a, dequant_w4(r2[d][0][t], msk, mag), acc2);
+          acc2 = mfma_bf16(a, dequant_w4(r2[d][1][t], msk, mag_hi), acc2);
+        }
+        if (!ALDS && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);
+      } else if constexpr (WF == WF_BF16) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+        acc = mfma_bf16(a, __builtin_bit_cast(bf16x8, r1[d][t]), acc);
+        if (DUAL) acc2 = mfma_bf16(a, __builtin_bit_cast(bf16x8, r2[d][t]), acc2);
+      } else {
+        const i32x4 a = __builtin_bit_cast(i32x4, av);
+        iacc = mfma_i8(a, __builtin_bit_cast(i32x4, r1[d][t]), iacc);
+        if (DUAL) iacc2 = mfma_i8(a, __builtin_bit_cast(i32x4, r2[d][t]), iacc2);
+      }
+    }
+  };
+
+  LLJ_STAMP(0);
+  // ---- epilogue operands, loaded first. Every prologue load is branch-free with a clamped
+  // (always valid) address and its validity applied where the value is used: a load under
+  // divergent control flow makes the compiler's wait before the first use a vmcnt(0), which
+  // would also wait for the weight prefetch issued after it.
+  const int n = n0 + row;
+  // accumulator rows a lane can hold a live output for: 4 (rows 4*grp + r), or 1 when the
+  // instantiation is for M == 1 (MB == 1), so per-row operands load once instead of 4 times
+  constexpr int RR = MB == 1 ? 1 : 4;
+  int e_ps[4] = {0, 0, 0, 0};
+  auto issue_pos = [&]() {
+    if constexpr (EP == EP_QKV) {
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        const int mm = 4 * grp + r < M ? 4 * grp + r : M - 1;
+        e_ps[r] = p.pos[(p.m0 + mm) % p.T];
+      }
+    }
+  };
+  float2 e_a = make_float2(1.f, 0.f), e_b = make_float2(1.f, 0.f);
+  bf16_t e_braw = 0;
+  float e_rs[4] = {0.f, 0.f, 0.f, 0.f};  // caller's row sums (p.rowsum) of rows 4*grp + r
+  auto issue_const = [&]() {  // weights-side epilogue operands (never written in a launch)
+    if constexpr (W4L) {
+      e_a = p.sz[n];
+      if (DUAL) e_b = p.sz2[n];
+      // an epilogue load under divergent control flow would put a vmcnt(0) between the
+      // row stores (stores count in vmcnt): read the row sums here (the branch is uniform)
+      if (p.rowsum) {
+#pragma unroll
+        for (int r = 0; r < RR; ++r) e_rs[r] = p.rowsum[4 * grp + r < M ? 4 * grp + r : M - 1];
+      }
+    } else if constexpr (I8) {
+      e_a.x = reinterpret_cast<const float*>(p.sz)[n];
+      if (DUAL) e_b.x = reinterpret_cast<const float*>(p.sz2)[n];
+    }
+    if (p.bias) e_braw = p.bias[n];
+  };
+  bf16_t e_xr[4] = {0, 0, 0, 0};
+  auto issue_xr = [&]() {  // residual stream values this workgroup updates
+    if constexpr (EP == EP_RESID) {
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        const int mm = 4 * grp + r < M ? 4 * grp + r : M - 1;
+        if constexpr (CH) {
+          const uint32_t w = ld4_sc1(p.C, (unsigned)(((size_t)mm * p.ldc + (n & ~1)) * 2));
+          e_xr[r] = (bf16_t)((n & 1) ? (w >> 16) : (w & 0xFFFFu));
+        } else {
+          e_xr[r] = p.C[(size_t)mm * p.ldc + n];
+        }
+      }
+    }
+  };
+
+  // ---- A prologue, register form (see APre) or LDS-staged after the prefetch (rs == 0)
+  constexpr bool NORM = (AM == AM_NORM);
+  constexpr int NT = NW * 64;
+  using AP = APre<MB, NORM>;
+  const int tid = threadIdx.x;
+  const int nvec = K >> 3;
+  const int JA = (nvec + NT - 1) / NT;
+  int rs = 0;
+  if (ALDS && !I8 && (LLJ_ABL & 1) == 0 && M <= MB) {
+    const bool st_ok = !NORM || !p.nst_in || p.nst_parts <= AP::ST * (NT / AP::SM);
+    const bool g_ok = !NORM || JA <= AP::GR;
+    if (st_ok && g_ok) {
+      if (MB == 1) rs = JA <= 1 ? 1 : JA <= 2 ? 2 : JA <= 4 ? 4 : JA <= AP::XR ? AP::XR : 0;
+      else if (JA <= 2) rs = 2;
+      else if (JA <= 4 && M <= 4) rs = 4;
+    }
+  }
+  rs = uniform(rs);
+  AP ap;
+  const u32x4* g4 = reinterpret_cast<const u32x4*>(p.norm_w);
+  auto a_issue = [&](auto rsc) {
+    constexpr int RS = decltype(rsc)::value;
+    constexpr int MR = MB == 1 ? 1 : AP::XR / RS;
+    if (NORM && p.nst_in) {
+      const int m = tid % AP::SM;
+      const int mm = m < M ? m : M - 1;
+#pragma unroll
+      for (int i = 0; i < AP::ST; ++i) {
+        const int q = tid / AP::SM + (NT / AP::SM) * i;
+        const int si = (q < p.nst_parts ? q : p.nst_parts - 1) * 8 + mm;
+        if constexpr (CH && !LLJ_CH_PLAIN_A) ap.st[i] = ld8d_sc1(p.nst_in, (unsigned)si * 8u);
+        else ap.st[i] = p.nst_in[si];
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const int v = tid + NT * j;
+        const int mm = m < M ? m : M - 1, vv = v < nvec ? v : nvec - 1;
+        const size_t eo = (size_t)mm * p.lda + 8 * vv;
+        if constexpr (CH && !LLJ_CH_PLAIN_A) ap.x[m * RS + j] = ld16_sc1(p.A, (unsigned)(eo * 2));
+        else ap.x[m * RS + j] = *reinterpret_cast<const u32x4*>(p.A + eo);
+      }
+    if (NORM) {
+      constexpr int GJ = RS < AP::GR ? RS : AP::GR;
+#pragma unroll
+      for (int j = 0; j < GJ; ++j) {
+        const int v = tid + NT * j;
+        ap.g[j] = g4[v < nvec ? v : nvec - 1];
+      }
+    }
+  };
+  auto a_finish = [&](auto rsc) {
+    constexpr int RS = decltype(rsc)::value;
+    constexpr int MR = MB == 1 ? 1 : AP::XR / RS;
+    if (NORM) {
+      double* redd = reinterpret_cast<double*>(tail + 32);  // [wave][8] fp64
+      float* redf = tail + 32;                              // [wave][8] fp32
+      if (p.nst_in) {
+        double sd = 0.0;
+        const bool mok = tid % AP::SM < M;
+#pragma unroll
+        for (int i = 0; i < AP::ST; ++i) {
+          const int q = tid / AP::SM + (NT / AP::SM) * i;
+          sd += (mok && q < p.nst_parts) ? ap.st[i] : 0.0;
+        }
+#pragma unroll
+        for (int o = 32; o >= AP::SM; o >>= 1) sd += __shfl_xor(sd, o, 64);
+        if (lane < AP::SM) redd[wave * 8 + lane] = sd;
+        __syncthreads();
+        if (tid < M) {
+          double t = 0.0;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) t += redd[w * 8 + tid];
+          tail[tid] = rms_rstd((float)(t / (double)K), p.eps);
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          float ss = 0.f;
+#pragma unroll
+          for (int j = 0; j < RS; ++j) {
+            const u32x4 xv = (m < M && tid + NT * j < nvec) ? ap.x[m * RS + j] : zero4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float a = bflo(xv[i]), b = bfhi(xv[i]);
+              ss += round_bf(a * a) + round_bf(b * b);
+            }
+          }
+          ss = wave_sum(ss);
+          if (lane == 0) redf[wave * 8 + m] = ss;
+        }
+        __syncthreads();
+        if (tid < M) {
+          float sf = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) sf += redf[w * 8 + tid];
+          tail[tid] = rms_rstd(sf / (float)K, p.eps);
+        }
+      }
+      __syncthreads();
+    }
+    bf16_t* As = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      float rsum = 0.f;
+      if (m < M) {
+        const float r = NORM ? tail[m] : 1.f;
+#pragma unroll
+        for (int j = 0; j < RS; ++j) {
+          const int v = tid + NT * j;
+          if (v < nvec) {
+            u32x4 o = ap.x[m * RS + j];
+            if (NORM) {
+              const uint4 nv = norm8(__builtin_bit_cast(uint4, o), __builtin_bit_cast(uint4, ap.g[j < AP::GR ? j : 0]), r);
+              o = __builtin_bit_cast(u32x4, nv);
+            }
+            *reinterpret_cast<u32x4*>(As + (size_t)m * a_stride + 8 * v) = o;
+            if (W4L && !p.rowsum) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) rsum += bflo(o[i]) + bfhi(o[i]);
+            }
+          }
+        }
+      }
+      if (W4L && m < M && !p.rowsum) {
+        rsum = wave_sum(rsum);
+        if (lane == 0) tail[96 + wave * 8 + m] = rsum;
+      }
+    }
+    __syncthreads();
+  };
+  auto a_issue_any = [&]() {
+    if constexpr (MB == 1) {
+      if (rs == 1) a_issue(IC<1>{});
+      else if (rs == 2) a_issue(IC<2>{});
+      else if (rs == 4) a_issue(IC<4>{});
+      else if (rs == AP::XR) a_issue(IC<AP::XR>{});
+    } else {
+      if (rs == 2) a_issue(IC<2>{});
+      else if (rs == 4) a_issue(IC<4>{});
+    }
+  };
+
+  if constexpr (!CH) {
+    // standalone launch: every input is final, so the A-side loads go first (a wait for
+    // them then never waits for the weight chunks issued after them)
+    issue_pos();
+    issue_const();
+    issue_xr();
+    a_issue_any();
+#pragma unroll
+    for (int d = 0; d < D; ++d) load(d, d);  // the weight stream starts before any A wait
+  } else {
+    // chained: the weight stream needs no producer, so it starts first; then wait for the
+    // producer op and read its results (sc1)
+    issue_const();
+#pragma unroll
+    for (int d = 0; d < D; ++d) load(d, d);
+    chain_wait(cc);
+    issue_pos();
+    issue_xr();
+    a_issue_any();
+  }
+  LLJ_STAMP(1);
+  float2 e_cs[4];
+  if constexpr (EP == EP_QKV) {  // RoPE rows of the rows' positions (needs e_ps: waits for it only)
+    const int Cd = p.n_head * p.head_size;
+    const int dd = (n - (n0 / Cd) * Cd) % p.head_size;
+#pragma unroll
+    for (int r = 0; r < RR; ++r)
+      e_cs[r] = *reinterpret_cast<const float2*>(p.rope + ((size_t)e_ps[r] * (p.head_size >> 1) + (dd >> 1)) * 2);
+  }
+  if constexpr ((LLJ_ABL & 1) != 0) {  // ablation: no A prologue (garbage A)
+  } else if constexpr (I8) {
+    stage_i8<NW>(p, reinterpret_cast<int8_t*>(smem), a_stride, sca);
+    __syncthreads();
+  } else if constexpr (ALDS) {
+    if (rs == 0) {
+      stage_a<NW, AM == AM_NORM>(p, reinterpret_cast<bf16_t*>(smem), a_stride, tail);
+      __syncthreads();
+      if (W4L && !p.rowsum) {  // row sums of the staged rows (offset removal, see header)
+        const bf16_t* As = reinterpret_cast<const bf16_t*>(smem);
+        for (int m = 0; m < M; ++m) {
+          float rsum = 0.f;
+          for (int v = tid; v < nvec; v += NT) {
+            const u32x4 o = *reinterpret_cast<const u32x4*>(As + (size_t)m * a_stride + 8 * v);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rsum += bflo(o[i]) + bfhi(o[i]);
+          }
+          rsum = wave_sum(rsum);
+          if (lane == 0) tail[96 + wave * 8 + m] = rsum;
+        }
+      }
+    } else if constexpr (MB == 1) {
+      if (rs == 1) a_finish(IC<1>{});
+      else if (rs == 2) a_finish(IC<2>{});
+      else if (rs == 4) a_finish(IC<4>{});
+      else a_finish(IC<AP::XR>{});
+    } else {
+      if (rs == 2) a_finish(IC<2>{});
+      else a_finish(IC<4>{});
+    }
+  }
+  LLJ_STAMP(2);
+  // chunk i lives in buffer i % D; after computing it the buffer is refilled with chunk i + D.
+  // The steady loop runs while every refill is a real chunk; the peeled tail (< 2D chunks)
+  // issues no loads past the last chunk, so nothing is in flight when the epilogue waits.
+  int i0 = 0;
+  for (; i0 + 2 * D <= nmy; i0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      compute(d, i0 + d);
+      load(d, i0 + d + D);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    if (i0 + d < nmy) compute(d, i0 + d);
+    if (i0 + d + D < nmy) load(d, i0 + d + D);
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (i0 + D + d < nmy) compute(d, i0 + D + d);
+  LLJ_STAMP(3);
+  // ---- reduce the NW partial tiles in LDS (each wave: 64 lanes x 12 words; int8 sums stay
+  // int32 — they exceed 2^24 at K = 11008, so they must not round-trip through fp32)
+  constexpr int NV = 12;
+  // int8 side products in the LDS beyond the reduction scratch (the A image is no longer read)
+  float* side = reinterpret_cast<float*>(smem + kRedBytes);
+  if (NW > 1) {
+    if (ALDS) __syncthreads();  // every wave is done reading the A image it aliases
+    if constexpr (I8) {
+      i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W), reinterpret_cast<const float*>(p.sz), n0, side,
+                       smem);
+      if (DUAL)
+        i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W2), reinterpret_cast<const float*>(p.sz2), n0,
+                         side + NW * 8 * 16, smem);
+    }
+    if constexpr (I8) {
+      int* mine = reinterpret_cast<int*>(red) + (size_t)(wave * 64 + lane) * NV;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        mine[r] = iacc[r];
+        mine[4 + r] = iacc2[r];
+      }
+    } else {
+      float* mine = red + (size_t)(wave * 64 + lane) * NV;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        mine[r] = acc[r];
+        mine[4 + r] = acc2[r];
+        mine[8 + r] = sacc[r];
+      }
+    }
+    __syncthreads();
+    if (wave != 0) {
+      if constexpr (EP == EP_RESID)
+        if (p.nn_ctr) resid_norm_tail<NW>(p, red, false);
+      return;
+    }
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      if constexpr (I8) {
+        const int* o = reinterpret_cast<const int*>(red) + (size_t)(w * 64 + lane) * NV;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          iacc[r] += o[r];
+          iacc2[r] += o[4 + r];
+        }
+      } else {
+        const float* o = red + (size_t)(w * 64 + lane) * NV;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc[r] += o[r];
+          acc2[r] += o[4 + r];
+          sacc[r] += o[8 + r];
+        }
+      }
+    }
+  }
+
+  LLJ_STAMP(4);
+  // ---- epilogue (wave 0): lane holds C[m = 4*grp + r][n = n0 + row]
+  if constexpr ((LLJ_ABL & 4) != 0) {  // ablation: minimal epilogue
+    if (acc[0] == 1234.5f && row < M) p.C[n] = f2bf(acc[1] + acc2[2]);
+    return;
+  }
+  const float s1 = e_a.x, o1 = e_a.y, s2 = e_b.x, o2 = e_b.y;
+  const float bias = p.bias ? bf2f(e_braw) : 0.f;
+#pragma unroll
+  for (int r = 0; r < RR; ++r) {
+    if (r >= M) break;  // m = 4 grp + r >= r: no lane of the wave has a row left (uniform)
+    const int m = 4 * grp + r;
+    float y, y2 = 0.f;
+    if (W4L) {
+      float sa = sacc[r];
+      if (p.rowsum) {
+        sa = e_rs[r];  // rows >= M hold a clamped copy; their outputs are not stored
+      } else if constexpr (ALDS) {
+        sa = 0.f;
+        if (m < M) {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) sa += tail[96 + w * 8 + m];
+        }
+      }
+      y = s1 * (acc[r] - o1 * sa);
+      if (DUAL) y2 = s2 * (acc2[r] - o2 * sa);
+    } else if (WF == WF_BF16) {
+      y = acc[r];
+      y2 = acc2[r];
+    } else {
+      // mm_dequant (fp16 out) + fp16 outlier product, then cast back (bnb MatMul8bitLt)
+      const float sa = m < M ? sca[m] : 0.f;
+      const float kq = 1.f / (127.f * 127.f);
+      y = (float)iacc[r] * (sa * s1 * kq);
+      if (DUAL) y2 = (float)iacc2[r] * (sa * s2 * kq);
+      if (m < M) {
+        float sd = 0.f, sd2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          sd += side[(w * 8 + m) * 16 + row];
+          if (DUAL) sd2 += side[NW * 128 + (w * 8 + m) * 16 + row];
+        }
+        y = (float)(_Float16)((float)(_Float16)y + sd);
+        if (DUAL) y2 = (float)(_Float16)((float)(_Float16)y2 + sd2);
+      }
+    }
+    y += bias;
+    if (EP == EP_QKV) {
+      // c_attn output rounded to bf16 (model.py:204), then RoPE in fp32 (model.py:318-329)
+      const float v = round_bf(y);
+      const float partner = lane_xor1(v);
+      if (m < M) {
+        // head_size is a power of two (64 / 128, checked on the host): shifts, no divisions
+        const int Cd = p.n_head * p.head_size;
+        const int hs_sh = uniform(31 - __builtin_clz(p.head_size));
+        const int region = uniform(n0 / Cd);  // 0 q, 1 k, 2 v (uniform per workgroup)
+        const int nc = n - region * Cd;
+        const int h = nc >> hs_sh, dd = nc & (p.head_size - 1);
+        const int mg = p.m0 + m;
+        const int b = p.T == 1 ? mg : mg / p.T;
+        const int ps = e_ps[r];
+        float out = v;
+        if (region < 2) {
+          const float c = e_cs[r].x, s = e_cs[r].y;
+          out = (dd & 1) ? (v * c + partner * s) : (v * c - partner * s);
+        }
+        const uint32_t ob = (uint32_t)f2bf(out);
+        const uint32_t pr = lane_xor1(ob);  // columns (dd, dd + 1) leave as one 4-byte store
+        if (!(dd & 1)) {
+          bf16_t* dst;
+          size_t ei;
+          if (region == 0) {
+            dst = p.q_out;
+            ei = (size_t)mg * Cd + nc;
+          } else {
+            const int slot = ps < p.S ? ps : ps % p.S;
+            dst = region == 1 ? p.kcache : p.vcache;
+            ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
+          }
+          if constexpr (CH) st4_sc1(dst, (unsigned)(ei * 2), ob | (pr << 16));
+          else *reinterpret_cast<uint32_t*>(dst + ei) = ob | (pr << 16);
+        }
+      }
+    } else if (EP == EP_RESID) {
+      // x = x + h in bf16 (model.py:172-173); optionally the partial sum_k bf16(x_new^2) of
+      // this workgroup's 16 columns for the next RMSNorm (part nt of nst_out)
+      const float xn = round_bf(bf2f(e_xr[r]) + round_bf(y));
+      const uint32_t xb = (uint32_t)f2bf(xn);
+      const uint32_t pr = lane_xor1(xb);
+      float sq = 0.f;
+      if (m < M) {
+        sq = round_bf(xn * xn);
+        if (!(row & 1)) {
+          const size_t ei = (size_t)m * p.ldc + n;
+          if (CH || p.nn_ctr) st4_sc1(p.C, (unsigned)(ei * 2), xb | (pr << 16));  // read by another workgroup
+          else *reinterpret_cast<uint32_t*>(p.C + ei) = xb | (pr << 16);
+        }
+      }
+      if (p.nst_out) {
+        sq = row16_sum(sq);
+        if (row == 0 && m < M) {
+          if constexpr (CH) st8d_sc1(p.nst_out, (unsigned)(nt * 8 + m) * 8u, (double)sq);
+          else p.nst_out[nt * 8 + m] = (double)sq;
+        }
+      }
+    } else {
+      const uint32_t ob = (uint32_t)f2bf(out_value<EP>(y, y2));
+      const uint32_t pr = lane_xor1(ob);
+      if (m < M && !(row & 1)) {
+        const size_t ei = (size_t)m * p.ldc + n;
+        if constexpr (CH) st4_sc1(p.C, (unsigned)(ei * 2), ob | (pr << 16));
+        else *reinterpret_cast<uint32_t*>(p.C + ei) = ob | (pr << 16);
+      }
+    }
+  }
+  if constexpr (CH) chain_signal(cc);
+  if constexpr (EP == EP_RESID)
+    if (p.nn_ctr) resid_norm_tail<NW>(p, red, true);
+  LLJ_STAMP(5);
+}
+
+template <int WF, int AM, int EP, int NW, int D, int MB>
+__global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  gemv_body<WF, AM, EP, NW, D, MB, false>(p, blockIdx.x, smem, ChainCtl{});
+}
+
+// ------------------------------------------------------------------------------------
+#ifndef LLJ_NW
+#define LLJ_NW 4  // waves per workgroup (K split across them)
+#endif
+#ifndef LLJ_D
+#define LLJ_D 4  // weight chunks in flight per wave
+#endif
+#ifndef LLJ_D1
+#define LLJ_D1 LLJ_D  // chunks in flight per wave for the single-matrix ops (QKV, c_proj, down, head)
+#endif
+// The residual ops have only N / 16 = C / 16 workgroups (256 at 7B, one per CU); with a long K
+// (mlp.c_proj, K = n_hidden) twice the waves keep twice the weight chunks in flight per CU
+// (measured 7B bs=1: 8.8 -> 8.2 us; c_proj with K = C gains nothing and keeps 4 waves).
+#ifndef LLJ_NWR
+#define LLJ_NWR 8  // waves per workgroup of a residual op with K >= LLJ_NWR_KMIN
+#endif
+#ifndef LLJ_NWR_KMIN
+#define LLJ_NWR_KMIN 8192
+#endif
+constexpr int kNW = LLJ_NW;
+constexpr int kD = LLJ_D;
+
+static inline size_t a_image_bytes(int wf, int am, int M, int K) {
+  if (wf == WF_I8) return (((size_t)M * (K + 16)) + 15) & ~(size_t)15;
+  if (am == AM_GLOBAL) return 0;
+  return (((size_t)M * (K + 8) * 2) + 15) & ~(size_t)15;
+}
+static inline size_t gemv_smem(int wf, int am, int M, int K, int nw = kNW) {
+  const size_t a = a_image_bytes(wf, am, M, K);
+  // int8: the side-product partials (2 matrices x NW x 8 rows x 16 columns) follow the scratch
+  const size_t red = (size_t)nw * 64 * 12 * 4 + (wf == WF_I8 ? (size_t)2 * nw * 8 * 16 * 4 : 0);
+  return (a > red ? a : red) + 128 * 4;
+}
+
+// the LDS A image must leave room for the reduction scratch: <= 96 KiB, M <= 8 rows
+static inline bool lds_fits(int wf, int M, int K) { return M <= 8 && a_image_bytes(wf, AM_LDS, M, K) <= 96 * 1024; }
+
+// waves per workgroup: the global-A form (rows whose A image does not fit the LDS) keeps twice
+// as many waves, each with fewer chunks, for more A-fragment loads in flight
+template <int AM>
+constexpr int nw_of() { return AM == AM_GLOBAL ? 2 * kNW : kNW; }
+template <int EP>
+constexpr int d_of() { return EP == EP_SWIGLU ? kD : LLJ_D1; }
+
+template <int WF, int AM, int EP, int MB, int NW = nw_of<AM>()>
+static int launch_mb(const GemvParams& p, hipStream_t s) {
+  const size_t sm = gemv_smem(WF, AM, p.M, p.K, NW);
+  auto kern = gemv_kernel<WF, AM, EP, NW, d_of<EP>(), MB>;
+  static bool attr_set = false;  // per instantiation; set before any graph capture
+  if (sm > 64 * 1024 && !attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(p.N / 16), dim3(NW * 64), sm, s, p);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int WF, int AM, int EP>
+static int launch(const GemvParams& p, hipStream_t s) {
+  // the register-staged prologue has an M == 1 class (bs = 1 decode) and an M <= 8 class
+  if constexpr (EP == EP_RESID && AM != AM_GLOBAL && LLJ_NWR != kNW) {
+    if (p.K >= LLJ_NWR_KMIN) {  // residual ops: 256 workgroups, more waves each
+      if (WF != WF_I8 && p.M == 1) return launch_mb<WF, AM, EP, 1, LLJ_NWR>(p, s);
+      return launch_mb<WF, AM, EP, 8, LLJ_NWR>(p, s);
+    }
+  }
+  if (WF != WF_I8 && AM != AM_GLOBAL && p.M == 1) return launch_mb<WF, AM, EP, 1>(p, s);
+  return launch_mb<WF, AM, EP, 8>(p, s);
+}
+
+// A mode for a call: fused RMSNorm needs the LDS image; otherwise stage when it fits.
+static int pick_am(int wf, const GemvParams& p) {
+  if (wf == WF_I8) return (p.norm_w || !p.i8ws || !lds_fits(wf, p.M, p.K)) ? -1 : AM_LDS;
+  if (p.norm_w) return lds_fits(wf, p.M, p.K) ? AM_NORM : -1;
+  return lds_fits(wf, p.M, p.K) ? AM_LDS : AM_GLOBAL;
+}
+
+static int check_shape(int wf, const GemvParams& p) {
+  if (p.M < 1 || p.M > 16 || p.N % 16 || p.K % 128 || p.K < 128) return LLJ_EINVAL;
+  if (wf != WF_W4 && wf != WF_BF16 && wf != WF_I8 && wf != WF_W8) return LLJ_EINVAL;
+  if (wf != WF_BF16 && !p.sz) return LLJ_EINVAL;
+  if (p.C && (p.ldc & 1)) return LLJ_EINVAL;  // epilogues store column pairs as 4-byte words
+  return 0;
+}
+
+// Per-weight-format launchers, one translation unit each (gemv_w4.hip, gemv_bf16.hip,
+// gemv_w8.hip, gemv_i8.hip) so the instantiations compile in parallel.
+int gemv_launch_w4(int am, int ep, const GemvParams& p, hipStream_t s);
+int gemv_launch_bf16(int am, int ep, const GemvParams& p, hipStream_t s);
+int gemv_launch_w8(int am, int ep, const GemvParams& p, hipStream_t s);
+int gemv_launch_i8(int am, int ep, const GemvParams& p, hipStream_t s);
+
+template <int WF, int AM>
+static int launch_ep(int ep, const GemvParams& p, hipStream_t s) {
+  switch (ep) {
+    case EP_STORE: return launch<WF, AM, EP_STORE>(p, s);
+    case EP_RESID: return launch<WF, AM, EP_RESID>(p, s);
+    case EP_QKV: return launch<WF, AM, EP_QKV>(p, s);
+    case EP_SWIGLU: return launch<WF, AM, EP_SWIGLU>(p, s);
+  }
+  return LLJ_EINVAL;
+}
+template <int WF>
+static int launch_fmt(int am, int ep, const GemvParams& p, hipStream_t s) {
+  if constexpr (WF == WF_I8) {
+    return launch_ep<WF_I8, AM_LDS>(ep, p, s);
+  } else {
+    if (am == AM_NORM) return launch_ep<WF, AM_NORM>(ep, p, s);
+    if (am == AM_LDS) return launch_ep<WF, AM_LDS>(ep, p, s);
+    return launch_ep<WF, AM_GLOBAL>(ep, p, s);
+  }
+}
+
+}  // namespace llj

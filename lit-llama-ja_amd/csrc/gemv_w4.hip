@@ -1,0 +1,10 @@
+// Instantiations of the GEMV kernels for weight format WF_W4 (gemv_impl.h).
+#include "gemv_impl.h"
+
+namespace llj {
+int gemv_launch_w4(int am, int ep, const GemvParams& p, hipStream_t s) { return launch_fmt<WF_W4>(am, ep, p, s); }
+}  // namespace llj
+
+extern "C" {
+LLJ_TRACE_EXPORT(w4)
+}

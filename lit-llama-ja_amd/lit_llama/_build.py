@@ -1,10 +1,13 @@
 """Build the in-tree HIP library (`_lljamd.so`) for gfx950 with hipcc. No torch in the ABI,
-so a plain `hipcc -shared` is enough; the .so lives next to this file so it travels with the
-repository snapshot to the GPU box."""
+so plain `hipcc` objects linked with `-shared` are enough; the .so lives next to this file so
+it travels with the repository snapshot to the GPU box. The translation units compile in
+parallel (one hipcc per .hip file), then link."""
 from __future__ import annotations
 
 import os
 import subprocess
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -12,6 +15,8 @@ CSRC = PKG.parent / "csrc"
 INCLUDE = PKG.parent.parent / "include"  # the public C ABI header (llj_layer)
 OUT = PKG / "_lljamd.so"
 ARCH = os.environ.get("LLJ_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-variable", "-Wno-unused-function",
+         "-munsafe-fp-atomics"]
 
 
 def sources():
@@ -25,19 +30,40 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in list(CSRC.glob("*")) + [INCLUDE / "lit_llama_amd.h"])
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: Path | None = None, defines=()) -> Path:
+    """Compile every csrc/*.hip for gfx950 and link `out` (default: the in-tree _lljamd.so).
+    `defines`: extra -D macros (profiling / experiment variants built next to the product)."""
+    out = Path(out) if out is not None else OUT
+    if out == OUT and not defines and not force and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmp = OUT.with_suffix(".so.tmp")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall",
-           "-Wno-unused-variable", "-Wno-unused-function", "-munsafe-fp-atomics", f"-I{INCLUDE}", "-o", str(tmp)] + [str(s) for s in sources()]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    extra = [f"-D{d}" for d in defines]
+    with tempfile.TemporaryDirectory(prefix="lljbuild") as td:
+        objs = []
+        cmds = []
+        for src in sources():
+            obj = Path(td) / (src.stem + ".o")
+            objs.append(obj)
+            cmds.append([hipcc, f"--offload-arch={ARCH}", *FLAGS, *extra, f"-I{INCLUDE}", "-c", str(src),
+                         "-o", str(obj)])
+
+        def run(cmd):
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+
+        with ThreadPoolExecutor(max_workers=len(cmds)) as ex:
+            list(ex.map(run, cmds))
+        tmp = out.with_suffix(".so.tmp")
+        link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs]
+        run(link)
+        os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    import sys
+
+    args = sys.argv[1:]
+    o = Path(args[0]) if args else None
+    print(build(force=True, verbose=True, out=o, defines=args[1:]))

@@ -86,6 +86,13 @@ CHAIN_LAYERS = False
 # but measured slower at 7B bs=8 (3.0 vs 2.2 ms/step): the write-through x stores every
 # workgroup must drain, plus the last workgroup's serial pass, cost more than the launch.
 FUSE_RESID_NORM = False
+# decode steps (T = 1, M <= 8): attention and attn.c_proj (+ residual) as ONE launch
+# (llj_attn_resid): the c_proj weight stream overlaps the attention, which leaves the chip
+# and HBM idle, and one kernel boundary per layer disappears. Bitwise equal to the two launches.
+ATTN_RESID = False
+# M == 1: RMSNorm row statistics handed from the residual epilogues to the next norm-fused
+# GEMV as per-workgroup partial sums (_Work.nst) instead of re-reduced by every consumer
+NST_STATS = False
 
 
 # weight formats whose kernels remove the nibble offset with the row sums of A (W4P, W8P)
@@ -140,7 +147,7 @@ class _Work:
             self.i8ws = torch.empty(nb, dtype=torch.uint8, device=device)
         else:
             self.i8ws = None
-        if M == 1 and not need_i8:
+        if M == 1 and not need_i8 and NST_STATS:
             parts = max(1, C // 16)
             self.nst = (torch.zeros(parts * 8, dtype=torch.float64, device=device),
                         torch.zeros(parts * 8, dtype=torch.float64, device=device))
@@ -287,7 +294,8 @@ class LLaMA(nn.Module):
         P = _hip.ptr
         w.xn_ready = False  # the embedding (or caller) just wrote a fresh x
         chained = T == 1 and M <= QKV_ROWS and w.nst is not None and CHAIN_LAYERS
-        if chained:
+        attn_resid = T == 1 and M <= QKV_ROWS and ATTN_RESID and not chained
+        if chained or attn_resid:
             w.ctr.zero_()
         for i, blk in enumerate(self.transformer.h):
             (fa, wa, sa), (fp, wp, sp), (f1, w1, s1), (f2, w2, s2), (fd, wd, sd) = specs["layers"][i]
@@ -322,18 +330,23 @@ class LLaMA(nn.Module):
                 _hip.call("llj_norm_qkv_rope", fa, src.data_ptr(), nw, blk.rms_1.eps, wa.data_ptr(), P(sa),
                           w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), B, T, C, nh,
                           S, r0, r, P(w.i8ws), w.nst_ptr(0), 1 if i == 0 else C // 16, P(rs), st)
-            # 2. attention
-            _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(), pos.data_ptr(),
-                      B, T, nh, C // nh, S, st)
-            # 3. c_proj + residual (+ rms_2 row statistics, or rms_2 itself for batched rows)
+            # 2.+3. attention, c_proj + residual (+ rms_2 row statistics, or rms_2 itself for
+            # batched rows); one launch for decode rows (llj_attn_resid)
             w.xn_ready = False
-            if w.nctr is not None and fp in (0, 1) and f1 in (0, 1):
-                _hip.call("llj_linear_resid_norm", fp, w.y.data_ptr(), C, wp.data_ptr(), P(sp), w.x.data_ptr(), C, M,
-                          C, C, blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(), w.rs.data_ptr(),
-                          w.nctr.data_ptr(), st)
-                w.xn_ready = True
+            if attn_resid and fp in (0, 1, 3) and w.nctr is None:
+                _hip.call("llj_attn_resid", fp, w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                          pos.data_ptr(), M, nh, S, wp.data_ptr(), P(sp), w.x.data_ptr(), C, w.nst_ptr(1),
+                          w.ctr[128 * i].data_ptr(), w.err.data_ptr(), st)
             else:
-                self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst_ptr(1))
+                _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                          pos.data_ptr(), B, T, nh, C // nh, S, st)
+                if w.nctr is not None and fp in (0, 1) and f1 in (0, 1):
+                    _hip.call("llj_linear_resid_norm", fp, w.y.data_ptr(), C, wp.data_ptr(), P(sp), w.x.data_ptr(),
+                              C, M, C, C, blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(),
+                              w.rs.data_ptr(), w.nctr.data_ptr(), st)
+                    w.xn_ready = True
+                else:
+                    self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst_ptr(1))
             # 4. rms_2 + fc1/fc2 + silu*mul
             if f1 != f2:
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")

@@ -339,3 +339,30 @@ def test_chained_layer_equals_five_launches(mode, n_embd, n_head, B):
         MD.CHAIN_LAYERS = False
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("mode", ["gptq.int4", None, "gptq.int8"])
+@pytest.mark.parametrize("n_embd,n_head,B", [(256, 4, 1), (256, 4, 3), (1024, 8, 1), (1024, 8, 8)])
+def test_attn_resid_launch_equals_separate_launches(mode, n_embd, n_head, B):
+    """Decode with attention + attn.c_proj fused into one launch (model.ATTN_RESID, the
+    default) produces bitwise the tokens and logits of the separate launches."""
+    from lit_llama import model as MD
+    from lit_llama.engine import DecodeSession
+
+    m = _random_int4_model(n_embd, n_head, mode=mode, seed=3 * n_embd + B)
+    prompt = torch.randint(3, 2048, (B, 6), generator=torch.Generator().manual_seed(B)).cuda()
+    outs = []
+    saved = MD.ATTN_RESID
+    try:
+        for fused in (False, True):
+            MD.ATTN_RESID = fused
+            s = DecodeSession(m, B, 64, 40)
+            s.prefill(prompt)
+            s.decode(24)
+            torch.cuda.synchronize()
+            assert int(s.work.err.sum()) == 0, "a dependency wait timed out"
+            outs.append((s.output().cpu().numpy(), s.logits.float().cpu().numpy()))
+    finally:
+        MD.ATTN_RESID = saved
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
