@@ -44,6 +44,11 @@ int llj_w4_scale_zero(const void* scales, const void* zeros, int dtype, void* sz
 int llj_w8_repack(const void* qweight_ref, void* packed, int N, int K, void* stream);
 int llj_w8_scale_zero(const void* scales, const void* zeros, int dtype, void* sz, int N, void* stream);
 
+/* Host-side tuning knob (no device work): at most `tiles` 16-column tiles per workgroup in the
+ * int4 / gptq.int8 GEMVs (default 4; 1 = one tile per workgroup). Results do not depend on it
+ * (tested bitwise). Returns the previous value. */
+int llj_set_tpw_max(int tiles);
+
 /* ---------------------------------------------------------------- linear layers
  * wfmt: 0 = int4 W4P (sz = (scale, 128+zero) pairs required), 1 = bf16 (N, K) row-major
  * (torch.nn.Linear.weight), 2 = LLM.int8() CB (N, K) int8 with sz = SCB (N) fp32,

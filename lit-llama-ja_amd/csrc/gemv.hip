@@ -5,6 +5,8 @@
 
 namespace llj {
 
+int g_tpw_max = LLJ_TPW_MAX;
+
 template <int EP>
 static int dispatch(int wf, int am, const GemvParams& p, hipStream_t s) {
   switch (wf) {
@@ -30,6 +32,13 @@ static int run(int wf, GemvParams& p, void* stream) {
 using namespace llj;
 
 extern "C" {
+// Cap on tiles per workgroup of the multi-tile GEMV forms (1 = one tile per workgroup);
+// returns the previous cap. A host-side launch parameter only (no device state).
+int llj_set_tpw_max(int tiles) {
+  const int old = g_tpw_max;
+  g_tpw_max = tiles < 1 ? 1 : tiles;
+  return old;
+}
 
 // C[M,N] = A[M,K] . W^T (+bias); bf16 in/out, fp32 accumulation, M <= 16 (int8: <= 8) per call.
 int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, const void* bias, void* C,

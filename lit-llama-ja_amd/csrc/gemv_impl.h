@@ -402,13 +402,27 @@ __device__ void resid_norm_tail(const GemvParams& p, float* red, bool storing_wa
   if (tid == 0) *p.nn_ctr = 0u;  // ready for the next launch (kernel boundaries order it)
 }
 
+#ifndef LLJ_ABAR
+#define LLJ_ABAR 0
+#endif
 #ifndef LLJ_ABL
 #define LLJ_ABL 0  // ablation switches for profiling only (1 no A prologue, 2 no compute, 4 no epilogue)
 #endif
 
-template <int WF, int AM, int EP, int NW, int D, int MB, bool CH>
-__device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, unsigned char* smem,
+// LDS tail (floats) behind the A image / reduction scratch: [0, 8) per-row RMSNorm rstd (int8:
+// SCA), [8, 8 + 16 NW) the norm's per-wave fp64 / fp32 row partials, then [TL_RS, TL_RS + 8 NW)
+// the per-wave row sums of the staged A (int4 / int8-GPTQ offset removal).
+__host__ __device__ constexpr int tail_floats(int nw) { return 8 + 24 * nw; }
+
+// One workgroup computes TPW consecutive 16-column tiles nt0 .. nt0 + TPW - 1 (tiles past the
+// last one are loaded as a copy of it and never stored): every wave streams its K-chunks of
+// all TPW tiles behind ONE staged A image, so the prologue (activation rows, RMSNorm) runs
+// once per workgroup instead of once per tile. TPW > 1 only for the standalone LDS-A forms.
+template <int WF, int AM, int EP, int NW, int D, int MB, bool CH, int TPW = 1>
+__device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, unsigned char* smem,
                                           const ChainCtl& cc) {
+  static_assert(TPW == 1 || (!CH && WF != WF_I8 && AM != AM_GLOBAL), "multi-tile: standalone LDS-A forms");
+  constexpr int TL_RS = 8 + 16 * NW;
   constexpr bool DUAL = (EP == EP_SWIGLU);
   constexpr bool I8 = (WF == WF_I8);
   constexpr bool W4L = (WF == WF_W4 || WF == WF_W8);  // nibble-coded: offset removed with row sums
@@ -417,14 +431,22 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   constexpr int NSTEP = I8 ? 2 : 4;
   const int lane = threadIdx.x & 63;
   const int wave = uniform(threadIdx.x >> 6);
-  const int n0 = nt * 16;
   const int K = p.K, M = p.M, KC = K >> 7;
+  const int ntiles = p.N >> 4;
+  int ntj[TPW];  // tile of slot j (clamped copy of the last tile past the end)
+  bool tvalid[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    tvalid[j] = nt0 + j < ntiles;
+    ntj[j] = tvalid[j] ? nt0 + j : ntiles - 1;
+  }
   const int row = lane & 15, grp = lane >> 4;
   // LDS carve: [A image, aliased after the main loop by the NW x 64 x 12-word reduction
   // scratch] [tail: 128 words for staging scratch / int8 SCA]
   const int a_stride = I8 ? K + 16 : K + 8;  // elements (bytes for int8)
   const size_t a_bytes = ALDS ? (((size_t)M * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15) : 0;
-  constexpr size_t kRedBytes = (size_t)NW * 64 * 12 * 4;
+  constexpr int NV = 8 * TPW + 4;  // reduction words per lane: acc, acc2 of every tile, sacc
+  constexpr size_t kRedBytes = (size_t)NW * 64 * NV * 4;
   constexpr size_t kScratch = kRedBytes + (I8 ? (size_t)2 * NW * 8 * 16 * 4 : 0);  // + int8 side partials
   float* red = reinterpret_cast<float*>(smem);
   float* tail = reinterpret_cast<float*>(smem + (a_bytes > kScratch ? a_bytes : kScratch));
@@ -449,44 +471,53 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   const u32x4 zero4 = {0, 0, 0, 0};
 
   // weight stream pointers (lane-resolved), in 16-byte units
-  const u32x4* w1;
-  const u32x4* w2 = nullptr;
+  const u32x4* w1[TPW];
+  const u32x4* w2[TPW];
   size_t wstep;  // 16-B units between consecutive chunks of this lane
   int vstride;   // 16-B units between the WV loads of one chunk
-  if (WF == WF_W4) {
-    w1 = reinterpret_cast<const u32x4*>(p.W) + (size_t)nt * KC * 64 + lane;
-    if (DUAL) w2 = reinterpret_cast<const u32x4*>(p.W2) + (size_t)nt * KC * 64 + lane;
-    wstep = 64; vstride = 0;
-  } else if (WF == WF_W8) {  // 2 KiB per (tile, chunk): low plane, then high plane
-    w1 = reinterpret_cast<const u32x4*>(p.W) + (size_t)nt * KC * 128 + lane;
-    if (DUAL) w2 = reinterpret_cast<const u32x4*>(p.W2) + (size_t)nt * KC * 128 + lane;
-    wstep = 128; vstride = 64;
-  } else if (WF == WF_BF16) {
-    const size_t off = (size_t)(n0 + row) * K + 8 * grp;  // elements
-    w1 = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.W) + off);
-    if (DUAL) w2 = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.W2) + off);
-    wstep = 16; vstride = 4;  // chunk = 256 B of a row; step t at +64 B
-  } else {
-    const size_t off = (size_t)(n0 + row) * K + 16 * grp;  // bytes
-    w1 = reinterpret_cast<const u32x4*>(reinterpret_cast<const int8_t*>(p.W) + off);
-    if (DUAL) w2 = reinterpret_cast<const u32x4*>(reinterpret_cast<const int8_t*>(p.W2) + off);
-    wstep = 8; vstride = 4;  // chunk = 128 B of a row; step t at +64 B
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int nt = ntj[j], n0 = nt * 16;
+    w2[j] = nullptr;
+    if (WF == WF_W4) {
+      w1[j] = reinterpret_cast<const u32x4*>(p.W) + (size_t)nt * KC * 64 + lane;
+      if (DUAL) w2[j] = reinterpret_cast<const u32x4*>(p.W2) + (size_t)nt * KC * 64 + lane;
+      wstep = 64; vstride = 0;
+    } else if (WF == WF_W8) {  // 2 KiB per (tile, chunk): low plane, then high plane
+      w1[j] = reinterpret_cast<const u32x4*>(p.W) + (size_t)nt * KC * 128 + lane;
+      if (DUAL) w2[j] = reinterpret_cast<const u32x4*>(p.W2) + (size_t)nt * KC * 128 + lane;
+      wstep = 128; vstride = 64;
+    } else if (WF == WF_BF16) {
+      const size_t off = (size_t)(n0 + row) * K + 8 * grp;  // elements
+      w1[j] = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.W) + off);
+      if (DUAL) w2[j] = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.W2) + off);
+      wstep = 16; vstride = 4;  // chunk = 256 B of a row; step t at +64 B
+    } else {
+      const size_t off = (size_t)(n0 + row) * K + 16 * grp;  // bytes
+      w1[j] = reinterpret_cast<const u32x4*>(reinterpret_cast<const int8_t*>(p.W) + off);
+      if (DUAL) w2[j] = reinterpret_cast<const u32x4*>(reinterpret_cast<const int8_t*>(p.W2) + off);
+      wstep = 8; vstride = 4;  // chunk = 128 B of a row; step t at +64 B
+    }
   }
 
-  f32x4 acc = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, sacc = {0, 0, 0, 0};
+  f32x4 acc[TPW], acc2[TPW], sacc = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = acc2[j] = sacc;
   i32x4 iacc = {0, 0, 0, 0}, iacc2 = {0, 0, 0, 0};
   const int nmy = uniform((KC - wave + NW - 1) / NW);
 
-  u32x4 r1[D][WV], r2[D][WV];
+  u32x4 r1[D][TPW][WV], r2[D][TPW][WV];
   u32x4 ra[D][4];
   auto load = [&](int d, int i) {
     int c = wave + NW * (i < nmy ? i : nmy - 1);
     c = c < 0 ? 0 : (c >= KC ? KC - 1 : c);  // always a valid chunk (loads past the end are unused)
 #pragma unroll
-    for (int v = 0; v < WV; ++v) {
-      r1[d][v] = __builtin_nontemporal_load(w1 + (size_t)c * wstep + vstride * v);
-      if (DUAL) r2[d][v] = __builtin_nontemporal_load(w2 + (size_t)c * wstep + vstride * v);
-    }
+    for (int j = 0; j < TPW; ++j)
+#pragma unroll
+      for (int v = 0; v < WV; ++v) {
+        r1[d][j][v] = __builtin_nontemporal_load(w1[j] + (size_t)c * wstep + vstride * v);
+        if (DUAL) r2[d][j][v] = __builtin_nontemporal_load(w2[j] + (size_t)c * wstep + vstride * v);
+      }
     if (!ALDS) {
 #pragma unroll
       for (int t = 0; t < NSTEP; ++t)
@@ -496,8 +527,11 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   auto compute = [&](int d, int i) {
     const int c = wave + NW * i;
     if constexpr ((LLJ_ABL & 2) != 0) {  // ablation: loads only
-      acc[0] += __builtin_bit_cast(float, (r1[d][0].x ^ r1[d][0].w) & 0x3FFu);
-      if (DUAL) acc2[0] += __builtin_bit_cast(float, (r2[d][0].x ^ r2[d][0].w) & 0x3FFu);
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        acc[j][0] += __builtin_bit_cast(float, (r1[d][j][0].x ^ r1[d][j][0].w) & 0x3FFu);
+        if (DUAL) acc2[j][0] += __builtin_bit_cast(float, (r2[d][j][0].x ^ r2[d][j][0].w) & 0x3FFu);
+      }
       return;
     }
 #pragma unroll
@@ -507,26 +541,35 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
       const u32x4 av = ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
       if constexpr (WF == WF_W4) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
-        acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
-        if (DUAL) acc2 = mfma_bf16(a, dequant_w4(r2[d][0][t], msk, mag), acc2);
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          acc[j] = mfma_bf16(a, dequant_w4(r1[d][j][0][t], msk, mag), acc[j]);
+          if (DUAL) acc2[j] = mfma_bf16(a, dequant_w4(r2[d][j][0][t], msk, mag), acc2[j]);
+        }
         if (!ALDS && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);  // else: row sums from the prologue / caller
       } else if constexpr (WF == WF_W8) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
-        acc = mfma_bf16(a, dequant_w4(r1[d][0][t], msk, mag), acc);
-        acc = mfma_bf16(a, dequant_w4(r1[d][1][t], msk, mag_hi), acc);
-        if (DUAL) {
-          acc2 = mfma_bf16(a, dequant_w4(r2[d][0][t], msk, mag), acc2);
-          acc2 = mfma_bf16(a, dequant_w4(r2[d][1][t], msk, mag_hi), acc2);
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          acc[j] = mfma_bf16(a, dequant_w4(r1[d][j][0][t], msk, mag), acc[j]);
+          acc[j] = mfma_bf16(a, dequant_w4(r1[d][j][1][t], msk, mag_hi), acc[j]);
+          if (DUAL) {
+            acc2[j] = mfma_bf16(a, dequant_w4(r2[d][j][0][t], msk, mag), acc2[j]);
+            acc2[j] = mfma_bf16(a, dequant_w4(r2[d][j][1][t], msk, mag_hi), acc2[j]);
+          }
         }
         if (!ALDS && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);
       } else if constexpr (WF == WF_BF16) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
-        acc = mfma_bf16(a, __builtin_bit_cast(bf16x8, r1[d][t]), acc);
-        if (DUAL) acc2 = mfma_bf16(a, __builtin_bit_cast(bf16x8, r2[d][t]), acc2);
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          acc[j] = mfma_bf16(a, __builtin_bit_cast(bf16x8, r1[d][j][t]), acc[j]);
+          if (DUAL) acc2[j] = mfma_bf16(a, __builtin_bit_cast(bf16x8, r2[d][j][t]), acc2[j]);
+        }
       } else {
         const i32x4 a = __builtin_bit_cast(i32x4, av);
-        iacc = mfma_i8(a, __builtin_bit_cast(i32x4, r1[d][t]), iacc);
-        if (DUAL) iacc2 = mfma_i8(a, __builtin_bit_cast(i32x4, r2[d][t]), iacc2);
+        iacc = mfma_i8(a, __builtin_bit_cast(i32x4, r1[d][0][t]), iacc);
+        if (DUAL) iacc2 = mfma_i8(a, __builtin_bit_cast(i32x4, r2[d][0][t]), iacc2);
       }
     }
   };
@@ -536,7 +579,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   // (always valid) address and its validity applied where the value is used: a load under
   // divergent control flow makes the compiler's wait before the first use a vmcnt(0), which
   // would also wait for the weight prefetch issued after it.
-  const int n = n0 + row;
+  int nj[TPW];  // output column of this lane in tile slot j
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) nj[j] = ntj[j] * 16 + row;
   // accumulator rows a lane can hold a live output for: 4 (rows 4*grp + r), or 1 when the
   // instantiation is for M == 1 (MB == 1), so per-row operands load once instead of 4 times
   constexpr int RR = MB == 1 ? 1 : 4;
@@ -550,36 +595,48 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
       }
     }
   };
-  float2 e_a = make_float2(1.f, 0.f), e_b = make_float2(1.f, 0.f);
-  bf16_t e_braw = 0;
+  float2 e_a[TPW], e_b[TPW];
+  bf16_t e_braw[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    e_a[j] = e_b[j] = make_float2(1.f, 0.f);
+    e_braw[j] = 0;
+  }
   float e_rs[4] = {0.f, 0.f, 0.f, 0.f};  // caller's row sums (p.rowsum) of rows 4*grp + r
   auto issue_const = [&]() {  // weights-side epilogue operands (never written in a launch)
-    if constexpr (W4L) {
-      e_a = p.sz[n];
-      if (DUAL) e_b = p.sz2[n];
-      // an epilogue load under divergent control flow would put a vmcnt(0) between the
-      // row stores (stores count in vmcnt): read the row sums here (the branch is uniform)
-      if (p.rowsum) {
 #pragma unroll
-        for (int r = 0; r < RR; ++r) e_rs[r] = p.rowsum[4 * grp + r < M ? 4 * grp + r : M - 1];
+    for (int j = 0; j < TPW; ++j) {
+      const int n = nj[j];
+      if constexpr (W4L) {
+        e_a[j] = p.sz[n];
+        if (DUAL) e_b[j] = p.sz2[n];
+      } else if constexpr (I8) {
+        e_a[j].x = reinterpret_cast<const float*>(p.sz)[n];
+        if (DUAL) e_b[j].x = reinterpret_cast<const float*>(p.sz2)[n];
       }
-    } else if constexpr (I8) {
-      e_a.x = reinterpret_cast<const float*>(p.sz)[n];
-      if (DUAL) e_b.x = reinterpret_cast<const float*>(p.sz2)[n];
+      if (p.bias) e_braw[j] = p.bias[n];
     }
-    if (p.bias) e_braw = p.bias[n];
+    // an epilogue load under divergent control flow would put a vmcnt(0) between the
+    // row stores (stores count in vmcnt): read the row sums here (the branch is uniform)
+    if (W4L && p.rowsum) {
+#pragma unroll
+      for (int r = 0; r < RR; ++r) e_rs[r] = p.rowsum[4 * grp + r < M ? 4 * grp + r : M - 1];
+    }
   };
-  bf16_t e_xr[4] = {0, 0, 0, 0};
+  bf16_t e_xr[TPW][4];
   auto issue_xr = [&]() {  // residual stream values this workgroup updates
     if constexpr (EP == EP_RESID) {
 #pragma unroll
+      for (int j = 0; j < TPW; ++j)
+#pragma unroll
       for (int r = 0; r < RR; ++r) {
         const int mm = 4 * grp + r < M ? 4 * grp + r : M - 1;
+        const int n = nj[j];
         if constexpr (CH) {
           const uint32_t w = ld4_sc1(p.C, (unsigned)(((size_t)mm * p.ldc + (n & ~1)) * 2));
-          e_xr[r] = (bf16_t)((n & 1) ? (w >> 16) : (w & 0xFFFFu));
+          e_xr[j][r] = (bf16_t)((n & 1) ? (w >> 16) : (w & 0xFFFFu));
         } else {
-          e_xr[r] = p.C[(size_t)mm * p.ldc + n];
+          e_xr[j][r] = p.C[(size_t)mm * p.ldc + n];
         }
       }
     }
@@ -642,8 +699,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     constexpr int RS = decltype(rsc)::value;
     constexpr int MR = MB == 1 ? 1 : AP::XR / RS;
     if (NORM) {
-      double* redd = reinterpret_cast<double*>(tail + 32);  // [wave][8] fp64
-      float* redf = tail + 32;                              // [wave][8] fp32
+      double* redd = reinterpret_cast<double*>(tail + 8);  // [wave][8] fp64
+      float* redf = tail + 8;                              // [wave][8] fp32
       if (p.nst_in) {
         double sd = 0.0;
         const bool mok = tid % AP::SM < M;
@@ -713,7 +770,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
       }
       if (W4L && m < M && !p.rowsum) {
         rsum = wave_sum(rsum);
-        if (lane == 0) tail[96 + wave * 8 + m] = rsum;
+        if (lane == 0) tail[TL_RS + wave * 8 + m] = rsum;
       }
     }
     __syncthreads();
@@ -737,6 +794,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     issue_const();
     issue_xr();
     a_issue_any();
+#if LLJ_ABAR
+    __builtin_amdgcn_s_barrier();  // experiment: every wave's A loads ahead of any weight load
+#endif
 #pragma unroll
     for (int d = 0; d < D; ++d) load(d, d);  // the weight stream starts before any A wait
   } else {
@@ -751,13 +811,17 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     a_issue_any();
   }
   LLJ_STAMP(1);
-  float2 e_cs[4];
+  float2 e_cs[TPW][4];
   if constexpr (EP == EP_QKV) {  // RoPE rows of the rows' positions (needs e_ps: waits for it only)
     const int Cd = p.n_head * p.head_size;
-    const int dd = (n - (n0 / Cd) * Cd) % p.head_size;
 #pragma unroll
-    for (int r = 0; r < RR; ++r)
-      e_cs[r] = *reinterpret_cast<const float2*>(p.rope + ((size_t)e_ps[r] * (p.head_size >> 1) + (dd >> 1)) * 2);
+    for (int j = 0; j < TPW; ++j) {
+      const int dd = (nj[j] - (ntj[j] * 16 / Cd) * Cd) % p.head_size;
+#pragma unroll
+      for (int r = 0; r < RR; ++r)
+        e_cs[j][r] =
+            *reinterpret_cast<const float2*>(p.rope + ((size_t)e_ps[r] * (p.head_size >> 1) + (dd >> 1)) * 2);
+    }
   }
   if constexpr ((LLJ_ABL & 1) != 0) {  // ablation: no A prologue (garbage A)
   } else if constexpr (I8) {
@@ -777,7 +841,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
             for (int i = 0; i < 4; ++i) rsum += bflo(o[i]) + bfhi(o[i]);
           }
           rsum = wave_sum(rsum);
-          if (lane == 0) tail[96 + wave * 8 + m] = rsum;
+          if (lane == 0) tail[TL_RS + wave * 8 + m] = rsum;
         }
       }
     } else if constexpr (MB == 1) {
@@ -811,19 +875,20 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   for (int d = 0; d < D; ++d)
     if (i0 + D + d < nmy) compute(d, i0 + D + d);
   LLJ_STAMP(3);
-  // ---- reduce the NW partial tiles in LDS (each wave: 64 lanes x 12 words; int8 sums stay
-  // int32 — they exceed 2^24 at K = 11008, so they must not round-trip through fp32)
-  constexpr int NV = 12;
+  // ---- reduce the NW partial tiles in LDS (each wave: 64 lanes x NV words; int8 sums stay
+  // int32 — they exceed 2^24 at K = 11008, so they must not round-trip through fp32). Tile slot
+  // j is finished by wave j % NW, which sums the NW partials in wave order (the same order for
+  // every TPW, so results do not depend on the tiling).
   // int8 side products in the LDS beyond the reduction scratch (the A image is no longer read)
   float* side = reinterpret_cast<float*>(smem + kRedBytes);
   if (NW > 1) {
     if (ALDS) __syncthreads();  // every wave is done reading the A image it aliases
     if constexpr (I8) {
-      i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W), reinterpret_cast<const float*>(p.sz), n0, side,
-                       smem);
+      i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W), reinterpret_cast<const float*>(p.sz), ntj[0] * 16,
+                       side, smem);
       if (DUAL)
-        i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W2), reinterpret_cast<const float*>(p.sz2), n0,
-                         side + NW * 8 * 16, smem);
+        i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W2), reinterpret_cast<const float*>(p.sz2),
+                         ntj[0] * 16, side + NW * 8 * 16, smem);
     }
     if constexpr (I8) {
       int* mine = reinterpret_cast<int*>(red) + (size_t)(wave * 64 + lane) * NV;
@@ -835,153 +900,170 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
     } else {
       float* mine = red + (size_t)(wave * 64 + lane) * NV;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        mine[r] = acc[r];
-        mine[4 + r] = acc2[r];
-        mine[8 + r] = sacc[r];
-      }
+      for (int j = 0; j < TPW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          mine[8 * j + r] = acc[j][r];
+          mine[8 * j + 4 + r] = acc2[j][r];
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mine[8 * TPW + r] = sacc[r];
     }
     __syncthreads();
-    if (wave != 0) {
+    if (wave >= TPW) {  // owns no tile slot
       if constexpr (EP == EP_RESID)
         if (p.nn_ctr) resid_norm_tail<NW>(p, red, false);
       return;
     }
+  }
+  LLJ_STAMP(4);
+
+  // ---- epilogue of tile slot j (its owner wave): lane holds C[m = 4*grp + r][n = nj[j]]
+  auto epilogue = [&](const int j, const f32x4 ya, const f32x4 yb, const f32x4 ys, const i32x4 yi,
+                      const i32x4 yi2) {
+    const int n = nj[j], n0 = ntj[j] * 16, nt = ntj[j];
+    if constexpr ((LLJ_ABL & 4) != 0) {  // ablation: minimal epilogue
+      if (ya[0] == 1234.5f && row < M) p.C[n] = f2bf(ya[1] + yb[2]);
+      return;
+    }
+    const float s1 = e_a[j].x, o1 = e_a[j].y, s2 = e_b[j].x, o2 = e_b[j].y;
+    const float bias = p.bias ? bf2f(e_braw[j]) : 0.f;
 #pragma unroll
-    for (int w = 1; w < NW; ++w) {
-      if constexpr (I8) {
-        const int* o = reinterpret_cast<const int*>(red) + (size_t)(w * 64 + lane) * NV;
+    for (int r = 0; r < RR; ++r) {
+      if (r >= M) break;  // m = 4 grp + r >= r: no lane of the wave has a row left (uniform)
+      const int m = 4 * grp + r;
+      float y, y2 = 0.f;
+      if (W4L) {
+        float sa = ys[r];
+        if (p.rowsum) {
+          sa = e_rs[r];  // rows >= M hold a clamped copy; their outputs are not stored
+        } else if constexpr (ALDS) {
+          sa = 0.f;
+          if (m < M) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          iacc[r] += o[r];
-          iacc2[r] += o[4 + r];
+            for (int w = 0; w < NW; ++w) sa += tail[TL_RS + w * 8 + m];
+          }
+        }
+        y = s1 * (ya[r] - o1 * sa);
+        if (DUAL) y2 = s2 * (yb[r] - o2 * sa);
+      } else if (WF == WF_BF16) {
+        y = ya[r];
+        y2 = yb[r];
+      } else {
+        // mm_dequant (fp16 out) + fp16 outlier product, then cast back (bnb MatMul8bitLt)
+        const float sa = m < M ? sca[m] : 0.f;
+        const float kq = 1.f / (127.f * 127.f);
+        y = (float)yi[r] * (sa * s1 * kq);
+        if (DUAL) y2 = (float)yi2[r] * (sa * s2 * kq);
+        if (m < M) {
+          float sd = 0.f, sd2 = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            sd += side[(w * 8 + m) * 16 + row];
+            if (DUAL) sd2 += side[NW * 128 + (w * 8 + m) * 16 + row];
+          }
+          y = (float)(_Float16)((float)(_Float16)y + sd);
+          if (DUAL) y2 = (float)(_Float16)((float)(_Float16)y2 + sd2);
+        }
+      }
+      y += bias;
+      if (EP == EP_QKV) {
+        // c_attn output rounded to bf16 (model.py:204), then RoPE in fp32 (model.py:318-329)
+        const float v = round_bf(y);
+        const float partner = lane_xor1(v);
+        if (m < M) {
+          // head_size is a power of two (64 / 128, checked on the host): shifts, no divisions
+          const int Cd = p.n_head * p.head_size;
+          const int hs_sh = uniform(31 - __builtin_clz(p.head_size));
+          const int region = uniform(n0 / Cd);  // 0 q, 1 k, 2 v (uniform per tile)
+          const int nc = n - region * Cd;
+          const int h = nc >> hs_sh, dd = nc & (p.head_size - 1);
+          const int mg = p.m0 + m;
+          const int b = p.T == 1 ? mg : mg / p.T;
+          const int ps = e_ps[r];
+          float out = v;
+          if (region < 2) {
+            const float c = e_cs[j][r].x, sn = e_cs[j][r].y;
+            out = (dd & 1) ? (v * c + partner * sn) : (v * c - partner * sn);
+          }
+          const uint32_t ob = (uint32_t)f2bf(out);
+          const uint32_t pr = lane_xor1(ob);  // columns (dd, dd + 1) leave as one 4-byte store
+          if (!(dd & 1)) {
+            bf16_t* dst;
+            size_t ei;
+            if (region == 0) {
+              dst = p.q_out;
+              ei = (size_t)mg * Cd + nc;
+            } else {
+              const int slot = ps < p.S ? ps : ps % p.S;
+              dst = region == 1 ? p.kcache : p.vcache;
+              ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
+            }
+            if constexpr (CH) st4_sc1(dst, (unsigned)(ei * 2), ob | (pr << 16));
+            else *reinterpret_cast<uint32_t*>(dst + ei) = ob | (pr << 16);
+          }
+        }
+      } else if (EP == EP_RESID) {
+        // x = x + h in bf16 (model.py:172-173); optionally the partial sum_k bf16(x_new^2) of
+        // this tile's 16 columns for the next RMSNorm (part nt of nst_out)
+        const float xn = round_bf(bf2f(e_xr[j][r]) + round_bf(y));
+        const uint32_t xb = (uint32_t)f2bf(xn);
+        const uint32_t pr = lane_xor1(xb);
+        float sq = 0.f;
+        if (m < M) {
+          sq = round_bf(xn * xn);
+          if (!(row & 1)) {
+            const size_t ei = (size_t)m * p.ldc + n;
+            if (CH || p.nn_ctr) st4_sc1(p.C, (unsigned)(ei * 2), xb | (pr << 16));  // read by another workgroup
+            else *reinterpret_cast<uint32_t*>(p.C + ei) = xb | (pr << 16);
+          }
+        }
+        if (p.nst_out) {
+          sq = row16_sum(sq);
+          if (row == 0 && m < M) {
+            if constexpr (CH) st8d_sc1(p.nst_out, (unsigned)(nt * 8 + m) * 8u, (double)sq);
+            else p.nst_out[nt * 8 + m] = (double)sq;
+          }
         }
       } else {
-        const float* o = red + (size_t)(w * 64 + lane) * NV;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          acc[r] += o[r];
-          acc2[r] += o[4 + r];
-          sacc[r] += o[8 + r];
-        }
-      }
-    }
-  }
-
-  LLJ_STAMP(4);
-  // ---- epilogue (wave 0): lane holds C[m = 4*grp + r][n = n0 + row]
-  if constexpr ((LLJ_ABL & 4) != 0) {  // ablation: minimal epilogue
-    if (acc[0] == 1234.5f && row < M) p.C[n] = f2bf(acc[1] + acc2[2]);
-    return;
-  }
-  const float s1 = e_a.x, o1 = e_a.y, s2 = e_b.x, o2 = e_b.y;
-  const float bias = p.bias ? bf2f(e_braw) : 0.f;
-#pragma unroll
-  for (int r = 0; r < RR; ++r) {
-    if (r >= M) break;  // m = 4 grp + r >= r: no lane of the wave has a row left (uniform)
-    const int m = 4 * grp + r;
-    float y, y2 = 0.f;
-    if (W4L) {
-      float sa = sacc[r];
-      if (p.rowsum) {
-        sa = e_rs[r];  // rows >= M hold a clamped copy; their outputs are not stored
-      } else if constexpr (ALDS) {
-        sa = 0.f;
-        if (m < M) {
-#pragma unroll
-          for (int w = 0; w < NW; ++w) sa += tail[96 + w * 8 + m];
-        }
-      }
-      y = s1 * (acc[r] - o1 * sa);
-      if (DUAL) y2 = s2 * (acc2[r] - o2 * sa);
-    } else if (WF == WF_BF16) {
-      y = acc[r];
-      y2 = acc2[r];
-    } else {
-      // mm_dequant (fp16 out) + fp16 outlier product, then cast back (bnb MatMul8bitLt)
-      const float sa = m < M ? sca[m] : 0.f;
-      const float kq = 1.f / (127.f * 127.f);
-      y = (float)iacc[r] * (sa * s1 * kq);
-      if (DUAL) y2 = (float)iacc2[r] * (sa * s2 * kq);
-      if (m < M) {
-        float sd = 0.f, sd2 = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-          sd += side[(w * 8 + m) * 16 + row];
-          if (DUAL) sd2 += side[NW * 128 + (w * 8 + m) * 16 + row];
-        }
-        y = (float)(_Float16)((float)(_Float16)y + sd);
-        if (DUAL) y2 = (float)(_Float16)((float)(_Float16)y2 + sd2);
-      }
-    }
-    y += bias;
-    if (EP == EP_QKV) {
-      // c_attn output rounded to bf16 (model.py:204), then RoPE in fp32 (model.py:318-329)
-      const float v = round_bf(y);
-      const float partner = lane_xor1(v);
-      if (m < M) {
-        // head_size is a power of two (64 / 128, checked on the host): shifts, no divisions
-        const int Cd = p.n_head * p.head_size;
-        const int hs_sh = uniform(31 - __builtin_clz(p.head_size));
-        const int region = uniform(n0 / Cd);  // 0 q, 1 k, 2 v (uniform per workgroup)
-        const int nc = n - region * Cd;
-        const int h = nc >> hs_sh, dd = nc & (p.head_size - 1);
-        const int mg = p.m0 + m;
-        const int b = p.T == 1 ? mg : mg / p.T;
-        const int ps = e_ps[r];
-        float out = v;
-        if (region < 2) {
-          const float c = e_cs[r].x, s = e_cs[r].y;
-          out = (dd & 1) ? (v * c + partner * s) : (v * c - partner * s);
-        }
-        const uint32_t ob = (uint32_t)f2bf(out);
-        const uint32_t pr = lane_xor1(ob);  // columns (dd, dd + 1) leave as one 4-byte store
-        if (!(dd & 1)) {
-          bf16_t* dst;
-          size_t ei;
-          if (region == 0) {
-            dst = p.q_out;
-            ei = (size_t)mg * Cd + nc;
-          } else {
-            const int slot = ps < p.S ? ps : ps % p.S;
-            dst = region == 1 ? p.kcache : p.vcache;
-            ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
-          }
-          if constexpr (CH) st4_sc1(dst, (unsigned)(ei * 2), ob | (pr << 16));
-          else *reinterpret_cast<uint32_t*>(dst + ei) = ob | (pr << 16);
-        }
-      }
-    } else if (EP == EP_RESID) {
-      // x = x + h in bf16 (model.py:172-173); optionally the partial sum_k bf16(x_new^2) of
-      // this workgroup's 16 columns for the next RMSNorm (part nt of nst_out)
-      const float xn = round_bf(bf2f(e_xr[r]) + round_bf(y));
-      const uint32_t xb = (uint32_t)f2bf(xn);
-      const uint32_t pr = lane_xor1(xb);
-      float sq = 0.f;
-      if (m < M) {
-        sq = round_bf(xn * xn);
-        if (!(row & 1)) {
+        const uint32_t ob = (uint32_t)f2bf(out_value<EP>(y, y2));
+        const uint32_t pr = lane_xor1(ob);
+        if (m < M && !(row & 1)) {
           const size_t ei = (size_t)m * p.ldc + n;
-          if (CH || p.nn_ctr) st4_sc1(p.C, (unsigned)(ei * 2), xb | (pr << 16));  // read by another workgroup
-          else *reinterpret_cast<uint32_t*>(p.C + ei) = xb | (pr << 16);
+          if constexpr (CH) st4_sc1(p.C, (unsigned)(ei * 2), ob | (pr << 16));
+          else *reinterpret_cast<uint32_t*>(p.C + ei) = ob | (pr << 16);
         }
-      }
-      if (p.nst_out) {
-        sq = row16_sum(sq);
-        if (row == 0 && m < M) {
-          if constexpr (CH) st8d_sc1(p.nst_out, (unsigned)(nt * 8 + m) * 8u, (double)sq);
-          else p.nst_out[nt * 8 + m] = (double)sq;
-        }
-      }
-    } else {
-      const uint32_t ob = (uint32_t)f2bf(out_value<EP>(y, y2));
-      const uint32_t pr = lane_xor1(ob);
-      if (m < M && !(row & 1)) {
-        const size_t ei = (size_t)m * p.ldc + n;
-        if constexpr (CH) st4_sc1(p.C, (unsigned)(ei * 2), ob | (pr << 16));
-        else *reinterpret_cast<uint32_t*>(p.C + ei) = ob | (pr << 16);
       }
     }
+  };
+
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    if (j % NW != wave || !tvalid[j]) continue;  // uniform
+    f32x4 ya = acc[j], yb = acc2[j], ys = sacc;
+    i32x4 yi = iacc, yi2 = iacc2;
+    if (NW > 1) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        if constexpr (I8) {
+          const int* o = reinterpret_cast<const int*>(red) + (size_t)(w * 64 + lane) * NV;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            yi[r] = w == 0 ? o[r] : yi[r] + o[r];
+            yi2[r] = w == 0 ? o[4 + r] : yi2[r] + o[4 + r];
+          }
+        } else {
+          const float* o = red + (size_t)(w * 64 + lane) * NV;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ya[r] = w == 0 ? o[8 * j + r] : ya[r] + o[8 * j + r];
+            yb[r] = w == 0 ? o[8 * j + 4 + r] : yb[r] + o[8 * j + 4 + r];
+            ys[r] = w == 0 ? o[8 * TPW + r] : ys[r] + o[8 * TPW + r];
+          }
+        }
+      }
+    }
+    epilogue(j, ya, yb, ys, yi, yi2);
   }
   if constexpr (CH) chain_signal(cc);
   if constexpr (EP == EP_RESID)
@@ -989,10 +1071,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt, uns
   LLJ_STAMP(5);
 }
 
-template <int WF, int AM, int EP, int NW, int D, int MB>
+template <int WF, int AM, int EP, int NW, int D, int MB, int TPW>
 __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  gemv_body<WF, AM, EP, NW, D, MB, false>(p, blockIdx.x, smem, ChainCtl{});
+  gemv_body<WF, AM, EP, NW, D, MB, false, TPW>(p, blockIdx.x * TPW, smem, ChainCtl{});
 }
 
 // ------------------------------------------------------------------------------------
@@ -1022,12 +1104,47 @@ static inline size_t a_image_bytes(int wf, int am, int M, int K) {
   if (am == AM_GLOBAL) return 0;
   return (((size_t)M * (K + 8) * 2) + 15) & ~(size_t)15;
 }
-static inline size_t gemv_smem(int wf, int am, int M, int K, int nw = kNW) {
+static inline size_t gemv_smem(int wf, int am, int M, int K, int nw = kNW, int tpw = 1) {
   const size_t a = a_image_bytes(wf, am, M, K);
-  // int8: the side-product partials (2 matrices x NW x 8 rows x 16 columns) follow the scratch
-  const size_t red = (size_t)nw * 64 * 12 * 4 + (wf == WF_I8 ? (size_t)2 * nw * 8 * 16 * 4 : 0);
-  return (a > red ? a : red) + 128 * 4;
+  // reduction scratch (8 words per tile slot + 4 per lane); int8: the side-product partials
+  // (2 matrices x NW x 8 rows x 16 columns) follow it
+  const size_t red = (size_t)nw * 64 * (8 * tpw + 4) * 4 + (wf == WF_I8 ? (size_t)2 * nw * 8 * 16 * 4 : 0);
+  return (a > red ? a : red) + (((size_t)tail_floats(nw) * 4 + 15) & ~(size_t)15);
 }
+
+#ifndef LLJ_TPW_MAX
+#define LLJ_TPW_MAX 4  // tiles per workgroup at most (1 = one tile per workgroup)
+#endif
+// run-time cap on tiles per workgroup (llj_set_tpw_max, gemv.hip; A/B and equality tests)
+extern int g_tpw_max;
+// Compute units of the current device (cached per device; the query is not a stream
+// operation, so it is legal while a graph is being captured).
+static inline int device_cus() {
+  static int cus[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+// tiles per workgroup: ceil(tiles / CUs), i.e. about one workgroup per CU with every CU's
+// share of tiles minimal, capped at LLJ_TPW_MAX and the run-time cap. Batched rows only
+// (M >= 2: one staged A image of M rows per CU instead of per tile, 1.966 -> 1.865 ms at 7B
+// bs=8); a single row keeps one tile per workgroup, where several workgroups per CU interleave
+// on each SIMD (measured 7B bs=1: 1.205 ms with one tile, 1.305 ms with three per workgroup).
+static inline int pick_tpw(int ntiles, int M) {
+  if (M < 2) return 1;
+  const int cu = device_cus();
+  const int cap = g_tpw_max < LLJ_TPW_MAX ? g_tpw_max : LLJ_TPW_MAX;
+  const int t = (ntiles + cu - 1) / cu;
+  return t < 1 ? 1 : (t > cap ? cap : t);
+}
+// multi-tile instantiations: nibble-coded weights with the LDS A image
+template <int WF, int AM>
+constexpr bool tpw_ok() { return (WF == WF_W4 || WF == WF_W8) && AM != AM_GLOBAL && LLJ_TPW_MAX > 1; }
 
 // the LDS A image must leave room for the reduction scratch: <= 96 KiB, M <= 8 rows
 static inline bool lds_fits(int wf, int M, int K) { return M <= 8 && a_image_bytes(wf, AM_LDS, M, K) <= 96 * 1024; }
@@ -1039,19 +1156,33 @@ constexpr int nw_of() { return AM == AM_GLOBAL ? 2 * kNW : kNW; }
 template <int EP>
 constexpr int d_of() { return EP == EP_SWIGLU ? kD : LLJ_D1; }
 
-template <int WF, int AM, int EP, int MB, int NW = nw_of<AM>()>
-static int launch_mb(const GemvParams& p, hipStream_t s) {
-  const size_t sm = gemv_smem(WF, AM, p.M, p.K, NW);
-  auto kern = gemv_kernel<WF, AM, EP, NW, d_of<EP>(), MB>;
+template <int WF, int AM, int EP, int MB, int NW, int TPW>
+static int launch_t(const GemvParams& p, hipStream_t s) {
+  const size_t sm = gemv_smem(WF, AM, p.M, p.K, NW, TPW);
+  auto kern = gemv_kernel<WF, AM, EP, NW, d_of<EP>(), MB, TPW>;
   static bool attr_set = false;  // per instantiation; set before any graph capture
   if (sm > 64 * 1024 && !attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(p.N / 16), dim3(NW * 64), sm, s, p);
+  const int ntiles = p.N / 16;
+  hipLaunchKernelGGL(kern, dim3((ntiles + TPW - 1) / TPW), dim3(NW * 64), sm, s, p);
   LLJ_CHECK_LAUNCH();
   return 0;
+}
+
+template <int WF, int AM, int EP, int MB, int NW = nw_of<AM>()>
+static int launch_mb(const GemvParams& p, hipStream_t s) {
+  if constexpr (tpw_ok<WF, AM>() && MB > 1) {  // M == 1 (MB 1) always one tile: pick_tpw
+    switch (pick_tpw(p.N / 16, p.M)) {
+      case 2: return launch_t<WF, AM, EP, MB, NW, 2>(p, s);
+      case 3: return launch_t<WF, AM, EP, MB, NW, 3>(p, s);
+      case 4: return launch_t<WF, AM, EP, MB, NW, 4>(p, s);
+      default: break;
+    }
+  }
+  return launch_t<WF, AM, EP, MB, NW, 1>(p, s);
 }
 
 template <int WF, int AM, int EP>

@@ -50,6 +50,7 @@ SIGNATURES = {
     "llj_rmsnorm_rows": [_P, _P, _F, _P, _P, _I, _I, _P],
     "llj_argmax": [_P, _I, _I, _I, _P, _P, _I, _P, _P],
     "llj_decode_layer": [_P, _P],
+    "llj_set_tpw_max": [_I],
 }
 
 _lib = None

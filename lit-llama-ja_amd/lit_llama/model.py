@@ -93,6 +93,9 @@ ATTN_RESID = False
 # M == 1: RMSNorm row statistics handed from the residual epilogues to the next norm-fused
 # GEMV as per-workgroup partial sums (_Work.nst) instead of re-reduced by every consumer
 NST_STATS = False
+# batched rows (M >= 2): each RMSNorm as its own launch (llj_rmsnorm_rows) feeding LDS-A GEMVs,
+# instead of normalized inside every norm-fused GEMV workgroup
+PRE_NORM_ROWS = True
 
 
 # weight formats whose kernels remove the nibble offset with the row sums of A (W4P, W8P)
@@ -133,7 +136,7 @@ class _Work:
         self.h = torch.empty(M, H, dtype=bf, device=device)
         # batched rows (M >= 2): each RMSNorm runs once (llj_rmsnorm_rows -> xn, rs = fp32 row
         # sums for the int4 offset term) instead of inside every norm-fused GEMV workgroup
-        self.pre = M >= 2 and not need_i8
+        self.pre = M >= 2 and not need_i8 and PRE_NORM_ROWS
         self.xn = torch.empty(M, C, dtype=bf, device=device) if (need_i8 or self.pre) else None
         self.rs = torch.empty(M, dtype=torch.float32, device=device) if self.pre else None
         # completion counter of llj_linear_resid_norm (M <= 8): the residual GEMV's last
@@ -406,7 +409,7 @@ class LLaMA(nn.Module):
         elif M >= 2 and w.xn_ready and x is w.x:  # ln_f already applied by the last mlp.c_proj
             xn, rs, use_nst = w.xn, (w.rs if f in _ROWSUM_FMTS else None), False
             src, nw = xn, None
-        elif M >= 2:  # batched rows: normalize once (see _Work.pre)
+        elif M >= 2 and w.pre:  # batched rows: normalize once (see _Work.pre)
             xn = torch.empty_like(x)
             rs = torch.empty(M, dtype=torch.float32, device=x.device) if f in _ROWSUM_FMTS else None
             _hip.call("llj_rmsnorm_rows", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), _hip.ptr(rs), M,

@@ -478,3 +478,76 @@ def test_attn_resid_equals_attention_then_resid(hip, wfmt, C, nh, B, S, p0):
         assert torch.equal(ya, yb)
         assert torch.equal(xa, xb)
         assert torch.equal(na, nb)
+
+
+@pytest.mark.parametrize("wfmt", [0, 3])
+@pytest.mark.parametrize("M", [2, 8])
+def test_multi_tile_workgroups_equal_single_tile(hip, wfmt, M):
+    """Several 16-column tiles per workgroup (7B / 13B shapes: QKV 768 tiles, SwiGLU 688 with a
+    partial last workgroup, lm_head 2000, 13B mlp.c_proj 320 tiles at 8 waves) give bitwise
+    the results of one tile per workgroup (llj_set_tpw_max(1)), and match the oracle."""
+    rng = np.random.default_rng(100 + M + wfmt)
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    C, nh, H, V = 4096, 32, 11008, 32000
+    x = bf16(rng.standard_normal((M, C)))
+    g = bf16(rng.uniform(0.5, 1.5, C))
+    xd, gd = T(x, torch.bfloat16), T(g, torch.bfloat16)
+    _, Wqd, sq = quant_operands(hip, rng, wfmt, 3 * C, C)
+    W1, W1d, s1 = quant_operands(hip, rng, wfmt, H, C)
+    W2, W2d, s2 = quant_operands(hip, rng, wfmt, H, C)
+    Wh, Whd, sh = quant_operands(hip, rng, wfmt, V, C)
+    C13, H13 = 5120, 13824
+    Wr, Wrd, sr = quant_operands(hip, rng, wfmt, C13, H13)
+    hx = bf16(rng.standard_normal((M, H13)))
+    hxd = T(hx, torch.bfloat16)
+    xr0 = T(bf16(rng.standard_normal((M, C13))), torch.bfloat16)
+    rope, pos, S = T(O.build_rope_cache(256, 128)), T(np.array([37], np.int32)), 64
+
+    def run():
+        q = torch.zeros(M, C, dtype=torch.bfloat16, device=dev)
+        kc = torch.zeros(M, nh, S, 128, dtype=torch.bfloat16, device=dev)
+        vc = torch.zeros_like(kc)
+        call(hip, "llj_norm_qkv_rope", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, Wqd.data_ptr(), P(sq), q.data_ptr(),
+             kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), M, 1, C, nh, S, 0, M, None, None, 0, None,
+             st())
+        h = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+        call(hip, "llj_norm_swiglu", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, W1d.data_ptr(), P(s1), W2d.data_ptr(),
+             P(s2), h.data_ptr(), M, H, C, None, 0, None, 0, None, st())
+        lg = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
+        call(hip, "llj_norm_linear", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, Whd.data_ptr(), P(sh), lg.data_ptr(),
+             V, M, V, C, None, 0, None, 0, None, st())
+        xr = xr0.clone()
+        call(hip, "llj_linear_resid", wfmt, hxd.data_ptr(), H13, Wrd.data_ptr(), P(sr), xr.data_ptr(), C13, M, C13,
+             H13, None, 0, None, st())
+        torch.cuda.synchronize()
+        return q, kc, vc, h, lg, xr
+
+    old = hip.llj_set_tpw_max(1)
+    try:
+        one = run()
+    finally:
+        hip.llj_set_tpw_max(old)
+    multi = run()
+    for name, a, b in zip(("q", "k cache", "v cache", "swiglu", "lm_head", "resid"), one, multi):
+        assert torch.equal(a, b), name
+    hn = bf16(O.rmsnorm(x, g))
+    hexp = bf16(bf16(O.silu(bf16(hn @ W1.T))) * bf16(hn @ W2.T))
+    assert_bf16_close(multi[3].float().cpu().numpy(), hexp, "swiglu", rel=3e-2)
+    assert_bf16_close(multi[4].float().cpu().numpy(), hn @ Wh.T, "lm_head")
+    assert_bf16_close(multi[5].float().cpu().numpy(), xr0.float().cpu().numpy() + bf16(hx @ Wr.T), "resid 13B")
+
+
+@pytest.mark.parametrize("wfmt", [0, 3])
+def test_long_k_residual_eight_waves_m1(hip, wfmt):
+    """mlp.c_proj at 7B (K = 11008 >= 8192: 8-wave workgroups, M = 1 register prologue): every
+    wave's A row sum lands in the LDS tail (the int4 / int8 offset removal needs all eight)."""
+    rng = np.random.default_rng(7 + wfmt)
+    N, K = 4096, 11008
+    W, Wd, szd = quant_operands(hip, rng, wfmt, N, K)
+    h = bf16(rng.standard_normal((1, K)))
+    x0 = bf16(rng.standard_normal((1, N)))
+    xd = T(x0, torch.bfloat16)
+    call(hip, "llj_linear_resid", wfmt, T(h, torch.bfloat16).data_ptr(), K, Wd.data_ptr(), szd.data_ptr(),
+         xd.data_ptr(), N, 1, N, K, None, 0, None, st())
+    torch.cuda.synchronize()
+    assert_bf16_close(xd.float().cpu().numpy(), x0 + bf16(h @ W.T), "resid K=11008 M=1")

@@ -4,6 +4,8 @@ prompt, S = 144). Variants are interleaved (rounds x variants) in one process on
 weights, so box-to-box and clock drift cancel. Prints one JSON line per (variant, batch).
 
   python tools/ab_decode.py --variants base:ATTN_RESID=0 fused:ATTN_RESID=1 --batch 1 8
+A variant may also name another build of the library (same ABI, e.g. other -D macros):
+  python tools/ab_decode.py --variants base d8:LIB=scratch/d8.so
 """
 from __future__ import annotations
 
@@ -28,7 +30,7 @@ def parse_variant(spec: str):
     flags = {}
     for a in filter(None, assigns.split(",")):
         k, v = a.split("=")
-        flags[k] = int(v) if v.lstrip("-").isdigit() else (v == "True")
+        flags[k] = v if k == "LIB" else (int(v) if v.lstrip("-").isdigit() else (v == "True"))
     return name, flags
 
 
@@ -45,15 +47,25 @@ def main():
     mode = None if args.quantize == "none" else args.quantize
     model = bench.build_model(args.model, mode)
     variants = [parse_variant(v) for v in args.variants]
-    defaults = {k: getattr(MD, k) for _, f in variants for k in f}
+    from lit_llama import _hip
+
+    default_lib = _hip.LIB_PATH
+    defaults = {k: getattr(MD, k) for _, f in variants for k in f if k not in ("LIB", "TPW")}
     res = {(n, b): [] for n, _ in variants for b in args.batch}
     for r in range(args.rounds):
         for b in args.batch:
             for name, flags in variants:
                 for k, v in defaults.items():
                     setattr(MD, k, v)
+                lib = Path(flags.get("LIB", default_lib))
+                if not lib.is_absolute():
+                    lib = REPO / lib
+                if _hip.LIB_PATH != lib:  # experiment variant of the library (same ABI)
+                    _hip.LIB_PATH, _hip._lib = lib, None
+                _hip.lib().llj_set_tpw_max(int(flags.get("TPW", 4)))
                 for k, v in flags.items():
-                    setattr(MD, k, v)
+                    if k not in ("LIB", "TPW"):
+                        setattr(MD, k, v)
                 t = bench.time_decode(model, b, 16, args.max_seq_length, 5, args.steps, 1)
                 ms = t["gpu_seconds"] / args.steps * 1e3
                 res[(name, b)].append(ms)
