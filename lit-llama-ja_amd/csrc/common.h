@@ -65,16 +65,6 @@ __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
   return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -102,6 +92,47 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_f32<kDppXor1>(v);
   v += dpp_f32<kDppXor2>(v);
   return v;
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f32<kDppHalfMirror>(v));
+  v = fmaxf(v, dpp_f32<kDppRowMirror>(v));
+  v = fmaxf(v, dpp_f32<kDppXor1>(v));
+  v = fmaxf(v, dpp_f32<kDppXor2>(v));
+  return v;
+}
+// The other half of each 32-lane pair of rows (lane i <- i ^ 16) and of the wave (i <- i ^ 32),
+// as the two halves that gfx950's v_permlane16_swap / v_permlane32_swap hand back: a VALU move
+// instead of __shfl_xor's ds_bpermute (an LDS round trip each). Inline asm: the ROCm 7.2
+// builtins (__builtin_amdgcn_permlane{16,32}_swap) miscompile here, the second result read
+// back as the first (lo + hi emitted as lo + lo). The asm pads its own hazards: s_nop 1 after
+// the VALU write of its operands and before their next VALU read.
+template <bool WIDE>
+__device__ __forceinline__ void lane_halves(float v, float& lo, float& hi) {
+  float a = v, b = v;
+  if constexpr (WIDE)
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  else
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  lo = a;
+  hi = b;
+}
+// Sum / max over the 64 lanes of the wave, the same value (bitwise) in every lane: DPP inside
+// each 16-lane row, then rows (0+1, 2+3) and halves (lo+hi), in one order for all lanes.
+__device__ __forceinline__ float wave_sum(float v) {
+  float lo, hi;
+  v = row16_sum(v);
+  lane_halves<false>(v, lo, hi);
+  v = lo + hi;
+  lane_halves<true>(v, lo, hi);
+  return lo + hi;
+}
+__device__ __forceinline__ float wave_max(float v) {
+  float lo, hi;
+  v = row16_max(v);
+  lane_halves<false>(v, lo, hi);
+  v = fmaxf(lo, hi);
+  lane_halves<true>(v, lo, hi);
+  return fmaxf(lo, hi);
 }
 
 }  // namespace llj
