@@ -98,7 +98,12 @@ def trace_phases(path):
             cur = []
     phases = {}
     for bsz, st in steps.items():
-        st = st[2:] if len(st) > 4 else st  # skip the first (warm-up / capture) steps
+        # decode steps only: the most common kernel count (prefill / setup groups differ)
+        mode = collections.Counter(len(s) for s in st).most_common(1)[0][0]
+        st = [s for s in st if len(s) == mode]
+        if len(st) < 4:
+            continue
+        st = st[2:]  # skip the first (warm-up / capture) steps
         per = collections.defaultdict(float)
         cnt = collections.defaultdict(int)
         span = []
