@@ -87,6 +87,14 @@ int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, co
                       int C, int n_head, int S, int row0, int rows, const void* i8ws, const double* nstat_in,
                       int nstat_parts, const float* rowsum, void* stream);
 
+/* llj_norm_qkv_rope for one decode row (M = B = 1, T = 1) that also computes the attention of
+ * every head (as llj_attention, model.py:237) into y (1, C): the workgroup completing a head's
+ * last q / k / v tile runs it (per-head arrival counters att_ctr: n_head words, zero before the
+ * first call and left zero). Bitwise equal to llj_norm_qkv_rope + llj_attention. wfmt 0, 1, 3. */
+int llj_norm_qkv_rope_attn(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
+                           void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int C,
+                           int n_head, int S, void* y, unsigned* att_ctr, void* stream);
+
 /* Causal attention of q (B*T, C) over the cache slots each query may see
  * (F.scaled_dot_product_attention with the tril mask rows, model.py:101-104, 237):
  * positions <= p, or all S slots once p >= S. y (B*T, C) bf16. head_size 64 or 128. */

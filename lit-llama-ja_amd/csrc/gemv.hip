@@ -125,4 +125,24 @@ int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, co
   return run<EP_QKV>(wfmt, p, stream);
 }
 
+// The same for one decode row (M == 1, T == 1), with the attention of every head computed in
+// the launch (GemvParams::att_ctr): y (1, C) = attention(q, caches) as llj_attention.
+// att_ctr: n_head words, zero before the first call, left zero by every call.
+int llj_norm_qkv_rope_attn(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
+                           void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int C,
+                           int n_head, int S, void* y, unsigned* att_ctr, void* stream) {
+  if (!y || !att_ctr || !norm_w || n_head < 1 || C % n_head || S < 1 || wfmt == WF_I8) return LLJ_EINVAL;
+  const int hs = C / n_head;
+  if (hs != 64 && hs != 128) return LLJ_EINVAL;
+  GemvParams p{};
+  p.A = (const bf16_t*)x; p.lda = C; p.norm_w = (const bf16_t*)norm_w; p.eps = eps;
+  p.M = 1; p.m0 = 0; p.N = 3 * C; p.K = C;
+  p.W = W; p.sz = (const float2*)sz; p.q_out = (bf16_t*)q_out; p.kcache = (bf16_t*)kcache;
+  p.vcache = (bf16_t*)vcache; p.rope = rope; p.pos = pos; p.n_head = n_head; p.head_size = hs;
+  p.S = S; p.T = 1;
+  p.att_ctr = att_ctr; p.att_y = (bf16_t*)y; p.att_sl2 = 1.4426950408889634f / sqrtf((float)hs);
+  if (check_shape(wfmt, p) || pick_am(wfmt, p) != AM_NORM) return LLJ_EINVAL;  // 4-wave norm-fused form
+  return run<EP_QKV>(wfmt, p, stream);
+}
+
 }  // extern "C"

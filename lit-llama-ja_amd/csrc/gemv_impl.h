@@ -90,6 +90,13 @@ struct GemvParams {
   bf16_t* nn_out;
   float* nn_rs;
   unsigned* nn_ctr;
+  // EP_QKV, one decode row (M == 1, T == 1): the attention of each head is computed in this
+  // launch by the workgroup that completes the head's last q / k / v tile (per-head arrival
+  // counters att_ctr[n_head], zero on entry, left zero; q / k / v stored write-through), into
+  // att_y (1, n_embd). nullptr = off (llj_attention runs as its own launch).
+  unsigned* att_ctr;
+  bf16_t* att_y;
+  float att_sl2;
 };
 
 // ------------------------------------------------------------------------------------
@@ -413,6 +420,42 @@ __device__ void resid_norm_tail(const GemvParams& p, float* red, bool storing_wa
 // SCA), [8, 8 + 16 NW) the norm's per-wave fp64 / fp32 row partials, then [TL_RS, TL_RS + 8 NW)
 // the per-wave row sums of the staged A (int4 / int8-GPTQ offset removal).
 __host__ __device__ constexpr int tail_floats(int nw) { return 8 + 24 * nw; }
+
+// Fused attention at the end of the QKV launch (GemvParams::att_ctr, M == 1, T == 1, one tile
+// per workgroup, NW * 64 == 256 threads = the attention block). Every wave of the workgroup
+// calls it after the epilogue: the storing wave drains its write-through q / k / v stores, one
+// lane counts the tile into its head's arrival counter, and the workgroup that completes the
+// head (3 * head_size / 16 tiles: q, k and v) resets the counter and runs attention_body over
+// the cache with write-through (sc1) loads — the same arithmetic as the standalone launch, so
+// the results are bitwise those of llj_attention.
+template <int NW>
+__device__ void qkv_attention_tail(const GemvParams& p, const int nt, unsigned char* smem) {
+  static_assert(NW * 64 == 256, "attention block is 256 threads");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's q / k / v stores acknowledged
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);
+  const int Cd = p.n_head * p.head_size;
+  const int n0 = nt * 16;
+  const int h = (n0 % Cd) / p.head_size;
+  if (threadIdx.x == 0) {
+    const unsigned target = 3u * (unsigned)(p.head_size / 16);
+    const unsigned old = __hip_atomic_fetch_add(p.att_ctr + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old + 1 == target;
+    if (last) __hip_atomic_store(p.att_ctr + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  __syncthreads();  // the flag word is attention scratch from here on
+  if (!last) return;
+  float* lds = reinterpret_cast<float*>(smem);
+  if (p.head_size == 128)
+    attention_body<128, 8, 256, true, false>(p.q_out, p.kcache, p.vcache, p.att_y, p.pos, 1, p.S, p.n_head,
+                                             p.att_sl2, h, 0, lds, ChainCtl{});
+  else
+    attention_body<64, 8, 256, true, false>(p.q_out, p.kcache, p.vcache, p.att_y, p.pos, 1, p.S, p.n_head,
+                                            p.att_sl2, h, 0, lds, ChainCtl{});
+}
 
 // One workgroup computes TPW consecutive 16-column tiles nt0 .. nt0 + TPW - 1 (tiles past the
 // last one are loaded as a copy of it and never stored): every wave streams its K-chunks of
@@ -913,6 +956,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     if (wave >= TPW) {  // owns no tile slot
       if constexpr (EP == EP_RESID)
         if (p.nn_ctr) resid_norm_tail<NW>(p, red, false);
+      if constexpr (EP == EP_QKV && !CH && TPW == 1 && NW * 64 == 256)
+        if (p.att_ctr) qkv_attention_tail<NW>(p, ntj[0], smem);  // every wave joins its barriers
       return;
     }
   }
@@ -999,7 +1044,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
               dst = region == 1 ? p.kcache : p.vcache;
               ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
             }
-            if constexpr (CH) st4_sc1(dst, (unsigned)(ei * 2), ob | (pr << 16));
+            if (CH || p.att_ctr) st4_sc1(dst, (unsigned)(ei * 2), ob | (pr << 16));  // read in-launch
             else *reinterpret_cast<uint32_t*>(dst + ei) = ob | (pr << 16);
           }
         }
@@ -1068,6 +1113,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   if constexpr (CH) chain_signal(cc);
   if constexpr (EP == EP_RESID)
     if (p.nn_ctr) resid_norm_tail<NW>(p, red, true);
+  if constexpr (EP == EP_QKV && !CH && TPW == 1 && NW * 64 == 256)
+    if (p.att_ctr) qkv_attention_tail<NW>(p, ntj[0], smem);
   LLJ_STAMP(5);
 }
 

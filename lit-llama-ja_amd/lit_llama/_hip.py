@@ -37,6 +37,7 @@ SIGNATURES = {
     "llj_w8_scale_zero": [_P, _P, _I, _P, _I, _P],
     "llj_linear": [_I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
     "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P],
+    "llj_norm_qkv_rope_attn": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P],
     "llj_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_attn_resid": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P],
     "llj_linear_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],

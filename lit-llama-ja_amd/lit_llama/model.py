@@ -90,6 +90,12 @@ FUSE_RESID_NORM = False
 # (llj_attn_resid): the c_proj weight stream overlaps the attention, which leaves the chip
 # and HBM idle, and one kernel boundary per layer disappears. Bitwise equal to the two launches.
 ATTN_RESID = False
+# one decode row (M == 1, T == 1): the attention of each head computed inside the QKV launch by
+# the workgroup that completes the head (llj_norm_qkv_rope_attn), one launch per layer fewer.
+# Bitwise equal to the separate llj_attention launch, but measured slower at 7B bs=1 (1.237 vs
+# 1.184 ms/token: the write-through drain, the arrival atomics and the attention's sc1 loads in
+# the QKV tail cost more than the attention launch). Off by default.
+QKV_ATTN = False
 # M == 1: RMSNorm row statistics handed from the residual epilogues to the next norm-fused
 # GEMV as per-workgroup partial sums (_Work.nst) instead of re-reduced by every consumer
 NST_STATS = False
@@ -160,6 +166,8 @@ class _Work:
         # zeroed once per step, and a timeout flag
         self.ctr = torch.zeros(cfg.n_layer * 128, dtype=torch.int32, device=device)
         self.err = torch.zeros(4, dtype=torch.int32, device=device)
+        # llj_norm_qkv_rope_attn: per-head arrival counters (zero; every launch leaves them zero)
+        self.actr = torch.zeros(cfg.n_head, dtype=torch.int32, device=device) if M == 1 else None
 
     def nst_ptr(self, which: int):
         return None if self.nst is None else self.nst[which].data_ptr()
@@ -328,7 +336,13 @@ class LLaMA(nn.Module):
                 src, nw = w.xn, None
             else:
                 src, nw = w.x, blk.rms_1.scale.data_ptr()
-            for r0 in range(0, M, QKV_ROWS):
+            qkv_attn = (QKV_ATTN and T == 1 and M == 1 and fa in (0, 1, 3) and nw is not None and w.nst is None
+                        and w.actr is not None and (C // nh) in (64, 128))
+            if qkv_attn:  # 1.+2. rms_1 + c_attn + rope + kv write + attention in one launch
+                _hip.call("llj_norm_qkv_rope_attn", fa, src.data_ptr(), nw, blk.rms_1.eps, wa.data_ptr(), P(sa),
+                          w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), C, nh, S,
+                          w.y.data_ptr(), w.actr.data_ptr(), st)
+            for r0 in range(0, 0 if qkv_attn else M, QKV_ROWS):
                 r = min(QKV_ROWS, M - r0)
                 _hip.call("llj_norm_qkv_rope", fa, src.data_ptr(), nw, blk.rms_1.eps, wa.data_ptr(), P(sa),
                           w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), B, T, C, nh,
@@ -336,13 +350,14 @@ class LLaMA(nn.Module):
             # 2.+3. attention, c_proj + residual (+ rms_2 row statistics, or rms_2 itself for
             # batched rows); one launch for decode rows (llj_attn_resid)
             w.xn_ready = False
-            if attn_resid and fp in (0, 1, 3) and w.nctr is None:
+            if attn_resid and not qkv_attn and fp in (0, 1, 3) and w.nctr is None:
                 _hip.call("llj_attn_resid", fp, w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
                           pos.data_ptr(), M, nh, S, wp.data_ptr(), P(sp), w.x.data_ptr(), C, w.nst_ptr(1),
                           w.ctr[128 * i].data_ptr(), w.err.data_ptr(), st)
             else:
-                _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
-                          pos.data_ptr(), B, T, nh, C // nh, S, st)
+                if not qkv_attn:
+                    _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                              pos.data_ptr(), B, T, nh, C // nh, S, st)
                 if w.nctr is not None and fp in (0, 1) and f1 in (0, 1):
                     _hip.call("llj_linear_resid_norm", fp, w.y.data_ptr(), C, wp.data_ptr(), P(sp), w.x.data_ptr(),
                               C, M, C, C, blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(),

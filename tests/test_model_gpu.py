@@ -366,3 +366,29 @@ def test_attn_resid_launch_equals_separate_launches(mode, n_embd, n_head, B):
         MD.ATTN_RESID = saved
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("mode", ["gptq.int4", None, "gptq.int8"])
+@pytest.mark.parametrize("n_embd,n_head", [(256, 4), (1024, 8)])
+def test_qkv_attn_launch_equals_separate_attention(mode, n_embd, n_head):
+    """Batch-1 decode with the attention inside the QKV launch (model.QKV_ATTN, off by default)
+    produces bitwise the tokens and logits of the separate attention launch."""
+    from lit_llama import model as MD
+    from lit_llama.engine import DecodeSession
+
+    m = _random_int4_model(n_embd, n_head, mode=mode, seed=5 * n_embd)
+    prompt = torch.randint(3, 2048, (1, 6), generator=torch.Generator().manual_seed(n_embd)).cuda()
+    outs = []
+    saved = MD.QKV_ATTN
+    try:
+        for fused in (False, True):
+            MD.QKV_ATTN = fused
+            s = DecodeSession(m, 1, 16, 40)  # S = 16 < 6 + 30: the ring wraps
+            s.prefill(prompt)
+            s.decode(30)
+            torch.cuda.synchronize()
+            outs.append((s.output().cpu().numpy(), s.logits.float().cpu().numpy()))
+    finally:
+        MD.QKV_ATTN = saved
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
