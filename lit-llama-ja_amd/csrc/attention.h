@@ -8,7 +8,7 @@
 // softmax is identical up to summation order.
 // 16 lanes per key (HS/16 dims each); NG = NTH/16 key groups, U keys per group per pass, so one
 // pass has NG*U keys in flight, all loads of a pass issued before any use. Per-group online
-// softmax, combined through LDS.
+// softmax; the groups of a wave merge through lane swaps, the waves through LDS.
 #pragma once
 #include "chain.h"
 #include "common.h"
@@ -17,8 +17,23 @@ namespace llj {
 
 template <int HS, int NTH>
 constexpr int attention_lds_floats() {
-  constexpr int NG = NTH / 16, PARTS = NTH / HS;
-  return 2 * NG + NG * (HS + 1) + PARTS * HS + PARTS;
+  constexpr int NWV = NTH / 64;  // waves: one (max, sum, HS outputs) partial each
+  return 2 * NWV + NWV * HS;
+}
+
+// Merge two online-softmax partials (running max, sum, outputs) of the same dims: the lanes
+// holding `lo` and `hi` compute the same expression, so both end bitwise equal.
+template <int DPL>
+__device__ __forceinline__ void softmax_merge(float& mx, float& l, float* o, const float mx_lo, const float mx_hi,
+                                              const float l_lo, const float l_hi, const float* o_lo,
+                                              const float* o_hi) {
+  const float M = fmaxf(mx_lo, mx_hi);
+  const float f_lo = mx_lo == -INFINITY ? 0.f : exp2f(mx_lo - M);
+  const float f_hi = mx_hi == -INFINITY ? 0.f : exp2f(mx_hi - M);
+  mx = M;
+  l = l_lo * f_lo + l_hi * f_hi;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) o[i] = o_lo[i] * f_lo + o_hi[i] * f_hi;
 }
 
 // CH: chained launch — wait for the QKV op, then read q and the cache with sc1 loads and
@@ -31,12 +46,10 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
                                                int h, int m, float* lds, const ChainCtl& cc) {
   constexpr int DPL = HS / 16;
   constexpr int NG = NTH / 16;
-  constexpr int PARTS = NTH / HS;
-  float* s_m = lds;
-  float* s_l = s_m + NG;
-  float* s_o = s_l + NG;                // [NG][HS + 1]
-  float* s_po = s_o + NG * (HS + 1);    // [PARTS][HS]
-  float* s_pl = s_po + PARTS * HS;      // [PARTS]
+  constexpr int NWV = NTH / 64;
+  float* s_m = lds;                     // [NWV]
+  float* s_l = s_m + NWV;               // [NWV]
+  float* s_o = s_l + NWV;               // [NWV][HS]
   LLJ_STAMP(0);
   if constexpr (CH) chain_wait(cc);
   LLJ_STAMP(1);
@@ -69,6 +82,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
       qf[3] = bfhi(a.y) * scale_log2;
     }
   }
+  LLJ_STAMP(2);
   float mx = -INFINITY, l = 0.f, o[DPL];
 #pragma unroll
   for (int i = 0; i < DPL; ++i) o[i] = 0.f;
@@ -122,36 +136,45 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
       mx = mn;
     }
   }
-  if (sub == 0) {
-    s_m[kg] = mx;
-    s_l[kg] = l;
-  }
-#pragma unroll
-  for (int i = 0; i < DPL; ++i) s_o[kg * (HS + 1) + sub * DPL + i] = o[i];
-  __syncthreads();
-  // combine the NG groups: HS output dims x PARTS partial sums over the groups
+  LLJ_STAMP(3);
+  // combine the key groups: the four 16-lane groups of a wave with lane swaps (rows 0+1 and
+  // 2+3, then the two halves; every lane of a group holds the group's max and sum and its
+  // DPL output dims), then the NWV wave partials through LDS in wave order
   {
-    const int d = threadIdx.x % HS, part = threadIdx.x / HS;
-    float M = -INFINITY;
-#pragma unroll 8
-    for (int g = 0; g < NG; ++g) M = fmaxf(M, s_m[g]);
-    float L = 0.f, O = 0.f;
-    for (int g = part; g < NG; g += PARTS) {
-      const float f = s_m[g] == -INFINITY ? 0.f : exp2f(s_m[g] - M);
-      L += s_l[g] * f;
-      O += s_o[g * (HS + 1) + d] * f;
+    float mlo, mhi, llo, lhi, olo[DPL], ohi[DPL];
+    lane_halves<false>(mx, mlo, mhi);
+    lane_halves<false>(l, llo, lhi);
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) lane_halves<false>(o[i], olo[i], ohi[i]);
+    softmax_merge<DPL>(mx, l, o, mlo, mhi, llo, lhi, olo, ohi);
+    lane_halves<true>(mx, mlo, mhi);
+    lane_halves<true>(l, llo, lhi);
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) lane_halves<true>(o[i], olo[i], ohi[i]);
+    softmax_merge<DPL>(mx, l, o, mlo, mhi, llo, lhi, olo, ohi);
+  }
+  const int wv = threadIdx.x >> 6;
+  if (kg % 4 == 0) {  // the first 16 lanes of each wave
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) s_o[wv * HS + sub * DPL + i] = o[i];
+    if (sub == 0) {
+      s_m[wv] = mx;
+      s_l[wv] = l;
     }
-    s_po[part * HS + d] = O;
-    if (d == 0) s_pl[part] = L;
   }
   __syncthreads();
+  LLJ_STAMP(4);
   if (threadIdx.x < HS) {  // waves 0 (and 1): adjacent dims leave as one 4-byte store
     const int d = threadIdx.x;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) M = fmaxf(M, s_m[w]);
     float L = 0.f, O = 0.f;
 #pragma unroll
-    for (int pp = 0; pp < PARTS; ++pp) {
-      L += s_pl[pp];
-      O += s_po[pp * HS + d];
+    for (int w = 0; w < NWV; ++w) {
+      const float f = s_m[w] == -INFINITY ? 0.f : exp2f(s_m[w] - M);
+      L += s_l[w] * f;
+      O += s_o[w * HS + d] * f;
     }
     const uint32_t ob = (uint32_t)f2bf(O / L);
     const uint32_t pr = lane_xor1(ob);

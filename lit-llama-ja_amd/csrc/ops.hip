@@ -181,6 +181,7 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const bf16_t* __restrict__
 using namespace llj;
 
 extern "C" {
+LLJ_TRACE_EXPORT(ops)
 
 int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, double* nstat_out,
                   void* stream) {
