@@ -101,6 +101,14 @@ int llj_norm_qkv_rope_attn(int wfmt, const void* x, const void* norm_w, float ep
 int llj_attention(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
                   int n_head, int head_size, int S, void* stream);
 
+/* Split-K form of llj_attention for long caches: the valid keys of every (row, head) split into
+ * nsplit equal ranges, one block each, writing unnormalized partials (outputs, max, sum) into
+ * part_ws (llj_attention_ws_bytes(B*T, n_head, head_size, nsplit) bytes), merged in split order
+ * by a second launch. nsplit <= 1 is llj_attention itself. Same softmax up to summation order. */
+size_t llj_attention_ws_bytes(int rows, int n_head, int head_size, int nsplit);
+int llj_attention_split(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                        int n_head, int head_size, int S, int nsplit, void* part_ws, void* stream);
+
 /* y = attention (as llj_attention, T = 1 decode rows, M = B <= 8) and then
  * x[M, C] += y . W_proj^T (as llj_linear_resid, attn.c_proj + residual, model.py:172,239-242),
  * in ONE launch: the c_proj workgroups load their weights while the attention runs and wait

@@ -39,11 +39,15 @@ __device__ __forceinline__ void softmax_merge(float& mx, float& l, float* o, con
 // CH: chained launch — wait for the QKV op, then read q and the cache with sc1 loads and
 // store y with sc1 stores (chain.h protocol).
 // SIG: signal a consumer op of the same launch (sc1 y stores, drain, count done); CH implies it.
-template <int HS, int U, int NTH, bool CH, bool SIG = CH>
+// PART: split-K over the keys (long contexts): this block takes key range `split` of `nsplit`
+// equal ranges (>= one pass of NG * U keys each) of the valid keys and writes its unnormalized partial (outputs, running max,
+// sum) to part[((m * nh + h) * nsplit + split) * (HS + 2)]; attention_combine_kernel merges.
+template <int HS, int U, int NTH, bool CH, bool SIG = CH, bool PART = false>
 __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                const int* __restrict__ pos, int T, int S, int nh, float scale_log2,
-                                               int h, int m, float* lds, const ChainCtl& cc) {
+                                               int h, int m, float* lds, const ChainCtl& cc, int nsplit = 1,
+                                               int split = 0, float* __restrict__ part = nullptr) {
   constexpr int DPL = HS / 16;
   constexpr int NG = NTH / 16;
   constexpr int NWV = NTH / 64;
@@ -56,6 +60,13 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   const int b = m / T, t = m % T;
   const int ps = pos[t];
   const int nvalid = ps < S ? ps + 1 : S;
+  // key range of this block (the whole valid range unless split)
+  int jbeg = 0, jend = nvalid;
+  if constexpr (PART) {  // ranges of at least one full pass (NG * U keys); the rest stay empty
+    const int chunk = max((nvalid + nsplit - 1) / nsplit, NG * U);
+    jbeg = split * chunk;
+    jend = min(nvalid, jbeg + chunk);
+  }
   const int sub = threadIdx.x & 15, kg = threadIdx.x >> 4;
   const int C = nh * HS;
   const size_t base = ((size_t)(b * nh + h) * S) * HS + sub * DPL;  // elements
@@ -87,11 +98,11 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
 #pragma unroll
   for (int i = 0; i < DPL; ++i) o[i] = 0.f;
 
-  for (int j0 = kg; j0 < nvalid; j0 += NG * U) {
+  for (int j0 = jbeg + kg; j0 < jend; j0 += NG * U) {
     uint32_t kw[U][DPL / 2], vw[U][DPL / 2];
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // every load of the pass first (clamped: always valid rows)
-      const int j = j0 + NG * u < nvalid ? j0 + NG * u : j0;
+      const int j = j0 + NG * u < jend ? j0 + NG * u : j0;
       const size_t eo = base + (size_t)j * HS;
       if constexpr (DPL == 8) {
         uint4 a, c;
@@ -123,7 +134,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
 #pragma unroll
       for (int i = 0; i < DPL / 2; ++i) s += qf[2 * i] * bflo(kw[u][i]) + qf[2 * i + 1] * bfhi(kw[u][i]);
       s = row16_sum(s);  // the 16 lanes of this key
-      if (j0 + NG * u >= nvalid) continue;
+      if (j0 + NG * u >= jend) continue;
       const float mn = fmaxf(mx, s);
       const float corr = exp2f(mx - mn);
       const float pj = exp2f(s - mn);
@@ -176,6 +187,16 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
       L += s_l[w] * f;
       O += s_o[w * HS + d] * f;
     }
+    if constexpr (PART) {  // unnormalized partial: outputs, then (max, sum)
+      float* dst = part + ((size_t)(m * nh + h) * nsplit + split) * (HS + 2);
+      dst[d] = O;
+      if (d == 0) {
+        dst[HS] = M;
+        dst[HS + 1] = L;
+      }
+      LLJ_STAMP(5);
+      return;
+    }
     const uint32_t ob = (uint32_t)f2bf(O / L);
     const uint32_t pr = lane_xor1(ob);
     if (!(d & 1)) {
@@ -191,6 +212,27 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
     if (threadIdx.x == 0) chain_count_done(cc);
   }
   LLJ_STAMP(5);
+}
+
+// Merge the nsplit partials of one (head, row) in split order: y = sum_s O_s f_s / sum_s L_s f_s
+// with f_s = exp2(M_s - max_s M_s) (empty ranges have M = -inf and contribute nothing).
+template <int HS>
+__global__ __launch_bounds__(HS) void attention_combine_kernel(const float* __restrict__ part, bf16_t* __restrict__ y,
+                                                               int nh, int nsplit) {
+  const int h = blockIdx.x, m = blockIdx.y, d = threadIdx.x;
+  const float* src = part + (size_t)(m * nh + h) * nsplit * (HS + 2);
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, src[(size_t)s * (HS + 2) + HS]);
+  float L = 0.f, O = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float* ps = src + (size_t)s * (HS + 2);
+    const float f = ps[HS] == -INFINITY ? 0.f : exp2f(ps[HS] - M);
+    L += ps[HS + 1] * f;
+    O += ps[d] * f;
+  }
+  const uint32_t ob = (uint32_t)f2bf(O / L);
+  const uint32_t pr = lane_xor1(ob);
+  if (!(d & 1)) *reinterpret_cast<uint32_t*>(y + (size_t)m * nh * HS + h * HS + d) = ob | (pr << 16);
 }
 
 }  // namespace llj

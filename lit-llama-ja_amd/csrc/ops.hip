@@ -118,6 +118,17 @@ __global__ __launch_bounds__(NTH) void attention_kernel(const bf16_t* __restrict
                                     ChainCtl{});
 }
 
+// split-K attention over the keys (long contexts): block (head, row, split) -> partial
+template <int HS, int U, int NTH>
+__global__ __launch_bounds__(NTH) void attention_part_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+                                                             const bf16_t* __restrict__ vc, const int* __restrict__ pos,
+                                                             int T, int S, int nh, float scale_log2, int nsplit,
+                                                             float* __restrict__ part) {
+  __shared__ float lds[attention_lds_floats<HS, NTH>()];
+  attention_body<HS, U, NTH, false, false, true>(q, kc, vc, nullptr, pos, T, S, nh, scale_log2, blockIdx.x,
+                                                  blockIdx.y, lds, ChainCtl{}, nsplit, blockIdx.z, part);
+}
+
 // ---- greedy next token: argmax over bf16 logits (lowest index on ties). Reference
 // generate.py:66-74 with top_k = 1 (multinomial over the kept maximum).
 __global__ __launch_bounds__(1024) void argmax_kernel(const bf16_t* __restrict__ logits, int ldl, int V,
@@ -215,6 +226,38 @@ int llj_attention(const void* q, const void* kcache, const void* vcache, void* y
   } else if (head_size == 64) {
     hipLaunchKernelGGL((attention_kernel<64, LLJ_ATT_U, LLJ_ATT_NTH>), grid, dim3(LLJ_ATT_NTH), 0, (hipStream_t)stream, (const bf16_t*)q,
                        (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
+  } else {
+    return LLJ_EINVAL;
+  }
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t llj_attention_ws_bytes(int rows, int n_head, int head_size, int nsplit) {
+  return (size_t)rows * n_head * (nsplit < 1 ? 1 : nsplit) * (head_size + 2) * sizeof(float);
+}
+
+int llj_attention_split(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                        int n_head, int head_size, int S, int nsplit, void* part_ws, void* stream) {
+  if (nsplit <= 1) return llj_attention(q, kcache, vcache, y, pos, B, T, n_head, head_size, S, stream);
+  LLJ_REQUIRE(B > 0 && T > 0 && n_head > 0 && S > 0 && part_ws && nsplit <= 1024);
+  const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
+  const dim3 grid(n_head, B * T, nsplit), cgrid(n_head, B * T);
+  hipStream_t st = (hipStream_t)stream;
+  if (head_size == 128) {
+    hipLaunchKernelGGL((attention_part_kernel<128, LLJ_ATT_U, LLJ_ATT_NTH>), grid, dim3(LLJ_ATT_NTH), 0, st,
+                       (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, pos, T, S, n_head, sl2, nsplit,
+                       (float*)part_ws);
+    LLJ_CHECK_LAUNCH();
+    hipLaunchKernelGGL((attention_combine_kernel<128>), cgrid, dim3(128), 0, st, (const float*)part_ws, (bf16_t*)y,
+                       n_head, nsplit);
+  } else if (head_size == 64) {
+    hipLaunchKernelGGL((attention_part_kernel<64, LLJ_ATT_U, LLJ_ATT_NTH>), grid, dim3(LLJ_ATT_NTH), 0, st,
+                       (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, pos, T, S, n_head, sl2, nsplit,
+                       (float*)part_ws);
+    LLJ_CHECK_LAUNCH();
+    hipLaunchKernelGGL((attention_combine_kernel<64>), cgrid, dim3(64), 0, st, (const float*)part_ws, (bf16_t*)y,
+                       n_head, nsplit);
   } else {
     return LLJ_EINVAL;
   }

@@ -38,6 +38,7 @@ SIGNATURES = {
     "llj_linear": [_I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
     "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P],
     "llj_norm_qkv_rope_attn": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "llj_attention_split": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
     "llj_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_attn_resid": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P],
     "llj_linear_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
@@ -75,6 +76,8 @@ def lib() -> ctypes.CDLL:
             f.restype = ctypes.c_int
         L.llj_i8_ws_bytes.argtypes = [_I, _I]
         L.llj_i8_ws_bytes.restype = ctypes.c_size_t
+        L.llj_attention_ws_bytes.argtypes = [_I, _I, _I, _I]
+        L.llj_attention_ws_bytes.restype = ctypes.c_size_t
         _lib = L
     return _lib
 

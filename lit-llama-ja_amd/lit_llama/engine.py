@@ -61,7 +61,7 @@ class DecodeSession:
         # decode-step operands (fixed for the session)
         self.specs = m._layer_specs()
         need_i8 = any(s[0] == 2 for layer in self.specs["layers"] for s in layer) or self.specs["head"][0] == 2
-        self.work = _Work(m.config, B, self.dev, need_i8)
+        self.work = _Work(m.config, B, self.dev, need_i8, self.S)
 
     def _step(self):
         m, w, B = self.model, self.work, self.B

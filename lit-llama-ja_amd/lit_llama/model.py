@@ -96,6 +96,17 @@ ATTN_RESID = False
 # 1.184 ms/token: the write-through drain, the arrival atomics and the attention's sc1 loads in
 # the QKV tail cost more than the attention launch). Off by default.
 QKV_ATTN = False
+# long caches: attention split over the keys (llj_attention_split) into ATTN_SPLIT_KEYS-key
+# ranges once the cache holds >= ATTN_SPLIT_MIN_S slots (32 heads x 1 row leave most CUs idle)
+ATTN_SPLIT_MIN_S = 512
+ATTN_SPLIT_KEYS = 256  # 7B bs=1 at p = 2000 (S = 2048): 33.1 us one block, 14.4 us in 8 ranges
+
+
+def attn_splits(S: int) -> int:
+    """key ranges per (row, head) for a cache of S slots (1 = the one-block attention)."""
+    if S < ATTN_SPLIT_MIN_S:
+        return 1
+    return min(64, (S + ATTN_SPLIT_KEYS - 1) // ATTN_SPLIT_KEYS)
 # M == 1: RMSNorm row statistics handed from the residual epilogues to the next norm-fused
 # GEMV as per-workgroup partial sums (_Work.nst) instead of re-reduced by every consumer
 NST_STATS = False
@@ -133,7 +144,7 @@ class _Work:
     instead of every norm-fused GEMV workgroup re-reducing the row. Buffer 0 feeds rms_1 /
     ln_f (written by the embedding, then by mlp.c_proj), buffer 1 feeds rms_2 (attn.c_proj)."""
 
-    def __init__(self, cfg: LLaMAConfig, M: int, device, need_i8: bool):
+    def __init__(self, cfg: LLaMAConfig, M: int, device, need_i8: bool, S: int = 0):
         C, H = cfg.n_embd, MLP.hidden(cfg)
         bf = torch.bfloat16
         self.x = torch.empty(M, C, dtype=bf, device=device)
@@ -166,6 +177,12 @@ class _Work:
         # zeroed once per step, and a timeout flag
         self.ctr = torch.zeros(cfg.n_layer * 128, dtype=torch.int32, device=device)
         self.err = torch.zeros(4, dtype=torch.int32, device=device)
+        # split-K attention partials for long caches (llj_attention_split)
+        self.nsplit = attn_splits(S)
+        self.att_ws = None
+        if self.nsplit > 1:
+            nb = _hip.lib().llj_attention_ws_bytes(M, cfg.n_head, C // cfg.n_head, self.nsplit)
+            self.att_ws = torch.empty(nb, dtype=torch.uint8, device=device)
         # llj_norm_qkv_rope_attn: per-head arrival counters (zero; every launch leaves them zero)
         self.actr = torch.zeros(cfg.n_head, dtype=torch.int32, device=device) if M == 1 else None
 
@@ -268,7 +285,7 @@ class LLaMA(nn.Module):
         dev = idx.device
         specs = self._layer_specs()
         need_i8 = any(s[0] == 2 for layer in specs["layers"] for s in layer) or specs["head"][0] == 2
-        w = _Work(cfg, M, dev, need_i8)
+        w = _Work(cfg, M, dev, need_i8, S)
         st = _hip.stream()
         ids = idx.reshape(-1).to(torch.int32)
         _hip.call("llj_embedding", ids.data_ptr(), self.transformer.wte.weight.data_ptr(), w.x.data_ptr(), M,
@@ -355,7 +372,10 @@ class LLaMA(nn.Module):
                           pos.data_ptr(), M, nh, S, wp.data_ptr(), P(sp), w.x.data_ptr(), C, w.nst_ptr(1),
                           w.ctr[128 * i].data_ptr(), w.err.data_ptr(), st)
             else:
-                if not qkv_attn:
+                if not qkv_attn and w.att_ws is not None:
+                    _hip.call("llj_attention_split", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                              pos.data_ptr(), B, T, nh, C // nh, S, w.nsplit, w.att_ws.data_ptr(), st)
+                elif not qkv_attn:
                     _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
                               pos.data_ptr(), B, T, nh, C // nh, S, st)
                 if w.nctr is not None and fp in (0, 1) and f1 in (0, 1):

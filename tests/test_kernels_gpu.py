@@ -593,3 +593,24 @@ def test_qkv_attn_launch_equals_qkv_then_attention(hip, wfmt, C, nh, S, p0):
         for name, a, b in zip(("q", "k cache", "v cache", "y"), *outs):
             assert torch.equal(a, b), f"{name} step {step}"
         assert int(ctr.abs().sum()) == 0, "arrival counters not reset"
+
+
+@pytest.mark.parametrize("hs,nh,B,T_,S,p0,nsplit", [(128, 4, 1, 1, 2048, 2000, 16), (128, 3, 2, 1, 2048, 40, 16),
+                                                   (64, 4, 2, 5, 600, 300, 5), (128, 2, 1, 1, 512, 900, 4),
+                                                   (128, 2, 8, 1, 1024, 1023, 8)])
+def test_attention_split_keys(hip, hs, nh, B, T_, S, p0, nsplit):
+    """Split-K attention (key ranges per block + in-order merge) against the oracle, incl. empty
+    ranges (p0 small), prefill rows (T > 1) and the rolled ring (p0 >= S)."""
+    rng = np.random.default_rng(hs + S + p0 + nsplit)
+    C = nh * hs
+    kc = bf16(rng.standard_normal((B, nh, S, hs)))
+    vc = bf16(rng.standard_normal((B, nh, S, hs)))
+    q = bf16(rng.standard_normal((B * T_, C)) * 2)
+    pos = np.arange(p0, p0 + T_, dtype=np.int32)
+    y = torch.empty(B * T_, C, dtype=torch.bfloat16, device=dev)
+    ws = torch.empty(hip.llj_attention_ws_bytes(B * T_, nh, hs, nsplit), dtype=torch.uint8, device=dev)
+    qd, kd, vd, pd = T(q, torch.bfloat16), T(kc, torch.bfloat16), T(vc, torch.bfloat16), T(pos)
+    call(hip, "llj_attention_split", qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), y.data_ptr(), pd.data_ptr(), B, T_,
+         nh, hs, S, nsplit, ws.data_ptr(), st())
+    torch.cuda.synchronize()
+    assert_bf16_close(y.float().cpu().numpy(), _attn_oracle(q, kc, vc, pos, S, T_, nh, hs), "split attention")

@@ -392,3 +392,29 @@ def test_qkv_attn_launch_equals_separate_attention(mode, n_embd, n_head):
         MD.QKV_ATTN = saved
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+def test_long_cache_split_attention_decode():
+    """A cache of >= ATTN_SPLIT_MIN_S slots decodes through the split-K attention; its logits
+    match the one-block attention's within bf16 summation-order noise."""
+    from lit_llama import model as MD
+    from lit_llama.engine import DecodeSession
+
+    m = _random_int4_model(256, 4, seed=77)
+    prompt = torch.randint(3, 2048, (1, 6), generator=torch.Generator().manual_seed(77)).cuda()
+    outs = []
+    saved = MD.ATTN_SPLIT_MIN_S, MD.ATTN_SPLIT_KEYS
+    try:
+        for min_s in (10 ** 9, 64):
+            MD.ATTN_SPLIT_MIN_S, MD.ATTN_SPLIT_KEYS = min_s, 32
+            s = DecodeSession(m, 1, 100, 40)
+            assert s.S == 100
+            s.prefill(prompt)
+            s.decode(20)
+            torch.cuda.synchronize()
+            assert (s.work.nsplit > 1) == (min_s == 64)
+            outs.append(s.logits.float().cpu().numpy())
+    finally:
+        MD.ATTN_SPLIT_MIN_S, MD.ATTN_SPLIT_KEYS = saved
+    ref, got = outs
+    assert np.abs(got - ref).max() <= 3e-2 * np.abs(ref).max()

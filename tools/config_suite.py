@@ -5,6 +5,8 @@
   C3  LLaMA-7B llm.int8, bs=8
   C4  LLaMA-13B gptq.int4, bs=1 (one replica; the driver runs the 8-replica scan)
   X-gptq.int8  LLaMA-7B gptq.int8 (ColBlock bits=8), bs=1 (not a BASELINE config; informational)
+  C2-long      LLaMA-7B gptq.int4, bs=1 with a 1900-token prompt in a 2048-slot cache (SURVEY §8d's
+               long-KV point; split-K attention)
 
 Synthetic weights of the exact shapes (bench.build_model), 16-token random prompts,
 max_seq_length 144, greedy; value = decode tokens/s, step_roofline = algorithmic bytes of a
@@ -28,8 +30,10 @@ sys.path.insert(0, str(REPO))
 import bench  # noqa: E402
 
 CONFIGS = [("C1", "7B", "none", 1), ("C2", "7B", "gptq.int4", 1), ("C2-bs8", "7B", "gptq.int4", 8),
+           ("C2-long", "7B", "gptq.int4", 1),
            ("C3", "7B", "llm.int8", 8), ("C4", "13B", "gptq.int4", 1),
            ("X-gptq.int8", "7B", "gptq.int8", 1)]  # extra: the reference's third --quantize mode
+LONG = {"C2-long": (1900, 2048)}  # (prompt length, max_seq_length)
 
 
 def main():
@@ -52,15 +56,17 @@ def main():
             torch.cuda.empty_cache()
             models[key] = bench.build_model(name, None if mode == "none" else mode)
         model = models[key]
-        r = bench.time_decode(model, B, 16, 144, a.warmup, a.steps, 1)
+        plen, S = LONG.get(tag, (16, 144))
+        r = bench.time_decode(model, B, plen, S, a.warmup, min(a.steps, 2048 - plen - 1 - a.warmup), 1)
         sb = bench.step_bytes(model, B, r["pos_mean"])
-        t_step = r["seconds"] / a.steps
-        line = {"config": tag, "model": f"LLaMA-{name}", "quantize": mode, "batch": B,
+        t_step = r["seconds"] / (r["tokens"] // B)
+        line = {"config": tag, "model": f"LLaMA-{name}", "quantize": mode, "batch": B, "prompt_len": plen,
+                "max_seq_length": S,
                 "value": round(r["tokens"] / r["seconds"], 2), "unit": "tokens/s",
                 "ms_per_step": round(t_step * 1e3, 4), "bytes_per_step": sb,
                 "step_roofline": {"achieved_GBps": round(sb / t_step / 1e9, 1),
                                   "frac": round(sb / t_step / 1e9 / bench.HBM_PEAK_GBS, 4)},
-                "data": "synthetic weights of the exact shapes, random 16-token prompts, greedy"}
+                "data": f"synthetic weights of the exact shapes, random {plen}-token prompts, greedy"}
         del r["session"]
         print(json.dumps(line), flush=True)
         results.append(line)
