@@ -705,9 +705,13 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   rs = uniform(rs);
   AP ap;
   const u32x4* g4 = reinterpret_cast<const u32x4*>(p.norm_w);
-  auto a_issue = [&](auto rsc) {
+  // rows held in registers: MB == 1 -> 1; else the smallest of 2 / 4 / 8 covering M (rows past M
+  // are clamped duplicates of row M-1: loaded, never used)
+  const int mr = MB == 1 ? 1 : uniform(M <= 2 ? 2 : M <= 4 ? 4 : 8);
+  auto a_issue = [&](auto rsc, auto mrc) {
     constexpr int RS = decltype(rsc)::value;
-    constexpr int MR = MB == 1 ? 1 : AP::XR / RS;
+    constexpr int MR = decltype(mrc)::value;
+    static_assert(MR * RS <= AP::XR, "A registers");
     if (NORM && p.nst_in) {
       const int m = tid % AP::SM;
       const int mm = m < M ? m : M - 1;
@@ -738,9 +742,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       }
     }
   };
-  auto a_finish = [&](auto rsc) {
+  auto a_finish = [&](auto rsc, auto mrc) {
     constexpr int RS = decltype(rsc)::value;
-    constexpr int MR = MB == 1 ? 1 : AP::XR / RS;
+    constexpr int MR = decltype(mrc)::value;
     if (NORM) {
       double* redd = reinterpret_cast<double*>(tail + 8);  // [wave][8] fp64
       float* redf = tail + 8;                              // [wave][8] fp32
@@ -818,17 +822,27 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     }
     __syncthreads();
   };
-  auto a_issue_any = [&]() {
-    if constexpr (MB == 1) {
-      if (rs == 1) a_issue(IC<1>{});
-      else if (rs == 2) a_issue(IC<2>{});
-      else if (rs == 4) a_issue(IC<4>{});
-      else if (rs == AP::XR) a_issue(IC<AP::XR>{});
-    } else {
-      if (rs == 2) a_issue(IC<2>{});
-      else if (rs == 4) a_issue(IC<4>{});
-    }
-  };
+  // one (RS, MR) instantiation per register layout, chosen uniformly (a macro, not a lambda
+  // taking the lambda: passing it through a call put the A registers in scratch)
+#define LLJ_A_DISPATCH(F)                              \
+  do {                                                 \
+    if constexpr (MB == 1) {                           \
+      if (rs == 1) F(IC<1>{}, IC<1>{});                \
+      else if (rs == 2) F(IC<2>{}, IC<1>{});           \
+      else if (rs == 4) F(IC<4>{}, IC<1>{});           \
+      else if (rs == AP::XR) F(IC<AP::XR>{}, IC<1>{}); \
+    } else {                                           \
+      if (rs == 2) {                                   \
+        if (mr == 2) F(IC<2>{}, IC<2>{});              \
+        else if (mr == 4) F(IC<2>{}, IC<4>{});         \
+        else F(IC<2>{}, IC<AP::XR / 2>{});             \
+      } else if (rs == 4) {                            \
+        if (mr == 2) F(IC<4>{}, IC<2>{});              \
+        else F(IC<4>{}, IC<AP::XR / 4>{});             \
+      }                                                \
+    }                                                  \
+  } while (0)
+  auto a_issue_any = [&]() { LLJ_A_DISPATCH(a_issue); };
 
   if constexpr (!CH) {
     // standalone launch: every input is final, so the A-side loads go first (a wait for
@@ -887,15 +901,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
           if (lane == 0) tail[TL_RS + wave * 8 + m] = rsum;
         }
       }
-    } else if constexpr (MB == 1) {
-      if (rs == 1) a_finish(IC<1>{});
-      else if (rs == 2) a_finish(IC<2>{});
-      else if (rs == 4) a_finish(IC<4>{});
-      else a_finish(IC<AP::XR>{});
     } else {
-      if (rs == 2) a_finish(IC<2>{});
-      else a_finish(IC<4>{});
+      LLJ_A_DISPATCH(a_finish);
     }
+#undef LLJ_A_DISPATCH
   }
   LLJ_STAMP(2);
   // chunk i lives in buffer i % D; after computing it the buffer is refilled with chunk i + D.
@@ -1182,8 +1191,14 @@ static inline int device_cus() {
 // (M >= 2: one staged A image of M rows per CU instead of per tile, 1.966 -> 1.865 ms at 7B
 // bs=8); a single row keeps one tile per workgroup, where several workgroups per CU interleave
 // on each SIMD (measured 7B bs=1: 1.205 ms with one tile, 1.305 ms with three per workgroup).
+// Below LLJ_TPW_MIN_M rows the staged image is small and one tile per workgroup wins (7B
+// decode ms/token, tiles per workgroup 1 vs ceil(tiles / CUs): bs=2 1.427 vs 1.509, bs=4 1.574
+// vs 1.646, bs=6 1.683 vs 1.722, bs=8 1.889 vs 1.793).
+#ifndef LLJ_TPW_MIN_M
+#define LLJ_TPW_MIN_M 7
+#endif
 static inline int pick_tpw(int ntiles, int M) {
-  if (M < 2) return 1;
+  if (M < LLJ_TPW_MIN_M) return 1;
   const int cu = device_cus();
   const int cap = g_tpw_max < LLJ_TPW_MAX ? g_tpw_max : LLJ_TPW_MAX;
   const int t = (ntiles + cu - 1) / cu;

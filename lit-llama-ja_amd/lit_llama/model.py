@@ -113,6 +113,7 @@ NST_STATS = False
 # batched rows (M >= 2): each RMSNorm as its own launch (llj_rmsnorm_rows) feeding LDS-A GEMVs,
 # instead of normalized inside every norm-fused GEMV workgroup
 PRE_NORM_ROWS = True
+PRE_NORM_MIN_M = 2  # smallest batch that takes the separate launch (measured best from bs=2 on)
 
 
 # weight formats whose kernels remove the nibble offset with the row sums of A (W4P, W8P)
@@ -153,7 +154,7 @@ class _Work:
         self.h = torch.empty(M, H, dtype=bf, device=device)
         # batched rows (M >= 2): each RMSNorm runs once (llj_rmsnorm_rows -> xn, rs = fp32 row
         # sums for the int4 offset term) instead of inside every norm-fused GEMV workgroup
-        self.pre = M >= 2 and not need_i8 and PRE_NORM_ROWS
+        self.pre = M >= max(2, PRE_NORM_MIN_M) and not need_i8 and PRE_NORM_ROWS
         self.xn = torch.empty(M, C, dtype=bf, device=device) if (need_i8 or self.pre) else None
         self.rs = torch.empty(M, dtype=torch.float32, device=device) if self.pre else None
         # completion counter of llj_linear_resid_norm (M <= 8): the residual GEMV's last
