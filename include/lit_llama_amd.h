@@ -187,6 +187,24 @@ int llj_i8_stats(const void* A, int lda, int M, int K, float threshold, void* ws
  * quantization.py:67-75). W (N, K) of dtype 0 fp32 / 1 bf16 / 2 fp16. */
 int llj_i8_quant_weight(const void* W, int dtype, void* CB, void* SCB, int N, int K, void* stream);
 
+/* ---------------------------------------------------------------- GPTQ producer */
+/* One 128-column block of GPTQQuantizer.quantize (reference quantization.py:568-596, groupsize
+ * -1): for rows n < N, quantize columns i1 .. i1+127 in order with the per-row (scale, zero)
+ * (quantize_weight, 470-473), propagate each column's error through the block with Hinv1 =
+ * hinv[i1:i1+128, i1:i1+128] (593). wt: the (permuted, running) weight TRANSPOSED, (K, N) fp32,
+ * its block rows updated in place; qt (K, N): reconstructions scale*(q - zero) of the block's
+ * rows; err (128, N): Err1; loss[n] += Σ_i (w - q)² / d² (Losses1 before the / 2). hinv: (K, K)
+ * fp32 upper Cholesky factor of H⁻¹. Requires i1 % 128 == 0, i1 + 128 <= K, bits in {2,4,8}.
+ * Each fp32 op rounded on its own in the reference's order (bitwise the reference's loop). The
+ * trailing update W[:, i2:] -= Err1 · Hinv[i1:i2, i2:] is a plain GEMM left to the caller. */
+int llj_gptq_block(const float* hinv, int K, int i1, float* wt, int N, const float* scale, const float* zero,
+                   int bits, float* qt, float* err, float* loss, void* stream);
+/* ColBlockQuantizedLinear.pack_weight (quantization.py:374-388) from reconstructions qt (K, N)
+ * fp32: code = uint8(clamp(q / scale + zero, 0, 2^bits - 1)) (truncating), entries_per_byte =
+ * 8/bits codes per byte; qw is quant_weight in its column-major storage: byte (n, j) at j*N + n. */
+int llj_colblock_pack(const float* qt, int K, int N, const float* scale, const float* zero, int bits,
+                      unsigned char* qw, void* stream);
+
 /* ---------------------------------------------------------------- small ops */
 /* out[m] = wte[idx[m]] (model.py:110); if pos_inc != NULL, *pos_inc += 1 (device-side
  * decode position, so a captured decode step advances itself); nstat_out: per-row sum of

@@ -19,6 +19,11 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-variable", "-Wno-un
          "-munsafe-fp-atomics"]
 
 
+# per-file flags: the GPTQ column loop reproduces the reference's fp32 op order bit for bit, so
+# no multiply-add contraction there (hipcc contracts by default and ignores the fp pragma)
+FILE_FLAGS = {"gptq.hip": ["-ffp-contract=off"]}
+
+
 def sources():
     return sorted(CSRC.glob("*.hip"))
 
@@ -44,7 +49,8 @@ def build(force: bool = False, verbose: bool = False, out: Path | None = None, d
         for src in sources():
             obj = Path(td) / (src.stem + ".o")
             objs.append(obj)
-            cmds.append([hipcc, f"--offload-arch={ARCH}", *FLAGS, *extra, f"-I{INCLUDE}", "-c", str(src),
+            cmds.append([hipcc, f"--offload-arch={ARCH}", *FLAGS, *FILE_FLAGS.get(src.name, []), *extra,
+                         f"-I{INCLUDE}", "-c", str(src),
                          "-o", str(obj)])
 
         def run(cmd):

@@ -255,3 +255,117 @@ class Linear8bitLt(torch.nn.Module):
             self._quantize_weight(self.weight)
         bias = None if self.bias is None else self.bias.to(torch.bfloat16)
         return int8_linear(x, self.weight, self.SCB, bias, self.threshold)
+
+
+class GPTQQuantizer:
+    """GPTQ producer (reference quantization.py:424-614; IST-DASLab GPTQ, arXiv:2210.17323):
+    same constructor, `collect_input_stats` forward hook and `quantize() -> (ColBlockQuantizedLinear,
+    error)`. The calibration Hessian, the Cholesky factors and the trailing block update are
+    library work on the device (torch GEMM / rocSOLVER); the sequential 128-column loop and the
+    ColBlock packing are the HIP kernels `llj_gptq_block` / `llj_colblock_pack` (csrc/gptq.hip).
+    Supported: the configuration quantize/gptq.py uses (per-channel, asymmetric, groupsize -1,
+    blocksize 128), in_features % 128 == 0. fp32 weights reproduce the reference's op order;
+    other weight dtypes are quantized from their fp32 value (the reference would round the
+    packing step in that dtype). No CPU path."""
+
+    def __init__(self, linear_module, *, bits, perchannel=True, sym=False, blocksize=128, percdamp=0.01,
+                 groupsize=-1, actorder=False):
+        assert isinstance(linear_module, torch.nn.Linear)
+        if not perchannel or sym or groupsize != -1 or blocksize != 128:
+            raise NotImplementedError("GPTQQuantizer HIP path: perchannel=True, sym=False, groupsize=-1, "
+                                      "blocksize=128 (the gptq.int4 / gptq.int8 producer configuration)")
+        self.linear_module = linear_module
+        self.dev = linear_module.weight.device
+        self.rows, self.columns = linear_module.weight.shape
+        if self.columns % 128:
+            raise NotImplementedError(f"GPTQQuantizer HIP path needs in_features % 128 == 0, got {self.columns}")
+        self.H = torch.zeros((self.columns, self.columns), device=self.dev)
+        self.nsamples = 0
+        self.bits = bits
+        self.maxq = 2 ** bits - 1
+        self.perchannel, self.sym, self.blocksize = perchannel, sym, blocksize
+        self.percdamp, self.groupsize, self.actorder = percdamp, groupsize, actorder
+        self.tile_cols = self.columns
+        self.scales = torch.zeros((self.rows, 1), dtype=linear_module.weight.dtype, device=self.dev)
+        self.zeros = torch.zeros_like(self.scales)
+
+    def find_params_weight(self, x):
+        """reference 475-514 (per-channel, asymmetric). The row min / max reduce on the device
+        (exact); the N-element divisions run on the host, because torch's device division by a
+        scalar multiplies by its reciprocal (not the reference's correctly rounded quotient)."""
+        tmp = torch.zeros(x.shape[0], device=x.device)
+        xmin = torch.minimum(x.min(1)[0], tmp).cpu()
+        xmax = torch.maximum(x.max(1)[0], tmp).cpu()
+        both0 = (xmin == 0) & (xmax == 0)
+        xmin[both0] = -1
+        xmax[both0] = +1
+        scale = (xmax - xmin) / self.maxq
+        zero = torch.round(-xmin / scale)
+        return scale.reshape(-1, 1).to(x.device), zero.reshape(-1, 1).to(x.device)
+
+    def collect_input_stats(self, _1, inp, _2):
+        """Forward hook, reference 516-530: running H = 2/n Σ x xᵀ (a device GEMM)."""
+        inp = inp[0].detach()
+        self.last_inp = inp
+        if len(inp.shape) == 2:
+            inp = inp.unsqueeze(0)
+        tmp = inp.shape[0]
+        if len(inp.shape) == 3:
+            inp = inp.reshape((-1, inp.shape[-1]))
+        inp = inp.t()
+        self.H *= self.nsamples / (self.nsamples + tmp)
+        self.nsamples += tmp
+        inp = math.sqrt(2 / self.nsamples) * inp.float()
+        self.H += inp.matmul(inp.t())
+
+    def quantize(self):
+        """reference 532-614 with the column loop on the GPU: returns (ColBlockQuantizedLinear, error)."""
+        _hip.require_device(self.linear_module.weight, "GPTQQuantizer linear_module.weight")
+        W = self.linear_module.weight.detach().to(dtype=torch.float, copy=True)
+        scale, zero = self.find_params_weight(W)
+        self.scales[:] = scale
+        self.zeros[:] = zero
+        H = self.H
+        del self.H
+        dead = torch.diag(H) == 0
+        H[dead, dead] = 1
+        W[:, dead] = 0
+        perm = None
+        if self.actorder:
+            perm = torch.argsort(torch.diag(H), descending=True, stable=True)
+            W = W[:, perm]
+            H = H[perm][:, perm]
+        damp = self.percdamp * torch.mean(torch.diag(H))
+        diag = torch.arange(self.columns, device=self.dev)
+        H[diag, diag] += damp
+        H = torch.linalg.cholesky(H)
+        H = torch.cholesky_inverse(H)
+        Hinv = torch.linalg.cholesky(H, upper=True).contiguous()
+        N, K, B = self.rows, self.columns, self.blocksize
+        Wt = W.t().contiguous()  # (K, N): column i of all rows is one coalesced row
+        Qt = torch.empty_like(Wt)
+        Err = torch.empty((B, N), dtype=torch.float32, device=self.dev)
+        loss = torch.zeros(N, dtype=torch.float32, device=self.dev)
+        sc = scale.reshape(-1).float().contiguous()
+        zr = zero.reshape(-1).float().contiguous()
+        s = _hip.stream()
+        for i1 in range(0, K, B):
+            i2 = i1 + B
+            _hip.call("llj_gptq_block", Hinv.data_ptr(), K, i1, Wt.data_ptr(), N, sc.data_ptr(), zr.data_ptr(),
+                      self.bits, Qt.data_ptr(), Err.data_ptr(), loss.data_ptr(), s)
+            if i2 < K:  # W[:, i2:] -= Err1 @ Hinv[i1:i2, i2:] (596), transposed
+                Wt[i2:] -= Hinv[i1:i2, i2:].t().matmul(Err)
+        if perm is not None:
+            Qt = Qt[torch.argsort(perm)].contiguous()
+        error = loss.sum().item() / 2
+        q_module = ColBlockQuantizedLinear(self.linear_module.in_features, self.linear_module.out_features,
+                                           self.linear_module.bias is not None, bits=self.bits,
+                                           tile_cols=self.groupsize).to(self.dev)
+        q_module.scales = self.scales
+        q_module.zeros = self.zeros
+        # pack_weight (374-388) into quant_weight's column-major storage ((K/epb, N) bytes)
+        assert q_module.quant_weight.stride() == (1, N)
+        _hip.call("llj_colblock_pack", Qt.data_ptr(), K, N, sc.data_ptr(), zr.data_ptr(), self.bits,
+                  q_module.quant_weight.data_ptr(), s)
+        q_module.bias = self.linear_module.bias
+        return q_module, error

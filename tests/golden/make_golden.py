@@ -237,6 +237,36 @@ def gen_int4_gptq():
     save("int4_gptq", **out)
 
 
+def gen_gptq():
+    """GPTQQuantizer (quantization.py:424-614) on single Linears: inputs W and calibration
+    activations X, the reference's accumulated Hessian H, and its packed outputs. Cases: one
+    128-column block (with a dead input column), three blocks, bits=8."""
+    out = {}
+    cases = {"a": (96, 128, 4, 11), "b": (160, 384, 4, 12), "c": (64, 256, 8, 13)}
+    for tag, (N, K, bits, seed) in cases.items():
+        rng = np.random.default_rng(seed)
+        W = (rng.standard_normal((N, K)) * 0.05).astype(np.float32)
+        W[:, :8] *= 4.0  # a few wide columns (act-order has something to sort)
+        X = rng.standard_normal((4, 32, K)).astype(np.float32) * rng.uniform(0.2, 2.0, K).astype(np.float32)
+        if tag == "a":
+            X[..., 5] = 0.0  # dead column: diag(H) == 0 (quantization.py:544-546)
+        lin = torch.nn.Linear(K, N, bias=False)
+        lin.weight.data = torch.from_numpy(W.copy())
+        gq = rq.GPTQQuantizer(lin, bits=bits, groupsize=-1, actorder=True)
+        h = lin.register_forward_hook(gq.collect_input_stats)
+        with torch.no_grad():
+            for j in range(X.shape[0]):  # one sample per call, as quantize/gptq.py:96-104
+                lin(torch.from_numpy(X[j:j + 1]))
+        h.remove()
+        H = gq.H.clone().numpy()
+        qm, err = gq.quantize()
+        out.update({f"{tag}_W": W, f"{tag}_X": X, f"{tag}_H": H, f"{tag}_bits": np.int64(bits),
+                    f"{tag}_quant_weight": qm.quant_weight.contiguous().numpy(),
+                    f"{tag}_scales": qm.scales.numpy().reshape(-1), f"{tag}_zeros": qm.zeros.numpy().reshape(-1),
+                    f"{tag}_error": np.float64(err)})
+    save("gptq", **out)
+
+
 def gen_kv_roll():
     """Sliding-window KV roll (model.py:221-225), as tests/test_generate.py:46 exercises."""
     cfg = Cfg(block_size=128, n_layer=1, n_head=4, n_embd=256, vocab_size=512)
@@ -317,6 +347,6 @@ def gen_eos():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos"]
+    which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq"]
     for w in which:
         globals()[f"gen_{w}"]()
