@@ -1,0 +1,104 @@
+"""Checkpoint formats: Hugging Face LLaMA shards -> lit-llama state dict.
+
+Mirrors reference scripts/convert_hf_checkpoint.py:19-138 (`convert_hf_checkpoint`, same keyword
+arguments and output file `lit-llama.pth`, tokenizer copied to the output's parent): the HF
+per-projection q / k / v weights are fused into `attn.c_attn.weight` with q and k rows permuted
+from HF's half-split rotary layout back to the interleaved pairs `apply_rope` uses
+(model.py:312-329; the inverse of transformers' convert_llama_weights_to_hf permute), every other
+tensor renamed by the reference's weight map, `rotary_emb.inv_freq` dropped. Shards are opened
+memory-mapped with `torch.load(weights_only=True, mmap=True)` (nothing in a checkpoint is
+executed) and the output written once with `torch.save`; `load_lit_checkpoint` streams a
+lit-llama.pth straight into a model's (device) parameters.
+"""
+from __future__ import annotations
+
+import json
+import shutil
+from pathlib import Path
+
+import torch
+
+from .model import LLaMAConfig
+
+# reference convert_hf_checkpoint.py:74-87
+WEIGHT_MAP = {
+    "self_attn.o_proj.weight": "attn.c_proj.weight",
+    "self_attn.q_proj.weight": "attn.c_attn.weight",
+    "self_attn.k_proj.weight": "attn.c_attn.weight",
+    "self_attn.v_proj.weight": "attn.c_attn.weight",
+    "mlp.gate_proj.weight": "mlp.c_fc1.weight",
+    "mlp.up_proj.weight": "mlp.c_fc2.weight",
+    "mlp.down_proj.weight": "mlp.c_proj.weight",
+    "input_layernorm.weight": "rms_1.scale",
+    "post_attention_layernorm.weight": "rms_2.scale",
+    "model.embed_tokens.weight": "transformer.wte.weight",
+    "model.norm.weight": "transformer.ln_f.scale",
+    "lm_head.weight": "lm_head.weight",
+}
+
+
+def unpermute_rotary(w: torch.Tensor, n_head: int) -> torch.Tensor:
+    """HF half-split rotary rows -> interleaved pairs (reference convert_hf_checkpoint.py:63-70):
+    within each head, row r of the first half and row r of the second half become rows 2r, 2r+1."""
+    dim = w.shape[1]
+    return w.view(n_head, 2, dim // n_head // 2, dim).transpose(1, 2).reshape(dim, dim)
+
+
+def convert_hf_state_dict(hf: dict, config: LLaMAConfig, dtype=torch.float32) -> dict:
+    """Map one HF LLaMA state dict (possibly merged from all shards) to lit-llama keys."""
+    out, qkv = {}, {}
+    for name, t in hf.items():
+        if "rotary_emb.inv_freq" in name:
+            continue
+        if "model.layers" in name:
+            parts = name.split(".")
+            key = f"transformer.h.{int(parts[2])}.{WEIGHT_MAP['.'.join(parts[3:])]}"
+            proj = parts[4] if parts[3] == "self_attn" and parts[4] in ("q_proj", "k_proj", "v_proj") else None
+            if proj is not None:
+                qkv.setdefault(key, {})[proj] = t
+                if len(qkv[key]) == 3:
+                    parts3 = qkv.pop(key)
+                    out[key] = torch.cat([unpermute_rotary(parts3["q_proj"].to(dtype), config.n_head),
+                                          unpermute_rotary(parts3["k_proj"].to(dtype), config.n_head),
+                                          parts3["v_proj"].to(dtype)], 0)
+                continue
+            out[key] = t.to(dtype)
+        else:
+            out[WEIGHT_MAP[name]] = t.to(dtype)
+    if qkv:  # reference convert_hf_checkpoint.py:137
+        raise AssertionError(f"unexpected partial weights {list(qkv)}")
+    return out
+
+
+@torch.no_grad()
+def convert_hf_checkpoint(*, output_dir: Path = Path("checkpoints/lit-llama/7B"),
+                          checkpoint_dir: Path = Path("checkpoints/hf-llama/7B"), model_size: str = "7B",
+                          dtype: str = "float32", verify: bool = False) -> None:
+    """File-level converter with the reference's arguments (verify needs transformers' model
+    download and is not supported offline)."""
+    output_dir, checkpoint_dir = Path(output_dir), Path(checkpoint_dir)
+    output_dir.mkdir(parents=True, exist_ok=True)
+    shutil.copy(checkpoint_dir / "tokenizer.model", output_dir.parent)
+    dt = getattr(torch, dtype, None)
+    if not isinstance(dt, torch.dtype):
+        raise ValueError(f"{dtype} is not a valid dtype.")
+    if verify:
+        raise NotImplementedError("verify=True compares against transformers' LlamaForCausalLM.from_pretrained")
+    config = LLaMAConfig.from_name(model_size)
+    with open(checkpoint_dir / "pytorch_model.bin.index.json") as f:
+        bin_index = json.load(f)
+    bin_files = sorted(set(checkpoint_dir / b for b in bin_index["weight_map"].values()))
+    if not bin_files:
+        raise ValueError(f"Expected {str(checkpoint_dir)!r} to contain .bin files")
+    hf = {}
+    for b in bin_files:  # memory-mapped: tensors are read when converted
+        hf.update(torch.load(b, map_location="cpu", weights_only=True, mmap=True))
+    torch.save(convert_hf_state_dict(hf, config, dt), output_dir / "lit-llama.pth")
+
+
+def load_lit_checkpoint(model: torch.nn.Module, path: Path, strict: bool = True):
+    """Load lit-llama.pth into `model` (its parameters may already live on the GPU): the file
+    is memory-mapped and each tensor copied into its parameter once (reference lazy_load +
+    load_state_dict, utils.py:200-376, without the custom unpickler)."""
+    sd = torch.load(Path(path), map_location="cpu", weights_only=True, mmap=True)
+    return model.load_state_dict(sd, strict=strict)

@@ -267,6 +267,50 @@ def gen_gptq():
     save("gptq", **out)
 
 
+def gen_hf_convert():
+    """The reference's scripts/convert_hf_checkpoint.py on a tiny synthetic HF LLaMA checkpoint
+    (two .bin shards, layer 1's q / k / v split across them, rotary inv_freq buffers), written to
+    a temporary directory; the fixture holds the HF tensors and the converted lit-llama tensors."""
+    import json
+    import tempfile
+
+    from lit_llama import model as rmodel
+    from scripts.convert_hf_checkpoint import convert_hf_checkpoint
+
+    rmodel.llama_configs["tinyhf"] = dict(n_layer=2, n_head=4, n_embd=64, vocab_size=128)
+    C, H, V, L = 64, 256, 128, 2
+    rng = np.random.default_rng(77)
+    t = lambda *sh: torch.from_numpy(rng.standard_normal(sh).astype(np.float32))  # noqa: E731
+    hf = {"model.embed_tokens.weight": t(V, C), "model.norm.weight": t(C), "lm_head.weight": t(V, C)}
+    for i in range(L):
+        p = f"model.layers.{i}."
+        hf.update({p + "self_attn.q_proj.weight": t(C, C), p + "self_attn.k_proj.weight": t(C, C),
+                   p + "self_attn.v_proj.weight": t(C, C), p + "self_attn.o_proj.weight": t(C, C),
+                   p + "self_attn.rotary_emb.inv_freq": t(C // 8), p + "mlp.gate_proj.weight": t(H, C),
+                   p + "mlp.up_proj.weight": t(H, C), p + "mlp.down_proj.weight": t(C, H),
+                   p + "input_layernorm.weight": t(C), p + "post_attention_layernorm.weight": t(C)})
+    shard1 = {k: v for k, v in hf.items() if "layers.1." not in k or "q_proj" in k}
+    shard2 = {k: v for k, v in hf.items() if k not in shard1}
+    with tempfile.TemporaryDirectory() as td:
+        ck, out = Path(td) / "hf" / "tinyhf", Path(td) / "lit" / "tinyhf"
+        ck.mkdir(parents=True)
+        (ck / "tokenizer.model").write_bytes(b"placeholder")
+        names = {"pytorch_model-00001-of-00002.bin": shard1, "pytorch_model-00002-of-00002.bin": shard2}
+        for fn, sd in names.items():
+            torch.save(sd, ck / fn)
+        wm = {k: fn for fn, sd in names.items() for k in sd}
+        (ck / "pytorch_model.bin.index.json").write_text(json.dumps({"metadata": {}, "weight_map": wm}))
+        with contextlib.redirect_stdout(io.StringIO()):
+            convert_hf_checkpoint(output_dir=out, checkpoint_dir=ck, model_size="tinyhf", dtype="float32")
+        from lit_llama.utils import lazy_load  # the reference's own reader of its incremental_save format
+        with lazy_load(out / "lit-llama.pth") as sd:
+            lit = {k: v._load_tensor() for k, v in sd.items()}
+    arrays = {"hf/" + k: v.numpy() for k, v in hf.items()}
+    arrays.update({"lit/" + k: v.numpy() for k, v in lit.items()})
+    arrays["shard1_keys"] = np.array(sorted(shard1))
+    save("hf_convert", **arrays)
+
+
 def gen_kv_roll():
     """Sliding-window KV roll (model.py:221-225), as tests/test_generate.py:46 exercises."""
     cfg = Cfg(block_size=128, n_layer=1, n_head=4, n_embd=256, vocab_size=512)
@@ -347,6 +391,6 @@ def gen_eos():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq"]
+    which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq", "hf_convert"]
     for w in which:
         globals()[f"gen_{w}"]()

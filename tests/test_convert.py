@@ -1,0 +1,92 @@
+"""HF -> lit-llama checkpoint conversion (reference
+scripts/convert_hf_checkpoint.py:19-138) against the reference's own conversion of a tiny
+synthetic two-shard HF checkpoint (tests/golden/hf_convert.npz, make_golden.py gen_hf_convert)."""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from lit_llama import convert as CV
+from lit_llama import model as M
+from oracle import llama_np as O
+
+GOLD = np.load(Path(__file__).parent / "golden" / "hf_convert.npz")
+HF = {k[3:]: torch.from_numpy(GOLD[k]) for k in GOLD.files if k.startswith("hf/")}
+LIT = {k[4:]: GOLD[k] for k in GOLD.files if k.startswith("lit/")}
+TINY = dict(n_layer=2, n_head=4, n_embd=64, vocab_size=128)
+
+
+@pytest.fixture
+def tiny_config(monkeypatch):
+    monkeypatch.setitem(M.llama_configs, "tinyhf", TINY)
+    return M.LLaMAConfig.from_name("tinyhf")
+
+
+def test_state_dict_conversion_matches_reference(tiny_config):
+    out = CV.convert_hf_state_dict(HF, tiny_config)
+    assert set(out) == set(LIT)
+    for k, v in out.items():
+        np.testing.assert_array_equal(v.numpy(), LIT[k], err_msg=k)
+
+
+def test_file_conversion_matches_reference(tiny_config, tmp_path):
+    ck = tmp_path / "hf" / "tinyhf"
+    ck.mkdir(parents=True)
+    (ck / "tokenizer.model").write_bytes(b"placeholder")
+    s1 = set(GOLD["shard1_keys"].tolist())
+    shards = {"pytorch_model-00001-of-00002.bin": {k: v for k, v in HF.items() if k in s1},
+              "pytorch_model-00002-of-00002.bin": {k: v for k, v in HF.items() if k not in s1}}
+    for fn, sd in shards.items():
+        torch.save(sd, ck / fn)
+    wm = {k: fn for fn, sd in shards.items() for k in sd}
+    (ck / "pytorch_model.bin.index.json").write_text(json.dumps({"metadata": {}, "weight_map": wm}))
+    out = tmp_path / "lit" / "tinyhf"
+    CV.convert_hf_checkpoint(output_dir=out, checkpoint_dir=ck, model_size="tinyhf", dtype="float32")
+    assert (out.parent / "tokenizer.model").exists()
+    sd = torch.load(out / "lit-llama.pth", map_location="cpu", weights_only=True)
+    assert set(sd) == set(LIT)
+    for k, v in sd.items():
+        np.testing.assert_array_equal(v.numpy(), LIT[k], err_msg=k)
+    with pytest.raises(ValueError):
+        CV.convert_hf_checkpoint(output_dir=out, checkpoint_dir=ck, model_size="tinyhf", dtype="float33")
+
+
+def test_partial_qkv_is_an_error(tiny_config):
+    hf = {k: v for k, v in HF.items() if k != "model.layers.1.self_attn.v_proj.weight"}
+    with pytest.raises(AssertionError, match="partial"):
+        CV.convert_hf_state_dict(hf, tiny_config)
+
+
+def test_unpermuted_rows_turn_hf_rotary_into_interleaved_rope():
+    """Why the permutation: HF's half-split rotary on q = W x equals, after unpermute_rotary on
+    the rows, the reference's interleaved apply_rope (model.py:312-329) on the converted rows."""
+    n_head, C, T = 4, 64, 5
+    hs = C // n_head
+    rng = np.random.default_rng(0)
+    W = rng.standard_normal((C, C)).astype(np.float32)
+    x = rng.standard_normal((T, C)).astype(np.float32)
+    q = (x @ W.T).reshape(T, n_head, hs)
+    theta = 1.0 / (10000 ** (np.arange(0, hs, 2, dtype=np.float32) / hs))
+    ang = np.arange(T, dtype=np.float32)[:, None] * theta[None, :]  # (T, hs/2)
+    cos, sin = np.cos(ang)[:, None, :], np.sin(ang)[:, None, :]
+    a, b = q[..., :hs // 2], q[..., hs // 2:]
+    hf_rot = np.concatenate([a * cos - b * sin, b * cos + a * sin], -1)  # rotate_half form
+    Wl = CV.unpermute_rotary(torch.from_numpy(W), n_head).numpy()
+    ql = (x @ Wl.T).reshape(1, T, n_head, hs)
+    rope = O.build_rope_cache(T, hs)
+    lit_rot = O.apply_rope(ql, rope)[0]
+    perm = np.stack([np.arange(hs // 2), np.arange(hs // 2) + hs // 2], 1).reshape(-1)  # lit row 2r / 2r+1
+    np.testing.assert_allclose(lit_rot, hf_rot[..., perm], rtol=1e-4, atol=1e-4)
+
+
+def test_load_lit_checkpoint_into_model(tiny_config, tmp_path):
+    torch.save({k: torch.from_numpy(v) for k, v in LIT.items()}, tmp_path / "lit-llama.pth")
+    tiny_config.block_size = 32
+    model = M.LLaMA(tiny_config)
+    CV.load_lit_checkpoint(model, tmp_path / "lit-llama.pth")
+    np.testing.assert_array_equal(model.transformer.h[1].attn.c_attn.weight.detach().numpy(),
+                                  LIT["transformer.h.1.attn.c_attn.weight"])
