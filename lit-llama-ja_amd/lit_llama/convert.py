@@ -102,3 +102,69 @@ def load_lit_checkpoint(model: torch.nn.Module, path: Path, strict: bool = True)
     load_state_dict, utils.py:200-376, without the custom unpickler)."""
     sd = torch.load(Path(path), map_location="cpu", weights_only=True, mmap=True)
     return model.load_state_dict(sd, strict=strict)
+
+
+# ----------------------------------------------------------------------- Meta (consolidated.*.pth)
+def convert_meta_state_dict(state_dict: dict, dtype=torch.float32) -> dict:
+    """reference scripts/convert_checkpoint.py:20-53: Meta names -> lit-llama names, wq / wk / wv
+    stacked into c_attn (Meta's rotary layout is already the interleaved one)."""
+    out = {"transformer.wte.weight": state_dict["tok_embeddings.weight"].to(dtype),
+           "lm_head.weight": state_dict["output.weight"].to(dtype),
+           "transformer.ln_f.scale": state_dict["norm.weight"].to(dtype)}
+    layers = sorted({k.split(".")[1] for k in state_dict if k.startswith("layers")})
+    for i in layers:
+        p, q = f"layers.{i}.", f"transformer.h.{i}."
+        out[q + "attn.c_attn.weight"] = torch.cat([state_dict[p + f"attention.{w}.weight"].to(dtype)
+                                                   for w in ("wq", "wk", "wv")])
+        out[q + "attn.c_proj.weight"] = state_dict[p + "attention.wo.weight"].to(dtype)
+        out[q + "mlp.c_fc1.weight"] = state_dict[p + "feed_forward.w1.weight"].to(dtype)
+        out[q + "mlp.c_proj.weight"] = state_dict[p + "feed_forward.w2.weight"].to(dtype)
+        out[q + "mlp.c_fc2.weight"] = state_dict[p + "feed_forward.w3.weight"].to(dtype)
+        out[q + "rms_1.scale"] = state_dict[p + "attention_norm.weight"].to(dtype)
+        out[q + "rms_2.scale"] = state_dict[p + "ffn_norm.weight"].to(dtype)
+    return out
+
+
+# model-parallel split dimension per tensor (reference convert_checkpoint.py:56-64)
+SHARD_DIMS = {"lm_head.weight": 0, "wte.weight": 1, "attn.c_attn.weight": 0, "attn.c_proj.weight": 1,
+              "mlp.c_fc1.weight": 0, "mlp.c_fc2.weight": 0, "mlp.c_proj.weight": 1}
+
+
+def merge_meta_shards(converted: list) -> dict:
+    """Concatenate the model-parallel parts (convert_checkpoint.py:95-113; unsharded tensors are
+    taken from the first part) and regroup c_attn from [Q1 K1 V1 Q2 K2 V2 ...] to
+    [Q1 Q2 ... K1 K2 ... V1 V2 ...] (115-131)."""
+    n = len(converted)
+    combined = dict(converted[0])
+    for part in converted[1:]:
+        for name, t in part.items():
+            dim = next((d for k, d in SHARD_DIMS.items() if k in name), None)
+            if dim is not None:
+                combined[name] = torch.cat((combined[name], t), dim=dim)
+    for name, t in combined.items():
+        if "c_attn" not in name:
+            continue
+        src = t.shape[0] // n
+        mat = src // 3
+        combined[name] = torch.cat([t[i * src + j * mat: i * src + (j + 1) * mat] for j in range(3) for i in range(n)])
+    return combined
+
+
+@torch.no_grad()
+def meta_weights_for_nano_model(*, output_dir: Path = Path("checkpoints/lit-llama"),
+                                checkpoint_dir: Path = Path("checkpoints/llama/"), model_size: str = "7B",
+                                dtype: str = "float32") -> None:
+    """reference convert_checkpoint.py:67-134 (same arguments and layout: <dir>/<size>/...)."""
+    output_dir, checkpoint_dir = Path(output_dir) / model_size, Path(checkpoint_dir) / model_size
+    output_dir.mkdir(parents=True, exist_ok=True)
+    shutil.copy(checkpoint_dir.parent / "tokenizer.model", output_dir.parent)
+    dt = getattr(torch, dtype, None)
+    if not isinstance(dt, torch.dtype):
+        raise ValueError(f"{dtype} is not a valid dtype.")
+    files = sorted(checkpoint_dir.glob("*.pth"))
+    if not files:
+        raise RuntimeError(f"No checkpoints were found at checkpoint_dir {checkpoint_dir}. "
+                           "`consolidated.0*.pth` files expected at that location.")
+    parts = [convert_meta_state_dict(torch.load(f, map_location="cpu", weights_only=True, mmap=True), dt)
+             for f in files]
+    torch.save(merge_meta_shards(parts), output_dir / "lit-llama.pth")

@@ -311,6 +311,42 @@ def gen_hf_convert():
     save("hf_convert", **arrays)
 
 
+def gen_meta_convert():
+    """The reference's scripts/convert_checkpoint.py (meta_weights_for_nano_model) on a tiny
+    synthetic Meta checkpoint split over two model-parallel files."""
+    import tempfile
+
+    from scripts.convert_checkpoint import meta_weights_for_nano_model
+
+    C, H, V, L, n = 64, 256, 128, 2, 2
+    rng = np.random.default_rng(78)
+    t = lambda *sh: torch.from_numpy(rng.standard_normal(sh).astype(np.float32))  # noqa: E731
+    parts = []
+    for _ in range(n):
+        sd = {"tok_embeddings.weight": t(V, C // n), "output.weight": t(V // n, C), "norm.weight": t(C)}
+        for i in range(L):
+            p = f"layers.{i}."
+            sd.update({p + "attention.wq.weight": t(C // n, C), p + "attention.wk.weight": t(C // n, C),
+                       p + "attention.wv.weight": t(C // n, C), p + "attention.wo.weight": t(C, C // n),
+                       p + "feed_forward.w1.weight": t(H // n, C), p + "feed_forward.w2.weight": t(C, H // n),
+                       p + "feed_forward.w3.weight": t(H // n, C), p + "attention_norm.weight": t(C),
+                       p + "ffn_norm.weight": t(C)})
+        parts.append(sd)
+    with tempfile.TemporaryDirectory() as td:
+        ck = Path(td) / "llama" / "tinymeta"
+        ck.mkdir(parents=True)
+        (ck.parent / "tokenizer.model").write_bytes(b"placeholder")
+        for r, sd in enumerate(parts):
+            torch.save(sd, ck / f"consolidated.{r:02d}.pth")
+        with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+            meta_weights_for_nano_model(output_dir=Path(td) / "lit", checkpoint_dir=Path(td) / "llama",
+                                        model_size="tinymeta")
+        lit = torch.load(Path(td) / "lit" / "tinymeta" / "lit-llama.pth", map_location="cpu", weights_only=True)
+    arrays = {f"meta{r}/" + k: v.numpy() for r, sd in enumerate(parts) for k, v in sd.items()}
+    arrays.update({"lit/" + k: v.numpy() for k, v in lit.items()})
+    save("meta_convert", **arrays)
+
+
 def gen_kv_roll():
     """Sliding-window KV roll (model.py:221-225), as tests/test_generate.py:46 exercises."""
     cfg = Cfg(block_size=128, n_layer=1, n_head=4, n_embd=256, vocab_size=512)
@@ -391,6 +427,6 @@ def gen_eos():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq", "hf_convert"]
+    which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq", "hf_convert", "meta_convert"]
     for w in which:
         globals()[f"gen_{w}"]()

@@ -90,3 +90,29 @@ def test_load_lit_checkpoint_into_model(tiny_config, tmp_path):
     CV.load_lit_checkpoint(model, tmp_path / "lit-llama.pth")
     np.testing.assert_array_equal(model.transformer.h[1].attn.c_attn.weight.detach().numpy(),
                                   LIT["transformer.h.1.attn.c_attn.weight"])
+
+
+# ------------------------------------------------------------------ Meta consolidated.*.pth
+MGOLD = np.load(Path(__file__).parent / "golden" / "meta_convert.npz")
+MPARTS = [{k.split("/", 1)[1]: torch.from_numpy(MGOLD[k]) for k in MGOLD.files if k.startswith(f"meta{r}/")}
+          for r in range(2)]
+MLIT = {k[4:]: MGOLD[k] for k in MGOLD.files if k.startswith("lit/")}
+
+
+def test_meta_conversion_matches_reference(tmp_path):
+    """Two model-parallel parts merged (sharded dims, c_attn regrouped to Q.. K.. V..) as the
+    reference's meta_weights_for_nano_model (convert_checkpoint.py:67-134)."""
+    ck = tmp_path / "llama" / "tinymeta"
+    ck.mkdir(parents=True)
+    (ck.parent / "tokenizer.model").write_bytes(b"placeholder")
+    for r, sd in enumerate(MPARTS):
+        torch.save(sd, ck / f"consolidated.{r:02d}.pth")
+    CV.meta_weights_for_nano_model(output_dir=tmp_path / "lit", checkpoint_dir=tmp_path / "llama",
+                                   model_size="tinymeta")
+    sd = torch.load(tmp_path / "lit" / "tinymeta" / "lit-llama.pth", map_location="cpu", weights_only=True)
+    assert set(sd) == set(MLIT)
+    for k, v in sd.items():
+        np.testing.assert_array_equal(v.numpy(), MLIT[k], err_msg=k)
+    with pytest.raises(RuntimeError, match="No checkpoints"):
+        CV.meta_weights_for_nano_model(output_dir=tmp_path / "lit", checkpoint_dir=tmp_path / "llama",
+                                       model_size="missing")
