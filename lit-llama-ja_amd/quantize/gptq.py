@@ -9,6 +9,15 @@ attention of a calibration window (prefill attention is SURVEY §8f row 3, not b
 are bf16 like the decode path (the reference's CPU runs calibrate in fp32)."""
 from __future__ import annotations
 
+import argparse
+import sys
+import time
+from pathlib import Path
+from typing import Optional
+
+if __name__ == "__main__":
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
 import torch
 import torch.nn.functional as F
 
@@ -72,3 +81,90 @@ def llama_blockwise_quantization(model, sample_inputs, working_device, *, bits=4
     handle.remove()
     model.lm_head, errors["lm_head"] = gq.quantize()
     return errors
+
+
+def get_sample_data(calibration_path=None) -> str:
+    """reference quantize/gptq.py:22-33. The reference downloads 1,000 random C4 documents; this
+    box has no network, so `calibration_path` (a UTF-8 text file) is the normal source and the
+    download is only attempted (as the reference does) when it is not given."""
+    if calibration_path is not None:
+        return Path(calibration_path).read_text(encoding="utf-8")
+    from datasets import load_dataset
+
+    traindata = load_dataset("allenai/c4", "allenai--c4",
+                             data_files={"train": "en/c4-train.00000-of-01024.json.gz"}, split="train")
+    return "\n".join(traindata[i]["text"] for i in torch.randperm(len(traindata))[:1000].tolist())
+
+
+def main(*, checkpoint_path: Path = Path("checkpoints/lit-llama/7B/lit-llama.pth"), output_path: Optional[Path] = None,
+         tokenizer_path: Path = Path("checkpoints/lit-llama/tokenizer.model"), n_samples: int = 128,
+         dtype: str = "float32", quantize: Optional[str] = None, calibration_path: Optional[Path] = None,
+         block_size: int = 2048) -> dict:
+    """reference quantize/gptq.py:150-237 (same arguments and checks; writes the quantized state
+    dict that generate.py --quantize gptq.int4 loads). Differences, all forced by the device path:
+    the whole model is loaded onto the GPU in bf16 (7B is 13.5 GB of 288 GB HBM, so the
+    reference's block-by-block CPU->GPU shuttling buys nothing; `dtype` is validated as in the
+    reference but the calibration runs in bf16, the decode kernels' type); the calibration text
+    comes from `calibration_path` (no network); `block_size` (the reference's fixed 2048) is an
+    argument so small models can be calibrated. Returns the per-Linear errors."""
+    from lit_llama import LLaMA, HFTokenizer
+    from lit_llama.utils import EmptyInitOnDevice, llama_model_lookup
+
+    assert checkpoint_path.is_file(), checkpoint_path
+    assert tokenizer_path.is_file(), tokenizer_path
+    if output_path is None:
+        output_path = checkpoint_path.parent / "llama-gptq.4bit.pth"
+    assert output_path.parent.is_dir() and (not output_path.exists() or output_path.is_file())
+    if not torch.cuda.is_available():
+        raise SystemExit("quantize/gptq.py runs on a ROCm GPU (MI355X) only")
+    dt = getattr(torch, dtype, None)
+    if not isinstance(dt, torch.dtype):
+        raise ValueError(f"{dtype} is not a valid dtype.")
+    if dt != torch.bfloat16:
+        print(f"note: calibrating in bfloat16 (requested {dtype})", file=sys.stderr)
+    if quantize == "gptq.int4":
+        bits = 4
+    elif quantize == "gptq.int8":
+        bits = 8
+    else:
+        raise RuntimeError(f"unknown/unsupported quantization mode {quantize}")
+
+    print("Loading model ...", file=sys.stderr)
+    t0 = time.time()
+    checkpoint = torch.load(checkpoint_path, map_location="cpu", mmap=True, weights_only=True)
+    with EmptyInitOnDevice(device=torch.device("cuda"), dtype=torch.bfloat16):
+        model = LLaMA.from_name(llama_model_lookup(checkpoint))
+    model.load_state_dict(checkpoint)
+    del checkpoint
+    print(f"Time to load model: {time.time() - t0:.02f} seconds.", file=sys.stderr)
+    model.eval()
+
+    tokenizer = HFTokenizer(tokenizer_path)
+    encoded_text = tokenizer.encode(get_sample_data(calibration_path), bos=True, eos=False)
+    encoded_text = encoded_text[: n_samples * block_size].reshape(n_samples, block_size)
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    errors = llama_blockwise_quantization(model, encoded_text, "cuda", bits=bits)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    print(f"\n\nTime for quantization: {t:.02f} sec total", file=sys.stderr)
+    print(f"Memory used: {torch.cuda.max_memory_reserved() / 1e9:.02f} GB", file=sys.stderr)
+    torch.save(model.state_dict(), output_path)
+    return errors
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser(description="GPTQ-quantize a lit-llama checkpoint (reference quantize/gptq.py).")
+    ap.add_argument("--checkpoint_path", type=Path, default=Path("checkpoints/lit-llama/7B/lit-llama.pth"))
+    ap.add_argument("--output_path", type=Path, default=None)
+    ap.add_argument("--tokenizer_path", type=Path, default=Path("checkpoints/lit-llama/tokenizer.model"))
+    ap.add_argument("--n_samples", type=int, default=128)
+    ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--quantize", default=None, choices=["gptq.int4", "gptq.int8"])
+    ap.add_argument("--calibration_path", type=Path, default=None)
+    ap.add_argument("--block_size", type=int, default=2048)
+    a = ap.parse_args()
+    main(checkpoint_path=a.checkpoint_path, output_path=a.output_path, tokenizer_path=a.tokenizer_path,
+         n_samples=a.n_samples, dtype=a.dtype, quantize=a.quantize, calibration_path=a.calibration_path,
+         block_size=a.block_size)

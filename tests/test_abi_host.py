@@ -202,3 +202,14 @@ def test_generate_cli_flags():
     for flag in ("--prompt", "--num_samples", "--max_new_tokens", "--top_k", "--temperature", "--checkpoint_path",
                  "--tokenizer_path", "--quantize"):
         assert flag in out.stdout
+
+
+def test_gptq_cli_flags():
+    """quantize/gptq.py keeps the reference CLI (quantize/gptq.py:150-158) plus the offline
+    calibration source."""
+    out = subprocess.run([sys.executable, str(REPO / "lit-llama-ja_amd" / "quantize" / "gptq.py"), "--help"],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    for flag in ("--checkpoint_path", "--output_path", "--tokenizer_path", "--n_samples", "--dtype", "--quantize",
+                 "--calibration_path", "--block_size"):
+        assert flag in out.stdout

@@ -176,3 +176,55 @@ def test_blockwise_driver_quantizes_like_reference(hip):
     e_ref = np.linalg.norm(ref_q - fp32) / np.linalg.norm(fp32)
     print("relative logit error vs the fp32 model: ours", e_ours, "reference GPTQ", e_ref)
     assert e_ours < 1.5 * e_ref + 2e-2, (e_ours, e_ref)
+
+
+@pytest.mark.gpu
+def test_gptq_cli_writes_a_checkpoint_generate_loads(hip, tmp_path):
+    """quantize/gptq.py main (reference quantize/gptq.py:150-237) end to end on a random 19M
+    checkpoint: tokenizer + calibration text -> llama_blockwise_quantization -> torch.save; the
+    written state dict loads strictly into an --quantize gptq.int4 model (the reference's
+    generate.py flow) whose logits stay near the bf16 model's and whose greedy decode runs."""
+    from tokenizers import Tokenizer as HFTok
+    from tokenizers.models import WordLevel
+    from tokenizers.pre_tokenizers import Whitespace
+    from oracle.weights import Cfg, make_params
+    from lit_llama import LLaMA
+    from lit_llama.utils import EmptyInitOnDevice
+    from quantize.gptq import main
+    import generate as G
+
+    cfg = Cfg(n_layer=6, n_head=8, n_embd=512, vocab_size=35000)  # llama_configs["19M"]
+    params = make_params(cfg, 11)
+    ck = tmp_path / "lit-llama.pth"
+    torch.save({k: torch.from_numpy(v) for k, v in params.items()}, ck)
+    words = [f"w{i}" for i in range(3, 3000)]
+    tok = HFTok(WordLevel({"<pad>": 0, "<s>": 1, "</s>": 2, **{w: i + 3 for i, w in enumerate(words)}},
+                          unk_token="<pad>"))
+    tok.pre_tokenizer = Whitespace()
+    tok.save(str(tmp_path / "tokenizer.json"))
+    rng = np.random.default_rng(5)
+    (tmp_path / "calib.txt").write_text(" ".join(rng.choice(words, 600)))
+    errs = main(checkpoint_path=ck, tokenizer_path=tmp_path / "tokenizer.json", n_samples=2, dtype="bfloat16",
+                quantize="gptq.int4", calibration_path=tmp_path / "calib.txt", block_size=256)
+    out = tmp_path / "llama-gptq.4bit.pth"
+    assert out.is_file() and len(errs) == 5 * cfg.n_layer + 1
+
+    sd = torch.load(out, map_location="cpu", weights_only=True)
+    with EmptyInitOnDevice(device=torch.device("cuda"), dtype=torch.bfloat16, quantization_mode="gptq.int4"):
+        qm = LLaMA.from_name("19M")
+    qm.load_state_dict(sd)  # strict: every key the quantized model expects, nothing else
+    with EmptyInitOnDevice(device=torch.device("cuda"), dtype=torch.bfloat16):
+        fm = LLaMA.from_name("19M")
+    fm.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    idx = torch.from_numpy(rng.integers(3, 3000, (1, 16))).cuda()
+    lq = qm.eval()(idx).float()[0, -1]
+    lf = fm.eval()(idx).float()[0, -1]
+    rel = float((lq - lf).norm() / lf.norm())
+    print("relative logit error of the CLI-quantized 19M model:", rel)
+    # sanity bound only: code parity is pinned by the tests above. Per-channel int4 on random
+    # weights costs ~0.27 relative logit error over 2 layers (reference's own run, int4_gptq
+    # fixture); over these 6 layers it compounds to ~0.55 (measured on MI355X).
+    assert rel < 0.75, rel
+    qm.reset_cache()
+    y = G.generate(qm, idx[0], 8, top_k=1)
+    assert y.shape[0] == 24
