@@ -93,6 +93,36 @@ def test_gptq_block_kernel_bitwise(hip, t):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N", [8192, 8273])
+def test_gptq_block_kernel_wide_bitwise(hip, N):
+    """Both launch shapes of llj_gptq_block (32 rows x 8 lanes for N <= 8192, 64 rows x 4 lanes
+    above; 8273 also leaves a ragged last workgroup): the fixture's rows tiled to N rows (rows are
+    independent), first block, bit for bit against the oracle's gptq_block of the original rows."""
+    W, X, H, bits, *_ = case(CASES[0])
+    from lit_llama import _hip
+    scale, zero = G.find_params_weight(W, bits)
+    Hinv, perm, dead = G.hinv_upper(H)
+    Wr = W.astype(np.float32).copy()
+    Wr[:, dead] = 0
+    Wr = Wr[:, perm]
+    n0, K = Wr.shape
+    Q1, E1, L1 = G.gptq_block(Wr[:, :128], Hinv[:128, :128], scale, zero, bits)
+    rep = lambda a: np.resize(a, (N,) + a.shape[1:])  # noqa: E731  (row r = original row r % n0)
+    wt = torch.from_numpy(np.ascontiguousarray(rep(Wr).T)).to(dev)
+    qt = torch.full((K, N), np.nan, dtype=torch.float32, device=dev)
+    err = torch.empty(128, N, dtype=torch.float32, device=dev)
+    loss = torch.zeros(N, dtype=torch.float32, device=dev)
+    sd = torch.from_numpy(rep(scale)).to(dev)
+    zd = torch.from_numpy(rep(zero)).to(dev)
+    _hip.call("llj_gptq_block", torch.from_numpy(Hinv).to(dev).data_ptr(), K, 0, wt.data_ptr(), N, sd.data_ptr(),
+              zd.data_ptr(), bits, qt.data_ptr(), err.data_ptr(), loss.data_ptr(), _st())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(qt[:128].cpu().numpy().T, rep(Q1))
+    np.testing.assert_array_equal(err.cpu().numpy().T, rep(E1))
+    np.testing.assert_allclose(loss.cpu().numpy(), rep(L1.sum(1)), rtol=1e-5)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bits", [4, 8])
 def test_colblock_pack_kernel_bitwise(hip, bits):
     from lit_llama import _hip
