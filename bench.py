@@ -10,8 +10,11 @@ ranks (B * K * world / max-over-ranks time of the K timed steps).
 
 Multi-GPU: replicas only (the path is not sharded; no collective on the data
 path). Every rank runs its own replica; the barrier and the max-over-ranks timing use
-torch.distributed (RCCL for GPUs). Launch: python -m torch.distributed.run --nproc-per-node N
-bench.py --gpus N.
+torch.distributed over gloo (host tensors; no RCCL communicator is created). Launch either
+with python -m torch.distributed.run --nproc-per-node N bench.py --gpus N, or plainly as
+bench.py --gpus N, which spawns the N replica processes itself (spawn_replicas).
+The C4 leg (`c4_13b`) runs LLaMA-13B gptq.int4 batch 1 on every replica (BASELINE configs[4]).
+The timed K steps are centred on position 80 where the cache allows (SURVEY §8d workload).
 
 Also reported, on the same JSON line:
   roofline      dominant kernel (rms_2 + c_fc1/c_fc2 int4 GEMV + silu*mul, 1 launch per
@@ -44,14 +47,44 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 # ----------------------------------------------------------------------------- distributed
 def dist_init():
+    """Process group from the torchrun-style environment. The replicas exchange nothing on the
+    data path, so the only collectives (the barrier around the timed region and the
+    max-over-ranks / sum-over-ranks of the result) run over gloo on host tensors: no RCCL
+    communicator is ever created (replicas only)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws > 1:
         import torch.distributed as dist
 
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        dist.init_process_group(backend=backend)
+        dist.init_process_group(backend="gloo")
         return dist.get_rank(), ws, int(os.environ.get("LOCAL_RANK", "0"))
     return 0, 1, 0
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_replicas(n: int, argv) -> int:
+    """`bench.py --gpus N` started without a launcher: start N child processes of this script
+    with the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), one per GPU
+    (LOCAL_RANK i -> cuda:i), BEFORE this process touches the GPU (it never does: only the
+    children initialise HIP), wait for all of them and return the worst exit code. Rank 0's
+    stdout carries the JSON line."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 def barrier(ws):
@@ -61,14 +94,14 @@ def barrier(ws):
         dist.barrier()
 
 
-def aggregate(local_seconds: float, local_tokens: int, ws: int, device=None):
-    """(max seconds over ranks, total tokens over ranks)."""
+def aggregate(local_seconds: float, local_tokens: int, ws: int):
+    """(max seconds over ranks, total tokens over ranks), over gloo on host tensors."""
     if ws == 1:
         return local_seconds, local_tokens
     import torch.distributed as dist
 
-    t = torch.tensor([local_seconds], dtype=torch.float64, device=device)
-    n = torch.tensor([float(local_tokens)], dtype=torch.float64, device=device)
+    t = torch.tensor([local_seconds], dtype=torch.float64)
+    n = torch.tensor([float(local_tokens)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.all_reduce(n, op=dist.ReduceOp.SUM)
     return float(t.item()), int(n.item())
@@ -133,11 +166,23 @@ def step_bytes(model, B: int, pos_mean: float) -> float:
 
 
 # ----------------------------------------------------------------------------- timing
+POS_CENTER = 80  # a 128-token generation after a 16-token prompt has mean position 80
+
+
+def untimed_steps(prompt_len: int, S: int, warmup: int, steps: int) -> int:
+    """Decode steps before the timed region: at least `warmup`, and enough that the K timed
+    steps are centred on position POS_CENTER (the §8d workload) when the cache allows it."""
+    centred = POS_CENTER - prompt_len - steps // 2
+    room = S - prompt_len - 1 - steps  # the timed steps must stay inside the S-slot cache
+    return max(warmup, min(centred, room))
+
+
 def time_decode(model, B, prompt_len, S, warmup, steps, ws, seed=1234):
     from lit_llama.engine import DecodeSession
 
     cfg = model.config
-    total = prompt_len + 1 + warmup + steps
+    skip = untimed_steps(prompt_len, S, warmup, steps)
+    total = prompt_len + 1 + skip + steps
     assert total <= cfg.block_size, "positions beyond block_size"
     g = torch.Generator().manual_seed(seed)
     prompts = torch.randint(3, cfg.vocab_size, (B, prompt_len), generator=g).cuda()
@@ -149,8 +194,8 @@ def time_decode(model, B, prompt_len, S, warmup, steps, ws, seed=1234):
     torch.cuda.synchronize()
     t_prefill = time.perf_counter() - t0
     sess.capture()
-    if warmup:
-        sess.decode(warmup)
+    if skip:
+        sess.decode(skip)
     barrier(ws)
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -162,9 +207,25 @@ def time_decode(model, B, prompt_len, S, warmup, steps, ws, seed=1234):
     wall = time.perf_counter() - t0
     barrier(ws)
     gpu_s = ev0.elapsed_time(ev1) / 1e3
-    pos_mean = prompt_len + warmup + (steps - 1) / 2.0
+    # the step that reads position p writes slot p and attends p + 1 keys; the first timed
+    # step runs at position prompt_len + skip
+    pos_mean = prompt_len + skip + (steps - 1) / 2.0
     return dict(seconds=max(wall, gpu_s), gpu_seconds=gpu_s, wall_seconds=wall, t_prefill=t_prefill,
                 pos_mean=pos_mean, tokens=B * steps, session=sess)
+
+
+def time_stub(steps, warmup, ws, step_s=1e-3):
+    """--stub: the replica / timing / aggregation plumbing without a GPU (CPU rehearsal of
+    `bench.py --gpus N`); one 'step' is a sleep. Never a measurement."""
+    for _ in range(warmup):
+        time.sleep(step_s)
+    barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        time.sleep(step_s)
+    wall = time.perf_counter() - t0
+    barrier(ws)
+    return dict(seconds=wall, tokens=steps)
 
 
 def time_dominant_kernel(model, B, iters=10):
@@ -283,6 +344,22 @@ def cpu_baseline(model, budget_s: float = 20.0):
 
 
 # ----------------------------------------------------------------------------- main
+def c4_leg(args, ws):
+    """C4 (BASELINE.json configs[4]): LLaMA-13B gptq.int4, batch 1, one replica per GPU; every
+    rank decodes its own sequence and `value` sums over the ranks."""
+    m13 = build_model("13B", "gptq.int4")
+    r = time_decode(m13, 1, args.prompt_len, args.max_seq_length, args.warmup, args.steps, ws)
+    t, tok = aggregate(r["seconds"], r["tokens"], ws)
+    sb = step_bytes(m13, 1, r["pos_mean"])
+    out = {"workload": "LLaMA-13B --quantize gptq.int4 greedy decode, batch 1 per replica",
+           "value": round(tok / t, 2), "unit": "tokens/s", "n_replicas": ws,
+           "ms_per_step": round(t / args.steps * 1e3, 4),
+           "step_roofline_frac": round(sb / (r["seconds"] / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}
+    del r["session"], m13
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -295,13 +372,34 @@ def main():
     ap.add_argument("--max-seq-length", type=int, default=144)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bs8", action="store_true")
+    ap.add_argument("--no-c4", action="store_true", help="skip the LLaMA-13B replica leg (C4)")
     ap.add_argument("--only-dominant", action="store_true",
                     help="profiling aid: only the dominant-kernel loop (for the PMC traffic passes)")
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU rehearsal of the replica launch / timing / aggregation (no GPU, no measurement)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start one replica process per GPU before anything touches the GPU
+        sys.exit(spawn_replicas(args.gpus, sys.argv[1:]))
     rank, ws, local_rank = dist_init()
     if ws != args.gpus:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {ws}", file=sys.stderr)
+
+    if args.stub:
+        r = time_stub(args.steps, args.warmup, ws)
+        t_max, tokens = aggregate(r["seconds"], r["tokens"], ws)
+        if rank == 0:
+            print(json.dumps({"metric": "stub (plumbing rehearsal, not a measurement)", "value": tokens / t_max,
+                              "unit": "steps/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+                              "ms_per_step": t_max / args.steps * 1e3, "stub": True,
+                              "config": {"parallelism": f"replicas x{ws}"}}), flush=True)
+        if ws > 1:
+            import torch.distributed as dist
+
+            dist.destroy_process_group()
+        return
+
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     mode = None if args.quantize == "none" else args.quantize
@@ -313,11 +411,14 @@ def main():
         print(json.dumps({"dominant_avg_us": round(k_s * 1e6, 2), "bytes_per_launch": k_bytes}), flush=True)
         return
     r = time_decode(model, args.batch, args.prompt_len, S, args.warmup, args.steps, ws)
-    t_max, tokens = aggregate(r["seconds"], r["tokens"], ws, dev)
+    t_max, tokens = aggregate(r["seconds"], r["tokens"], ws)
     value = tokens / t_max
     ms_per_step = t_max / args.steps * 1e3
     sb = step_bytes(model, args.batch, r["pos_mean"])
     step_gbs = sb / (r["seconds"] / args.steps) / 1e9
+    mem = {"max_reserved_gb": round(torch.cuda.max_memory_reserved() / 1e9, 3),
+           "max_allocated_gb": round(torch.cuda.max_memory_allocated() / 1e9, 3),
+           "reference_gb": "~5 (README.md:108, 7B gptq.int4)"}
 
     k_s, k_bytes = time_dominant_kernel(model, args.batch)
     k_gbs = k_bytes / k_s / 1e9
@@ -327,7 +428,7 @@ def main():
     if not args.no_bs8 and args.batch != 8:
         del r["session"]
         r8 = time_decode(model, 8, args.prompt_len, S, args.warmup, args.steps, ws)
-        t8, tok8 = aggregate(r8["seconds"], r8["tokens"], ws, dev)
+        t8, tok8 = aggregate(r8["seconds"], r8["tokens"], ws)
         sb8 = step_bytes(model, 8, r8["pos_mean"])
         bs8 = {"value": tok8 / t8, "unit": "tokens/s", "ms_per_step": t8 / args.steps * 1e3,
                "step_roofline_frac": sb8 / (r8["seconds"] / args.steps) / 1e9 / HBM_PEAK_GBS}
@@ -337,8 +438,15 @@ def main():
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and mode == "gptq.int4":
         cpu = cpu_baseline(model)
 
+    c4 = None
+    if not args.no_c4 and args.model == "7B" and mode == "gptq.int4":
+        del model
+        torch.cuda.empty_cache()
+        c4 = c4_leg(args, ws)
+
     if rank == 0:
         name = {"gptq.int4": "gptq.int4", "llm.int8": "llm.int8", "none": "bf16"}[args.quantize]
+        head7 = args.batch == 1 and mode == "gptq.int4" and args.model == "7B"
         line = {
             "metric": f"decode tokens/sec LLaMA-{args.model} {name} bs={args.batch}, 1xMI355X per replica",
             "value": round(value, 2),
@@ -357,18 +465,21 @@ def main():
             "config": {"workload": f"LLaMA-{args.model} --quantize {args.quantize} greedy decode, batch {args.batch}, "
                                    f"prompt {args.prompt_len}, max_seq_length {S}",
                        "batch_per_gpu": args.batch, "prompt_len": args.prompt_len, "max_seq_length": S,
+                       "timed_positions_mean": r["pos_mean"],
                        "parallelism": f"replicas x{ws} (no collective on the data path)"},
             "roofline": {"bound": "hbm", "achieved": round(k_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(k_gbs / HBM_PEAK_GBS, 4),
-                         "traffic": round(pmc[0]) if pmc and args.batch == 1 and mode == "gptq.int4" and args.model == "7B" else None,
+                         "traffic": round(pmc[0]) if pmc and head7 else None,
                          "traffic_source": (f"profiles/{pmc[1]} (PMC, rocprof avg {pmc[2]:.2f} us)"
-                                            if pmc and args.batch == 1 and mode == "gptq.int4" and args.model == "7B" else None),
+                                            if pmc and head7 else None),
                          "kernel": "gemv_kernel<W4,NORM,SWIGLU> (rms_2 + c_fc1/c_fc2 + silu*mul)",
                          "bytes_per_launch": k_bytes, "avg_launch_us": round(k_s * 1e6, 2)},
             "step_roofline": {"bytes_per_step": sb, "achieved": round(step_gbs, 1), "frac": round(step_gbs / HBM_PEAK_GBS, 4)},
             "reference_formula_tokens_per_s": round(r["tokens"] / (r["seconds"] + r["t_prefill"]), 2),
+            "memory": mem,
             "cpu_baseline": cpu,
             "bs8": bs8,
+            "c4_13b": c4,
         }
         print(json.dumps(line), flush=True)
     if ws > 1:

@@ -55,3 +55,21 @@ def test_single_process_is_identity():
 
     assert bench.aggregate(2.0, 7, 1) == (2.0, 7)
     assert not torch.distributed.is_initialized()
+
+
+def test_bench_spawns_its_own_replicas():
+    """`bench.py --gpus 2` started WITHOUT a launcher spawns one replica process per GPU with
+    the torchrun environment (the driver's SCALE runs and C4 rely on it); --stub replaces the
+    GPU work so the launch / barrier / aggregation path runs here on CPU with gloo."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--stub", "--steps", "3",
+                          "--warmup", "1"], env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 alone prints
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["stub"] is True and line["steps"] == 3
+    assert line["value"] > 0
