@@ -67,11 +67,6 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
  * (Block.forward, lit_llama/model.py:162-175, split at its four Linear boundaries).
  * norm_w == NULL means the input is used as is (no fused RMSNorm); int8 (wfmt 2) takes
  * already-normalised input (its statistics are computed on it).
- * RMSNorm row statistics (optional, decode path, <= 8 rows): fp64 partial sums of
- * bf16(x^2) laid out [part][8 rows]. llj_embedding writes part 0 (whole rows);
- * llj_linear_resid writes part n/16 for its 16-column tile n (N/16 parts); the norm-fused
- * ops read `nstat_parts` parts (1 after the embedding, n_embd/16 after a residual GEMV)
- * instead of re-reducing the row in every workgroup. NULL = off (row reduced in-kernel).
  * rowsum (int4 only, optional): fp32 sum over k of each row of A exactly as the MFMA reads it
  * (i.e. after the RMSNorm when norm_w is given), from llj_rmsnorm_rows; used for the int4
  * offset term instead of a per-workgroup reduction. NULL = reduced in-kernel. */
@@ -84,16 +79,8 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
  * Handles rows [row0, row0 + rows) of the B*T rows; rows <= 8 (RMSNorm staged in LDS). */
 int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                       void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
-                      int C, int n_head, int S, int row0, int rows, const void* i8ws, const double* nstat_in,
-                      int nstat_parts, const float* rowsum, void* stream);
-
-/* llj_norm_qkv_rope for one decode row (M = B = 1, T = 1) that also computes the attention of
- * every head (as llj_attention, model.py:237) into y (1, C): the workgroup completing a head's
- * last q / k / v tile runs it (per-head arrival counters att_ctr: n_head words, zero before the
- * first call and left zero). Bitwise equal to llj_norm_qkv_rope + llj_attention. wfmt 0, 1, 3. */
-int llj_norm_qkv_rope_attn(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
-                           void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int C,
-                           int n_head, int S, void* y, unsigned* att_ctr, void* stream);
+                      int C, int n_head, int S, int row0, int rows, const void* i8ws, const float* rowsum,
+                      void* stream);
 
 /* Causal attention of q (B*T, C) over the cache slots each query may see
  * (F.scaled_dot_product_attention with the tril mask rows, model.py:101-104, 237):
@@ -109,73 +96,19 @@ size_t llj_attention_ws_bytes(int rows, int n_head, int head_size, int nsplit);
 int llj_attention_split(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
                         int n_head, int head_size, int S, int nsplit, void* part_ws, void* stream);
 
-/* y = attention (as llj_attention, T = 1 decode rows, M = B <= 8) and then
- * x[M, C] += y . W_proj^T (as llj_linear_resid, attn.c_proj + residual, model.py:172,239-242),
- * in ONE launch: the c_proj workgroups load their weights while the attention runs and wait
- * for it on a completion counter. counters: 32 words the caller zeroes before every call;
- * err: set non-zero if the wait timed out (never expected). wfmt 0, 1 or 3. Bitwise equal
- * to llj_attention + llj_linear_resid. */
-int llj_attn_resid(int wfmt, const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int M,
-                   int n_head, int S, const void* W, const void* sz, void* x, int C, double* nstat_out,
-                   unsigned* counters, unsigned* err, void* stream);
-
 /* x[M, N] += A[M, K] . W^T (attn.c_proj / mlp.c_proj + residual add, model.py:172-173). */
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
-                     int N, int K, const void* i8ws, int i8_row0, double* nstat_out, void* stream);
-
-/* The same, then the next RMSNorm of the updated rows (rms_2 after c_proj, the next layer's
- * rms_1 / ln_f after mlp.c_proj; model.py:173, 171, 125): xn[M, N] = RMSNorm(x) with scale
- * norm_w, rowsum[m] = fp32 sum of the normalized row (or NULL). Computed once, by the last
- * workgroup to finish (agent release/acquire + the completion `counter`, one word the caller
- * zeroes once; the kernel leaves it 0). M <= 8, wfmt 0 or 1. Batched decode (M >= 2) uses it
- * instead of a separate llj_rmsnorm_rows launch. */
-int llj_linear_resid_norm(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
-                          int N, int K, const void* norm_w, float eps, void* xn, float* rowsum, unsigned* counter,
-                          void* stream);
+                     int N, int K, const void* i8ws, int i8_row0, void* stream);
 
 /* h[M, H] = silu(rms_2(x) . W1^T) * (rms_2(x) . W2^T)  (model.py:173, 258). M <= 8. */
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,
-                    const double* nstat_in, int nstat_parts, const float* rowsum, void* stream);
+                    const float* rowsum, void* stream);
 
 /* out[M, N] = RMSNorm(x) . W^T  (ln_f + lm_head, model.py:125-127). M <= 8. */
 int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
-                    void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const double* nstat_in,
-                    int nstat_parts, const float* rowsum, void* stream);
-
-/* ---------------------------------------------------------------- one decode layer, one launch
- * Block.forward (model.py:162-175) for a decode step (T = 1, M = B <= 8 rows) with int4 W4P
- * (wfmt 0), bf16 (wfmt 1) or int8 W8P (wfmt 3, always as separate launches) linears: rms_1 + c_attn + RoPE + KV write -> attention -> c_proj +
- * residual -> rms_2 + c_fc1/c_fc2 + silu*mul -> mlp.c_proj + residual. Same math and results
- * as the five entry points above; when the shapes allow, all five run in ONE launch whose
- * consumer workgroups start streaming their weights before their producer op has finished
- * (completion counters, sc1 write-through hand-offs), otherwise as separate launches.
- * counters: 128 words the caller zeroes before every call; err: set non-zero if a
- * dependency wait timed out (never expected; a diagnostic, results then invalid). */
-typedef struct llj_layer {
-  int wfmt, M, C, H, n_head, S;
-  void* x;                       /* (M, C) residual stream, updated in place */
-  const void* rms1;
-  const void* rms2;
-  float eps;
-  const void* w_qkv;  const void* sz_qkv;
-  const void* w_proj; const void* sz_proj;
-  const void* w_fc1;  const void* sz_fc1;
-  const void* w_fc2;  const void* sz_fc2;
-  const void* w_down; const void* sz_down;
-  void* q;                       /* (M, C) scratch */
-  void* kcache; void* vcache;    /* (M, n_head, S, C/n_head), ring slot pos % S */
-  const float* rope;
-  const int* pos;                /* device position of the decode token */
-  void* y;                       /* (M, C) attention output scratch */
-  void* h;                       /* (M, H) MLP hidden scratch */
-  const double* nst_in; int nst_in_parts;  /* RMSNorm statistics of x for rms_1 (or NULL) */
-  double* nst_mid;               /* written by c_proj, read by rms_2: C/16 parts x 8 rows */
-  double* nst_out;               /* written by mlp.c_proj for the next layer's rms_1 */
-  unsigned* counters;
-  unsigned* err;
-} llj_layer;
-int llj_decode_layer(const llj_layer* layer, void* stream);
+                    void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const float* rowsum,
+                    void* stream);
 
 /* ---------------------------------------------------------------- LLM.int8() */
 /* Bytes of the activation-statistics workspace for an (M, K) activation (host function). */
@@ -207,10 +140,8 @@ int llj_colblock_pack(const float* qt, int K, int N, const float* scale, const f
 
 /* ---------------------------------------------------------------- small ops */
 /* out[m] = wte[idx[m]] (model.py:110); if pos_inc != NULL, *pos_inc += 1 (device-side
- * decode position, so a captured decode step advances itself); nstat_out: per-row sum of
- * bf16(x^2) (see "RMSNorm row statistics" above) or NULL. */
-int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, double* nstat_out,
-                  void* stream);
+ * decode position, so a captured decode step advances itself). */
+int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, void* stream);
 
 /* Standalone RMSNorm (model.py:276-283) for rows the fused prologue does not take. */
 int llj_rmsnorm(const void* x, const void* w, float eps, void* y, int M, int C, void* stream);

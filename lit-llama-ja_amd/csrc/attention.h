@@ -1,5 +1,4 @@
-// Decode attention over the KV cache (device code shared by the standalone launch in ops.hip
-// and the chained decode-layer launch in gemv.hip).
+// Decode attention over the KV cache (device code of the launches in ops.hip).
 //
 // Query rows m = b*T + t against cache slots of sequence b. Reference semantics
 // (model.py:101-104, 218-237): the query at absolute position p attends the slots holding
@@ -10,7 +9,6 @@
 // pass has NG*U keys in flight, all loads of a pass issued before any use. Per-group online
 // softmax; the groups of a wave merge through lane swaps, the waves through LDS.
 #pragma once
-#include "chain.h"
 #include "common.h"
 
 namespace llj {
@@ -36,17 +34,14 @@ __device__ __forceinline__ void softmax_merge(float& mx, float& l, float* o, con
   for (int i = 0; i < DPL; ++i) o[i] = o_lo[i] * f_lo + o_hi[i] * f_hi;
 }
 
-// CH: chained launch — wait for the QKV op, then read q and the cache with sc1 loads and
-// store y with sc1 stores (chain.h protocol).
-// SIG: signal a consumer op of the same launch (sc1 y stores, drain, count done); CH implies it.
 // PART: split-K over the keys (long contexts): this block takes key range `split` of `nsplit`
 // equal ranges (>= one pass of NG * U keys each) of the valid keys and writes its unnormalized partial (outputs, running max,
 // sum) to part[((m * nh + h) * nsplit + split) * (HS + 2)]; attention_combine_kernel merges.
-template <int HS, int U, int NTH, bool CH, bool SIG = CH, bool PART = false>
+template <int HS, int U, int NTH, bool PART = false>
 __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                const int* __restrict__ pos, int T, int S, int nh, float scale_log2,
-                                               int h, int m, float* lds, const ChainCtl& cc, int nsplit = 1,
+                                               int h, int m, float* lds, int nsplit = 1,
                                                int split = 0, float* __restrict__ part = nullptr) {
   constexpr int DPL = HS / 16;
   constexpr int NG = NTH / 16;
@@ -55,8 +50,6 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   float* s_l = s_m + NWV;               // [NWV]
   float* s_o = s_l + NWV;               // [NWV][HS]
   LLJ_STAMP(0);
-  if constexpr (CH) chain_wait(cc);
-  LLJ_STAMP(1);
   const int b = m / T, t = m % T;
   const int ps = pos[t];
   const int nvalid = ps < S ? ps + 1 : S;
@@ -74,9 +67,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   {
     const size_t qo = (size_t)m * C + h * HS + sub * DPL;
     if constexpr (DPL == 8) {
-      uint4 a;
-      if constexpr (CH) a = __builtin_bit_cast(uint4, ld16_sc1(q, (unsigned)(qo * 2)));
-      else a = *reinterpret_cast<const uint4*>(q + qo);
+      const uint4 a = *reinterpret_cast<const uint4*>(q + qo);
       const uint32_t w[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -84,9 +75,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
         qf[2 * i + 1] = bfhi(w[i]) * scale_log2;
       }
     } else {
-      uint2 a;
-      if constexpr (CH) a = ld8_sc1(q, (unsigned)(qo * 2));
-      else a = *reinterpret_cast<const uint2*>(q + qo);
+      const uint2 a = *reinterpret_cast<const uint2*>(q + qo);
       qf[0] = bflo(a.x) * scale_log2;
       qf[1] = bfhi(a.x) * scale_log2;
       qf[2] = bflo(a.y) * scale_log2;
@@ -105,25 +94,13 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
       const int j = j0 + NG * u < jend ? j0 + NG * u : j0;
       const size_t eo = base + (size_t)j * HS;
       if constexpr (DPL == 8) {
-        uint4 a, c;
-        if constexpr (CH) {
-          a = __builtin_bit_cast(uint4, ld16_sc1(kc, (unsigned)(eo * 2)));
-          c = __builtin_bit_cast(uint4, ld16_sc1(vc, (unsigned)(eo * 2)));
-        } else {
-          a = *reinterpret_cast<const uint4*>(kc + eo);
-          c = *reinterpret_cast<const uint4*>(vc + eo);
-        }
+        const uint4 a = *reinterpret_cast<const uint4*>(kc + eo);
+        const uint4 c = *reinterpret_cast<const uint4*>(vc + eo);
         kw[u][0] = a.x; kw[u][1] = a.y; kw[u][2] = a.z; kw[u][3] = a.w;
         vw[u][0] = c.x; vw[u][1] = c.y; vw[u][2] = c.z; vw[u][3] = c.w;
       } else {
-        uint2 a, c;
-        if constexpr (CH) {
-          a = ld8_sc1(kc, (unsigned)(eo * 2));
-          c = ld8_sc1(vc, (unsigned)(eo * 2));
-        } else {
-          a = *reinterpret_cast<const uint2*>(kc + eo);
-          c = *reinterpret_cast<const uint2*>(vc + eo);
-        }
+        const uint2 a = *reinterpret_cast<const uint2*>(kc + eo);
+        const uint2 c = *reinterpret_cast<const uint2*>(vc + eo);
         kw[u][0] = a.x; kw[u][1] = a.y;
         vw[u][0] = c.x; vw[u][1] = c.y;
       }
@@ -201,15 +178,8 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
     const uint32_t pr = lane_xor1(ob);
     if (!(d & 1)) {
       const size_t eo = (size_t)m * C + h * HS + d;
-      if constexpr (SIG) st4_sc1(y, (unsigned)(eo * 2), ob | (pr << 16));
-      else *reinterpret_cast<uint32_t*>(y + eo) = ob | (pr << 16);
+      *reinterpret_cast<uint32_t*>(y + eo) = ob | (pr << 16);
     }
-  }
-  if constexpr (SIG) {
-    // every storing wave drains; the workgroup counts done once all have (LDS barrier)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) chain_count_done(cc);
   }
   LLJ_STAMP(5);
 }

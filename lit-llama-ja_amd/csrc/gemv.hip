@@ -1,6 +1,5 @@
 // C-ABI entry points of the weight-streaming GEMV family (device code: gemv_impl.h; the
-// per-format instantiations: gemv_w4.hip, gemv_bf16.hip, gemv_w8.hip, gemv_i8.hip; the fused
-// multi-op launches: gemv_fused.hip).
+// per-format instantiations: gemv_w4.hip, gemv_bf16.hip, gemv_w8.hip, gemv_i8.hip).
 #include "gemv_impl.h"
 
 namespace llj {
@@ -53,13 +52,10 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
 
 // out[M,N] = RMSNorm(x)[M,K] . W^T  (ln_f + lm_head, model.py:125-127); norm_w NULL = no norm.
 int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
-                    void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const double* nstat_in,
-                    int nstat_parts, const float* rowsum, void* stream) {
+                    void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const float* rowsum,
+                    void* stream) {
   GemvParams p{};
   p.rowsum = rowsum;
-  if (nstat_in && (M > 8 || nstat_parts < 1)) return LLJ_EINVAL;
-  p.nst_in = nstat_in;
-  p.nst_parts = nstat_parts;
   p.A = (const bf16_t*)x; p.lda = K; p.norm_w = (const bf16_t*)norm_w; p.eps = eps; p.M = M; p.N = N; p.K = K;
   p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)out; p.ldc = ldo;
   p.i8ws = i8ws; p.m0 = i8_row0;
@@ -67,21 +63,9 @@ int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, cons
 }
 
 // x[M,N] += A[M,K] . W^T, bf16 residual add (attn.c_proj / mlp.c_proj + model.py:172-173).
-int llj_linear_resid_norm(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
-                          int N, int K, const void* norm_w, float eps, void* xn, float* rowsum, unsigned* counter,
-                          void* stream) {
-  GemvParams p{};
-  if (M > 8 || !norm_w || !xn || !counter || N % 8) return LLJ_EINVAL;
-  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K;
-  p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)x; p.ldc = ldx;
-  p.nn_w = (const bf16_t*)norm_w; p.nn_eps = eps; p.nn_out = (bf16_t*)xn; p.nn_rs = rowsum; p.nn_ctr = counter;
-  return run<EP_RESID>(wfmt, p, stream);
-}
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
-                     int N, int K, const void* i8ws, int i8_row0, double* nstat_out, void* stream) {
+                     int N, int K, const void* i8ws, int i8_row0, void* stream) {
   GemvParams p{};
-  if (nstat_out && M > 8) return LLJ_EINVAL;
-  p.nst_out = nstat_out;
   p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K;
   p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)x; p.ldc = ldx;
   p.i8ws = i8ws; p.m0 = i8_row0;
@@ -91,12 +75,9 @@ int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void
 // h[M,H] = silu(RMSNorm(x) . W1^T) * (RMSNorm(x) . W2^T)  (rms_2 + model.py:258).
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,
-                    const double* nstat_in, int nstat_parts, const float* rowsum, void* stream) {
+                    const float* rowsum, void* stream) {
   GemvParams p{};
   p.rowsum = rowsum;
-  if (nstat_in && (M > 8 || nstat_parts < 1)) return LLJ_EINVAL;
-  p.nst_in = nstat_in;
-  p.nst_parts = nstat_parts;
   p.A = (const bf16_t*)x; p.lda = K; p.norm_w = (const bf16_t*)norm_w; p.eps = eps; p.M = M; p.N = H; p.K = K;
   p.W = W1; p.W2 = W2; p.sz = (const float2*)sz1; p.sz2 = (const float2*)sz2; p.C = (bf16_t*)h; p.ldc = H;
   p.i8ws = i8ws; p.m0 = i8_row0;
@@ -108,13 +89,10 @@ int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, cons
 // q_out (B*T, C); caches (B, n_head, S, hs).
 int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                       void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
-                      int C, int n_head, int S, int row0, int rows, const void* i8ws, const double* nstat_in,
-                      int nstat_parts, const float* rowsum, void* stream) {
+                      int C, int n_head, int S, int row0, int rows, const void* i8ws, const float* rowsum,
+                      void* stream) {
   GemvParams p{};
   p.rowsum = rowsum ? rowsum + row0 : nullptr;
-  if (nstat_in && (row0 + rows > 8 || nstat_parts < 1)) return LLJ_EINVAL;
-  p.nst_in = nstat_in ? nstat_in + row0 : nullptr;
-  p.nst_parts = nstat_parts;
   if (row0 < 0 || rows < 1 || row0 + rows > B * T || n_head < 1 || C % n_head || S < 1) return LLJ_EINVAL;
   p.A = (const bf16_t*)x + (size_t)row0 * C; p.lda = C; p.norm_w = (const bf16_t*)norm_w; p.eps = eps;
   p.M = rows; p.m0 = row0; p.N = 3 * C; p.K = C;
@@ -122,26 +100,6 @@ int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, co
   p.vcache = (bf16_t*)vcache; p.rope = rope; p.pos = pos; p.n_head = n_head; p.head_size = C / n_head;
   p.S = S; p.T = T; p.i8ws = i8ws;
   if (p.head_size < 2 || (p.head_size & (p.head_size - 1)) || rows > 8) return LLJ_EINVAL;  // power of two
-  return run<EP_QKV>(wfmt, p, stream);
-}
-
-// The same for one decode row (M == 1, T == 1), with the attention of every head computed in
-// the launch (GemvParams::att_ctr): y (1, C) = attention(q, caches) as llj_attention.
-// att_ctr: n_head words, zero before the first call, left zero by every call.
-int llj_norm_qkv_rope_attn(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
-                           void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int C,
-                           int n_head, int S, void* y, unsigned* att_ctr, void* stream) {
-  if (!y || !att_ctr || !norm_w || n_head < 1 || C % n_head || S < 1 || wfmt == WF_I8) return LLJ_EINVAL;
-  const int hs = C / n_head;
-  if (hs != 64 && hs != 128) return LLJ_EINVAL;
-  GemvParams p{};
-  p.A = (const bf16_t*)x; p.lda = C; p.norm_w = (const bf16_t*)norm_w; p.eps = eps;
-  p.M = 1; p.m0 = 0; p.N = 3 * C; p.K = C;
-  p.W = W; p.sz = (const float2*)sz; p.q_out = (bf16_t*)q_out; p.kcache = (bf16_t*)kcache;
-  p.vcache = (bf16_t*)vcache; p.rope = rope; p.pos = pos; p.n_head = n_head; p.head_size = hs;
-  p.S = S; p.T = 1;
-  p.att_ctr = att_ctr; p.att_y = (bf16_t*)y; p.att_sl2 = 1.4426950408889634f / sqrtf((float)hs);
-  if (check_shape(wfmt, p) || pick_am(wfmt, p) != AM_NORM) return LLJ_EINVAL;  // 4-wave norm-fused form
   return run<EP_QKV>(wfmt, p, stream);
 }
 

@@ -37,7 +37,6 @@
 #include <algorithm>
 
 #include "common.h"
-#include "chain.h"
 #include "i8ws.h"
 #include "attention.h"
 #include "lit_llama_amd.h"
@@ -72,31 +71,9 @@ struct GemvParams {
   int n_head, head_size, S, T;
   int m0;  // global row index of local row 0 (QKV row chunks; int8 statistics rows)
   const void* i8ws;
-  // RMSNorm row statistics, sum_k bf16(x[m,k]^2), produced once instead of re-reduced by
-  // every norm-fused workgroup: partial sums in fp64 laid out [part][8 rows] (M <= 8).
-  // EP_RESID writes one part per workgroup (its 16 columns, plain stores: no atomics, so
-  // no same-address contention and a deterministic order); AM_NORM sums nst_parts parts.
-  const double* nst_in;
-  int nst_parts;
-  double* nst_out;
   // int4: sum_k A[m,k] of this call's rows as the MFMA sees them (pre-normalized rows,
   // llj_rmsnorm_rows); nullptr = computed in the prologue
   const float* rowsum;
-  // EP_RESID: RMSNorm of the updated residual rows, computed once by the LAST workgroup to
-  // finish (completion counter nn_ctr; it resets the counter): xn = RMSNorm(x) with scale
-  // nn_w / eps nn_eps, nn_rs[m] = fp32 sum of the normalized bf16 row. nullptr = off.
-  const bf16_t* nn_w;
-  float nn_eps;
-  bf16_t* nn_out;
-  float* nn_rs;
-  unsigned* nn_ctr;
-  // EP_QKV, one decode row (M == 1, T == 1): the attention of each head is computed in this
-  // launch by the workgroup that completes the head's last q / k / v tile (per-head arrival
-  // counters att_ctr[n_head], zero on entry, left zero; q / k / v stored write-through), into
-  // att_y (1, n_embd). nullptr = off (llj_attention runs as its own launch).
-  unsigned* att_ctr;
-  bf16_t* att_y;
-  float att_sl2;
 };
 
 // ------------------------------------------------------------------------------------
@@ -125,25 +102,6 @@ __device__ void stage_a(const GemvParams& p, bf16_t* As, int a_stride, float* re
   constexpr int NT = NW * 64;
   const int K = p.K, M = p.M;
   const int nvec = K >> 3;
-  if (NORM && p.nst_in) {  // statistics precomputed by the producer: one pass
-    const int lane = tid & 63, wave = tid >> 6;
-    for (int m = wave; m < M; m += NW) {
-      double s = 0.0;
-      for (int q = lane; q < p.nst_parts; q += 64) s += p.nst_in[q * 8 + m];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-      if (lane == 0) red[m] = rms_rstd((float)(s / (double)K), p.eps);
-    }
-    __syncthreads();
-    const uint4* g4 = reinterpret_cast<const uint4*>(p.norm_w);
-    for (int m = 0; m < M; ++m) {
-      const float r = red[m];
-      const uint4* src = reinterpret_cast<const uint4*>(p.A + (size_t)m * p.lda);
-      uint4* dst = reinterpret_cast<uint4*>(As + (size_t)m * a_stride);
-      for (int v = tid; v < nvec; v += NT) dst[v] = norm8(src[v], g4[v], r);
-    }
-    return;
-  }
   float ss[8];
 #pragma unroll
   for (int m = 0; m < 8; ++m) ss[m] = 0.f;
@@ -297,10 +255,6 @@ __device__ __forceinline__ float out_value(float y, float y2) {
 }
 
 
-#ifndef LLJ_CH_PLAIN_A
-#define LLJ_CH_PLAIN_A 0  // experiment only: chained consumers read A with plain loads
-#endif
-
 template <int V>
 struct IC {
   static constexpr int value = V;
@@ -312,102 +266,14 @@ struct IC {
 // weight chunks' HBM latency, and the LDS image is written while the weights are in flight.
 // MB = row class of the instantiation (1: M == 1; 8: M <= 8); register budget per lane:
 //   XR 16-byte activation registers (MB 1: one row of K <= 8*XR*NT; MB 8: RS = 2 per row for
-//   M <= 8, K <= 16*NT, or RS = 4 for M <= 4), GR norm-weight registers, ST fp64 partials.
+//   M <= 8, K <= 16*NT, or RS = 4 for M <= 4), GR norm-weight registers.
 template <int MB, bool NORM>
 struct APre {
   static constexpr int XR = MB == 1 ? (NORM ? 4 : 8) : 16;
   static constexpr int GR = NORM ? 4 : 1;
-  static constexpr int SM = MB == 1 ? 1 : 8;  // statistics rows interleaved over threads
-  static constexpr int ST = MB == 1 ? 2 : 8;  // partials per thread
   u32x4 x[XR];
   u32x4 g[GR];
-  double st[ST];
 };
-
-// Last-arriver RMSNorm after a residual GEMV (GemvParams::nn_*): every workgroup stores its x
-// columns write-through (sc1), drains them and counts itself done; the one whose add returns
-// nwg - 1 reads the rows back with sc1 loads (chain.h protocol) and normalizes them with the bf16
-// rounding points of model.py:281-283 (as rmsnorm_kernel), so the consumer GEMVs read a
-// finished xn instead of a separate norm launch. `red` = LDS scratch (>= 64 floats). All
-// waves of the workgroup call it (wave 0 after its epilogue stores).
-template <int NW>
-__device__ void resid_norm_tail(const GemvParams& p, float* red, bool storing_wave) {
-  constexpr int NT = NW * 64;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int M = p.M, C = p.N;
-  int* flag = reinterpret_cast<int*>(red + 64);
-  if (storing_wave) {  // x columns were stored sc1 (write-through): drain, then count done
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(p.nn_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __shfl(old, 0, 64);
-    if (lane == 0) *flag = old + 1 == gridDim.x ? 1 : 0;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  // the last workgroup: sum_k bf16(x^2) per row
-  const int nvec = C >> 3;
-  float ss[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int v = tid; v < nvec; v += NT) {
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      if (m < M) {
-        const u32x4 a = ld16_sc1(p.C, (unsigned)(((size_t)m * p.ldc + 8 * v) * 2));  // other workgroups' x
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          ss[m] += round_bf(bflo(a[i]) * bflo(a[i])) + round_bf(bfhi(a[i]) * bfhi(a[i]));
-      }
-    }
-  }
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const float t = wave_sum(ss[m]);
-    if (lane == 0) red[wave * 8 + m] = t;
-  }
-  __syncthreads();
-  float r[8];
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) t += red[w * 8 + m];
-    r[m] = round_bf(rsqrtf(round_bf(round_bf(t / (float)C) + p.nn_eps)));
-  }
-  __syncthreads();
-  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const uint4* g4 = reinterpret_cast<const uint4*>(p.nn_w);
-  for (int v = tid; v < nvec; v += NT) {
-    const uint4 g = g4[v];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      if (m < M) {
-        const u32x4 a = ld16_sc1(p.C, (unsigned)(((size_t)m * p.ldc + 8 * v) * 2));
-        uint32_t o[4];
-        const uint32_t aw[4] = {a[0], a[1], a[2], a[3]}, gw[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          o[i] = pack2bf(round_bf(bflo(gw[i]) * round_bf(bflo(aw[i]) * r[m])),
-                         round_bf(bfhi(gw[i]) * round_bf(bfhi(aw[i]) * r[m])));
-          rs[m] += bflo(o[i]) + bfhi(o[i]);
-        }
-        *reinterpret_cast<uint4*>(p.nn_out + (size_t)m * C + 8 * v) = make_uint4(o[0], o[1], o[2], o[3]);
-      }
-    }
-  }
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const float t = wave_sum(rs[m]);
-    if (lane == 0) red[wave * 8 + m] = t;
-  }
-  __syncthreads();
-  if (tid < M && p.nn_rs) {
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) t += red[w * 8 + tid];
-    p.nn_rs[tid] = t;
-  }
-  if (tid == 0) *p.nn_ctr = 0u;  // ready for the next launch (kernel boundaries order it)
-}
 
 #ifndef LLJ_ABAR
 #define LLJ_ABAR 0
@@ -421,50 +287,13 @@ __device__ void resid_norm_tail(const GemvParams& p, float* red, bool storing_wa
 // the per-wave row sums of the staged A (int4 / int8-GPTQ offset removal).
 __host__ __device__ constexpr int tail_floats(int nw) { return 8 + 24 * nw; }
 
-// Fused attention at the end of the QKV launch (GemvParams::att_ctr, M == 1, T == 1, one tile
-// per workgroup, NW * 64 == 256 threads = the attention block). Every wave of the workgroup
-// calls it after the epilogue: the storing wave drains its write-through q / k / v stores, one
-// lane counts the tile into its head's arrival counter, and the workgroup that completes the
-// head (3 * head_size / 16 tiles: q, k and v) resets the counter and runs attention_body over
-// the cache with write-through (sc1) loads — the same arithmetic as the standalone launch, so
-// the results are bitwise those of llj_attention.
-template <int NW>
-__device__ void qkv_attention_tail(const GemvParams& p, const int nt, unsigned char* smem) {
-  static_assert(NW * 64 == 256, "attention block is 256 threads");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's q / k / v stores acknowledged
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(smem);
-  const int Cd = p.n_head * p.head_size;
-  const int n0 = nt * 16;
-  const int h = (n0 % Cd) / p.head_size;
-  if (threadIdx.x == 0) {
-    const unsigned target = 3u * (unsigned)(p.head_size / 16);
-    const unsigned old = __hip_atomic_fetch_add(p.att_ctr + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = old + 1 == target;
-    if (last) __hip_atomic_store(p.att_ctr + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last ? 1 : 0;
-  }
-  __syncthreads();
-  const bool last = *flag != 0;
-  __syncthreads();  // the flag word is attention scratch from here on
-  if (!last) return;
-  float* lds = reinterpret_cast<float*>(smem);
-  if (p.head_size == 128)
-    attention_body<128, 8, 256, true, false>(p.q_out, p.kcache, p.vcache, p.att_y, p.pos, 1, p.S, p.n_head,
-                                             p.att_sl2, h, 0, lds, ChainCtl{});
-  else
-    attention_body<64, 8, 256, true, false>(p.q_out, p.kcache, p.vcache, p.att_y, p.pos, 1, p.S, p.n_head,
-                                            p.att_sl2, h, 0, lds, ChainCtl{});
-}
-
 // One workgroup computes TPW consecutive 16-column tiles nt0 .. nt0 + TPW - 1 (tiles past the
 // last one are loaded as a copy of it and never stored): every wave streams its K-chunks of
 // all TPW tiles behind ONE staged A image, so the prologue (activation rows, RMSNorm) runs
 // once per workgroup instead of once per tile. TPW > 1 only for the standalone LDS-A forms.
-template <int WF, int AM, int EP, int NW, int D, int MB, bool CH, int TPW = 1>
-__device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, unsigned char* smem,
-                                          const ChainCtl& cc) {
-  static_assert(TPW == 1 || (!CH && WF != WF_I8 && AM != AM_GLOBAL), "multi-tile: standalone LDS-A forms");
+template <int WF, int AM, int EP, int NW, int D, int MB, int TPW = 1>
+__device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, unsigned char* smem) {
+  static_assert(TPW == 1 || (WF != WF_I8 && AM != AM_GLOBAL), "multi-tile: LDS-A forms");
   constexpr int TL_RS = 8 + 16 * NW;
   constexpr bool DUAL = (EP == EP_SWIGLU);
   constexpr bool I8 = (WF == WF_I8);
@@ -675,12 +504,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       for (int r = 0; r < RR; ++r) {
         const int mm = 4 * grp + r < M ? 4 * grp + r : M - 1;
         const int n = nj[j];
-        if constexpr (CH) {
-          const uint32_t w = ld4_sc1(p.C, (unsigned)(((size_t)mm * p.ldc + (n & ~1)) * 2));
-          e_xr[j][r] = (bf16_t)((n & 1) ? (w >> 16) : (w & 0xFFFFu));
-        } else {
-          e_xr[j][r] = p.C[(size_t)mm * p.ldc + n];
-        }
+        e_xr[j][r] = p.C[(size_t)mm * p.ldc + n];
       }
     }
   };
@@ -694,9 +518,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   const int JA = (nvec + NT - 1) / NT;
   int rs = 0;
   if (ALDS && !I8 && (LLJ_ABL & 1) == 0 && M <= MB) {
-    const bool st_ok = !NORM || !p.nst_in || p.nst_parts <= AP::ST * (NT / AP::SM);
     const bool g_ok = !NORM || JA <= AP::GR;
-    if (st_ok && g_ok) {
+    if (g_ok) {
       if (MB == 1) rs = JA <= 1 ? 1 : JA <= 2 ? 2 : JA <= 4 ? 4 : JA <= AP::XR ? AP::XR : 0;
       else if (JA <= 2) rs = 2;
       else if (JA <= 4 && M <= 4) rs = 4;
@@ -712,17 +535,6 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     constexpr int RS = decltype(rsc)::value;
     constexpr int MR = decltype(mrc)::value;
     static_assert(MR * RS <= AP::XR, "A registers");
-    if (NORM && p.nst_in) {
-      const int m = tid % AP::SM;
-      const int mm = m < M ? m : M - 1;
-#pragma unroll
-      for (int i = 0; i < AP::ST; ++i) {
-        const int q = tid / AP::SM + (NT / AP::SM) * i;
-        const int si = (q < p.nst_parts ? q : p.nst_parts - 1) * 8 + mm;
-        if constexpr (CH && !LLJ_CH_PLAIN_A) ap.st[i] = ld8d_sc1(p.nst_in, (unsigned)si * 8u);
-        else ap.st[i] = p.nst_in[si];
-      }
-    }
 #pragma unroll
     for (int m = 0; m < MR; ++m)
 #pragma unroll
@@ -730,8 +542,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         const int v = tid + NT * j;
         const int mm = m < M ? m : M - 1, vv = v < nvec ? v : nvec - 1;
         const size_t eo = (size_t)mm * p.lda + 8 * vv;
-        if constexpr (CH && !LLJ_CH_PLAIN_A) ap.x[m * RS + j] = ld16_sc1(p.A, (unsigned)(eo * 2));
-        else ap.x[m * RS + j] = *reinterpret_cast<const u32x4*>(p.A + eo);
+        ap.x[m * RS + j] = *reinterpret_cast<const u32x4*>(p.A + eo);
       }
     if (NORM) {
       constexpr int GJ = RS < AP::GR ? RS : AP::GR;
@@ -746,27 +557,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     constexpr int RS = decltype(rsc)::value;
     constexpr int MR = decltype(mrc)::value;
     if (NORM) {
-      double* redd = reinterpret_cast<double*>(tail + 8);  // [wave][8] fp64
-      float* redf = tail + 8;                              // [wave][8] fp32
-      if (p.nst_in) {
-        double sd = 0.0;
-        const bool mok = tid % AP::SM < M;
-#pragma unroll
-        for (int i = 0; i < AP::ST; ++i) {
-          const int q = tid / AP::SM + (NT / AP::SM) * i;
-          sd += (mok && q < p.nst_parts) ? ap.st[i] : 0.0;
-        }
-#pragma unroll
-        for (int o = 32; o >= AP::SM; o >>= 1) sd += __shfl_xor(sd, o, 64);
-        if (lane < AP::SM) redd[wave * 8 + lane] = sd;
-        __syncthreads();
-        if (tid < M) {
-          double t = 0.0;
-#pragma unroll
-          for (int w = 0; w < NW; ++w) t += redd[w * 8 + tid];
-          tail[tid] = rms_rstd((float)(t / (double)K), p.eps);
-        }
-      } else {
+      float* redf = tail + 8;  // [wave][8] fp32
+      {
 #pragma unroll
         for (int m = 0; m < MR; ++m) {
           float ss = 0.f;
@@ -844,29 +636,17 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   } while (0)
   auto a_issue_any = [&]() { LLJ_A_DISPATCH(a_issue); };
 
-  if constexpr (!CH) {
-    // standalone launch: every input is final, so the A-side loads go first (a wait for
-    // them then never waits for the weight chunks issued after them)
-    issue_pos();
-    issue_const();
-    issue_xr();
-    a_issue_any();
+  // every input is final when the launch starts, so the A-side loads go first (a wait for
+  // them then never waits for the weight chunks issued after them)
+  issue_pos();
+  issue_const();
+  issue_xr();
+  a_issue_any();
 #if LLJ_ABAR
-    __builtin_amdgcn_s_barrier();  // experiment: every wave's A loads ahead of any weight load
+  __builtin_amdgcn_s_barrier();  // experiment: every wave's A loads ahead of any weight load
 #endif
 #pragma unroll
-    for (int d = 0; d < D; ++d) load(d, d);  // the weight stream starts before any A wait
-  } else {
-    // chained: the weight stream needs no producer, so it starts first; then wait for the
-    // producer op and read its results (sc1)
-    issue_const();
-#pragma unroll
-    for (int d = 0; d < D; ++d) load(d, d);
-    chain_wait(cc);
-    issue_pos();
-    issue_xr();
-    a_issue_any();
-  }
+  for (int d = 0; d < D; ++d) load(d, d);  // the weight stream starts before any A wait
   LLJ_STAMP(1);
   float2 e_cs[TPW][4];
   if constexpr (EP == EP_QKV) {  // RoPE rows of the rows' positions (needs e_ps: waits for it only)
@@ -962,20 +742,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       for (int r = 0; r < 4; ++r) mine[8 * TPW + r] = sacc[r];
     }
     __syncthreads();
-    if (wave >= TPW) {  // owns no tile slot
-      if constexpr (EP == EP_RESID)
-        if (p.nn_ctr) resid_norm_tail<NW>(p, red, false);
-      if constexpr (EP == EP_QKV && !CH && TPW == 1 && NW * 64 == 256)
-        if (p.att_ctr) qkv_attention_tail<NW>(p, ntj[0], smem);  // every wave joins its barriers
-      return;
-    }
+    if (wave >= TPW) return;  // owns no tile slot
   }
   LLJ_STAMP(4);
 
   // ---- epilogue of tile slot j (its owner wave): lane holds C[m = 4*grp + r][n = nj[j]]
   auto epilogue = [&](const int j, const f32x4 ya, const f32x4 yb, const f32x4 ys, const i32x4 yi,
                       const i32x4 yi2) {
-    const int n = nj[j], n0 = ntj[j] * 16, nt = ntj[j];
+    const int n = nj[j], n0 = ntj[j] * 16;
     if constexpr ((LLJ_ABL & 4) != 0) {  // ablation: minimal epilogue
       if (ya[0] == 1234.5f && row < M) p.C[n] = f2bf(ya[1] + yb[2]);
       return;
@@ -1053,39 +827,21 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
               dst = region == 1 ? p.kcache : p.vcache;
               ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
             }
-            if (CH || p.att_ctr) st4_sc1(dst, (unsigned)(ei * 2), ob | (pr << 16));  // read in-launch
-            else *reinterpret_cast<uint32_t*>(dst + ei) = ob | (pr << 16);
+            *reinterpret_cast<uint32_t*>(dst + ei) = ob | (pr << 16);
           }
         }
       } else if (EP == EP_RESID) {
-        // x = x + h in bf16 (model.py:172-173); optionally the partial sum_k bf16(x_new^2) of
-        // this tile's 16 columns for the next RMSNorm (part nt of nst_out)
+        // x = x + h in bf16 (model.py:172-173)
         const float xn = round_bf(bf2f(e_xr[j][r]) + round_bf(y));
         const uint32_t xb = (uint32_t)f2bf(xn);
         const uint32_t pr = lane_xor1(xb);
-        float sq = 0.f;
-        if (m < M) {
-          sq = round_bf(xn * xn);
-          if (!(row & 1)) {
-            const size_t ei = (size_t)m * p.ldc + n;
-            if (CH || p.nn_ctr) st4_sc1(p.C, (unsigned)(ei * 2), xb | (pr << 16));  // read by another workgroup
-            else *reinterpret_cast<uint32_t*>(p.C + ei) = xb | (pr << 16);
-          }
-        }
-        if (p.nst_out) {
-          sq = row16_sum(sq);
-          if (row == 0 && m < M) {
-            if constexpr (CH) st8d_sc1(p.nst_out, (unsigned)(nt * 8 + m) * 8u, (double)sq);
-            else p.nst_out[nt * 8 + m] = (double)sq;
-          }
-        }
+        if (m < M && !(row & 1)) *reinterpret_cast<uint32_t*>(p.C + (size_t)m * p.ldc + n) = xb | (pr << 16);
       } else {
         const uint32_t ob = (uint32_t)f2bf(out_value<EP>(y, y2));
         const uint32_t pr = lane_xor1(ob);
         if (m < M && !(row & 1)) {
           const size_t ei = (size_t)m * p.ldc + n;
-          if constexpr (CH) st4_sc1(p.C, (unsigned)(ei * 2), ob | (pr << 16));
-          else *reinterpret_cast<uint32_t*>(p.C + ei) = ob | (pr << 16);
+          *reinterpret_cast<uint32_t*>(p.C + ei) = ob | (pr << 16);
         }
       }
     }
@@ -1119,18 +875,13 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     }
     epilogue(j, ya, yb, ys, yi, yi2);
   }
-  if constexpr (CH) chain_signal(cc);
-  if constexpr (EP == EP_RESID)
-    if (p.nn_ctr) resid_norm_tail<NW>(p, red, true);
-  if constexpr (EP == EP_QKV && !CH && TPW == 1 && NW * 64 == 256)
-    if (p.att_ctr) qkv_attention_tail<NW>(p, ntj[0], smem);
   LLJ_STAMP(5);
 }
 
 template <int WF, int AM, int EP, int NW, int D, int MB, int TPW>
 __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  gemv_body<WF, AM, EP, NW, D, MB, false, TPW>(p, blockIdx.x * TPW, smem, ChainCtl{});
+  gemv_body<WF, AM, EP, NW, D, MB, TPW>(p, blockIdx.x * TPW, smem);
 }
 
 // ------------------------------------------------------------------------------------

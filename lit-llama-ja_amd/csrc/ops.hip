@@ -10,25 +10,11 @@ namespace llj {
 // ---- embedding: out[m] = wte[idx[m]]  (reference model.py:110). Optionally bumps the
 // device-side decode position (*pos_inc += 1) so a captured decode step is self-advancing.
 __global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ idx, const uint4* __restrict__ wte,
-                                                        uint4* __restrict__ out, int C8, int* pos_inc, double* nstat) {
-  __shared__ float red[4];
+                                                        uint4* __restrict__ out, int C8, int* pos_inc) {
   const int m = blockIdx.x;
   const size_t r = (size_t)idx[m];
-  float ss = 0.f;
-  for (int v = threadIdx.x; v < C8; v += blockDim.x) {
-    const uint4 x = wte[r * C8 + v];
-    out[(size_t)m * C8 + v] = x;
-    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ss += round_bf(bflo(w[i]) * bflo(w[i])) + round_bf(bfhi(w[i]) * bfhi(w[i]));
-  }
+  for (int v = threadIdx.x; v < C8; v += blockDim.x) out[(size_t)m * C8 + v] = wte[r * C8 + v];
   if (pos_inc && m == 0 && threadIdx.x == 0) *pos_inc += 1;
-  if (nstat) {  // sum_k bf16(x^2) of the row for the first RMSNorm (see gemv.hip nst_in)
-    ss = wave_sum(ss);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
-    __syncthreads();
-    if (threadIdx.x == 0) nstat[m] = (double)red[0] + (double)red[1] + (double)red[2] + (double)red[3];  // part 0
-  }
 }
 
 // ---- RMSNorm with the bf16 rounding points of model.py:281-283 on bf16 tensors. One block
@@ -103,10 +89,10 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__
 
 // ---- attention (attention.h): one block per (head, query row)
 #ifndef LLJ_ATT_NTH
-#define LLJ_ATT_NTH 256  // threads per (row, head) block (= the chained layer launch, same sums)
+#define LLJ_ATT_NTH 256  // threads per (row, head) block
 #endif
 #ifndef LLJ_ATT_U
-#define LLJ_ATT_U 8  // keys per 16-lane group per pass (= kAttU in gemv.hip)
+#define LLJ_ATT_U 8  // keys per 16-lane group per pass
 #endif
 template <int HS, int U, int NTH>
 __global__ __launch_bounds__(NTH) void attention_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
@@ -114,8 +100,7 @@ __global__ __launch_bounds__(NTH) void attention_kernel(const bf16_t* __restrict
                                                         const int* __restrict__ pos, int T, int S, int nh,
                                                         float scale_log2) {
   __shared__ float lds[attention_lds_floats<HS, NTH>()];
-  attention_body<HS, U, NTH, false>(q, kc, vc, y, pos, T, S, nh, scale_log2, blockIdx.x, blockIdx.y, lds,
-                                    ChainCtl{});
+  attention_body<HS, U, NTH>(q, kc, vc, y, pos, T, S, nh, scale_log2, blockIdx.x, blockIdx.y, lds);
 }
 
 // split-K attention over the keys (long contexts): block (head, row, split) -> partial
@@ -125,8 +110,8 @@ __global__ __launch_bounds__(NTH) void attention_part_kernel(const bf16_t* __res
                                                              int T, int S, int nh, float scale_log2, int nsplit,
                                                              float* __restrict__ part) {
   __shared__ float lds[attention_lds_floats<HS, NTH>()];
-  attention_body<HS, U, NTH, false, false, true>(q, kc, vc, nullptr, pos, T, S, nh, scale_log2, blockIdx.x,
-                                                  blockIdx.y, lds, ChainCtl{}, nsplit, blockIdx.z, part);
+  attention_body<HS, U, NTH, true>(q, kc, vc, nullptr, pos, T, S, nh, scale_log2, blockIdx.x, blockIdx.y, lds, nsplit,
+                                   blockIdx.z, part);
 }
 
 // ---- greedy next token: argmax over bf16 logits (lowest index on ties). Reference
@@ -194,11 +179,10 @@ using namespace llj;
 extern "C" {
 LLJ_TRACE_EXPORT(ops)
 
-int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, double* nstat_out,
-                  void* stream) {
+int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, void* stream) {
   LLJ_REQUIRE(M > 0 && C % 8 == 0);
   hipLaunchKernelGGL(embedding_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, idx, (const uint4*)wte,
-                     (uint4*)out, C / 8, pos_inc, nstat_out);
+                     (uint4*)out, C / 8, pos_inc);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

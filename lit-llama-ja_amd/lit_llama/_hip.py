@@ -18,16 +18,6 @@ _I = ctypes.c_int
 _F = ctypes.c_float
 
 
-class LlLayer(ctypes.Structure):
-    """`llj_layer` of include/lit_llama_amd.h (one decode layer, llj_decode_layer)."""
-    _fields_ = [(n, _I) for n in ("wfmt", "M", "C", "H", "n_head", "S")] + [
-        ("x", _P), ("rms1", _P), ("rms2", _P), ("eps", _F),
-        ("w_qkv", _P), ("sz_qkv", _P), ("w_proj", _P), ("sz_proj", _P), ("w_fc1", _P), ("sz_fc1", _P),
-        ("w_fc2", _P), ("sz_fc2", _P), ("w_down", _P), ("sz_down", _P),
-        ("q", _P), ("kcache", _P), ("vcache", _P), ("rope", _P), ("pos", _P), ("y", _P), ("h", _P),
-        ("nst_in", _P), ("nst_in_parts", _I), ("nst_mid", _P), ("nst_out", _P), ("counters", _P), ("err", _P)]
-
-
 # name -> argtypes (every function returns int: 0 ok, hipError_t, or 1000 = EINVAL)
 SIGNATURES = {
     "llj_w4_repack": [_P, _P, _I, _I, _P],
@@ -36,24 +26,20 @@ SIGNATURES = {
     "llj_w8_repack": [_P, _P, _I, _I, _P],
     "llj_w8_scale_zero": [_P, _P, _I, _P, _I, _P],
     "llj_linear": [_I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
-    "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P],
-    "llj_norm_qkv_rope_attn": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
     "llj_attention_split": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
     "llj_gptq_block": [_P, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P],
     "llj_colblock_pack": [_P, _I, _I, _P, _P, _I, _P, _P],
     "llj_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
-    "llj_attn_resid": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P],
-    "llj_linear_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
-    "llj_linear_resid_norm": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _F, _P, _P, _P, _P],
-    "llj_norm_swiglu": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P],
-    "llj_norm_linear": [_I, _P, _P, _F, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P],
+    "llj_linear_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P],
+    "llj_norm_swiglu": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P],
+    "llj_norm_linear": [_I, _P, _P, _F, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
     "llj_i8_stats": [_P, _I, _I, _I, _F, _P, _P],
     "llj_i8_quant_weight": [_P, _I, _P, _P, _I, _I, _P],
-    "llj_embedding": [_P, _P, _P, _I, _I, _P, _P, _P],
+    "llj_embedding": [_P, _P, _P, _I, _I, _P, _P],
     "llj_rmsnorm": [_P, _P, _F, _P, _I, _I, _P],
     "llj_rmsnorm_rows": [_P, _P, _F, _P, _P, _I, _I, _P],
     "llj_argmax": [_P, _I, _I, _I, _P, _P, _I, _P, _P],
-    "llj_decode_layer": [_P, _P],
     "llj_set_tpw_max": [_I],
 }
 

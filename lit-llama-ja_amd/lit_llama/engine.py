@@ -68,7 +68,7 @@ class DecodeSession:
         cfg = m.config
         st = _hip.stream()
         _hip.call("llj_embedding", self.cur.data_ptr(), m.transformer.wte.weight.data_ptr(), w.x.data_ptr(), B,
-                  cfg.n_embd, self.pos.data_ptr(), w.nst_ptr(0), st)
+                  cfg.n_embd, self.pos.data_ptr(), st)
         m._blocks(w, self.specs, m.kv_caches, self.pos, B, 1, self.S, st)
         m._head(w.x, B, self.specs, self.logits, st, w)
         _hip.call("llj_argmax", self.logits.data_ptr(), self.logits.stride(0), B, cfg.padded_vocab_size,

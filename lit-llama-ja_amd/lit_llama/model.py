@@ -22,8 +22,6 @@ there is no CPU path.
 """
 from __future__ import annotations
 
-import ctypes
-
 import math
 import types
 from dataclasses import dataclass
@@ -76,26 +74,6 @@ llama_configs = {
 QKV_ROWS = 8    # fused-norm kernels stage <= 8 rows in LDS
 LIN_ROWS = 16   # plain linear kernels take <= 16 rows per launch
 I8_ROWS = 8     # int8 kernels quantize <= 8 rows in LDS
-# decode steps (T = 1) can run each layer as ONE chained launch (llj_decode_layer) instead of
-# five. Same results (tests compare them bitwise), but measured 3x SLOWER at 7B: the sc1
-# write-through stores each producer must drain before signalling take 6-10 us to be
-# acknowledged while the weight stream saturates the fabric. Off by default.
-CHAIN_LAYERS = False
-# batched rows: fold each RMSNorm into the residual GEMV before it (llj_linear_resid_norm, the
-# last workgroup normalizes) instead of a separate llj_rmsnorm_rows launch. Correct (tested)
-# but measured slower at 7B bs=8 (3.0 vs 2.2 ms/step): the write-through x stores every
-# workgroup must drain, plus the last workgroup's serial pass, cost more than the launch.
-FUSE_RESID_NORM = False
-# decode steps (T = 1, M <= 8): attention and attn.c_proj (+ residual) as ONE launch
-# (llj_attn_resid): the c_proj weight stream overlaps the attention, which leaves the chip
-# and HBM idle, and one kernel boundary per layer disappears. Bitwise equal to the two launches.
-ATTN_RESID = False
-# one decode row (M == 1, T == 1): the attention of each head computed inside the QKV launch by
-# the workgroup that completes the head (llj_norm_qkv_rope_attn), one launch per layer fewer.
-# Bitwise equal to the separate llj_attention launch, but measured slower at 7B bs=1 (1.237 vs
-# 1.184 ms/token: the write-through drain, the arrival atomics and the attention's sc1 loads in
-# the QKV tail cost more than the attention launch). Off by default.
-QKV_ATTN = False
 # long caches: attention split over the keys (llj_attention_split) into ATTN_SPLIT_KEYS-key
 # ranges once the cache holds >= ATTN_SPLIT_MIN_S slots (32 heads x 1 row leave most CUs idle)
 ATTN_SPLIT_MIN_S = 512
@@ -107,9 +85,6 @@ def attn_splits(S: int) -> int:
     if S < ATTN_SPLIT_MIN_S:
         return 1
     return min(64, (S + ATTN_SPLIT_KEYS - 1) // ATTN_SPLIT_KEYS)
-# M == 1: RMSNorm row statistics handed from the residual epilogues to the next norm-fused
-# GEMV as per-workgroup partial sums (_Work.nst) instead of re-reduced by every consumer
-NST_STATS = False
 # batched rows (M >= 2): each RMSNorm as its own launch (llj_rmsnorm_rows) feeding LDS-A GEMVs,
 # instead of normalized inside every norm-fused GEMV workgroup
 PRE_NORM_ROWS = True
@@ -137,13 +112,7 @@ def _wspec(lin: nn.Module):
 
 
 class _Work:
-    """Per-call scratch for M rows (allocated from torch's caching allocator).
-
-    With M <= QKV_ROWS and no int8 Linear, RMSNorm row statistics flow between kernels
-    (`nst` = two fp64 [n_embd/16][8] partial-sum buffers, see include/lit_llama_amd.h "RMSNorm
-    row statistics"): the embedding / residual epilogues produce sum(bf16(x^2)) per row once,
-    instead of every norm-fused GEMV workgroup re-reducing the row. Buffer 0 feeds rms_1 /
-    ln_f (written by the embedding, then by mlp.c_proj), buffer 1 feeds rms_2 (attn.c_proj)."""
+    """Per-call scratch for M rows (allocated from torch's caching allocator)."""
 
     def __init__(self, cfg: LLaMAConfig, M: int, device, need_i8: bool, S: int = 0):
         C, H = cfg.n_embd, MLP.hidden(cfg)
@@ -157,38 +126,18 @@ class _Work:
         self.pre = M >= max(2, PRE_NORM_MIN_M) and not need_i8 and PRE_NORM_ROWS
         self.xn = torch.empty(M, C, dtype=bf, device=device) if (need_i8 or self.pre) else None
         self.rs = torch.empty(M, dtype=torch.float32, device=device) if self.pre else None
-        # completion counter of llj_linear_resid_norm (M <= 8): the residual GEMV's last
-        # workgroup writes the next RMSNorm into xn / rs (kernel leaves it 0)
-        self.nctr = (torch.zeros(4, dtype=torch.int32, device=device)
-                     if FUSE_RESID_NORM and self.pre and M <= 8 else None)
-        self.xn_ready = False  # xn / rs hold the norm the next op needs (set by a fused resid)
         if need_i8:
             L = _hip.lib()
             nb = max(L.llj_i8_ws_bytes(M, C), L.llj_i8_ws_bytes(M, H))
             self.i8ws = torch.empty(nb, dtype=torch.uint8, device=device)
         else:
             self.i8ws = None
-        if M == 1 and not need_i8 and NST_STATS:
-            parts = max(1, C // 16)
-            self.nst = (torch.zeros(parts * 8, dtype=torch.float64, device=device),
-                        torch.zeros(parts * 8, dtype=torch.float64, device=device))
-        else:
-            self.nst = None
-        # llj_decode_layer (one launch per decode layer): 128 completion-counter words per layer,
-        # zeroed once per step, and a timeout flag
-        self.ctr = torch.zeros(cfg.n_layer * 128, dtype=torch.int32, device=device)
-        self.err = torch.zeros(4, dtype=torch.int32, device=device)
         # split-K attention partials for long caches (llj_attention_split)
         self.nsplit = attn_splits(S)
         self.att_ws = None
         if self.nsplit > 1:
             nb = _hip.lib().llj_attention_ws_bytes(M, cfg.n_head, C // cfg.n_head, self.nsplit)
             self.att_ws = torch.empty(nb, dtype=torch.uint8, device=device)
-        # llj_norm_qkv_rope_attn: per-head arrival counters (zero; every launch leaves them zero)
-        self.actr = torch.zeros(cfg.n_head, dtype=torch.int32, device=device) if M == 1 else None
-
-    def nst_ptr(self, which: int):
-        return None if self.nst is None else self.nst[which].data_ptr()
 
 
 class LLaMA(nn.Module):
@@ -290,7 +239,7 @@ class LLaMA(nn.Module):
         st = _hip.stream()
         ids = idx.reshape(-1).to(torch.int32)
         _hip.call("llj_embedding", ids.data_ptr(), self.transformer.wte.weight.data_ptr(), w.x.data_ptr(), M,
-                  cfg.n_embd, None, w.nst_ptr(0), st)
+                  cfg.n_embd, None, st)
         self._blocks(w, specs, kv, pos, B, T, S, st)
         V = cfg.padded_vocab_size
         if last_only_out is not None:
@@ -298,7 +247,7 @@ class LLaMA(nn.Module):
                 self._head(w.x, B, specs, last_only_out, st, w)
             else:
                 rows = w.x.view(B, T, -1)[:, -1].contiguous()
-                self._head(rows, B, specs, last_only_out, st, w, use_nst=False)
+                self._head(rows, B, specs, last_only_out, st, w)
             return last_only_out
         logits = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
         self._head(w.x, M, specs, logits, st, w)
@@ -321,24 +270,9 @@ class LLaMA(nn.Module):
         M = B * T
         rope = self.rope_cache
         P = _hip.ptr
-        w.xn_ready = False  # the embedding (or caller) just wrote a fresh x
-        chained = T == 1 and M <= QKV_ROWS and w.nst is not None and CHAIN_LAYERS
-        attn_resid = T == 1 and M <= QKV_ROWS and ATTN_RESID and not chained
-        if chained or attn_resid:
-            w.ctr.zero_()
         for i, blk in enumerate(self.transformer.h):
             (fa, wa, sa), (fp, wp, sp), (f1, w1, s1), (f2, w2, s2), (fd, wd, sd) = specs["layers"][i]
             kc, vc = kv[i]
-            if chained and fa == fp == f1 == f2 == fd and fa in (0, 1):
-                # the five ops of this layer in one launch (include/lit_llama_amd.h llj_decode_layer)
-                L = _hip.LlLayer(fa, M, C, H, nh, S, w.x.data_ptr(), blk.rms_1.scale.data_ptr(),
-                                 blk.rms_2.scale.data_ptr(), blk.rms_1.eps, wa.data_ptr(), P(sa), wp.data_ptr(),
-                                 P(sp), w1.data_ptr(), P(s1), w2.data_ptr(), P(s2), wd.data_ptr(), P(sd),
-                                 w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(),
-                                 w.y.data_ptr(), w.h.data_ptr(), w.nst_ptr(0), 1 if i == 0 else C // 16,
-                                 w.nst_ptr(1), w.nst_ptr(0), w.ctr[128 * i].data_ptr(), w.err.data_ptr())
-                _hip.call("llj_decode_layer", ctypes.addressof(L), st)
-                continue
             # 1. rms_1 + c_attn + rope + kv write
             rs = None
             if fa == 2:
@@ -348,44 +282,24 @@ class LLaMA(nn.Module):
                 src, nw = w.xn, None
             elif w.pre:
                 rs = w.rs if fa in _ROWSUM_FMTS else None
-                if not w.xn_ready:
-                    _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
-                              w.xn.data_ptr(), P(rs), M, C, st)
+                _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
+                          w.xn.data_ptr(), P(rs), M, C, st)
                 src, nw = w.xn, None
             else:
                 src, nw = w.x, blk.rms_1.scale.data_ptr()
-            qkv_attn = (QKV_ATTN and T == 1 and M == 1 and fa in (0, 1, 3) and nw is not None and w.nst is None
-                        and w.actr is not None and (C // nh) in (64, 128))
-            if qkv_attn:  # 1.+2. rms_1 + c_attn + rope + kv write + attention in one launch
-                _hip.call("llj_norm_qkv_rope_attn", fa, src.data_ptr(), nw, blk.rms_1.eps, wa.data_ptr(), P(sa),
-                          w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), C, nh, S,
-                          w.y.data_ptr(), w.actr.data_ptr(), st)
-            for r0 in range(0, 0 if qkv_attn else M, QKV_ROWS):
+            for r0 in range(0, M, QKV_ROWS):
                 r = min(QKV_ROWS, M - r0)
                 _hip.call("llj_norm_qkv_rope", fa, src.data_ptr(), nw, blk.rms_1.eps, wa.data_ptr(), P(sa),
                           w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), B, T, C, nh,
-                          S, r0, r, P(w.i8ws), w.nst_ptr(0), 1 if i == 0 else C // 16, P(rs), st)
-            # 2.+3. attention, c_proj + residual (+ rms_2 row statistics, or rms_2 itself for
-            # batched rows); one launch for decode rows (llj_attn_resid)
-            w.xn_ready = False
-            if attn_resid and not qkv_attn and fp in (0, 1, 3) and w.nctr is None:
-                _hip.call("llj_attn_resid", fp, w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
-                          pos.data_ptr(), M, nh, S, wp.data_ptr(), P(sp), w.x.data_ptr(), C, w.nst_ptr(1),
-                          w.ctr[128 * i].data_ptr(), w.err.data_ptr(), st)
+                          S, r0, r, P(w.i8ws), P(rs), st)
+            # 2. attention, 3. c_proj + residual
+            if w.att_ws is not None:
+                _hip.call("llj_attention_split", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                          pos.data_ptr(), B, T, nh, C // nh, S, w.nsplit, w.att_ws.data_ptr(), st)
             else:
-                if not qkv_attn and w.att_ws is not None:
-                    _hip.call("llj_attention_split", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
-                              pos.data_ptr(), B, T, nh, C // nh, S, w.nsplit, w.att_ws.data_ptr(), st)
-                elif not qkv_attn:
-                    _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
-                              pos.data_ptr(), B, T, nh, C // nh, S, st)
-                if w.nctr is not None and fp in (0, 1) and f1 in (0, 1):
-                    _hip.call("llj_linear_resid_norm", fp, w.y.data_ptr(), C, wp.data_ptr(), P(sp), w.x.data_ptr(),
-                              C, M, C, C, blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(),
-                              w.rs.data_ptr(), w.nctr.data_ptr(), st)
-                    w.xn_ready = True
-                else:
-                    self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst_ptr(1))
+                _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                          pos.data_ptr(), B, T, nh, C // nh, S, st)
+            self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st)
             # 4. rms_2 + fc1/fc2 + silu*mul
             if f1 != f2:
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")
@@ -397,41 +311,29 @@ class LLaMA(nn.Module):
                 src, nw, step = w.xn, None, I8_ROWS
             elif w.pre:
                 rs = w.rs if f1 in _ROWSUM_FMTS else None
-                if not w.xn_ready:
-                    _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
-                              w.xn.data_ptr(), P(rs), M, C, st)
+                _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
+                          w.xn.data_ptr(), P(rs), M, C, st)
                 src, nw, step = w.xn, None, QKV_ROWS
             else:
                 src, nw, step = w.x, blk.rms_2.scale.data_ptr(), QKV_ROWS
             for r0 in range(0, M, step):
                 r = min(step, M - r0)
                 _hip.call("llj_norm_swiglu", f1, src[r0].data_ptr(), nw, blk.rms_2.eps, w1.data_ptr(), P(s1),
-                          w2.data_ptr(), P(s2), w.h[r0].data_ptr(), r, H, C, P(w.i8ws), r0, w.nst_ptr(1),
-                          C // 16, None if rs is None else rs[r0].data_ptr(), st)
-            # 5. mlp.c_proj + residual (+ next rms_1 / ln_f row statistics, or that norm itself)
-            last = i + 1 == len(self.transformer.h)
-            nxt_norm = self.transformer.ln_f if last else self.transformer.h[i + 1].rms_1
-            nxt_fmt = specs["head"][0] if last else specs["layers"][i + 1][0][0]
-            w.xn_ready = False
-            if w.nctr is not None and fd in (0, 1) and nxt_fmt in (0, 1):
-                _hip.call("llj_linear_resid_norm", fd, w.h.data_ptr(), H, wd.data_ptr(), P(sd), w.x.data_ptr(), C, M,
-                          C, H, nxt_norm.scale.data_ptr(), nxt_norm.eps, w.xn.data_ptr(), w.rs.data_ptr(),
-                          w.nctr.data_ptr(), st)
-                w.xn_ready = True
-            else:
-                self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st, w.nst_ptr(0))
+                          w2.data_ptr(), P(s2), w.h[r0].data_ptr(), r, H, C, P(w.i8ws), r0,
+                          None if rs is None else rs[r0].data_ptr(), st)
+            # 5. mlp.c_proj + residual
+            self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st)
 
-    def _resid(self, f, A, W, sz, x, M, N, K, w, st, nst_out=None):
+    def _resid(self, f, A, W, sz, x, M, N, K, w, st):
         if f == 2:
             self._i8_prep(A, M, K, w, st)
         step = I8_ROWS if f == 2 else LIN_ROWS
         for r0 in range(0, M, step):
             r = min(step, M - r0)
             _hip.call("llj_linear_resid", f, A[r0].data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz),
-                      x[r0].data_ptr(), x.stride(0), r, N, K, _hip.ptr(w.i8ws), r0,
-                      nst_out, st)
+                      x[r0].data_ptr(), x.stride(0), r, N, K, _hip.ptr(w.i8ws), r0, st)
 
-    def _head(self, x, M, specs, out, st, w, use_nst=True):
+    def _head(self, x, M, specs, out, st, w):
         cfg = self.config
         C, V = cfg.n_embd, cfg.padded_vocab_size
         f, W, sz = specs["head"]
@@ -442,23 +344,18 @@ class LLaMA(nn.Module):
             _hip.call("llj_rmsnorm", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), M, C, st)
             self._i8_prep(xn, M, C, w, st)
             src, nw = xn, None
-        elif M >= 2 and w.xn_ready and x is w.x:  # ln_f already applied by the last mlp.c_proj
-            xn, rs, use_nst = w.xn, (w.rs if f in _ROWSUM_FMTS else None), False
-            src, nw = xn, None
         elif M >= 2 and w.pre:  # batched rows: normalize once (see _Work.pre)
             xn = torch.empty_like(x)
             rs = torch.empty(M, dtype=torch.float32, device=x.device) if f in _ROWSUM_FMTS else None
             _hip.call("llj_rmsnorm_rows", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), _hip.ptr(rs), M,
                       C, st)
-            src, nw, use_nst = xn, None, False
+            src, nw = xn, None
         else:
             src, nw = x, ln.scale.data_ptr()
         for r0 in range(0, M, QKV_ROWS):
             r = min(QKV_ROWS, M - r0)
-            nin = w.nst_ptr(0) if use_nst else None
-            parts = 1 if cfg.n_layer == 0 else C // 16
             _hip.call("llj_norm_linear", f, src[r0].data_ptr(), nw, ln.eps, W.data_ptr(), _hip.ptr(sz),
-                      out[r0].data_ptr(), out.stride(0), r, V, C, _hip.ptr(w.i8ws), r0, nin, parts,
+                      out[r0].data_ptr(), out.stride(0), r, V, C, _hip.ptr(w.i8ws), r0,
                       None if rs is None else rs[r0].data_ptr(), st)
 
 
@@ -574,7 +471,7 @@ class MLP(nn.Module):
         for r0 in range(0, M, step):
             r = min(step, M - r0)
             _hip.call("llj_norm_swiglu", f1, x2[r0].data_ptr(), None, 0.0, w1.data_ptr(), _hip.ptr(s1), w2.data_ptr(),
-                      _hip.ptr(s2), h[r0].data_ptr(), r, H, K, _hip.ptr(ws), r0, None, 0, None, st)
+                      _hip.ptr(s2), h[r0].data_ptr(), r, H, K, _hip.ptr(ws), r0, None, st)
         out = torch.empty(M, self.c_proj.out_features, dtype=torch.bfloat16, device=x.device)
         if fd == 2:
             _hip.call("llj_i8_stats", h.data_ptr(), H, M, H, Linear8bitLtThreshold, ws.data_ptr(), st)

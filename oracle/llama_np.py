@@ -60,6 +60,20 @@ def rmsnorm(x: np.ndarray, scale: np.ndarray, eps: float = 1e-5) -> np.ndarray:
     return (scale.astype(F32) * (x * (F32(1.0) / np.sqrt(ms + F32(eps))))).astype(F32)
 
 
+def rmsnorm_bf16(x: np.ndarray, scale: np.ndarray, eps: float = 1e-5, cpu_rsqrt: bool = False) -> np.ndarray:
+    """reference model.py:276-283 evaluated on bf16 tensors (the reference's GPU precision): every
+    torch op rounds its result to bf16 -- x*x, mean (fp32 accumulation inside), + eps, rsqrt,
+    x * r, scale * x_normed. rsqrt is one rounding of the fp32 value (the CUDA kernel); torch's
+    CPU bf16 rsqrt instead rounds sqrt first and then the reciprocal (cpu_rsqrt=True, which
+    reproduces the reference's bf16 CPU output bit for bit, tests/test_oracle_golden.py)."""
+    x = bf16_round(x)
+    xx = bf16_round(x * x)
+    ms = bf16_round(np.mean(xx, axis=-1, keepdims=True, dtype=F32))
+    e = bf16_round(ms + F32(eps))
+    r = bf16_round(F32(1.0) / (bf16_round(np.sqrt(e)) if cpu_rsqrt else np.sqrt(e)))
+    return bf16_round(bf16_round(scale.astype(F32)) * bf16_round(x * r))
+
+
 def silu(x: np.ndarray) -> np.ndarray:
     x = x.astype(F32)
     return (x / (F32(1.0) + np.exp(-x))).astype(F32)
@@ -149,7 +163,8 @@ def int8_linear(x: np.ndarray, cb: np.ndarray, scb: np.ndarray, threshold: float
     safe = np.where(sca == 0, F32(1.0), sca)
     ca = np.rint(inl * (F32(127.0) / safe[:, None])).clip(-127, 127)
     ca[:, outl] = 0
-    acc = ca.astype(np.int64) @ cb.astype(np.int64).T  # exact int32-range accumulation
+    # int32-range accumulation, exact in float64 (|sum| <= 127^2 * K < 2^53) and BLAS-fast
+    acc = ca.astype(np.float64) @ cb.astype(np.float64).T
     out = acc.astype(F32) * (sca[:, None] * scb[None, :] / F32(127.0 * 127.0))
     if outl.size:
         wsub = (cb[:, outl].astype(F32) * (scb[:, None] / F32(127.0))).astype(np.float16).astype(F32)
@@ -180,10 +195,12 @@ class LinearSpec:
 class OracleLLaMA:
     """reference lit_llama/model.py:59-151 with the KV-cache path (input_pos given)."""
 
-    def __init__(self, cfg: Cfg, params: dict, linears: dict | None = None, act_bf16: bool = False):
+    def __init__(self, cfg: Cfg, params: dict, linears: dict | None = None, act_bf16: bool = False,
+                 cpu_rsqrt: bool = False):
         self.cfg = cfg
         self.p = params
         self.act_bf16 = act_bf16  # round activations to bf16 at module boundaries
+        self.cpu_rsqrt = cpu_rsqrt  # bf16 RMSNorm with torch's CPU rsqrt (see rmsnorm_bf16)
         self.lin = {}
         for name in [k[:-len(".weight")] for k in params if k.endswith(".weight") and "wte" not in k]:
             self.lin[name] = LinearSpec("dense", w=params[name + ".weight"].astype(F32))
@@ -194,6 +211,9 @@ class OracleLLaMA:
 
     def _r(self, x):
         return bf16_round(x) if self.act_bf16 else x
+
+    def _norm(self, x, scale):
+        return rmsnorm_bf16(x, scale, cpu_rsqrt=self.cpu_rsqrt) if self.act_bf16 else rmsnorm(x, scale)
 
     def reset_cache(self):
         """reference model.py:146-151"""
@@ -220,7 +240,7 @@ class OracleLLaMA:
                        for _ in range(cfg.n_layer)]
         for i in range(cfg.n_layer):
             x = self._block(i, x, rope, mask, S, input_pos)
-        x = self._r(rmsnorm(x, self.p["transformer.ln_f.scale"]))
+        x = self._norm(x, self.p["transformer.ln_f.scale"])
         return self._r(self.lin["lm_head"](x))
 
     __call__ = forward
@@ -230,7 +250,7 @@ class OracleLLaMA:
         cfg, p, pre = self.cfg, self.p, f"transformer.h.{i}."
         B, T, C = x.shape
         nh, hs = cfg.n_head, cfg.head_size
-        h = self._r(rmsnorm(x, p[pre + "rms_1.scale"]))
+        h = self._norm(x, p[pre + "rms_1.scale"])
         qkv = self._r(self.lin[pre + "attn.c_attn"](h))
         q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
         q = self._r(apply_rope(q.reshape(B, T, nh, hs), rope)).transpose(0, 2, 1, 3)
@@ -256,7 +276,7 @@ class OracleLLaMA:
         y = (a @ v).astype(F32).transpose(0, 2, 1, 3).reshape(B, T, C)
         y = self._r(y)
         x = self._r(x + self._r(self.lin[pre + "attn.c_proj"](y)))
-        h = self._r(rmsnorm(x, p[pre + "rms_2.scale"]))
+        h = self._norm(x, p[pre + "rms_2.scale"])
         a1 = self._r(self.lin[pre + "mlp.c_fc1"](h))
         a2 = self._r(self.lin[pre + "mlp.c_fc2"](h))
         m = self._r(self._r(silu(a1)) * a2)

@@ -96,3 +96,23 @@ def make_prompt(n: int, vocab: int, seed: int, batch: int | None = None) -> np.n
     rng = np.random.default_rng(seed + 7919)
     shape = (n,) if batch is None else (batch, n)
     return rng.integers(3, vocab, size=shape).astype(np.int32)
+
+
+def ref_init_params(cfg: Cfg, seed: int) -> dict[str, np.ndarray]:
+    """fp32 parameters at the reference's own init scale (lit_llama/model.py:78-82,
+    LLaMA._init_weights: every Linear and the Embedding ~ N(0, 0.02 / sqrt(2 * n_layer)); RMSNorm
+    scales stay 1, model.py:270), drawn from numpy's PCG64 so a fixture made by the reference
+    and a test on the GPU box see identical weights. This is the regime of the reference's bf16
+    acceptance test (tests/test_model.py:103-131)."""
+    rng = np.random.default_rng(seed)
+    std = np.float32(0.02 / np.sqrt(2 * cfg.n_layer))
+    C = cfg.n_embd
+    p: dict[str, np.ndarray] = {}
+    p["transformer.wte.weight"] = rng.standard_normal((cfg.padded_vocab_size, C), dtype=np.float32) * std
+    for name, n_out, n_in in linear_shapes(cfg):
+        p[name + ".weight"] = rng.standard_normal((n_out, n_in), dtype=np.float32) * std
+    for i in range(cfg.n_layer):
+        p[f"transformer.h.{i}.rms_1.scale"] = np.ones(C, np.float32)
+        p[f"transformer.h.{i}.rms_2.scale"] = np.ones(C, np.float32)
+    p["transformer.ln_f.scale"] = np.ones(C, np.float32)
+    return p

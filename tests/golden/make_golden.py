@@ -56,7 +56,7 @@ from lit_llama import quantization as rq  # noqa: E402
 import generate as rgen  # noqa: E402
 from quantize.gptq import llama_blockwise_quantization  # noqa: E402
 
-from oracle.weights import Cfg, make_params, make_prompt  # noqa: E402
+from oracle.weights import Cfg, make_params, make_prompt, ref_init_params  # noqa: E402
 
 torch.set_num_threads(8)
 TOPK = 5
@@ -426,7 +426,27 @@ def gen_eos():
          first_eos_step=np.int64(first), stopped=stopped)
 
 
+def gen_bf16_init():
+    """The reference's bf16 acceptance test (tests/test_model.py:103-131) at a shape the gfx950
+    kernels take: an fp32 LLaMA at the reference's init scale (ref_init_params = _init_weights'
+    N(0, 0.02/sqrt(2 n_layer))), 16 layers, batch 3, a full block of 64 tokens through the no-cache
+    forward; the expected fp32 logits of every position. The test loads the same weights into a
+    bf16 model on the GPU and applies the reference's criterion assert_close(atol=5e-3, rtol=1e-3).
+    Differences from the reference test: n_embd 256 / n_head 4 (hs 64) instead of 32 / 16 (hs 2),
+    vocab 512 instead of 32000 (fixture size), numpy instead of torch RNG for the weights."""
+    cfg = Cfg(block_size=64, n_layer=16, n_head=4, n_embd=256, vocab_size=512)
+    seed = 103
+    params = ref_init_params(cfg, seed)
+    m = ref_model(cfg, params)
+    rng = np.random.default_rng(seed)
+    tokens = rng.integers(0, cfg.vocab_size, size=(3, cfg.block_size)).astype(np.int64)
+    with torch.no_grad():
+        expected = m(torch.from_numpy(tokens)).float().numpy()
+    save("bf16_init", seed=np.int64(seed), tokens=tokens, expected=expected.astype(np.float32))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq", "hf_convert", "meta_convert"]
+    which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq", "hf_convert",
+                             "meta_convert", "bf16_init"]
     for w in which:
         globals()[f"gen_{w}"]()
