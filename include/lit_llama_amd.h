@@ -154,6 +154,16 @@ int llj_rmsnorm_rows(const void* x, const void* w, float eps, void* y, float* ro
 int llj_argmax(const void* logits, int ldl, int M, int V, int* out_idx, int* tokens_out, int tok_stride,
                const int* pos, void* stream);
 
+/* Sampled next token (generate.py:66-74, top_k > 1 or top_k <= 0 = None): x = bf16(logits /
+ * temperature), keep x >= the top_k-th largest x (ties kept, torch.topk + torch.where),
+ * probs = bf16(softmax(x)), then one draw: the first index whose running sum of probs (index
+ * order) exceeds u * sum(probs). u in [0, 1): if u != NULL, u[(*pos + 1) * M + m] (a table of
+ * uniforms per output position; u[m] when pos == NULL), otherwise a counter-based hash of
+ * (seed, *pos, m), so a captured decode step draws a fresh u each step. Writes out_idx[m]
+ * and, if tokens_out != NULL, tokens_out[m*tok_stride + *pos + 1]. One block per row. */
+int llj_sample(const void* logits, int ldl, int M, int V, float temperature, int top_k, const float* u,
+               unsigned long long seed, int* out_idx, int* tokens_out, int tok_stride, const int* pos, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -172,6 +172,179 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const bf16_t* __restrict__
   }
 }
 
+
+// ---- sampled next token (generate.py:66-74 with top_k > 1 / None and a temperature):
+//   x = bf16(logits * (1 / temperature)) (a bf16 tensor divided by a scalar on the device),
+//   keep x >= the top_k-th largest x (torch.topk + where(x < v[-1], -inf): ties at the
+//   threshold are kept), probs = bf16(softmax(x)) (fp32 inside), then one draw from probs.
+// The draw is the inverse CDF over the kept probabilities in index order at a uniform u in
+// [0, 1): the first index whose running sum exceeds u * sum(probs). torch.multinomial draws
+// from the same distribution with its own generator (exponential race); u is either given
+// (u_in, tests) or a counter-based hash of (seed, decode position, row), so a captured decode
+// graph samples a fresh u every step without the host.
+// One 1024-thread block per row. The top_k threshold is an exact radix select on the 16-bit
+// order-preserving keys of the bf16 values (a 2048-bin histogram of key >> 5, then a 32-bin one
+// inside the selected bin, each walked with a block suffix scan), so no sort is needed.
+__device__ __forceinline__ uint32_t bf_key(uint32_t b) { return (b & 0x8000u) ? (~b & 0xFFFFu) : (b | 0x8000u); }
+__device__ __forceinline__ float key_bf(uint32_t k) {
+  const uint32_t b = (k & 0x8000u) ? (k & 0x7FFFu) : (~k & 0xFFFFu);
+  return bf2f((bf16_t)b);
+}
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+constexpr int kSampNT = 1024;
+// Exclusive suffix sum over the block (thread order): sum of v over threads > tid.
+__device__ __forceinline__ uint32_t block_suffix_excl(uint32_t v, uint32_t* wsum) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_down((int)x, o, 64);
+    if (lane + o < 64) x += y;
+  }
+  if (lane == 0) wsum[wv] = x;
+  __syncthreads();
+  uint32_t above = 0;
+  for (int w = wv + 1; w < kSampNT / 64; ++w) above += wsum[w];
+  __syncthreads();
+  return x - v + above;
+}
+
+__global__ __launch_bounds__(kSampNT) void sample_kernel(const bf16_t* __restrict__ logits, int ldl, int V, float inv_t,
+                                                        int top_k, const float* __restrict__ u_in, uint64_t seed,
+                                                        int* __restrict__ out_idx, int* __restrict__ tokens_out,
+                                                        int tok_stride, const int* __restrict__ pos) {
+  constexpr int HB = 2048;  // first pass: key >> 5 (2048 bins); second: key & 31 inside the chosen bin
+  __shared__ uint32_t hist[HB];
+  __shared__ float fred[kSampNT / 64];
+  __shared__ uint32_t ured[kSampNT / 64];
+  __shared__ float chunk_excl[kSampNT];
+  __shared__ uint32_t sel[4];
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const bf16_t* lr = logits + (size_t)m * ldl;
+  auto xkey = [&](int i) -> uint32_t { return bf_key(f2bf(bf2f(lr[i]) * inv_t)); };
+  const int k = top_k < 1 || top_k > V ? V : top_k;
+  // ---- radix select: thr = the k-th largest key; keep key >= thr
+  uint32_t prefix = 0, want = (uint32_t)k;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int b = tid; b < HB; b += kSampNT) hist[b] = 0;
+    __syncthreads();
+    for (int i = tid; i < V; i += kSampNT) {
+      const uint32_t key = xkey(i);
+      if (pass == 0) atomicAdd(&hist[key >> 5], 1u);
+      else if ((key >> 5) == prefix) atomicAdd(&hist[key & 31u], 1u);
+    }
+    __syncthreads();
+    // thread t owns bins 2t, 2t + 1 (pass 1: bin t < 32); counts above them by a suffix scan
+    const int nb = pass == 0 ? 2 : (tid < 32 ? 1 : 0);
+    const int b0 = pass == 0 ? 2 * tid : tid;
+    uint32_t c = 0;
+    for (int q = 0; q < nb; ++q) c += hist[b0 + q];
+    const uint32_t above = block_suffix_excl(c, ured);
+    if (above < want && want <= above + c) {  // exactly one thread
+      uint32_t a = above;
+      int b = b0 + nb - 1;
+      for (; b > b0; --b) {
+        if (a + hist[b] >= want) break;
+        a += hist[b];
+      }
+      sel[0] = (uint32_t)b;
+      sel[1] = want - a;
+    }
+    __syncthreads();
+    prefix = pass == 0 ? sel[0] : (prefix << 5) | sel[0];
+    want = sel[1];
+    __syncthreads();
+  }
+  const uint32_t thr = prefix;
+  // ---- max and sum of exp over the kept values (fp32, fixed reduction order)
+  uint32_t kmax = 0;
+  for (int i = tid; i < V; i += kSampNT) kmax = max(kmax, xkey(i));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+  if (lane == 0) ured[wv] = kmax;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t mk = 0;
+    for (int w = 0; w < kSampNT / 64; ++w) mk = max(mk, ured[w]);
+    sel[2] = mk;
+  }
+  __syncthreads();
+  const float xmax = key_bf(sel[2]);
+  // each thread owns a contiguous index range (the CDF is taken in index order)
+  const int per = (V + kSampNT - 1) / kSampNT;
+  const int i0 = tid * per, i1 = min(V, i0 + per);
+  float esum = 0.f;
+  for (int i = i0; i < i1; ++i) {
+    const uint32_t key = xkey(i);
+    if (key >= thr) esum += __expf(key_bf(key) - xmax);
+  }
+  float t = wave_sum(esum);
+  if (lane == 0) fred[wv] = t;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < kSampNT / 64; ++w) tot += fred[w];
+  const float rinv = 1.f / tot;
+  // bf16 probabilities, chunk sums, exclusive scan over the chunks (thread order = index order)
+  float csum = 0.f;
+  for (int i = i0; i < i1; ++i) {
+    const uint32_t key = xkey(i);
+    if (key >= thr) csum += bf2f(f2bf(__expf(key_bf(key) - xmax) * rinv));
+  }
+  chunk_excl[tid] = csum;
+  __syncthreads();
+  if (tid == 0) {  // sequential scan of 1024 chunk sums: deterministic
+    float run = 0.f;
+    for (int c = 0; c < kSampNT; ++c) {
+      const float v = chunk_excl[c];
+      chunk_excl[c] = run;
+      run += v;
+    }
+    float u;
+    if (u_in) {  // row m of the uniforms of this position (or of the only position without pos)
+      u = u_in[(size_t)(pos ? pos[0] + 1 : 0) * gridDim.x + m];
+    } else {
+      const uint64_t h = splitmix64(seed ^ ((uint64_t)(pos ? pos[0] + 1 : 0) << 20) ^ (uint64_t)m);
+      u = (float)(h >> 40) * (1.0f / 16777216.0f);
+    }
+    fred[0] = u * run;
+    sel[3] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  const float target = fred[0];
+  const float base = chunk_excl[tid];
+  const float next = tid + 1 < kSampNT ? chunk_excl[tid + 1] : 3.4e38f;
+  if (i0 < i1 && base <= target && target < next) {
+    float run = base;
+    int pick = -1, last = -1;
+    for (int i = i0; i < i1; ++i) {
+      const uint32_t key = xkey(i);
+      if (key < thr) continue;
+      last = i;
+      run += bf2f(f2bf(__expf(key_bf(key) - xmax) * rinv));
+      if (run > target) { pick = i; break; }
+    }
+    if (pick < 0) pick = last;
+    if (pick >= 0) atomicMin(&sel[3], (uint32_t)pick);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t pick = sel[3];
+    if (pick == 0xFFFFFFFFu) {  // u * sum at the very end (rounding): the last kept index
+      for (int i = V - 1; i >= 0; --i)
+        if (xkey(i) >= thr) { pick = (uint32_t)i; break; }
+    }
+    out_idx[m] = (int)pick;
+    if (tokens_out) tokens_out[(size_t)m * tok_stride + pos[0] + 1] = (int)pick;
+  }
+}
+
 }  // namespace llj
 
 using namespace llj;
@@ -245,6 +418,15 @@ int llj_attention_split(const void* q, const void* kcache, const void* vcache, v
   } else {
     return LLJ_EINVAL;
   }
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_sample(const void* logits, int ldl, int M, int V, float temperature, int top_k, const float* u,
+               unsigned long long seed, int* out_idx, int* tokens_out, int tok_stride, const int* pos, void* stream) {
+  LLJ_REQUIRE(M > 0 && V > 0 && temperature > 0.f && (!tokens_out || pos) && (u || pos));
+  hipLaunchKernelGGL(sample_kernel, dim3(M), dim3(kSampNT), 0, (hipStream_t)stream, (const bf16_t*)logits, ldl, V,
+                     1.f / temperature, top_k, u, (uint64_t)seed, out_idx, tokens_out, tok_stride, pos);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

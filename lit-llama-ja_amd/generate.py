@@ -2,11 +2,13 @@
 
 `generate()` keeps the reference signature and semantics (generate.py:18-89): 1-D prompt,
 `max_seq_length = min(T + max_new_tokens, block_size)` by default, temperature + top-k
-sampling, EOS returns idx[:input_pos] (the EOS token itself is NOT included). Greedy
-decoding (top_k=1, the reference's deterministic mode) runs as a captured HIP graph per
-token; other top_k use the reference's sampling ops on the GPU logits.
+sampling, EOS returns idx[:input_pos] (the EOS token itself is NOT included). Every decode
+step runs as one captured HIP graph replay: greedy (top_k=1) ends in the argmax kernel, other
+top_k / temperatures in the device top-k sampler.
 
 CLI flags follow reference generate.py:92-102 (argparse; jsonargparse is not installed).
+The default CLI decode (top_k=200, temperature=0.8) runs the same captured graph as greedy, with
+the device sampler (llj_sample) in place of the argmax.
 """
 from __future__ import annotations
 
@@ -31,28 +33,31 @@ EOS_CHECK_EVERY = 16  # greedy graph path: host looks at the ids once per 16 tok
 @torch.no_grad()
 def generate(model: LLaMA, idx: torch.Tensor, max_new_tokens: int, *, max_seq_length: Optional[int] = None,
              temperature: float = 1.0, top_k: Optional[int] = None, eos_id: Optional[int] = None) -> torch.Tensor:
-    """Takes a conditioning sequence (prompt) as input and continues to generate as many tokens as requested."""
+    """Takes a conditioning sequence (prompt) as input and continues to generate as many tokens as requested.
+
+    Reference generate.py:18-89. Every decode step, greedy (top_k=1) or sampled, is one replay of
+    the captured HIP graph; sampling draws its uniforms from a counter hash seeded from torch's
+    default generator, so torch.manual_seed makes a run reproducible as in the reference."""
     T = idx.size(0)
     T_new = T + max_new_tokens
     if max_seq_length is None:
         max_seq_length = min(T_new, model.config.block_size)
     if max_new_tokens <= 0:
         return idx.clone()
-    if top_k == 1:
-        return _generate_greedy(model, idx, max_new_tokens, max_seq_length, eos_id)
-    return _generate_sampled(model, idx, max_new_tokens, max_seq_length, temperature, top_k, eos_id)
+    seed = 0 if top_k == 1 else int(torch.randint(0, 2 ** 62, (1,)))
+    sess = DecodeSession(model, 1, max_seq_length, T_new, temperature=temperature, top_k=top_k, seed=seed)
+    return _run_session(sess, idx, max_new_tokens, eos_id)
 
 
-def _generate_greedy(model, idx, max_new_tokens, max_seq_length, eos_id):
+def _run_session(sess, idx, max_new_tokens, eos_id):
     T = idx.size(0)
-    sess = DecodeSession(model, 1, max_seq_length, T + max_new_tokens)
     sess.prefill(idx.view(1, -1))
     left = max_new_tokens - 1
     while True:
         if eos_id is not None:
             gen = sess.output()[0, T:]
             hit = (gen == eos_id).nonzero()
-            if hit.numel():
+            if hit.numel():  # the reference returns idx[:input_pos]: the EOS token is excluded
                 return sess.output()[0, :T + int(hit[0, 0])].to(idx.dtype)
         if left == 0:
             break
@@ -60,32 +65,6 @@ def _generate_greedy(model, idx, max_new_tokens, max_seq_length, eos_id):
         sess.decode(n)
         left -= n
     return sess.output()[0].to(idx.dtype)
-
-
-def _generate_sampled(model, idx, max_new_tokens, max_seq_length, temperature, top_k, eos_id):
-    """The reference loop (generate.py:61-87) over LLaMA.forward; sampling with torch ops."""
-    T = idx.size(0)
-    T_new = T + max_new_tokens
-    device, dtype = idx.device, idx.dtype
-    empty = torch.empty(T_new, dtype=dtype, device=device)
-    empty[:T] = idx
-    idx = empty
-    input_pos = torch.arange(0, T, device=device)
-    model.reset_cache()
-    for _ in range(max_new_tokens):
-        x = idx.index_select(0, input_pos).view(1, -1)
-        logits = model(x, max_seq_length, input_pos)
-        logits = logits[0, -1].float() / temperature
-        if top_k is not None:
-            v, _ = torch.topk(logits, min(top_k, logits.size(-1)))
-            logits = torch.where(logits < v[[-1]], -float("Inf"), logits)
-        probs = torch.nn.functional.softmax(logits, dim=-1)
-        idx_next = torch.multinomial(probs, num_samples=1).to(dtype=dtype)
-        input_pos = input_pos[-1:] + 1
-        idx = idx.index_copy(0, input_pos, idx_next)
-        if eos_id is not None and idx_next == eos_id:
-            return idx[:input_pos]  # excludes the EOS token, as the reference does
-    return idx
 
 
 @torch.no_grad()

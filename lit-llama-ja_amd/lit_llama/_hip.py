@@ -40,6 +40,7 @@ SIGNATURES = {
     "llj_rmsnorm": [_P, _P, _F, _P, _I, _I, _P],
     "llj_rmsnorm_rows": [_P, _P, _F, _P, _P, _I, _I, _P],
     "llj_argmax": [_P, _I, _I, _I, _P, _P, _I, _P, _P],
+    "llj_sample": [_P, _I, _I, _I, _F, _I, _P, ctypes.c_ulonglong, _P, _P, _I, _P, _P],
     "llj_set_tpw_max": [_I],
 }
 

@@ -2,10 +2,13 @@
 captured once into a HIP graph.
 
 One decode step = embedding of the current token (which also advances the device-side
-position), the n_layer fused blocks, ln_f + lm_head and the greedy argmax that writes the
-next token both into `cur` and into the output id buffer. Nothing in the step reads the
-host, so replaying the graph K times generates K tokens with no host round trip (the
-reference syncs per layer at model.py:221 and per token at generate.py:86).
+position), the n_layer fused blocks, ln_f + lm_head and the next-token choice -- the greedy
+argmax (top_k = 1) or the temperature / top-k sampler (llj_sample, generate.py:66-74; its
+uniform comes from a counter hash of (seed, position, row), or from a caller's table of
+uniforms per position) -- which writes the next token both into `cur` and into the output id
+buffer. Nothing in the step reads the host, so replaying the graph K times generates K tokens
+with no host round trip (the reference syncs per layer at model.py:221 and per token at
+generate.py:86).
 
 Batch B > 1 decodes B equal-length prompts together (each row equals an independent B=1
 run: tests/test_model_gpu.py); the reference's generate() is batch 1 only (generate.py:62).
@@ -19,7 +22,12 @@ from .model import LLaMA, QKV_ROWS, _Work
 
 
 class DecodeSession:
-    def __init__(self, model: LLaMA, batch: int, max_seq_length: int, total_len: int, use_graph: bool = True):
+    def __init__(self, model: LLaMA, batch: int, max_seq_length: int, total_len: int, use_graph: bool = True,
+                 temperature: float = 1.0, top_k: int | None = 1, seed: int = 0,
+                 uniforms: torch.Tensor | None = None):
+        """top_k == 1: greedy; otherwise sampling at `temperature` over the top_k logits (None:
+        all). uniforms: optional (total_len, batch) fp32 device table, row p = the uniforms of the
+        token at position p (tests replay a reference run's draws)."""
         cfg = model.config
         assert max_seq_length <= cfg.block_size
         self.model, self.B, self.S, self.total = model, batch, max_seq_length, total_len
@@ -38,6 +46,24 @@ class DecodeSession:
         self.steps_done = 0
         self.specs = None
         self.work = None
+        self.temperature = float(temperature)
+        self.top_k = 0 if top_k is None else int(top_k)
+        self.seed = int(seed) & ((1 << 64) - 1)
+        if uniforms is not None:
+            assert uniforms.dtype == torch.float32 and uniforms.shape == (total_len, batch) and uniforms.is_contiguous()
+            _hip.require_device(uniforms, "uniforms")
+        self.uniforms = uniforms
+
+    def _choose(self, st):
+        """next token of every row from self.logits -> cur and tokens[:, pos + 1]"""
+        cfg = self.model.config
+        if self.top_k == 1:
+            _hip.call("llj_argmax", self.logits.data_ptr(), self.logits.stride(0), self.B, cfg.padded_vocab_size,
+                      self.cur.data_ptr(), self.tokens.data_ptr(), self.total, self.pos.data_ptr(), st)
+        else:
+            _hip.call("llj_sample", self.logits.data_ptr(), self.logits.stride(0), self.B, cfg.padded_vocab_size,
+                      self.temperature, self.top_k, _hip.ptr(self.uniforms), self.seed, self.cur.data_ptr(),
+                      self.tokens.data_ptr(), self.total, self.pos.data_ptr(), st)
 
     # -- prefill: eager (rows = B*T); fills the caches, picks the first new token
     @torch.no_grad()
@@ -54,8 +80,7 @@ class DecodeSession:
         st = _hip.stream()
         self.tokens[:, :T] = prompts.to(torch.int32)
         self.pos.fill_(T - 1)
-        _hip.call("llj_argmax", self.logits.data_ptr(), self.logits.stride(0), B, m.config.padded_vocab_size,
-                  self.cur.data_ptr(), self.tokens.data_ptr(), self.total, self.pos.data_ptr(), st)
+        self._choose(st)
         self.t_prompt = T
         self.steps_done = 1
         # decode-step operands (fixed for the session)
@@ -71,8 +96,7 @@ class DecodeSession:
                   cfg.n_embd, self.pos.data_ptr(), st)
         m._blocks(w, self.specs, m.kv_caches, self.pos, B, 1, self.S, st)
         m._head(w.x, B, self.specs, self.logits, st, w)
-        _hip.call("llj_argmax", self.logits.data_ptr(), self.logits.stride(0), B, cfg.padded_vocab_size,
-                  self.cur.data_ptr(), self.tokens.data_ptr(), self.total, self.pos.data_ptr(), st)
+        self._choose(st)
 
     def capture(self):
         if self.graph is not None or not self.use_graph:

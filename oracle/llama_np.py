@@ -318,3 +318,26 @@ def topk_filter(logits: np.ndarray, top_k: int, temperature: float = 1.0) -> np.
     l = np.where(l < v, -np.inf, l)
     e = np.exp(l - l.max())
     return e / e.sum()
+
+
+def sample_inverse_cdf(logits: np.ndarray, temperature: float, top_k: int | None, u: float):
+    """reference generate.py:66-74 on a bf16 logits row (its GPU precision), with the draw of
+    torch.multinomial written as an inverse CDF at the uniform u (any exact sampler of the same
+    probabilities is the reference's distribution; torch's own generator stream cannot be
+    reproduced): x = bf16(logits * (1 / temperature)); keep x >= the top_k-th largest x (ties
+    kept); probs = bf16(exp(x - max) * (1 / sum)); return (first index whose running sum of probs
+    in index order exceeds u * sum(probs), probs)."""
+    x = bf16_round(bf16_round(logits).astype(F32) * F32(1.0 / temperature))
+    V = x.shape[-1]
+    k = V if top_k is None or top_k < 1 or top_k > V else top_k
+    thr = np.sort(x)[::-1][k - 1]
+    keep = x >= thr
+    xmax = x.max()
+    e = np.where(keep, np.exp((x - xmax).astype(F32)), F32(0)).astype(F32)
+    tot = F32(e.sum(dtype=F32))
+    p = np.where(keep, bf16_round(e * (F32(1.0) / tot)), F32(0)).astype(F32)
+    cdf = np.cumsum(p, dtype=F32)
+    target = F32(u) * cdf[-1]
+    hit = np.nonzero(cdf > target)[0]
+    idx = int(hit[0]) if hit.size else int(np.nonzero(keep)[0][-1])
+    return idx, p

@@ -426,6 +426,38 @@ def gen_eos():
          first_eos_step=np.int64(first), stopped=stopped)
 
 
+def gen_sampled():
+    """Sampled decoding (generate.py:66-74: temperature 0.8, top_k 50) through the reference's own
+    generate() on a bf16 model, with torch.multinomial replaced by an inverse-CDF draw at recorded
+    uniforms (the first index whose running sum of the probs it is handed exceeds u * sum). The
+    fixture keeps the uniforms, the probability rows the reference computed, and the ids."""
+    cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=2048)
+    seed = 4242
+    params = make_params(cfg, seed)
+    prompt = make_prompt(8, cfg.vocab_size, seed)
+    m = ref_model(cfg, params, dtype=torch.bfloat16)
+    rng = np.random.default_rng(seed)
+    us, probs = [], []
+
+    def inv_cdf(p, num_samples=1):
+        u = float(rng.random())
+        us.append(u)
+        probs.append(p.float().numpy().copy())
+        c = torch.cumsum(p.double(), -1)
+        i = int(torch.nonzero(c > u * c[-1])[0, 0])
+        return torch.tensor([i])
+
+    orig = torch.multinomial
+    torch.multinomial = inv_cdf
+    try:
+        with torch.no_grad():
+            out = rgen.generate(m, torch.from_numpy(prompt.astype(np.int32)), 16, temperature=0.8, top_k=50)
+    finally:
+        torch.multinomial = orig
+    save("sampled", seed=np.int64(seed), prompt=prompt, ids=out.numpy().astype(np.int32),
+         u=np.array(us, np.float32), probs=np.stack(probs).astype(np.float32))
+
+
 def gen_bf16_init():
     """The reference's bf16 acceptance test (tests/test_model.py:103-131) at a shape the gfx950
     kernels take: an fp32 LLaMA at the reference's init scale (ref_init_params = _init_weights'
@@ -447,6 +479,6 @@ def gen_bf16_init():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq", "hf_convert",
-                             "meta_convert", "bf16_init"]
+                             "meta_convert", "bf16_init", "sampled"]
     for w in which:
         globals()[f"gen_{w}"]()

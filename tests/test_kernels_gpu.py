@@ -561,3 +561,62 @@ def test_int8_fused_ops_7b_shapes(hip, M):
          ws.data_ptr(), 0, st())
     torch.cuda.synchronize()
     assert_bf16_close(xr.float().cpu().numpy(), x + bf16(O.int8_linear(hh, cbd_, scbd_)), f"int8 resid M={M}")
+
+
+@pytest.mark.parametrize("temperature,top_k", [(0.8, 200), (1.0, 50), (0.5, 2), (1.3, 0), (1.0, 32000)])
+def test_sample_inverse_cdf_vs_oracle(hip, temperature, top_k):
+    """llj_sample with given uniforms against the oracle's restatement of generate.py:66-74 (the
+    draw as an inverse CDF at the same u): identical indices, except where u * sum lands within
+    fp32 summation noise (1e-4 of the sum) of a CDF step (the sums are associated differently;
+    with all 32000 tokens kept the steps are ~3e-5 apart, so such draws are frequent there)."""
+    rng = np.random.default_rng(int(temperature * 10) + top_k)
+    M, V = 6, 32000
+    L = bf16(rng.standard_normal((M, V)) * 3)
+    L[1, 100:140] = L[1].max()  # a tie block at the maximum (all kept by torch.topk + where)
+    Ld = T(L, torch.bfloat16)
+    out = torch.empty(M, dtype=torch.int32, device=dev)
+    mism = 0
+    for rep in range(40):
+        u = rng.random(M).astype(np.float32)
+        u[0] = 0.0 if rep == 0 else u[0]
+        ud = T(u)
+        call(hip, "llj_sample", Ld.data_ptr(), V, M, V, temperature, top_k, ud.data_ptr(), 0, out.data_ptr(), None, 0,
+             None, st())
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        for m in range(M):
+            want, p = O.sample_inverse_cdf(L[m], temperature, top_k, float(u[m]))
+            assert p[got[m]] > 0, "picked a filtered index"
+            if got[m] != want:
+                cdf = np.cumsum(p, dtype=np.float64)
+                gap = np.abs(cdf - u[m] * cdf[-1]).min()
+                assert gap < 1e-4 * cdf[-1], (rep, m, got[m], want, gap)
+                mism += 1
+    if top_k <= 200:  # a few hundred CDF steps: near-boundary draws are rare
+        assert mism <= 2, mism
+
+
+def test_sample_device_rng_distribution(hip):
+    """The in-graph path (u from the counter hash of seed, position and row): 8192 rows of the same
+    logits draw from the top_k = 8 softmax with the oracle's probabilities (4-sigma bound per
+    token), and a different position gives different draws."""
+    rng = np.random.default_rng(77)
+    V, M, k, temp = 32000, 8192, 8, 0.7
+    row = bf16(rng.standard_normal(V) * 2)
+    L = T(np.broadcast_to(row, (M, V)).copy(), torch.bfloat16)
+    out = torch.empty(M, dtype=torch.int32, device=dev)
+    pos = torch.tensor([41], dtype=torch.int32, device=dev)
+    call(hip, "llj_sample", L.data_ptr(), V, M, V, temp, k, None, 1234, out.data_ptr(), None, 0, pos.data_ptr(), st())
+    torch.cuda.synchronize()
+    draws = out.cpu().numpy()
+    _, p = O.sample_inverse_cdf(row, temp, k, 0.5)
+    p = p / p.sum()
+    assert set(np.unique(draws)) <= set(np.nonzero(p)[0])
+    freq = np.bincount(draws, minlength=V) / M
+    for i in np.nonzero(p)[0]:
+        assert abs(freq[i] - p[i]) < 4 * np.sqrt(p[i] * (1 - p[i]) / M) + 1e-3, (i, freq[i], p[i])
+    pos.fill_(42)
+    out2 = torch.empty_like(out)
+    call(hip, "llj_sample", L.data_ptr(), V, M, V, temp, k, None, 1234, out2.data_ptr(), None, 0, pos.data_ptr(), st())
+    torch.cuda.synchronize()
+    assert (out2.cpu().numpy() != draws).mean() > 0.3

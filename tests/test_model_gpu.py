@@ -356,3 +356,75 @@ def test_bf16_reference_criterion(golden):
     m = build(cfg, ref_init_params(cfg, int(g["seed"])))
     out = m(torch.from_numpy(g["tokens"]).cuda()).float().cpu()
     torch.testing.assert_close(out, torch.from_numpy(g["expected"]), atol=5e-3, rtol=1e-3)
+
+
+def test_sampled_decode_replays_reference_draws(golden):
+    """Sampled decoding (temperature 0.8, top_k 50) against the reference's own generate() run
+    (tests/golden/sampled.npz: a bf16 model, torch.multinomial replaced by an inverse-CDF draw at
+    recorded uniforms). The session replays the same uniforms (device table indexed by position):
+    every step's probability row matches the reference's within bf16 logit noise, and the ids are
+    the reference's until a step whose u lies within that noise of a CDF step (then the contexts
+    part). The captured graph reproduces the eager session bitwise."""
+    from lit_llama.engine import DecodeSession
+
+    g = golden("sampled")
+    cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=2048)
+    m = build(cfg, make_params(cfg, int(g["seed"])))
+    T, n = len(g["prompt"]), len(g["u"])
+    table = torch.zeros(T + n, 1, dtype=torch.float32, device="cuda")
+    table[T:, 0] = torch.from_numpy(g["u"]).cuda()
+    prompt = torch.from_numpy(g["prompt"]).cuda().view(1, -1)
+    sess = DecodeSession(m, 1, T + n, T + n, use_graph=False, temperature=0.8, top_k=50, uniforms=table)
+    sess.prefill(prompt)
+    ours = []
+    for s in range(n):
+        ours.append(sess.logits[0].float().cpu().numpy())
+        if s + 1 < n:
+            sess.decode(1)
+    ids = sess.output()[0].cpu().numpy()
+    matched = 0
+    for s in range(n):
+        pick, p = O.sample_inverse_cdf(ours[s], 0.8, 50, float(g["u"][s]))
+        assert pick == ids[T + s]  # the kernel's draw is the restatement's on our logits
+        pref = g["probs"][s]
+        # the logits near the top are O(7): one bf16 ulp there is 0.03, i.e. ~4 % of a probability
+        # at temperature 0.8; the reference's CPU bf16 and the GPU path may differ by 2-3 ulps
+        dev_ = np.abs(p - pref).max() / pref.max()
+        assert dev_ < 0.15, f"step {s}: probabilities differ by {dev_:.3f} of the largest"
+        assert np.count_nonzero((p > 0) != (pref > 0)) <= 3, f"step {s}: kept sets differ"
+        if ids[T + s] != g["ids"][T + s]:
+            c_ref = np.cumsum(pref, dtype=np.float64)
+            c_our = np.cumsum(p, dtype=np.float64)
+            gap = np.abs(c_ref / c_ref[-1] - g["u"][s]).min()
+            noise = np.abs(c_ref / c_ref[-1] - c_our / c_our[-1]).max()
+            assert gap <= noise + 1e-6, f"step {s}: diverged with u {g['u'][s]} {gap:.2e} from a step (noise {noise:.2e})"
+            break
+        matched += 1
+    assert matched >= 8, matched
+    gsess = DecodeSession(m, 1, T + n, T + n, temperature=0.8, top_k=50, uniforms=table)
+    gsess.prefill(prompt)
+    gsess.decode(n - 1)
+    np.testing.assert_array_equal(gsess.output()[0].cpu().numpy(), ids)
+
+
+def test_generate_default_cli_sampling_is_seeded():
+    """generate() with the CLI defaults (top_k 200, temperature 0.8) goes through the captured
+    graph with the device sampler: prompt ++ new tokens, ids inside the vocabulary, reproducible
+    under torch.manual_seed and different under another seed."""
+    cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=2048)
+    m = build(cfg, make_params(cfg, 5))
+    prompt = np.random.default_rng(1).integers(3, 2048, 7).astype(np.int32)
+    outs = []
+    for seed in (1234, 1234, 99):
+        torch.manual_seed(seed)
+        outs.append(gen_kw(m, prompt, 40, top_k=200, temperature=0.8))
+    assert outs[0].shape == (47,) and (outs[0][:7] == prompt).all()
+    assert ((outs[0] >= 0) & (outs[0] < 2048)).all()
+    np.testing.assert_array_equal(outs[0], outs[1])
+    assert (outs[0][7:] != outs[2][7:]).any()
+
+
+def gen_kw(model, prompt, n, **kw):
+    import generate as G
+
+    return G.generate(model, torch.from_numpy(prompt).cuda(), n, **kw).cpu().numpy()
