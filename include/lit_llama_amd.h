@@ -42,6 +42,7 @@ int llj_w4_scale_zero(const void* scales, const void* zeros, int dtype, void* sz
  * the low nibbles followed by the W4P tile of the high nibbles (2 KiB). `packed` holds N*K
  * bytes. sz[2n] = scales[n], sz[2n+1] = 2176 + zeros[n] (the W8P magic offset). */
 int llj_w8_repack(const void* qweight_ref, void* packed, int N, int K, void* stream);
+int llj_w8_unpack(const void* packed, void* qweight_ref, int N, int K, void* stream);
 int llj_w8_scale_zero(const void* scales, const void* zeros, int dtype, void* sz, int N, void* stream);
 
 /* Host-side tuning knob (no device work): at most `tiles` 16-column tiles per workgroup in the

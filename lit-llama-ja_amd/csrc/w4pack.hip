@@ -80,6 +80,22 @@ __global__ void w4_unpack_kernel(const uint32_t* __restrict__ in, uint8_t* __res
   }
 }
 
+__global__ void w8_unpack_kernel(const uint32_t* __restrict__ in, uint8_t* __restrict__ ref, int N, int K) {
+  const size_t total = (size_t)N * K;  // bytes of the reference buffer (one code each)
+  const int KC = K >> 7;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int n = (int)(i % N);
+    const int k = (int)(i / N);
+    const int kc = k >> 7, w = k & 127;
+    const int g = w >> 5, t = (w & 31) >> 3, j = w & 7;
+    const int l = 16 * g + (n & 15);
+    const size_t tile = (size_t)(n >> 4) * KC + kc;
+    const uint32_t lo = in[(tile * 128 + l) * 4 + t];       // low-nibble plane
+    const uint32_t hi = in[(tile * 128 + 64 + l) * 4 + t];  // high-nibble plane
+    ref[i] = (uint8_t)(((lo >> w4p_bit(j)) & 0xF) | (((hi >> w4p_bit(j)) & 0xF) << 4));
+  }
+}
+
 // sz[n] = (scale[n], off + zero[n]) in fp32 from the module's scale/zero buffers (any of
 // fp32 / bf16 / fp16, given by dtype code 0/1/2; one group per row: tile_cols = -1); off is the
 // magic-exponent offset of the format (W4P 128, W8P 128 + 2048).
@@ -137,6 +153,16 @@ int llj_w8_repack(const void* qweight_ref, void* packed, int N, int K, void* str
   int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
   hipLaunchKernelGGL(w8_repack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)qweight_ref,
                      (uint32_t*)packed, N, K);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_w8_unpack(const void* packed, void* qweight_ref, int N, int K, void* stream) {
+  LLJ_REQUIRE(N > 0 && K > 0 && N % 16 == 0 && K % 128 == 0);
+  const size_t total = (size_t)N * K;
+  int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  hipLaunchKernelGGL(w8_unpack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint32_t*)packed,
+                     (uint8_t*)qweight_ref, N, K);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

@@ -3,9 +3,12 @@
 Drop-in for reference lit_llama/quantization.py:
   * ColBlockQuantizedLinear (338-421): same constructor, buffers and state_dict keys
     (`quant_weight` (N, K*bits/8) uint8 column-major, `scales`, `zeros`, `bias`); forward
-    runs the gfx950 GEMV on a repacked copy of `quant_weight` (bits=4: W4P layout, bits=8:
-    W8P = two nibble planes in W4P tiles; csrc/w4pack.hip) kept as a non-persistent buffer
-    and refreshed whenever the reference buffers change. The reference computes bits=8 (and
+    runs the gfx950 GEMV on the streaming tiling of the codes (bits=4: W4P, bits=8: W8P = two
+    nibble planes in W4P tiles; csrc/w4pack.hip), into which `quant_weight` is repacked IN
+    PLACE the first time the module runs (one copy of the weights on the device, ~3.3 GB at
+    7B). state_dict(), get_weight() and .to()/.cuda() see the reference layout (unpacked on
+    demand); any write to `quant_weight` (load_state_dict, pack_weight, in-place ops) is
+    taken as a new reference-layout buffer and repacked on the next forward. The reference computes bits=8 (and
     any non-Triton case) as F.linear(inp, get_weight(inp.dtype)) (409-421), i.e. with weights
     rounded to bf16((q - z) * s); the kernel applies s to the exact integer sum instead
     (difference <= 1 bf16 ulp per weight, covered by the tests' tolerance).
@@ -70,10 +73,10 @@ class ColBlockQuantizedLinear(torch.nn.Module):
             self.register_buffer("bias", torch.empty((self.out_features,)))
         else:
             self.register_buffer("bias", None)
-        # derived device-side operands of the HIP kernel (not part of the state_dict)
-        self.register_buffer("_w4p", None, persistent=False)
+        # derived device-side operand of the HIP kernel (not part of the state_dict)
         self.register_buffer("_sz", None, persistent=False)
-        self._key = None
+        self._qkey = None   # (data_ptr, version) of quant_weight right after its in-place repack
+        self._szkey = None  # (scales, zeros) identity the _sz pairs were built from
 
     # ---- reference buffer utilities (quantization.py:374-409) -------------------------
     def pack_weight(self, weight):
@@ -89,10 +92,11 @@ class ColBlockQuantizedLinear(torch.nn.Module):
 
     def get_weight(self, dtype=torch.float):
         """reference quantization.py:390-409: the dequantized (N, K) weight."""
-        weight = torch.empty((self.out_features, self.in_features), device=self.quant_weight.device, dtype=dtype)
+        qw = self._reference_codes()
+        weight = torch.empty((self.out_features, self.in_features), device=qw.device, dtype=dtype)
         mask = (1 << self.bits) - 1
         for nr in range(self.entries_per_byte):
-            weight[:, nr::self.entries_per_byte] = ((self.quant_weight >> (nr * self.bits)) & mask).float()
+            weight[:, nr::self.entries_per_byte] = ((qw >> (nr * self.bits)) & mask).float()
         for j in range(self.scales.size(1)):
             weight[:, j * self.tile_cols:(j + 1) * self.tile_cols] -= self.zeros[:, j:j + 1]
             weight[:, j * self.tile_cols:(j + 1) * self.tile_cols] *= self.scales[:, j:j + 1]
@@ -103,12 +107,28 @@ class ColBlockQuantizedLinear(torch.nn.Module):
         return self.bits in (4, 8) and self.scales.shape[1] == 1 and self.out_features % 16 == 0 \
             and self.in_features % 128 == 0
 
+    def _is_packed(self) -> bool:
+        """quant_weight currently holds the streaming tiling (not the reference layout)."""
+        qw = self.quant_weight
+        return self._qkey is not None and self._qkey == (qw.data_ptr(), qw._version)
+
+    def _reference_codes(self) -> torch.Tensor:
+        """quant_weight in the reference layout: the buffer itself, or an unpacked copy."""
+        qw = self.quant_weight
+        if not self._is_packed():
+            return qw
+        N, K = self.out_features, self.in_features
+        out = torch.empty((N, K // self.entries_per_byte), dtype=torch.uint8, device=qw.device).t().contiguous().t()
+        _hip.call("llj_w4_unpack" if self.bits == 4 else "llj_w8_unpack", qw.data_ptr(), out.data_ptr(), N, K,
+                  _hip.stream())
+        return out
+
     def _prepare(self):
-        """(Re)build the W4P copy and the fp32 (scale, 128 + zero) pairs when the reference
-        buffers changed (pointer or in-place version)."""
+        """Repack quant_weight in place when it holds reference-layout codes (first run, or written
+        since), and (re)build the fp32 (scale, offset + zero) pairs when scales / zeros changed."""
         qw, sc, zr = self.quant_weight, self.scales, self.zeros
-        key = (qw.data_ptr(), qw._version, sc.data_ptr(), sc._version, zr.data_ptr(), zr._version, qw.device)
-        if key == self._key:
+        szkey = (sc.data_ptr(), sc._version, zr.data_ptr(), zr._version, qw.device)
+        if self._is_packed() and szkey == self._szkey:
             return
         _hip.require_device(qw, "ColBlockQuantizedLinear.quant_weight")
         if not self._supported():
@@ -118,26 +138,45 @@ class ColBlockQuantizedLinear(torch.nn.Module):
                 "(gptq.int4 / gptq.int8 with tile_cols=-1, N % 16 == 0, K % 128 == 0 is supported)")
         N, K = self.out_features, self.in_features
         s = _hip.stream()
-        ref = qw.t()  # physical (K*bits/8, N) row-major when quant_weight keeps the reference strides
-        if not ref.is_contiguous():
-            ref = ref.contiguous()
-        nbytes = N * K * self.bits // 8
-        if self._w4p is None or self._w4p.numel() != nbytes or self._w4p.device != qw.device:
-            self._w4p = torch.empty(nbytes, dtype=torch.uint8, device=qw.device)
-            self._sz = torch.empty(N, 2, dtype=torch.float32, device=qw.device)
-        _hip.call("llj_w4_repack" if self.bits == 4 else "llj_w8_repack", ref.data_ptr(), self._w4p.data_ptr(),
-                  N, K, s)
-        sc1, zr1 = sc.reshape(N).contiguous(), zr.reshape(N).contiguous()
-        if sc1.dtype not in _DTYPE_CODE or zr1.dtype != sc1.dtype:
-            sc1, zr1 = sc1.float(), zr1.float()
-        _hip.call("llj_w4_scale_zero" if self.bits == 4 else "llj_w8_scale_zero", sc1.data_ptr(), zr1.data_ptr(),
-                  _DTYPE_CODE[sc1.dtype], self._sz.data_ptr(), N, s)
-        self._key = key
+        if not self._is_packed():
+            if not qw.t().is_contiguous():  # keep the reference's column-major storage
+                self.quant_weight = qw = qw.t().contiguous().t()
+            flat = qw.t().view(-1)  # physical (K*bits/8, N) row-major bytes
+            tmp = torch.empty_like(flat)
+            _hip.call("llj_w4_repack" if self.bits == 4 else "llj_w8_repack", flat.data_ptr(), tmp.data_ptr(), N, K,
+                      s)
+            flat.copy_(tmp)
+            del tmp
+            self._qkey = (qw.data_ptr(), qw._version)
+        if szkey != self._szkey or self._sz is None or self._sz.device != qw.device:
+            if self._sz is None or self._sz.device != qw.device:
+                self._sz = torch.empty(N, 2, dtype=torch.float32, device=qw.device)
+            sc1, zr1 = sc.reshape(N).contiguous(), zr.reshape(N).contiguous()
+            if sc1.dtype not in _DTYPE_CODE or zr1.dtype != sc1.dtype:
+                sc1, zr1 = sc1.float(), zr1.float()
+            _hip.call("llj_w4_scale_zero" if self.bits == 4 else "llj_w8_scale_zero", sc1.data_ptr(), zr1.data_ptr(),
+                      _DTYPE_CODE[sc1.dtype], self._sz.data_ptr(), N, s)
+            self._szkey = szkey
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+        if self._is_packed():  # the state dict carries the reference layout
+            destination[prefix + "quant_weight"] = self._reference_codes()
+
+    def _apply(self, fn, *args, **kwargs):
+        # moving / casting the module: put the reference layout back first so the moved buffer
+        # is what it claims to be (repacked again on its next forward)
+        if self._is_packed():
+            ref = self._reference_codes()
+            self.quant_weight.t().view(-1).copy_(ref.t().reshape(-1))
+            self._qkey = None
+        self._szkey = None
+        return super()._apply(fn, *args, **kwargs)
 
     def _wspec(self):
         """(wfmt, weight operand, sz operand) for the fused model kernels."""
         self._prepare()
-        return self.wfmt, self._w4p, self._sz
+        return self.wfmt, self.quant_weight, self._sz
 
     @property
     def wfmt(self) -> int:
@@ -153,7 +192,7 @@ class ColBlockQuantizedLinear(torch.nn.Module):
         x2 = _as_rows(inp, K)
         out = torch.empty((x2.shape[0], N), dtype=inp.dtype, device=inp.device)
         bias = None if self.bias is None else self.bias.to(torch.bfloat16)
-        _linear_rows(self.wfmt, x2, self._w4p, self._sz, bias, out, N, K)
+        _linear_rows(self.wfmt, x2, self.quant_weight, self._sz, bias, out, N, K)
         return out.reshape(*inp.shape[:-1], N)
 
 

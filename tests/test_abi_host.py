@@ -36,6 +36,8 @@ def _header_decls():
                 kinds.append("f")
             elif a.startswith("int"):
                 kinds.append("i")
+            elif a.startswith("unsigned long long"):
+                kinds.append("u64")
             else:
                 raise AssertionError(f"unexpected argument kind {a!r} in {name}")
         decls[name] = (ret, kinds)
@@ -82,7 +84,7 @@ def test_library_loads_and_binds_without_gpu():
 def test_ctypes_table_matches_header():
     from lit_llama import _hip
 
-    kind = {ctypes.c_void_p: "p", ctypes.c_int: "i", ctypes.c_float: "f"}
+    kind = {ctypes.c_void_p: "p", ctypes.c_int: "i", ctypes.c_float: "f", ctypes.c_ulonglong: "u64"}
     decls = _header_decls()
     for name, argt in _hip.SIGNATURES.items():
         assert name in decls, name

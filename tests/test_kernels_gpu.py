@@ -132,7 +132,12 @@ def test_w4_linear_shapes(hip, M, N, K):
 def test_w8_repack_layout(hip, N, K):
     rng = np.random.default_rng(3 * N + K)
     qw = rng.integers(0, 256, size=(N, K), dtype=np.uint8)
-    np.testing.assert_array_equal(repack8(hip, qw).cpu().numpy(), w8p_pack_np(qw))
+    packed = repack8(hip, qw)
+    np.testing.assert_array_equal(packed.cpu().numpy(), w8p_pack_np(qw))
+    back = torch.empty(K, N, dtype=torch.uint8, device=dev)
+    call(hip, "llj_w8_unpack", packed.data_ptr(), back.data_ptr(), N, K, st())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(back.cpu().numpy().T, qw)
 
 
 def test_w8_linear_reference_fixture(hip, golden):
