@@ -56,6 +56,21 @@ class LLaMAConfig:
     def from_name(cls, name: str) -> Self:
         return cls(**llama_configs[name])
 
+    def kernel_support(self) -> Optional[str]:
+        """None if the gfx950 kernels take this configuration, else why not. The GEMVs stream
+        128-deep K chunks and 16-column tiles (n_embd % 128 == 0; n_hidden, 3 n_embd and the padded
+        vocab are then multiples of 16), the fused RoPE / attention kernels take head_size 64 or
+        128. The JA fork's 19M / 49M configs (head 64), 7B / 13B / 30B / 65B (head 128) run; its
+        125M config (n_embd 780, head 78) and the reference test's n_embd 32 / head 2 do not."""
+        hs = self.n_embd // self.n_head
+        if self.n_embd % self.n_head:
+            return f"n_embd {self.n_embd} is not a multiple of n_head {self.n_head}"
+        if self.n_embd % 128:
+            return f"n_embd {self.n_embd} is not a multiple of 128 (the GEMV K chunk)"
+        if hs not in (64, 128):
+            return f"head_size {hs} is not 64 or 128 (fused RoPE / attention kernels)"
+        return None
+
     def debug(self):
         for k in ("block_size", "vocab_size", "padded_vocab_size", "n_layer", "n_head", "n_embd"):
             print(f"{k}: ", getattr(self, k))
@@ -156,6 +171,12 @@ class LLaMA(nn.Module):
         self.rope_cache: Optional[RoPECache] = None
         self.mask_cache: Optional[MaskCache] = None
         self.kv_caches: List[KVCache] = []
+        # a model built on the GPU must be one the kernels take: fail here, with the reason, rather
+        # than with EINVAL in the middle of a forward (CPU / meta construction stays allowed for
+        # checkpoint conversion and state-dict work; forward is GPU-only anyway)
+        why = config.kernel_support()
+        if why is not None and self.lm_head.weight.device.type == "cuda":
+            raise NotImplementedError(f"LLaMAConfig not supported by the MI355X kernels: {why}")
 
     def _init_weights(self, module: nn.Module) -> None:
         """reference model.py:78-82"""
@@ -192,6 +213,9 @@ class LLaMA(nn.Module):
         assert max_seq_length <= block_size, f"Cannot attend to {max_seq_length}, block size is only {block_size}"
         assert T <= block_size, f"Cannot forward sequence of length {T}, block size is only {block_size}"
         _hip.require_device(idx, "idx")
+        why = self.config.kernel_support()
+        if why is not None:
+            raise NotImplementedError(f"LLaMAConfig not supported by the MI355X kernels: {why}")
         self._check_dtype()
         if self.rope_cache is None:
             self.rope_cache = self.build_rope_cache(idx)

@@ -180,6 +180,17 @@ def test_product_path_has_no_cpu_fallback():
         m(torch.zeros(1, 4, dtype=torch.int32))
 
 
+def test_unsupported_configs_are_named():
+    """Configurations the kernels do not take are reported with the reason (LLaMAConfig.
+    kernel_support), and a GPU-side construction of one raises instead of failing mid-forward."""
+    from lit_llama import LLaMAConfig
+
+    assert "780" in LLaMAConfig.from_name("125M").kernel_support()  # JA fork config, reference model.py:48-51
+    assert "not a multiple of 128" in LLaMAConfig(n_layer=16, n_head=16, n_embd=32).kernel_support()
+    for name in ("19M", "49M", "7B", "13B", "30B", "65B"):
+        assert LLaMAConfig.from_name(name).kernel_support() is None, name
+
+
 def test_model_api_surface():
     import lit_llama
     from lit_llama import LLaMA, LLaMAConfig
