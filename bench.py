@@ -177,7 +177,7 @@ def untimed_steps(prompt_len: int, S: int, warmup: int, steps: int) -> int:
     return max(warmup, min(centred, room))
 
 
-def time_decode(model, B, prompt_len, S, warmup, steps, ws, seed=1234):
+def time_decode(model, B, prompt_len, S, warmup, steps, ws, seed=1234, use_graph=True):
     from lit_llama.engine import DecodeSession
 
     cfg = model.config
@@ -186,7 +186,7 @@ def time_decode(model, B, prompt_len, S, warmup, steps, ws, seed=1234):
     assert total <= cfg.block_size, "positions beyond block_size"
     g = torch.Generator().manual_seed(seed)
     prompts = torch.randint(3, cfg.vocab_size, (B, prompt_len), generator=g).cuda()
-    sess = DecodeSession(model, B, S, total)
+    sess = DecodeSession(model, B, S, total, use_graph=use_graph)
     sess.prefill(prompts)  # one-time work (int4 repack, kernel attributes) stays out of the timings
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -375,6 +375,8 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the LLaMA-13B replica leg (C4)")
     ap.add_argument("--only-dominant", action="store_true",
                     help="profiling aid: only the dominant-kernel loop (for the PMC traffic passes)")
+    ap.add_argument("--eager", action="store_true",
+                    help="profiling aid: decode steps launched one by one instead of graph replays (PMC passes)")
     ap.add_argument("--stub", action="store_true",
                     help="CPU rehearsal of the replica launch / timing / aggregation (no GPU, no measurement)")
     args = ap.parse_args()
@@ -410,7 +412,7 @@ def main():
         k_s, k_bytes = time_dominant_kernel(model, args.batch)
         print(json.dumps({"dominant_avg_us": round(k_s * 1e6, 2), "bytes_per_launch": k_bytes}), flush=True)
         return
-    r = time_decode(model, args.batch, args.prompt_len, S, args.warmup, args.steps, ws)
+    r = time_decode(model, args.batch, args.prompt_len, S, args.warmup, args.steps, ws, use_graph=not args.eager)
     t_max, tokens = aggregate(r["seconds"], r["tokens"], ws)
     value = tokens / t_max
     ms_per_step = t_max / args.steps * 1e3

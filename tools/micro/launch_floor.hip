@@ -36,6 +36,28 @@ __global__ void stream_k(const uint4* __restrict__ w_, uint32_t* __restrict__ ou
   if (t < 16) out[blockIdx.x * 16 + t] = r[t] ^ r[t + 16];
 }
 
+template <int U>
+__global__ void stream_u_k(const uint4* __restrict__ w_, uint32_t* __restrict__ out, int per_wg16) {
+  // U independent 16-B loads per thread in flight before any use
+  const u32x4v* w = reinterpret_cast<const u32x4v*>(w_) + (size_t)blockIdx.x * per_wg16;
+  const int t = threadIdx.x, nt = blockDim.x;
+  uint32_t s = 0;
+  for (int i0 = t; i0 < per_wg16; i0 += U * nt) {
+    u32x4v v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * nt;
+      v[u] = __builtin_nontemporal_load(w + (i < per_wg16 ? i : t));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+  }
+  __shared__ uint32_t r[1024];
+  r[t] = s;
+  __syncthreads();
+  if (t < 16) out[blockIdx.x * 16 + t] = r[t] ^ r[t + 16];
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
 int main() {
@@ -84,6 +106,40 @@ int main() {
       printf("{\"kind\": %d, \"grid\": %d, \"bytes\": %zu, \"us_per_launch\": %.3f, \"GBps\": %.1f}\n", kind, grid,
              mb[kind], us, kind >= 2 ? mb[kind] / us / 1e3 : 0.0);
       CK(hipGraphExecDestroy(ge)); CK(hipGraphDestroy(g));
+    }
+  }
+  // sweep: bytes x grid x threads x loads in flight
+  for (size_t bytes : {(size_t)8400000, (size_t)22500000, (size_t)25200000, (size_t)45200000}) {
+    for (int grid : {256, 512, 768, 1024, 2048}) {
+      for (int nt : {256, 512}) {
+        for (int U : {4, 8}) {
+          const int per_wg16 = (int)(bytes / 16 / grid);
+          hipGraph_t g; hipGraphExec_t ge;
+          CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+          for (int i = 0; i < N; ++i) {
+            const size_t off16 = ((size_t)i * bytes / 16) % (wbytes / 16 - bytes / 16);
+            if (U == 4) hipLaunchKernelGGL(stream_u_k<4>, dim3(grid), dim3(nt), 0, s, w + off16, out, per_wg16);
+            else hipLaunchKernelGGL(stream_u_k<8>, dim3(grid), dim3(nt), 0, s, w + off16, out, per_wg16);
+          }
+          CK(hipStreamEndCapture(s, &g));
+          CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+          CK(hipGraphLaunch(ge, s));
+          CK(hipStreamSynchronize(s));
+          float best = 1e30f;
+          for (int r = 0; r < 5; ++r) {
+            CK(hipEventRecord(e0, s));
+            CK(hipGraphLaunch(ge, s));
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+            if (ms < best) best = ms;
+          }
+          const double us = best * 1e3 / N;
+          printf("{\"sweep\": 1, \"bytes\": %zu, \"grid\": %d, \"threads\": %d, \"U\": %d, \"us_per_launch\": %.3f, \"GBps\": %.1f}\n",
+                 bytes, grid, nt, U, us, bytes / us / 1e3);
+          CK(hipGraphExecDestroy(ge)); CK(hipGraphDestroy(g));
+        }
+      }
     }
   }
   return 0;
