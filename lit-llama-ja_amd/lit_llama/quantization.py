@@ -385,8 +385,11 @@ class GPTQQuantizer:
         Qt = torch.empty_like(Wt)
         Err = torch.empty((B, N), dtype=torch.float32, device=self.dev)
         loss = torch.zeros(N, dtype=torch.float32, device=self.dev)
-        sc = scale.reshape(-1).float().contiguous()
-        zr = zero.reshape(-1).float().contiguous()
+        # the stored (scale, zero) -- rounded to the buffers' dtype, e.g. bf16 -- are what decode
+        # dequantizes with, so the column loop's reconstructions and error feedback use them too
+        # (fp32 buffers: the reference's values exactly)
+        sc = self.scales.reshape(-1).float().contiguous()
+        zr = self.zeros.reshape(-1).float().contiguous()
         s = _hip.stream()
         for i1 in range(0, K, B):
             i2 = i1 + B

@@ -226,3 +226,26 @@ def test_gptq_cli_flags():
     for flag in ("--checkpoint_path", "--output_path", "--tokenizer_path", "--n_samples", "--dtype", "--quantize",
                  "--calibration_path", "--block_size"):
         assert flag in out.stdout
+
+
+def test_gptq_cli_tokenizer_selection(tmp_path):
+    """quantize/gptq.py takes the reference's SentencePiece Tokenizer for its default
+    `tokenizer.model` path (reference quantize/gptq.py:17, 207) and the HF JSON tokenizer for a
+    `.json` file; a SentencePiece model trained here encodes with BOS like the reference's."""
+    sentencepiece = pytest.importorskip("sentencepiece")
+    from lit_llama import HFTokenizer, Tokenizer
+    from quantize.gptq import tokenizer_for
+
+    corpus = tmp_path / "c.txt"
+    corpus.write_text("\n".join(f"the quick brown fox {i} jumps over the lazy dog" for i in range(200)))
+    Tokenizer.train(str(corpus), str(tmp_path), vocab_size=60)
+    tok = tokenizer_for(tmp_path / "tokenizer.model")
+    assert isinstance(tok, Tokenizer)
+    ids = tok.encode("the quick brown fox", bos=True)
+    assert int(ids[0]) == tok.bos_id and len(ids) > 2
+    assert tok.decode(ids[1:]) == "the quick brown fox"
+    from tokenizers import Tokenizer as HFTok
+    from tokenizers.models import WordLevel
+
+    HFTok(WordLevel({"<pad>": 0, "a": 1}, unk_token="<pad>")).save(str(tmp_path / "t.json"))
+    assert isinstance(tokenizer_for(tmp_path / "t.json"), HFTokenizer)

@@ -171,42 +171,58 @@ def test_gptq_quantizer_matches_reference(hip, t):
 @pytest.mark.gpu
 def test_blockwise_driver_quantizes_like_reference(hip):
     """llama_blockwise_quantization (quantize/gptq.py:36-148) on the int4_gptq fixture's model and
-    calibration tokens (make_golden.py gen_int4_gptq): every Linear replaced by a
-    ColBlockQuantizedLinear whose codes mostly agree with the reference's own GPTQ run (which
-    calibrated in fp32; ours in bf16), and the quantized model's logits as close to the fp32
-    model's as the reference's quantized model is. Parity unpinned beyond these bounds."""
+    calibration tokens (make_golden.py gen_int4_gptq), calibrating in fp32 as the reference run
+    did: every Linear replaced by a ColBlockQuantizedLinear whose scales / zeros are the
+    reference's and whose codes are the reference's within one step, on all but a few entries
+    (device GEMM / Cholesky summation order, compounded over the blocks); the quantized model,
+    loaded into a bf16 gptq.int4 model, gives the reference's quantized logits within bf16 noise."""
     from oracle import llama_np as O
     from oracle.weights import Cfg, make_params
-    from tests.test_model_gpu import build
+    from lit_llama import LLaMA, LLaMAConfig
     from lit_llama.quantization import ColBlockQuantizedLinear
+    from lit_llama.utils import EmptyInitOnDevice
     from quantize.gptq import llama_blockwise_quantization
+    from tests.test_model_gpu import build
 
     g = np.load(Path(__file__).parent / "golden" / "int4_gptq.npz")
     cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=2048)
     seed = int(g["seed"])
     params = make_params(cfg, seed)
-    model = build(cfg, params)
+    with EmptyInitOnDevice(device=torch.device("cuda"), dtype=torch.float32):
+        model = LLaMA(LLaMAConfig(block_size=128, vocab_size=2048, n_layer=2, n_head=4, n_embd=256))
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
     gen = torch.Generator().manual_seed(seed)
     calib = torch.randint(3, cfg.vocab_size, (4, cfg.block_size), generator=gen)  # as make_golden.py
     errs = llama_blockwise_quantization(model, calib, "cuda", bits=4)
     assert len(errs) == 5 * cfg.n_layer + 1 and np.all(np.isfinite(list(errs.values())))
-    agree = {}
+    agree, within1 = {}, {}
     for k in [k[3:] for k in g.files if k.startswith("sd/") and k.endswith(".quant_weight")]:
-        mod = model.get_submodule(k[:-len(".quant_weight")])
+        name = k[:-len(".quant_weight")]
+        mod = model.get_submodule(name)
         assert isinstance(mod, ColBlockQuantizedLinear)
-        qw = mod.state_dict()["quant_weight"].cpu().numpy()  # reference layout (the buffer may hold W4P)
-        agree[k] = float((codes_of(qw, 4) == codes_of(g["sd/" + k], 4)).mean())
+        sd = mod.state_dict()
+        np.testing.assert_allclose(sd["scales"].cpu().numpy(), g["sd/" + name + ".scales"], rtol=1e-6)
+        np.testing.assert_array_equal(sd["zeros"].cpu().numpy(), g["sd/" + name + ".zeros"])
+        a, b = codes_of(sd["quant_weight"].cpu().numpy(), 4), codes_of(g["sd/" + k], 4)
+        agree[k] = float((a == b).mean())
+        within1[k] = float((np.abs(a.astype(int) - b) <= 1).mean())
     print("code agreement with the reference's GPTQ run:", agree)
-    assert min(agree.values()) > 0.5, agree
-    model.reset_cache()
+    print("within one step:", within1)
+    assert min(within1.values()) == 1.0, within1
+    assert min(agree.values()) > 0.99, agree
+    # the quantized checkpoint in a bf16 gptq.int4 model (the generate.py flow)
+    qsd = {k: v for k, v in model.state_dict().items()}
+    qm = build(cfg, params, mode="gptq.int4", packed={k: v.cpu().numpy() for k, v in qsd.items()
+                                                      if k.endswith((".quant_weight", ".scales", ".zeros"))})
     idx = torch.from_numpy(g["prompt"][None].astype(np.int64)).cuda()
-    ours = model(idx).float().cpu().numpy()[0, -1]
-    fp32 = O.OracleLLaMA(cfg, params).forward(g["prompt"][None].astype(np.int64))[0, -1]
+    ours = qm(idx).float().cpu().numpy()[0, -1]
     ref_q = g["fp32_logits_step0"]
+    fp32 = O.OracleLLaMA(cfg, params).forward(g["prompt"][None].astype(np.int64))[0, -1]
     e_ours = np.linalg.norm(ours - fp32) / np.linalg.norm(fp32)
     e_ref = np.linalg.norm(ref_q - fp32) / np.linalg.norm(fp32)
-    print("relative logit error vs the fp32 model: ours", e_ours, "reference GPTQ", e_ref)
-    assert e_ours < 1.5 * e_ref + 2e-2, (e_ours, e_ref)
+    d_ref = np.linalg.norm(ours - ref_q) / np.linalg.norm(ref_q)
+    print("relative logit error vs the fp32 model: ours", e_ours, "reference GPTQ", e_ref, "ours vs ref", d_ref)
+    assert d_ref < 3e-2, d_ref  # bf16 activations vs the reference's fp32 forward of the same codes
 
 
 @pytest.mark.gpu
@@ -235,7 +251,7 @@ def test_gptq_cli_writes_a_checkpoint_generate_loads(hip, tmp_path):
     tok.save(str(tmp_path / "tokenizer.json"))
     rng = np.random.default_rng(5)
     (tmp_path / "calib.txt").write_text(" ".join(rng.choice(words, 600)))
-    errs = main(checkpoint_path=ck, tokenizer_path=tmp_path / "tokenizer.json", n_samples=2, dtype="bfloat16",
+    errs = main(checkpoint_path=ck, tokenizer_path=tmp_path / "tokenizer.json", n_samples=2, dtype="float32",
                 quantize="gptq.int4", calibration_path=tmp_path / "calib.txt", block_size=256)
     out = tmp_path / "llama-gptq.4bit.pth"
     assert out.is_file() and len(errs) == 5 * cfg.n_layer + 1

@@ -454,3 +454,28 @@ def test_unsupported_config_raises_at_construction():
     with pytest.raises(NotImplementedError, match="780"):
         with EmptyInitOnDevice(device=torch.device("cuda"), dtype=torch.bfloat16):
             LLaMA.from_name("125M")
+
+
+def test_generate_main_end_to_end(tmp_path, capsys):
+    """generate.py main (reference generate.py:92-155) end to end on a random 19M checkpoint:
+    checkpoint -> llama_model_lookup -> HF tokenizer encode -> generate with the CLI defaults
+    (top_k 200, temperature 0.8) -> decode; stdout carries only the decoded samples, stderr the
+    load time, tokens/s and memory lines."""
+    import generate as G
+    from tokenizers import Tokenizer as HFTok
+    from tokenizers.models import WordLevel
+    from tokenizers.pre_tokenizers import Whitespace
+
+    cfg = Cfg(n_layer=6, n_head=8, n_embd=512, vocab_size=35000)  # llama_configs["19M"]
+    ck = tmp_path / "lit-llama.pth"
+    torch.save({k: torch.from_numpy(v) for k, v in make_params(cfg, 3).items()}, ck)
+    words = [f"w{i}" for i in range(3, 500)]
+    tok = HFTok(WordLevel({"<pad>": 0, "<s>": 1, "</s>": 2, **{w: i + 3 for i, w in enumerate(words)}},
+                          unk_token="<pad>"))
+    tok.pre_tokenizer = Whitespace()
+    tok.save(str(tmp_path / "tokenizer.json"))
+    G.main("w3 w4 w5", num_samples=2, max_new_tokens=10, checkpoint_path=ck, tokenizer_path=tmp_path / "tokenizer.json")
+    out, err = capsys.readouterr()
+    lines = [l for l in out.splitlines() if l.strip()]
+    assert len(lines) == 2 and all(l.startswith("w3 w4 w5") for l in lines), out
+    assert err.count("tokens/sec") == 2 and "Time to load model" in err and "Memory used" in err
