@@ -400,7 +400,9 @@ def test_sampled_decode_replays_reference_draws(golden):
         # at temperature 0.8; the reference's CPU bf16 and the GPU path may differ by 2-3 ulps
         dev_ = np.abs(p - pref).max() / pref.max()
         assert dev_ < 0.15, f"step {s}: probabilities differ by {dev_:.3f} of the largest"
-        assert np.count_nonzero((p > 0) != (pref > 0)) <= 3, f"step {s}: kept sets differ"
+        # entries on either side of the top-50 threshold (bf16 ties there) may swap: little mass
+        diff = (p > 0) != (pref > 0)
+        assert (p[diff].sum() + pref[diff].sum()) / pref.sum() < 0.1, f"step {s}: kept sets differ"
         if got != g["ids"][T + s]:
             c_ref = np.cumsum(pref, dtype=np.float64)
             c_our = np.cumsum(p, dtype=np.float64)
@@ -469,7 +471,7 @@ def test_generate_main_end_to_end(tmp_path, capsys):
     cfg = Cfg(n_layer=6, n_head=8, n_embd=512, vocab_size=35000)  # llama_configs["19M"]
     ck = tmp_path / "lit-llama.pth"
     torch.save({k: torch.from_numpy(v) for k, v in make_params(cfg, 3).items()}, ck)
-    words = [f"w{i}" for i in range(3, 500)]
+    words = [f"w{i}" for i in range(3, 35000)]  # every id decodes to a word
     tok = HFTok(WordLevel({"<pad>": 0, "<s>": 1, "</s>": 2, **{w: i + 3 for i, w in enumerate(words)}},
                           unk_token="<pad>"))
     tok.pre_tokenizer = Whitespace()
@@ -477,5 +479,7 @@ def test_generate_main_end_to_end(tmp_path, capsys):
     G.main("w3 w4 w5", num_samples=2, max_new_tokens=10, checkpoint_path=ck, tokenizer_path=tmp_path / "tokenizer.json")
     out, err = capsys.readouterr()
     lines = [l for l in out.splitlines() if l.strip()]
-    assert len(lines) == 2 and all(l.startswith("<s> w3 w4 w5 ") for l in lines), out  # BOS decodes as a word here
+    assert len(lines) == 2, out
+    for l in lines:  # BOS decodes as a word with this tokenizer; 10 new tokens follow the prompt
+        assert l.startswith("<s> w3 w4 w5 ") and len(l.split()) >= 4 + 10 - 2, l
     assert err.count("tokens/sec") == 2 and "Time to load model" in err and "Memory used" in err
