@@ -111,6 +111,25 @@ int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, cons
                     void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const float* rowsum,
                     void* stream);
 
+/* ---------------------------------------------------------------- prefill GEMMs (many rows)
+ * The same Linear layers for M >> 16 rows (a prompt, a perplexity window: LLaMA.forward over
+ * T tokens, model.py:84-128), MFMA-tiled 128 x 128 per workgroup with the chunk tiles staged
+ * through LDS (csrc/gemm.hip). wfmt 0 (int4 W4P, sz = (scale, 128 + zero)) or 1 (bf16 (N, K)).
+ * N % 128 == 0, K % 128 == 0, lda % 8 == 0; any M >= 1. Same epilogue semantics as the GEMVs. */
+int llj_gemm_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, void* C, int ldc, int M, int N,
+                    int K, void* stream);
+/* x[M, N] += A . W^T (bf16 residual add, model.py:172-173). */
+int llj_gemm_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M, int N,
+                   int K, void* stream);
+/* h[M, N] = bf16(silu(h)) * bf16(A . W^T), h holding bf16(rms_2(x) . W_fc1^T) from a llj_gemm_linear
+ * pass (model.py:258; two passes instead of a dual-weight tile). */
+int llj_gemm_silu_mul(int wfmt, const void* A, int lda, const void* W, const void* sz, void* h, int ldh, int M, int N,
+                      int K, void* stream);
+/* c_attn + split + RoPE(q, k) + KV-cache write for B*T pre-normalized rows x (as llj_norm_qkv_rope
+ * with norm_w NULL; model.py:204-228). */
+int llj_gemm_qkv_rope(int wfmt, const void* x, const void* W, const void* sz, void* q_out, void* kcache, void* vcache,
+                      const float* rope, const int* pos, int B, int T, int C, int n_head, int S, void* stream);
+
 /* ---------------------------------------------------------------- LLM.int8() */
 /* Bytes of the activation-statistics workspace for an (M, K) activation (host function). */
 size_t llj_i8_ws_bytes(int M, int K);

@@ -1,0 +1,301 @@
+// Prefill GEMM (many rows: a prompt / a perplexity window) for gfx950, the compute-bound
+// regime of the same Linear layers the decode GEMVs stream (gemv_impl.h).
+//
+// Replaces, for M >> 16 rows: reference lit_llama/quantization.py:282-331
+// (qlinear_4bit_weight / Triton linear_kernel_4bit_weight, which pads M to 256 and runs an
+// autotuned tl.dot GEMM) and torch.nn.Linear (F.linear) of the bf16 model, with the block's
+// elementwise work in the epilogue: model.py:204-228 (c_attn split, RoPE, KV-cache write),
+// :172-173 (residual adds), :258 (silu(c_fc1) * c_fc2).
+//
+// Tiling: a 256-thread workgroup owns a 128 x 128 output tile and walks K in 128-deep chunks;
+// the chunk's A tile (128 rows x 128 k bf16) and B tile (W4P: the eight 1 KiB W4P tiles of its
+// 128 columns; bf16: 128 rows x 128 k) are staged through double-buffered LDS (one barrier per
+// chunk: the loads of chunk c + 1 are in flight while chunk c is multiplied). The 4 waves form
+// a 2 x 2 grid of 64 x 64 sub-tiles = 4 x 4 MFMA 16x16x32 bf16 accumulators each. int4 codes
+// are dequantized from LDS into bf16 (128 + q) with one v_and_or_b32 per pair (the W4P lane
+// layout is the MFMA B fragment, as in the GEMV); the 128 + zero offset is removed in the
+// epilogue with the row sums of A, accumulated while the A tile is staged:
+//   y[m,n] = s[n] * (sum_k A[m,k] (128 + q[k,n]) - (128 + z[n]) * sum_k A[m,k]).
+// Tile order is XCD-aware: the 8 XCDs take contiguous ranges of tiles, n fastest inside a
+// range, so an XCD's L2 keeps one 128-row A panel while it sweeps the weight columns.
+#include "common.h"
+#include "lit_llama_amd.h"
+
+namespace llj {
+
+enum : int { GWF_W4 = 0, GWF_BF16 = 1 };
+enum : int { GEP_STORE = 0, GEP_RESID = 1, GEP_QKV = 2, GEP_SILU_MUL = 3 };
+
+struct GemmParams {
+  const bf16_t* A;  // (M, K) rows with stride lda
+  int lda;
+  int M, N, K;
+  const void* W;      // GWF_W4: W4P tiles; GWF_BF16: (N, K) bf16 row-major
+  const float2* sz;   // GWF_W4: per column (scale, 128 + zero)
+  bf16_t* C;          // STORE: out; RESID: residual (updated); SILU_MUL: h (holds bf16 fc1 output)
+  int ldc;
+  // GEP_QKV
+  bf16_t* q_out;
+  bf16_t* kcache;
+  bf16_t* vcache;
+  const float* rope;
+  const int* pos;
+  int n_head, head_size, S, T;
+};
+
+constexpr int kGBM = 128, kGBN = 128, kGBK = 128, kGNT = 256;
+constexpr int kAP = kGBK + 8;  // A / bf16-B LDS row pitch (elements): 272 B, conflict-free 16-B reads
+
+template <int WF>
+constexpr size_t gemm_b_bytes() { return WF == GWF_W4 ? (size_t)kGBN * kGBK / 2 : (size_t)kGBN * kAP * 2; }
+template <int WF>
+constexpr size_t gemm_lds_bytes() {
+  return 2 * ((size_t)kGBM * kAP * 2 + gemm_b_bytes<WF>()) + kGBM * sizeof(float);
+}
+
+template <int WF, int EP>
+__global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave & 1, wc = wave >> 1;
+  const int row = lane & 15, g = lane >> 4;
+  const int M = p.M, K = p.K, KC = K / kGBK;
+  const int mtiles = (M + kGBM - 1) / kGBM, ntiles = p.N / kGBN;
+  const int total = mtiles * ntiles;
+  int t = blockIdx.x;
+  if (total % 8 == 0) t = (t % 8) * (total / 8) + t / 8;  // contiguous tile range per XCD
+  const int nb = t % ntiles, mb = t / ntiles;            // n fastest: the A panel stays in L2
+  const int m0 = mb * kGBM, n0 = nb * kGBN;
+
+  // LDS: [A buf 0][A buf 1][B buf 0][B buf 1][row sums]
+  constexpr size_t kAB = (size_t)kGBM * kAP * 2, kBB = gemm_b_bytes<WF>();
+  auto As = [&](int b) { return reinterpret_cast<bf16_t*>(smem + b * kAB); };
+  auto Bs = [&](int b) { return smem + 2 * kAB + b * kBB; };
+  float* rs_lds = reinterpret_cast<float*>(smem + 2 * (kAB + kBB));
+
+  // ---- staging: thread -> (A row, half of the 256-B chunk row); B: W4 2 x 16 B, bf16 8 x 16 B
+  const int ar = tid >> 1, ah = tid & 1;
+  const int agm = m0 + ar < M ? m0 + ar : M - 1;  // rows past M: a clamped copy, never stored
+  const bf16_t* asrc = p.A + (size_t)agm * p.lda + ah * 64;
+  u32x4 areg[8], breg[8];
+  auto load_chunk = [&](int c) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) areg[v] = *reinterpret_cast<const u32x4*>(asrc + (size_t)c * kGBK + 8 * v);
+    if constexpr (WF == GWF_W4) {
+      // the 8 W4P tiles (16 columns x 128 k, 1 KiB each) of columns n0 .. n0 + 127, chunk c
+      const u32x4* w = reinterpret_cast<const u32x4*>(p.W);
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const int idx = tid + kGNT * v;  // 0..511: tile idx >> 6, lane idx & 63
+        const size_t nt = (size_t)(n0 / 16 + (idx >> 6));
+        breg[v] = __builtin_nontemporal_load(w + (nt * KC + c) * 64 + (idx & 63));
+      }
+    } else {
+      const bf16_t* w = reinterpret_cast<const bf16_t*>(p.W) + (size_t)(n0 + ar) * K + (size_t)c * kGBK + ah * 64;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) breg[v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w + 8 * v));
+    }
+  };
+  float rsum = 0.f;  // this thread's share of sum_k A[ar, k]
+  auto store_chunk = [&](int buf) {
+    bf16_t* a = As(buf) + ar * kAP + ah * 64;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      *reinterpret_cast<u32x4*>(a + 8 * v) = areg[v];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rsum += bflo(areg[v][i]) + bfhi(areg[v][i]);
+    }
+    if constexpr (WF == GWF_W4) {
+#pragma unroll
+      for (int v = 0; v < 2; ++v) reinterpret_cast<u32x4*>(Bs(buf))[tid + kGNT * v] = breg[v];
+    } else {
+      bf16_t* b = reinterpret_cast<bf16_t*>(Bs(buf)) + ar * kAP + ah * 64;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) *reinterpret_cast<u32x4*>(b + 8 * v) = breg[v];
+    }
+  };
+
+  uint32_t msk = 0x000F000Fu, mag = 0x43004300u;
+  asm volatile("" : "+s"(msk));
+  asm volatile("" : "+v"(mag));
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_chunk(0);
+  for (int c = 0; c < KC; ++c) {
+    const int buf = c & 1;
+    store_chunk(buf);
+    __syncthreads();  // chunk c staged; every wave is done with chunk c - 1's buffer
+    if (c + 1 < KC) load_chunk(c + 1);
+    const bf16_t* a = As(buf);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {  // MFMA k-steps of the chunk
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wr * 64 + 16 * i + row;
+        const int k = WF == GWF_W4 ? 32 * g + 8 * s : 32 * s + 8 * g;  // W4P k order, as the GEMV
+        af[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(a + r * kAP + k));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (WF == GWF_W4) {
+          const u32x4 wv = reinterpret_cast<const u32x4*>(Bs(buf))[(wc * 4 + j) * 64 + lane];
+          const uint32_t w = wv[s];
+          const uint4 d = make_uint4(and_or(w, msk, mag), and_or(w >> 4, msk, mag), and_or(w >> 8, msk, mag),
+                                     and_or(w >> 12, msk, mag));
+          bfr[j] = __builtin_bit_cast(bf16x8, d);
+        } else {
+          const int n = wc * 64 + 16 * j + row;
+          bfr[j] = __builtin_bit_cast(
+              bf16x8, *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(Bs(buf)) + n * kAP + 32 * s + 8 * g));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+    }
+  }
+  // row sums of A (both halves of a row are adjacent lanes)
+  rsum += lane_xor1(rsum);
+  if (!ah) rs_lds[ar] = rsum;
+  __syncthreads();
+
+  // ---- epilogue: lane holds rows m0 + wr*64 + 16i + 4g + r, column n0 + wc*64 + 16j + row
+  const int Cd = p.n_head * p.head_size;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc * 64 + 16 * j + row;
+    float2 szn = make_float2(1.f, 0.f);
+    if constexpr (WF == GWF_W4) szn = p.sz[n];
+    const int nblk = n0 + wc * 64 + 16 * j;  // first column of this 16-column block
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ml = wr * 64 + 16 * i + 4 * g + r;
+        const int m = m0 + ml;
+        float y = acc[i][j][r];
+        if constexpr (WF == GWF_W4) y = szn.x * (y - szn.y * rs_lds[ml]);
+        const bool live = m < M;
+        if constexpr (EP == GEP_QKV) {
+          const float v = round_bf(y);  // c_attn output in bf16 (model.py:204), RoPE in fp32
+          const float partner = lane_xor1(v);
+          const int region = nblk / Cd;  // 0 q, 1 k, 2 v: uniform per 16-column block
+          const int nc = n - region * Cd;
+          const int h = nc / p.head_size, dd = nc % p.head_size;
+          const int mm = live ? m : M - 1;
+          const int b = mm / p.T, ps = p.pos[mm % p.T];
+          float out = v;
+          if (region < 2) {
+            const float2 cs = *reinterpret_cast<const float2*>(p.rope + ((size_t)ps * (p.head_size >> 1) + (dd >> 1)) * 2);
+            out = (dd & 1) ? (v * cs.x + partner * cs.y) : (v * cs.x - partner * cs.y);
+          }
+          const uint32_t ob = (uint32_t)f2bf(out);
+          const uint32_t pr = lane_xor1(ob);
+          if (live && !(dd & 1)) {
+            bf16_t* dst;
+            size_t ei;
+            if (region == 0) {
+              dst = p.q_out;
+              ei = (size_t)mm * Cd + nc;
+            } else {
+              const int slot = ps < p.S ? ps : ps % p.S;
+              dst = region == 1 ? p.kcache : p.vcache;
+              ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
+            }
+            *reinterpret_cast<uint32_t*>(dst + ei) = ob | (pr << 16);
+          }
+        } else {
+          bf16_t* cp = p.C + (size_t)(live ? m : M - 1) * p.ldc + n;
+          float o;
+          if constexpr (EP == GEP_RESID) {
+            o = round_bf(bf2f(*cp) + round_bf(y));  // x + y in bf16 (model.py:172-173)
+          } else if constexpr (EP == GEP_SILU_MUL) {
+            const float a1 = bf2f(*cp);  // bf16(c_fc1 x), stored by the first pass
+            const float sl = round_bf(a1 / (1.f + __expf(-a1)));  // F.silu in bf16
+            o = sl * round_bf(y);
+          } else {
+            o = y;
+          }
+          const uint32_t ob = (uint32_t)f2bf(o);
+          const uint32_t pr = lane_xor1(ob);
+          if (live && !(row & 1)) *reinterpret_cast<uint32_t*>(cp) = ob | (pr << 16);
+        }
+      }
+    }
+  }
+}
+
+template <int WF, int EP>
+static int gemm_launch(const GemmParams& p, hipStream_t s) {
+  auto kern = gemm_kernel<WF, EP>;
+  static bool attr_set = false;  // per instantiation, before any graph capture
+  const size_t lds = gemm_lds_bytes<WF>();
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  const int tiles = ((p.M + kGBM - 1) / kGBM) * (p.N / kGBN);
+  hipLaunchKernelGGL(kern, dim3(tiles), dim3(kGNT), lds, s, p);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int EP>
+static int gemm_run(int wfmt, GemmParams& p, void* stream) {
+  if (p.M < 1 || p.N % kGBN || p.K % kGBK || p.K < kGBK || (p.lda & 7)) return LLJ_EINVAL;
+  if (EP != GEP_QKV && (!p.C || (p.ldc & 1))) return LLJ_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (wfmt == GWF_W4) return p.sz ? gemm_launch<GWF_W4, EP>(p, s) : LLJ_EINVAL;
+  if (wfmt == GWF_BF16) return gemm_launch<GWF_BF16, EP>(p, s);
+  return LLJ_EINVAL;
+}
+
+}  // namespace llj
+
+using namespace llj;
+
+extern "C" {
+
+int llj_gemm_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, void* C, int ldc, int M, int N,
+                    int K, void* stream) {
+  GemmParams p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = W; p.sz = (const float2*)sz;
+  p.C = (bf16_t*)C; p.ldc = ldc;
+  return gemm_run<GEP_STORE>(wfmt, p, stream);
+}
+
+int llj_gemm_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M, int N,
+                   int K, void* stream) {
+  GemmParams p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = W; p.sz = (const float2*)sz;
+  p.C = (bf16_t*)x; p.ldc = ldx;
+  return gemm_run<GEP_RESID>(wfmt, p, stream);
+}
+
+int llj_gemm_silu_mul(int wfmt, const void* A, int lda, const void* W, const void* sz, void* h, int ldh, int M, int N,
+                      int K, void* stream) {
+  GemmParams p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = W; p.sz = (const float2*)sz;
+  p.C = (bf16_t*)h; p.ldc = ldh;
+  return gemm_run<GEP_SILU_MUL>(wfmt, p, stream);
+}
+
+int llj_gemm_qkv_rope(int wfmt, const void* x, const void* W, const void* sz, void* q_out, void* kcache, void* vcache,
+                      const float* rope, const int* pos, int B, int T, int C, int n_head, int S, void* stream) {
+  if (B < 1 || T < 1 || n_head < 1 || C % n_head || S < 1 || !pos || !rope) return LLJ_EINVAL;
+  GemmParams p{};
+  p.A = (const bf16_t*)x; p.lda = C; p.M = B * T; p.N = 3 * C; p.K = C; p.W = W; p.sz = (const float2*)sz;
+  p.q_out = (bf16_t*)q_out; p.kcache = (bf16_t*)kcache; p.vcache = (bf16_t*)vcache; p.rope = rope; p.pos = pos;
+  p.n_head = n_head; p.head_size = C / n_head; p.S = S; p.T = T;
+  if (p.head_size & 1 || C % 16) return LLJ_EINVAL;
+  return gemm_run<GEP_QKV>(wfmt, p, stream);
+}
+
+}  // extern "C"

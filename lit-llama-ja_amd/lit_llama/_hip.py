@@ -43,6 +43,10 @@ SIGNATURES = {
     "llj_argmax": [_P, _I, _I, _I, _P, _P, _I, _P, _P],
     "llj_sample": [_P, _I, _I, _I, _F, _I, _P, ctypes.c_ulonglong, _P, _P, _I, _P, _P],
     "llj_set_tpw_max": [_I],
+    "llj_gemm_linear": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
+    "llj_gemm_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
+    "llj_gemm_silu_mul": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
+    "llj_gemm_qkv_rope": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
 }
 
 _lib = None

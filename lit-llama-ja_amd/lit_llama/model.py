@@ -106,6 +106,13 @@ PRE_NORM_ROWS = True
 PRE_NORM_MIN_M = 2  # smallest batch that takes the separate launch (measured best from bs=2 on)
 
 
+# prefill / no-cache calls with at least this many rows (B * T) run the MFMA-tiled GEMMs
+# (llj_gemm_*) instead of the weight-streaming GEMVs in 8 / 16-row slices, when every Linear of
+# the model is int4 W4P or bf16 and the shapes tile by 128 (LLM.int8 and gptq.int8 keep the
+# GEMV slices)
+GEMM_MIN_ROWS = 32
+_GEMM_FMTS = (0, 1)
+
 # weight formats whose kernels remove the nibble offset with the row sums of A (W4P, W8P)
 _ROWSUM_FMTS = (0, 3)
 
@@ -129,9 +136,10 @@ def _wspec(lin: nn.Module):
 class _Work:
     """Per-call scratch for M rows (allocated from torch's caching allocator)."""
 
-    def __init__(self, cfg: LLaMAConfig, M: int, device, need_i8: bool, S: int = 0):
+    def __init__(self, cfg: LLaMAConfig, M: int, device, need_i8: bool, S: int = 0, gemm: bool = False):
         C, H = cfg.n_embd, MLP.hidden(cfg)
         bf = torch.bfloat16
+        self.gemm = gemm  # many rows: the prefill GEMMs (LLaMA._blocks_gemm)
         self.x = torch.empty(M, C, dtype=bf, device=device)
         self.q = torch.empty(M, C, dtype=bf, device=device)
         self.y = torch.empty(M, C, dtype=bf, device=device)
@@ -139,7 +147,7 @@ class _Work:
         # batched rows (M >= 2): each RMSNorm runs once (llj_rmsnorm_rows -> xn, rs = fp32 row
         # sums for the int4 offset term) instead of inside every norm-fused GEMV workgroup
         self.pre = M >= max(2, PRE_NORM_MIN_M) and not need_i8 and PRE_NORM_ROWS
-        self.xn = torch.empty(M, C, dtype=bf, device=device) if (need_i8 or self.pre) else None
+        self.xn = torch.empty(M, C, dtype=bf, device=device) if (need_i8 or self.pre or gemm) else None
         self.rs = torch.empty(M, dtype=torch.float32, device=device) if self.pre else None
         if need_i8:
             L = _hip.lib()
@@ -259,7 +267,7 @@ class LLaMA(nn.Module):
         dev = idx.device
         specs = self._layer_specs()
         need_i8 = any(s[0] == 2 for layer in specs["layers"] for s in layer) or specs["head"][0] == 2
-        w = _Work(cfg, M, dev, need_i8, S)
+        w = _Work(cfg, M, dev, need_i8, S, gemm=self._gemm_ok(specs, M))
         st = _hip.stream()
         ids = idx.reshape(-1).to(torch.int32)
         _hip.call("llj_embedding", ids.data_ptr(), self.transformer.wte.weight.data_ptr(), w.x.data_ptr(), M,
@@ -288,12 +296,49 @@ class LLaMA(nn.Module):
     def _i8_prep(self, A, M, K, w, st):
         _hip.call("llj_i8_stats", A.data_ptr(), A.stride(0), M, K, Linear8bitLtThreshold, w.i8ws.data_ptr(), st)
 
+    def _gemm_ok(self, specs, M):
+        cfg = self.config
+        C, H = cfg.n_embd, MLP.hidden(cfg)
+        fmts = {s[0] for layer in specs["layers"] for s in layer}
+        return (M >= GEMM_MIN_ROWS and fmts <= set(_GEMM_FMTS) and C % 128 == 0 and H % 128 == 0
+                and specs["head"][0] in _GEMM_FMTS)
+
+    def _blocks_gemm(self, w, specs, kv, pos, B, T, S, st):
+        """The n_layer blocks for many rows through the prefill GEMMs (csrc/gemm.hip): per layer
+        rms_1 (llj_rmsnorm_rows) -> c_attn + RoPE + KV write -> attention -> c_proj + residual ->
+        rms_2 -> c_fc1, then c_fc2 with the silu * mul epilogue -> mlp.c_proj + residual."""
+        cfg = self.config
+        C, H, nh = cfg.n_embd, MLP.hidden(cfg), cfg.n_head
+        M = B * T
+        P = _hip.ptr
+        for i, blk in enumerate(self.transformer.h):
+            (fa, wa, sa), (fp, wp, sp), (f1, w1, s1), (f2, w2, s2), (fd, wd, sd) = specs["layers"][i]
+            kc, vc = kv[i]
+            _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps, w.xn.data_ptr(),
+                      None, M, C, st)
+            _hip.call("llj_gemm_qkv_rope", fa, w.xn.data_ptr(), wa.data_ptr(), P(sa), w.q.data_ptr(), kc.data_ptr(),
+                      vc.data_ptr(), self.rope_cache.data_ptr(), pos.data_ptr(), B, T, C, nh, S, st)
+            if w.att_ws is not None:
+                _hip.call("llj_attention_split", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                          pos.data_ptr(), B, T, nh, C // nh, S, w.nsplit, w.att_ws.data_ptr(), st)
+            else:
+                _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                          pos.data_ptr(), B, T, nh, C // nh, S, st)
+            _hip.call("llj_gemm_resid", fp, w.y.data_ptr(), C, wp.data_ptr(), P(sp), w.x.data_ptr(), C, M, C, C, st)
+            _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(),
+                      None, M, C, st)
+            _hip.call("llj_gemm_linear", f1, w.xn.data_ptr(), C, w1.data_ptr(), P(s1), w.h.data_ptr(), H, M, H, C, st)
+            _hip.call("llj_gemm_silu_mul", f2, w.xn.data_ptr(), C, w2.data_ptr(), P(s2), w.h.data_ptr(), H, M, H, C, st)
+            _hip.call("llj_gemm_resid", fd, w.h.data_ptr(), H, wd.data_ptr(), P(sd), w.x.data_ptr(), C, M, C, H, st)
+
     def _blocks(self, w, specs, kv, pos, B, T, S, st):
         cfg = self.config
         C, H, nh = cfg.n_embd, MLP.hidden(cfg), cfg.n_head
         M = B * T
         rope = self.rope_cache
         P = _hip.ptr
+        if w.gemm:
+            return self._blocks_gemm(w, specs, kv, pos, B, T, S, st)
         for i, blk in enumerate(self.transformer.h):
             (fa, wa, sa), (fp, wp, sp), (f1, w1, s1), (f2, w2, s2), (fd, wd, sd) = specs["layers"][i]
             kc, vc = kv[i]
@@ -368,6 +413,12 @@ class LLaMA(nn.Module):
             _hip.call("llj_rmsnorm", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), M, C, st)
             self._i8_prep(xn, M, C, w, st)
             src, nw = xn, None
+        elif M >= GEMM_MIN_ROWS and f in _GEMM_FMTS and C % 128 == 0 and V % 128 == 0:  # many rows: GEMM
+            xn = torch.empty_like(x)
+            _hip.call("llj_rmsnorm_rows", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), None, M, C, st)
+            _hip.call("llj_gemm_linear", f, xn.data_ptr(), C, W.data_ptr(), _hip.ptr(sz), out.data_ptr(), out.stride(0),
+                      M, V, C, st)
+            return
         elif M >= 2 and w.pre:  # batched rows: normalize once (see _Work.pre)
             xn = torch.empty_like(x)
             rs = torch.empty(M, dtype=torch.float32, device=x.device) if f in _ROWSUM_FMTS else None

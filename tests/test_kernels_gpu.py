@@ -625,3 +625,77 @@ def test_sample_device_rng_distribution(hip):
     call(hip, "llj_sample", L.data_ptr(), V, M, V, temp, k, None, 1234, out2.data_ptr(), None, 0, pos.data_ptr(), st())
     torch.cuda.synchronize()
     assert (out2.cpu().numpy() != draws).mean() > 0.3
+
+
+@pytest.mark.parametrize("wfmt", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(17, 256, 128), (100, 4096, 4096), (300, 11008, 4096), (256, 4096, 11008),
+                                   (129, 384, 1024)])
+def test_gemm_linear_and_resid(hip, wfmt, M, N, K):
+    """Prefill GEMM (llj_gemm_linear / llj_gemm_resid, MFMA 128 x 128 tiles) against the oracle:
+    int4 W4P with the row-sum offset removal and bf16 weights, ragged M (rows past M are never
+    stored), 7B shapes."""
+    rng = np.random.default_rng(M + N + K + wfmt)
+    Wref, Wd, szd = quant_operands(hip, rng, wfmt, N, K)
+    x = bf16(rng.standard_normal((M, K)).astype(np.float32))
+    xd = T(x, torch.bfloat16)
+    out = torch.full((M + 1, N), 7.0, dtype=torch.bfloat16, device=dev)  # row M: canary
+    call(hip, "llj_gemm_linear", wfmt, xd.data_ptr(), K, Wd.data_ptr(), None if szd is None else szd.data_ptr(),
+         out.data_ptr(), N, M, N, K, st())
+    x0 = bf16(rng.standard_normal((M, N)).astype(np.float32))
+    xr = T(x0, torch.bfloat16)
+    call(hip, "llj_gemm_resid", wfmt, xd.data_ptr(), K, Wd.data_ptr(), None if szd is None else szd.data_ptr(),
+         xr.data_ptr(), N, M, N, K, st())
+    torch.cuda.synchronize()
+    y = x @ Wref.T
+    o = out.float().cpu().numpy()
+    assert_bf16_close(o[:M], y, f"gemm wfmt={wfmt} M={M} N={N} K={K}")
+    assert (o[M] == 7.0).all(), "wrote past row M"
+    assert_bf16_close(xr.float().cpu().numpy(), x0 + bf16(y), f"gemm resid wfmt={wfmt}")
+
+
+@pytest.mark.parametrize("wfmt", [0, 1])
+def test_gemm_swiglu_two_pass(hip, wfmt):
+    """c_fc1 into h (llj_gemm_linear), then c_fc2 with the silu * mul epilogue in place
+    (llj_gemm_silu_mul): model.py:258 with the reference's bf16 rounding points."""
+    rng = np.random.default_rng(70 + wfmt)
+    M, C, H = 150, 1024, 2816
+    W1, W1d, s1 = quant_operands(hip, rng, wfmt, H, C)
+    W2, W2d, s2 = quant_operands(hip, rng, wfmt, H, C)
+    x = bf16(rng.standard_normal((M, C)).astype(np.float32))
+    xd = T(x, torch.bfloat16)
+    h = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    call(hip, "llj_gemm_linear", wfmt, xd.data_ptr(), C, W1d.data_ptr(), P(s1), h.data_ptr(), H, M, H, C, st())
+    call(hip, "llj_gemm_silu_mul", wfmt, xd.data_ptr(), C, W2d.data_ptr(), P(s2), h.data_ptr(), H, M, H, C, st())
+    torch.cuda.synchronize()
+    hexp = bf16(bf16(O.silu(bf16(x @ W1.T))) * bf16(x @ W2.T))
+    assert_bf16_close(h.float().cpu().numpy(), hexp, f"gemm swiglu wfmt={wfmt}", rel=3e-2)
+
+
+@pytest.mark.parametrize("wfmt", [0, 1])
+@pytest.mark.parametrize("B,T_,nh,hs", [(1, 200, 32, 128), (3, 40, 4, 64)])
+def test_gemm_qkv_rope_kv(hip, wfmt, B, T_, nh, hs):
+    """llj_gemm_qkv_rope: c_attn + RoPE + KV-cache write for a whole prompt (ring slots p % S)."""
+    rng = np.random.default_rng(B * T_ + wfmt)
+    C, S = nh * hs, 256
+    M = B * T_
+    x = bf16(rng.standard_normal((M, C)).astype(np.float32))
+    rope = O.build_rope_cache(512, hs)
+    pos = np.arange(5, 5 + T_, dtype=np.int32)
+    Wref, Wd, szd = quant_operands(hip, rng, wfmt, 3 * C, C)
+    q = torch.zeros(M, C, dtype=torch.bfloat16, device=dev)
+    kc = torch.zeros(B, nh, S, hs, dtype=torch.bfloat16, device=dev)
+    vc = torch.zeros_like(kc)
+    xd, rd, pd = T(x, torch.bfloat16), T(rope), T(pos)
+    call(hip, "llj_gemm_qkv_rope", wfmt, xd.data_ptr(), Wd.data_ptr(), None if szd is None else szd.data_ptr(),
+         q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rd.data_ptr(), pd.data_ptr(), B, T_, C, nh, S, st())
+    torch.cuda.synchronize()
+    qkv = bf16(x @ Wref.T)
+    qe = O.apply_rope(qkv[:, :C].reshape(B, T_, nh, hs), rope[pos]).reshape(M, C)
+    ke = O.apply_rope(qkv[:, C:2 * C].reshape(B, T_, nh, hs), rope[pos])
+    ve = qkv[:, 2 * C:].reshape(B, T_, nh, hs)
+    assert_bf16_close(q.float().cpu().numpy(), qe, "gemm q")
+    kcn, vcn = kc.float().cpu().numpy(), vc.float().cpu().numpy()
+    slots = pos % S
+    assert_bf16_close(kcn[:, :, slots].transpose(0, 2, 1, 3), ke, "gemm k cache")
+    assert_bf16_close(vcn[:, :, slots].transpose(0, 2, 1, 3), ve, "gemm v cache")
