@@ -89,6 +89,13 @@ int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, co
 int llj_attention(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
                   int n_head, int head_size, int S, void* stream);
 
+/* Causal attention of T prompt rows per sequence on the MFMA units (flash-style: 64-query x
+ * 64-key tiles, online softmax; csrc/attention_prefill.hip): query t of sequence b sits at position
+ * pos[0] + t and attends cache slots 0 .. pos[0] + t. Requires contiguous positions pos[t] = pos[0]
+ * + t with pos[0] + T <= S (no ring wrap; the caller checks). head_size 64 or 128. */
+int llj_attention_prefill(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                          int n_head, int head_size, int S, void* stream);
+
 /* Split-K form of llj_attention for long caches: the valid keys of every (row, head) split into
  * nsplit equal ranges, one block each, writing unnormalized partials (outputs, max, sum) into
  * part_ws (llj_attention_ws_bytes(B*T, n_head, head_size, nsplit) bytes), merged in split order

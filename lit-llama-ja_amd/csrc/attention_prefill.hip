@@ -1,0 +1,196 @@
+// Causal attention of a whole prompt / perplexity window (T query rows per sequence) on the
+// MFMA units: the prefill / no-cache path of reference model.py:237 (F.scaled_dot_product_attention
+// with the tril mask rows of positions p0 .. p0 + T - 1, model.py:101-104), flash-style (online
+// softmax over 64-key tiles, nothing of size T x T is materialized).
+//
+// One 256-thread workgroup per (64-query block, head, sequence); wave w owns queries
+// 16w .. 16w + 15 of the block. Everything is computed transposed so that no operand needs a
+// register transpose: S^T = K . Q^T (MFMA 16x16x32 bf16; A = K rows from LDS, B = the wave's Q
+// fragments held in registers for the whole walk), so a lane's accumulator column is its query
+// and the softmax statistics are per-lane; P^T goes straight from the S^T accumulators into the
+// B operand of O^T = V^T . P^T (the 32-key MFMA step's k order is chosen as
+// key = 4 g + (j & 3) + 16 (j >> 2) in each of its two 16-key halves, which is exactly what lane
+// group g holds), with V^T staged in LDS at load time. Keys are the cache slots 0 .. p of a query
+// at position p (no ring wrap: p0 + T <= S, checked by the caller), masked on the diagonal tile.
+#include "common.h"
+#include "lit_llama_amd.h"
+
+namespace llj {
+
+constexpr int kFQ = 64;   // queries per workgroup
+constexpr int kFK = 64;   // keys per tile
+constexpr int kVtP = 72;  // V^T LDS row pitch (keys): 144 B, 8-B aligned, spreads the d rows over banks
+
+template <int HS>
+__global__ __launch_bounds__(256) void flash_prefill_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+                                                            const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
+                                                            const int* __restrict__ pos, int T, int S, int nh,
+                                                            float sl2) {
+  constexpr int KP = HS + 8;  // K tile pitch (elements)
+  constexpr int KS = HS / 32;  // MFMA k-steps over the head dim
+  constexpr int DB = HS / 16;  // 16-row output blocks of O^T
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[kFK * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t Vt[HS * kVtP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int qb = gridDim.x - 1 - blockIdx.x;  // long (late) query blocks first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int C = nh * HS;
+  const int p0 = pos[0];
+  const int t = qb * kFQ + wave * 16 + col;  // this lane's query row
+  const int tq = t < T ? t : T - 1;
+  const int qpos = p0 + t;  // its position (rows past T are computed on a copy, never stored)
+  // Q^T fragments: lane holds Q[t][32 kk + 8 g .. + 8]
+  u32x4 qf[KS];
+  const bf16_t* qrow = q + ((size_t)b * T + tq) * C + h * HS;
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) qf[kk] = *reinterpret_cast<const u32x4*>(qrow + 32 * kk + 8 * g);
+  const int tlast = min(T, qb * kFQ + kFQ) - 1;
+  const int kmax = p0 + tlast;  // last key any query of the block attends
+  const int ntile = kmax / kFK + 1;
+  const bf16_t* kbase = kc + ((size_t)(b * nh + h) * S) * HS;
+  const bf16_t* vbase = vc + ((size_t)(b * nh + h) * S) * HS;
+  // staging map: 64 keys x HS/8 vectors = 64 * HS / 8 16-B pieces over 256 threads
+  constexpr int PV = kFK * HS / 8 / 256;
+  u32x4 kreg[PV], vreg[PV];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < PV; ++i) {
+      const int piece = tid + 256 * i;
+      const int key = piece / (HS / 8), v8 = piece % (HS / 8);
+      int slot = kt * kFK + key;
+      slot = slot <= kmax ? slot : kmax;  // clamped: masked below
+      kreg[i] = *reinterpret_cast<const u32x4*>(kbase + (size_t)slot * HS + 8 * v8);
+      vreg[i] = *reinterpret_cast<const u32x4*>(vbase + (size_t)slot * HS + 8 * v8);
+    }
+  };
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 acc_o[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d) acc_o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load_tile(0);
+  for (int kt = 0; kt < ntile; ++kt) {
+    __syncthreads();  // the previous tile's readers are done with Ks / Vt
+#pragma unroll
+    for (int i = 0; i < PV; ++i) {
+      const int piece = tid + 256 * i;
+      const int key = piece / (HS / 8), v8 = piece % (HS / 8);
+      *reinterpret_cast<u32x4*>(Ks + key * KP + 8 * v8) = kreg[i];
+      const u32x4 vv = vreg[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // V^T: element (key, d) at Vt[d * kVtP + key]
+        Vt[(8 * v8 + 2 * e) * kVtP + key] = (bf16_t)(vv[e] & 0xFFFFu);
+        Vt[(8 * v8 + 2 * e + 1) * kVtP + key] = (bf16_t)(vv[e] >> 16);
+      }
+    }
+    __syncthreads();
+    if (kt + 1 < ntile) load_tile(kt + 1);  // in flight during this tile's MFMAs
+    // S^T = K . Q^T for the tile's four 16-key blocks
+    f32x4 s[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Ks + (16 * j + col) * KP + 32 * kk + 8 * g));
+        s[j] = mfma_bf16(a, __builtin_bit_cast(bf16x8, qf[kk]), s[j]);
+      }
+    }
+    // mask (key slot > query position) and scale into log2 units; per-query max
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * kFK + 16 * j + 4 * g + r;
+        const float v = key <= qpos ? s[j][r] * sl2 : -INFINITY;
+        s[j][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    {  // max over the 4 lane groups holding this query's keys (lanes col, col+16, col+32, col+48)
+      float lo, hi;
+      lane_halves<false>(mx, lo, hi);
+      mx = fmaxf(lo, hi);
+      lane_halves<true>(mx, lo, hi);
+      mx = fmaxf(lo, hi);
+    }
+    const float m_new = fmaxf(m_run, mx);
+    const float corr = m_run == -INFINITY ? 0.f : exp2f(m_run - m_new);
+    float psum = 0.f;
+    uint32_t pb[4][2];  // bf16 P^T pairs per key block: (r0, r1), (r2, r3)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float pr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pr[r] = s[j][r] == -INFINITY ? 0.f : exp2f(s[j][r] - m_new);
+        psum += pr[r];
+      }
+      pb[j][0] = pack2bf(pr[0], pr[1]);
+      pb[j][1] = pack2bf(pr[2], pr[3]);
+    }
+    {
+      float lo, hi;
+      lane_halves<false>(psum, lo, hi);
+      psum = lo + hi;
+      lane_halves<true>(psum, lo, hi);
+      psum = lo + hi;
+    }
+    l_run = l_run * corr + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int d = 0; d < DB; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc_o[d][r] *= corr;
+    // O^T += V^T . P^T, two 32-key steps
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const u32x4 bw = {pb[2 * u][0], pb[2 * u][1], pb[2 * u + 1][0], pb[2 * u + 1][1]};
+      const bf16x8 bfrag = __builtin_bit_cast(bf16x8, bw);
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        const bf16_t* vr = Vt + (16 * d + col) * kVtP + 32 * u + 4 * g;
+        const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+        const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+        const u32x4 aw = {lo.x, lo.y, hi.x, hi.y};
+        acc_o[d] = mfma_bf16(__builtin_bit_cast(bf16x8, aw), bfrag, acc_o[d]);
+      }
+    }
+  }
+  // y[b*T + t][h*HS + d] = O / l; lane holds d = 16 db + 4 g + r of its query
+  if (t < T) {
+    const float inv = 1.f / l_run;
+    bf16_t* yrow = y + ((size_t)b * T + t) * C + h * HS;
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+      const uint2 o = make_uint2(pack2bf(acc_o[d][0] * inv, acc_o[d][1] * inv), pack2bf(acc_o[d][2] * inv, acc_o[d][3] * inv));
+      *reinterpret_cast<uint2*>(yrow + 16 * d + 4 * g) = o;
+    }
+  }
+}
+
+}  // namespace llj
+
+using namespace llj;
+
+extern "C" {
+
+int llj_attention_prefill(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                          int n_head, int head_size, int S, void* stream) {
+  LLJ_REQUIRE(B > 0 && T > 0 && n_head > 0 && S > 0 && pos);
+  const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
+  const dim3 grid((T + kFQ - 1) / kFQ, n_head, B);
+  hipStream_t st = (hipStream_t)stream;
+  if (head_size == 128)
+    hipLaunchKernelGGL(flash_prefill_kernel<128>, grid, dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)kcache,
+                       (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
+  else if (head_size == 64)
+    hipLaunchKernelGGL(flash_prefill_kernel<64>, grid, dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)kcache,
+                       (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
+  else
+    return LLJ_EINVAL;
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

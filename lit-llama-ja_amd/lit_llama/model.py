@@ -95,6 +95,11 @@ ATTN_SPLIT_MIN_S = 512
 ATTN_SPLIT_KEYS = 256  # 7B bs=1 at p = 2000 (S = 2048): 33.1 us one block, 14.4 us in 8 ranges
 
 
+# prompts of at least this many tokens run the MFMA flash attention (llj_attention_prefill) when
+# their positions are contiguous and do not wrap the ring
+FLASH_MIN_T = 32
+
+
 def attn_splits(S: int) -> int:
     """key ranges per (row, head) for a cache of S slots (1 = the one-block attention)."""
     if S < ATTN_SPLIT_MIN_S:
@@ -140,6 +145,7 @@ class _Work:
         C, H = cfg.n_embd, MLP.hidden(cfg)
         bf = torch.bfloat16
         self.gemm = gemm  # many rows: the prefill GEMMs (LLaMA._blocks_gemm)
+        self.flash = False  # T-row prompt attention on the MFMA flash kernel (set by LLaMA._run)
         self.x = torch.empty(M, C, dtype=bf, device=device)
         self.q = torch.empty(M, C, dtype=bf, device=device)
         self.y = torch.empty(M, C, dtype=bf, device=device)
@@ -268,6 +274,7 @@ class LLaMA(nn.Module):
         specs = self._layer_specs()
         need_i8 = any(s[0] == 2 for layer in specs["layers"] for s in layer) or specs["head"][0] == 2
         w = _Work(cfg, M, dev, need_i8, S, gemm=self._gemm_ok(specs, M))
+        w.flash = self._flash_ok(pos, T, S)
         st = _hip.stream()
         ids = idx.reshape(-1).to(torch.int32)
         _hip.call("llj_embedding", ids.data_ptr(), self.transformer.wte.weight.data_ptr(), w.x.data_ptr(), M,
@@ -296,6 +303,29 @@ class LLaMA(nn.Module):
     def _i8_prep(self, A, M, K, w, st):
         _hip.call("llj_i8_stats", A.data_ptr(), A.stride(0), M, K, Linear8bitLtThreshold, w.i8ws.data_ptr(), st)
 
+    def _flash_ok(self, pos, T, S):
+        """prompt rows attend through the flash kernel: T >= FLASH_MIN_T, head_size 64 / 128,
+        positions contiguous and inside the cache without wrapping (one host read of pos; prompts
+        only, never inside a captured decode step)."""
+        hs = self.config.n_embd // self.config.n_head
+        if T < FLASH_MIN_T or hs not in (64, 128):
+            return False
+        p = pos.cpu()
+        return bool((p[1:] - p[:-1] == 1).all()) and int(p[0]) + T <= S
+
+    def _attention(self, w, kc, vc, pos, B, T, S, st):
+        cfg = self.config
+        C, nh = cfg.n_embd, cfg.n_head
+        if w.flash:
+            _hip.call("llj_attention_prefill", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                      pos.data_ptr(), B, T, nh, C // nh, S, st)
+        elif w.att_ws is not None:
+            _hip.call("llj_attention_split", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                      pos.data_ptr(), B, T, nh, C // nh, S, w.nsplit, w.att_ws.data_ptr(), st)
+        else:
+            _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                      pos.data_ptr(), B, T, nh, C // nh, S, st)
+
     def _gemm_ok(self, specs, M):
         cfg = self.config
         C, H = cfg.n_embd, MLP.hidden(cfg)
@@ -318,12 +348,7 @@ class LLaMA(nn.Module):
                       None, M, C, st)
             _hip.call("llj_gemm_qkv_rope", fa, w.xn.data_ptr(), wa.data_ptr(), P(sa), w.q.data_ptr(), kc.data_ptr(),
                       vc.data_ptr(), self.rope_cache.data_ptr(), pos.data_ptr(), B, T, C, nh, S, st)
-            if w.att_ws is not None:
-                _hip.call("llj_attention_split", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
-                          pos.data_ptr(), B, T, nh, C // nh, S, w.nsplit, w.att_ws.data_ptr(), st)
-            else:
-                _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
-                          pos.data_ptr(), B, T, nh, C // nh, S, st)
+            self._attention(w, kc, vc, pos, B, T, S, st)
             _hip.call("llj_gemm_resid", fp, w.y.data_ptr(), C, wp.data_ptr(), P(sp), w.x.data_ptr(), C, M, C, C, st)
             _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(),
                       None, M, C, st)
@@ -362,12 +387,7 @@ class LLaMA(nn.Module):
                           w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), B, T, C, nh,
                           S, r0, r, P(w.i8ws), P(rs), st)
             # 2. attention, 3. c_proj + residual
-            if w.att_ws is not None:
-                _hip.call("llj_attention_split", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
-                          pos.data_ptr(), B, T, nh, C // nh, S, w.nsplit, w.att_ws.data_ptr(), st)
-            else:
-                _hip.call("llj_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
-                          pos.data_ptr(), B, T, nh, C // nh, S, st)
+            self._attention(w, kc, vc, pos, B, T, S, st)
             self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st)
             # 4. rms_2 + fc1/fc2 + silu*mul
             if f1 != f2:
@@ -495,6 +515,9 @@ class _OneBlock:
 
     def _resid(self, *a):
         LLaMA._resid(self, *a)
+
+    def _attention(self, *a):
+        LLaMA._attention(self, *a)
 
 
 class CausalSelfAttention(nn.Module):

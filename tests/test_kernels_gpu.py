@@ -699,3 +699,23 @@ def test_gemm_qkv_rope_kv(hip, wfmt, B, T_, nh, hs):
     slots = pos % S
     assert_bf16_close(kcn[:, :, slots].transpose(0, 2, 1, 3), ke, "gemm k cache")
     assert_bf16_close(vcn[:, :, slots].transpose(0, 2, 1, 3), ve, "gemm v cache")
+
+
+@pytest.mark.parametrize("hs,nh,B,T_,S,p0", [(128, 4, 1, 200, 256, 0), (64, 4, 2, 130, 160, 17), (128, 2, 1, 64, 64, 0),
+                                            (128, 3, 1, 33, 2048, 1000)])
+def test_attention_prefill_flash(hip, hs, nh, B, T_, S, p0):
+    """The MFMA flash attention for prompt rows (llj_attention_prefill) against the oracle: causal
+    over cache slots 0 .. p0 + t, partial last query block, ragged key tiles, earlier context (p0 > 0)."""
+    rng = np.random.default_rng(hs + T_ + p0)
+    C = nh * hs
+    kc = bf16(rng.standard_normal((B, nh, S, hs)))
+    vc = bf16(rng.standard_normal((B, nh, S, hs)))
+    q = bf16(rng.standard_normal((B * T_, C)) * 2)
+    pos = np.arange(p0, p0 + T_, dtype=np.int32)
+    y = torch.empty(B * T_, C, dtype=torch.bfloat16, device=dev)
+    qd, kd, vd, pd = T(q, torch.bfloat16), T(kc, torch.bfloat16), T(vc, torch.bfloat16), T(pos)
+    call(hip, "llj_attention_prefill", qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), y.data_ptr(), pd.data_ptr(), B, T_,
+         nh, hs, S, st())
+    torch.cuda.synchronize()
+    # P is rounded to bf16 before the P.V MFMA (as flash kernels do): ~1 bf16 ulp on the weights
+    assert_bf16_close(y.float().cpu().numpy(), _attn_oracle(q, kc, vc, pos, S, T_, nh, hs), "flash prefill", rel=2e-2)

@@ -518,3 +518,25 @@ def test_prefill_gemm_path_equals_gemv_path(mode):
     # measured on MI355X 0.5e-2 (bf16) / 1.0e-2 (int4)
     assert rel < 2e-2, rel
     np.testing.assert_array_equal(ids[0][0, :97], ids[1][0, :97])  # prompt + first token (argmax margin)
+
+
+def test_prefill_flash_attention_equals_row_attention():
+    """A 100-token prompt attends through the MFMA flash kernel (model.FLASH_MIN_T); its logits
+    match the per-row attention kernel's within bf16 noise."""
+    from lit_llama import model as MD
+
+    m = _random_int4_model(1024, 8, seed=150)
+    prompt = torch.randint(3, 2048, (1, 100), generator=torch.Generator().manual_seed(5)).cuda()
+    outs = []
+    saved = MD.FLASH_MIN_T
+    try:
+        for thr in (10 ** 9, 32):
+            MD.FLASH_MIN_T = thr
+            m.reset_cache()
+            outs.append(m(prompt, 120, torch.arange(100).cuda()).float().cpu().numpy()[0])
+    finally:
+        MD.FLASH_MIN_T = saved
+    ref, got = outs
+    rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    print(f"[flash] rel vs row attention {rel:.3e}")
+    assert rel < 2e-2, rel

@@ -1,0 +1,56 @@
+"""Prefill / perplexity-window throughput: LLaMA.forward over a (1, T) window
+(no cache: every position's logits, as reference evaluate/full.py:118-125 calls it) on synthetic
+7B weights (bench.build_model), for gptq.int4 and bf16. Prints one JSON line per (mode, T) with
+the window time, tokens/s and the achieved dense FLOP/s of the Linear layers (2 * params * T)
+over the whole forward; per-kernel times come from a rocprofv3 run of this script.
+
+  python tools/prefill_bench.py [--T 512 2048] [--modes gptq.int4 none] [--iters 3]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--T", nargs="+", type=int, default=[512, 2048])
+    ap.add_argument("--modes", nargs="+", default=["gptq.int4", "none"])
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--model", default="7B")
+    a = ap.parse_args()
+    for mode in a.modes:
+        model = bench.build_model(a.model, None if mode == "none" else mode)
+        cfg = model.config
+        lin_params = sum(m.in_features * m.out_features for m in model.modules()
+                         if hasattr(m, "in_features") and hasattr(m, "out_features"))
+        for T in a.T:
+            idx = torch.randint(3, cfg.vocab_size, (1, T), generator=torch.Generator().manual_seed(T)).cuda()
+            with torch.no_grad():
+                model(idx)  # warm-up (repack, attributes)
+                torch.cuda.synchronize()
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record()
+                for _ in range(a.iters):
+                    model(idx)
+                ev1.record()
+                torch.cuda.synchronize()
+            s = ev0.elapsed_time(ev1) / 1e3 / a.iters
+            flops = 2.0 * lin_params * T
+            print(json.dumps({"mode": mode, "model": a.model, "T": T, "ms_per_window": round(s * 1e3, 3),
+                              "tokens_per_s": round(T / s, 1), "linear_tflops": round(flops / s / 1e12, 1),
+                              "linear_mfma_frac_of_2.5PF": round(flops / s / 2.5e15, 4)}), flush=True)
+        del model
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
