@@ -458,6 +458,28 @@ def gen_sampled():
          u=np.array(us, np.float32), probs=np.stack(probs).astype(np.float32))
 
 
+def gen_ppl():
+    """The reference's perplexity loop (evaluate/full.py:114-128) on the tiny C0 model in fp32: a
+    300-token stream cut into block_size (128) windows, logits[:-1] scored against inp[1:] with a
+    summed cross entropy."""
+    cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=32000)
+    seed = 31
+    m = ref_model(cfg, make_params(cfg, seed))
+    tokens = make_prompt(300, cfg.vocab_size, seed)[None].astype(np.int64)
+    enc = torch.from_numpy(tokens)
+    nlls, toks, per = 0.0, 0, []
+    with torch.inference_mode():
+        for i in range(0, enc.shape[1], cfg.block_size):
+            inp = enc[:, i:i + cfg.block_size]
+            logits = m(inp)[0]
+            nll = torch.nn.functional.cross_entropy(logits[:-1], inp[0, 1:].to(dtype=torch.long), reduction="sum")
+            toks += inp.size(1) - 1
+            nlls += nll.item()
+            per.append(nll.item())
+    save("ppl", seed=np.int64(seed), tokens=tokens, nll_per_window=np.array(per), toks=np.int64(toks),
+         ppl=np.float64(np.exp(nlls / toks)))
+
+
 def gen_bf16_init():
     """The reference's bf16 acceptance test (tests/test_model.py:103-131) at a shape the gfx950
     kernels take: an fp32 LLaMA at the reference's init scale (ref_init_params = _init_weights'
@@ -479,6 +501,6 @@ def gen_bf16_init():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq", "hf_convert",
-                             "meta_convert", "bf16_init", "sampled"]
+                             "meta_convert", "bf16_init", "sampled", "ppl"]
     for w in which:
         globals()[f"gen_{w}"]()

@@ -540,3 +540,23 @@ def test_prefill_flash_attention_equals_row_attention():
     rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
     print(f"[flash] rel vs row attention {rel:.3e}")
     assert rel < 2e-2, rel
+
+
+def test_perplexity_matches_reference(golden):
+    """evaluate/full.py's perplexity loop (reference evaluate/full.py:114-128) on the GPU path
+    (bf16 model; 128-token windows of the C0 model through the prefill GEMMs and flash attention)
+    against the reference's fp32 run of the same loop: per-window NLL within 1 %, ppl within 5 %
+    (bf16 activations; ppl = exp of the mean NLL amplifies its error)."""
+    import sys as _s
+    from pathlib import Path as _P
+
+    _s.path.insert(0, str(_P(__file__).resolve().parents[1] / "lit-llama-ja_amd"))
+    from evaluate.full import perplexity
+
+    g = golden("ppl")
+    m = build(C0, make_params(C0, int(g["seed"])))
+    ppl, nll, toks = perplexity(m, torch.from_numpy(g["tokens"]).cuda())
+    assert toks == int(g["toks"])
+    print(f"[ppl] ours {ppl:.1f} reference {float(g['ppl']):.1f}")
+    assert abs(nll - g["nll_per_window"].sum()) / g["nll_per_window"].sum() < 1e-2
+    assert abs(ppl - float(g["ppl"])) / float(g["ppl"]) < 5e-2
