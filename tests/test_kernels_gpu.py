@@ -178,16 +178,19 @@ def test_bf16_linear(hip, M, N, K):
     assert_bf16_close(got, x @ W.T + bias, f"bf16 M={M}")
 
 
-@pytest.mark.parametrize("outliers", [False, True])
+@pytest.mark.parametrize("outliers", [0, 3, 300, 700])
 @pytest.mark.parametrize("M", [1, 8])
 def test_int8_linear_vs_restatement(hip, M, outliers):
-    """LLM.int8() against the oracle's restatement (bitsandbytes absent: parity unpinned)."""
+    """LLM.int8() against the oracle's restatement (bitsandbytes absent: parity unpinned). 300
+    outlier columns (about what the synthetic 7B down projection sees at bs=8) run the side
+    product from the LDS stash of CB bytes; 700 (> kStashCols = 512) also the global-read tail."""
     rng = np.random.default_rng(M + 100 * outliers)
-    N, K = 256, 4096
+    N, K = (256, 4096) if outliers <= 3 else (256, 11008)
     W = bf16(rng.standard_normal((N, K)) * 0.02)
     x = rng.standard_normal((M, K)).astype(np.float32)
     if outliers:
-        x[:, [17, 1000, 4000]] *= 25.0
+        cols = [17, 1000, 4000] if outliers == 3 else rng.choice(K, outliers, replace=False)
+        x[:, cols] *= 25.0
     x = bf16(x)
     Wd = T(W, torch.bfloat16)
     cb = torch.empty(N, K, dtype=torch.int8, device=dev)

@@ -1,0 +1,61 @@
+"""Timing of the int8 (LLM.int8) GEMV entry points on one shape, with and without outlier
+columns (profiling aid): python tools/i8_bench.py"""
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "lit-llama-ja_amd"))
+from lit_llama import _hip  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda")
+    L = _hip.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device=dev).manual_seed(0)
+    NC = 8  # weight copies streamed in turn (> the 256 MB MALL): every launch reads cold weights
+    for (N, K) in [(4096, 11008), (4096, 4096), (12288, 4096)]:
+        W = torch.randn(N, K, device=dev, dtype=torch.bfloat16, generator=g) * 0.02
+        cb = torch.empty(N, K, dtype=torch.int8, device=dev)
+        scb = torch.empty(N, dtype=torch.float32, device=dev)
+        _hip.call("llj_i8_quant_weight", W.data_ptr(), 1, cb.data_ptr(), scb.data_ptr(), N, K, st)
+        cbs = [cb] + [cb.clone() for _ in range(NC - 1)]
+        del W
+        for M in (1, 8):
+            for nout in (0, 40, 300):
+                x = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
+                if nout:
+                    cols = torch.randperm(K, device=dev, generator=g)[:nout]
+                    x[:, cols] *= 25
+                ws = torch.empty(L.llj_i8_ws_bytes(M, K), dtype=torch.uint8, device=dev)
+                y = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+                _hip.call("llj_i8_stats", x.data_ptr(), K, M, K, 6.0, ws.data_ptr(), st)
+
+                it = [0]
+
+                def run():
+                    c = cbs[it[0] % NC]
+                    it[0] += 1
+                    _hip.call("llj_linear_resid", 2, x.data_ptr(), K, c.data_ptr(), scb.data_ptr(), y.data_ptr(), N,
+                              M, N, K, ws.data_ptr(), 0, st)
+                for _ in range(5):
+                    run()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(200):
+                    run()
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / 200
+                print(json.dumps({"N": N, "K": K, "M": M, "outliers": nout, "us": round(us, 2),
+                                  "GBps": round(N * K / us / 1e3, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
