@@ -248,7 +248,7 @@ def time_dominant_kernel(model, B, iters=10):
     def run_all():
         for f1, rms, w1, s1, w2, s2 in specs:
             _hip.call("llj_norm_swiglu", f1, x.data_ptr(), rms.scale.data_ptr(), rms.eps, w1.data_ptr(), _hip.ptr(s1),
-                      w2.data_ptr(), _hip.ptr(s2), h.data_ptr(), B, H, C, None, 0, None, st)
+                      w2.data_ptr(), _hip.ptr(s2), h.data_ptr(), B, H, C, None, 0, None, None, 0, st)
 
     run_all()
     torch.cuda.synchronize()

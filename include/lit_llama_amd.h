@@ -65,6 +65,10 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
                int M, int N, int K, const void* i8ws, int i8_row0, const float* rowsum, void* stream);
 
 /* ---------------------------------------------------------------- fused decode-layer ops
+ * nstat / npart (optional, norm-fused forms with M <= 16, not int8): the RMSNorm's sum of
+ * squares of each row comes from npart <= 512 partials nstat[p * 16 + m] written by the residual
+ * op that produced x (llj_linear_resid's nstat_out) instead of being recomputed from x in every
+ * workgroup; NULL = computed from x.
  * (Block.forward, lit_llama/model.py:162-175, split at its four Linear boundaries).
  * norm_w == NULL means the input is used as is (no fused RMSNorm); int8 (wfmt 2) takes
  * already-normalised input (its statistics are computed on it).
@@ -81,7 +85,7 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
 int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                       void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
                       int C, int n_head, int S, int row0, int rows, const void* i8ws, const float* rowsum,
-                      void* stream);
+                      const float* nstat, int npart, void* stream);
 
 /* Causal attention of q (B*T, C) over the cache slots each query may see
  * (F.scaled_dot_product_attention with the tril mask rows, model.py:101-104, 237):
@@ -104,19 +108,22 @@ size_t llj_attention_ws_bytes(int rows, int n_head, int head_size, int nsplit);
 int llj_attention_split(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
                         int n_head, int head_size, int S, int nsplit, void* part_ws, void* stream);
 
-/* x[M, N] += A[M, K] . W^T (attn.c_proj / mlp.c_proj + residual add, model.py:172-173). */
+/* x[M, N] += A[M, K] . W^T (attn.c_proj / mlp.c_proj + residual add, model.py:172-173).
+ * nstat_out (optional, M <= 16, not int8): per 16-column tile t of the new x, the bf16-rounded
+ * squares summed over the tile's columns, nstat_out[t * 16 + m] (fp32; N / 16 partials): the
+ * statistics of the next RMSNorm (model.py:281), handed to the norm-fused op that follows. */
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
-                     int N, int K, const void* i8ws, int i8_row0, void* stream);
+                     int N, int K, const void* i8ws, int i8_row0, float* nstat_out, void* stream);
 
 /* h[M, H] = silu(rms_2(x) . W1^T) * (rms_2(x) . W2^T)  (model.py:173, 258). M <= 8. */
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,
-                    const float* rowsum, void* stream);
+                    const float* rowsum, const float* nstat, int npart, void* stream);
 
 /* out[M, N] = RMSNorm(x) . W^T  (ln_f + lm_head, model.py:125-127). M <= 8. */
 int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                     void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const float* rowsum,
-                    void* stream);
+                    const float* nstat, int npart, void* stream);
 
 /* ---------------------------------------------------------------- prefill GEMMs (many rows)
  * The same Linear layers for M >> 16 rows (a prompt, a perplexity window: LLaMA.forward over

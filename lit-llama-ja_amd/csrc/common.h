@@ -52,6 +52,14 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
 }
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
 
+// packed pairs: one v_pk_mul_f32 / v_cvt_pk_bf16_f32 for two values
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 unpk(uint32_t w) { return f32x2{bflo(w), bfhi(w)}; }
+__device__ __forceinline__ uint32_t cvt_pk(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
+}
+
 // (x & m) | c: the compiler selects one v_and_or_b32 when m is in an SGPR (pass it through
 // uniform()). Not inline asm: the hazard recognizer cannot see inside asm blocks, and an asm
 // VALU write to a VGPR an in-flight MFMA still reads as its B operand is a WAR hazard that

@@ -20,6 +20,11 @@ static int dispatch(int wf, int am, const GemvParams& p, hipStream_t s) {
 template <int EP>
 static int run(int wf, GemvParams& p, void* stream) {
   if (int e = check_shape(wf, p)) return e;
+  // norm statistics hand-off: partial sums of squares [npart][16] (row slot = row of the call),
+  // written by a residual op, read by the next norm-fused op; at most 16 rows, 2 partials per thread
+  if (p.nstat_out && p.M > kNstRows) return LLJ_EINVAL;
+  if (p.nstat && (!p.norm_w || wf == WF_I8 || p.M > kNstRows || p.npart < 1 || p.npart > 2 * kNW * 64))
+    return LLJ_EINVAL;
   if (EP == EP_SWIGLU && wf != WF_BF16 && !p.sz2) return LLJ_EINVAL;
   const int am = pick_am(wf, p);
   if (am < 0) return LLJ_EINVAL;
@@ -53,9 +58,10 @@ int llj_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, 
 // out[M,N] = RMSNorm(x)[M,K] . W^T  (ln_f + lm_head, model.py:125-127); norm_w NULL = no norm.
 int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                     void* out, int ldo, int M, int N, int K, const void* i8ws, int i8_row0, const float* rowsum,
-                    void* stream) {
+                    const float* nstat, int npart, void* stream) {
   GemvParams p{};
   p.rowsum = rowsum;
+  p.nstat = nstat; p.npart = npart;
   p.A = (const bf16_t*)x; p.lda = K; p.norm_w = (const bf16_t*)norm_w; p.eps = eps; p.M = M; p.N = N; p.K = K;
   p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)out; p.ldc = ldo;
   p.i8ws = i8ws; p.m0 = i8_row0;
@@ -64,8 +70,9 @@ int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, cons
 
 // x[M,N] += A[M,K] . W^T, bf16 residual add (attn.c_proj / mlp.c_proj + model.py:172-173).
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
-                     int N, int K, const void* i8ws, int i8_row0, void* stream) {
+                     int N, int K, const void* i8ws, int i8_row0, float* nstat_out, void* stream) {
   GemvParams p{};
+  p.nstat_out = nstat_out;
   p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K;
   p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)x; p.ldc = ldx;
   p.i8ws = i8ws; p.m0 = i8_row0;
@@ -75,9 +82,10 @@ int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void
 // h[M,H] = silu(RMSNorm(x) . W1^T) * (RMSNorm(x) . W2^T)  (rms_2 + model.py:258).
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,
-                    const float* rowsum, void* stream) {
+                    const float* rowsum, const float* nstat, int npart, void* stream) {
   GemvParams p{};
   p.rowsum = rowsum;
+  p.nstat = nstat; p.npart = npart;
   p.A = (const bf16_t*)x; p.lda = K; p.norm_w = (const bf16_t*)norm_w; p.eps = eps; p.M = M; p.N = H; p.K = K;
   p.W = W1; p.W2 = W2; p.sz = (const float2*)sz1; p.sz2 = (const float2*)sz2; p.C = (bf16_t*)h; p.ldc = H;
   p.i8ws = i8ws; p.m0 = i8_row0;
@@ -90,9 +98,10 @@ int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, cons
 int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, const void* W, const void* sz,
                       void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
                       int C, int n_head, int S, int row0, int rows, const void* i8ws, const float* rowsum,
-                      void* stream) {
+                      const float* nstat, int npart, void* stream) {
   GemvParams p{};
   p.rowsum = rowsum ? rowsum + row0 : nullptr;
+  p.nstat = nstat ? nstat + row0 : nullptr; p.npart = npart;
   if (row0 < 0 || rows < 1 || row0 + rows > B * T || n_head < 1 || C % n_head || S < 1) return LLJ_EINVAL;
   p.A = (const bf16_t*)x + (size_t)row0 * C; p.lda = C; p.norm_w = (const bf16_t*)norm_w; p.eps = eps;
   p.M = rows; p.m0 = row0; p.N = 3 * C; p.K = C;

@@ -74,7 +74,17 @@ struct GemvParams {
   // int4: sum_k A[m,k] of this call's rows as the MFMA sees them (pre-normalized rows,
   // llj_rmsnorm_rows); nullptr = computed in the prologue
   const float* rowsum;
+  // RMSNorm statistics hand-off (M <= kNstRows): nstat[q * kNstRows + m], q < npart, partial sums
+  // of the bf16-rounded squares of row m (consumer, norm-fused forms); nstat_out: the same,
+  // written per 16-column tile by a residual op (producer)
+  const float* nstat;
+  int npart;
+  float* nstat_out;
 };
+constexpr int kNstRows = 16;
+#ifndef LLJ_SACC_NORM
+#define LLJ_SACC_NORM 0  // 7B bs=8 hand-off: 1.877 -> 1.800 ms, bs=2: 1.339 -> 1.353 (the hand-off runs at bs=2 only)
+#endif
 
 // ------------------------------------------------------------------------------------
 // Stage A rows [0, M) into LDS (row stride K + 8 elements; MFMA lanes of rows >= M read row 0
@@ -85,15 +95,21 @@ __device__ __forceinline__ float rms_rstd(float sumsq_over_k, float eps) {
   return round_bf(rsqrtf(round_bf(round_bf(sumsq_over_k) + eps)));
 }
 
+// g * bf16(x * r), rounded to bf16, two elements per packed op (model.py:283 in bf16)
 __device__ __forceinline__ uint4 norm8(uint4 x, uint4 g, float r) {
   uint32_t xw[4] = {x.x, x.y, x.z, x.w}, gw[4] = {g.x, g.y, g.z, g.w}, o[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float lo = round_bf(bflo(gw[i]) * round_bf(bflo(xw[i]) * r));
-    float hi = round_bf(bfhi(gw[i]) * round_bf(bfhi(xw[i]) * r));
-    o[i] = pack2bf(lo, hi);
-  }
+  for (int i = 0; i < 4; ++i) o[i] = cvt_pk(unpk(gw[i]) * unpk(cvt_pk(unpk(xw[i]) * r)));
   return make_uint4(o[0], o[1], o[2], o[3]);
+}
+// sum of the bf16-rounded squares of the 8 elements (model.py:281: x * x in bf16)
+__device__ __forceinline__ f32x2 sumsq8(const u32x4 x, f32x2 acc) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 v = unpk(x[i]);
+    acc += unpk(cvt_pk(v * v));
+  }
+  return acc;
 }
 
 template <int NW, bool NORM>
@@ -105,23 +121,21 @@ __device__ void stage_a(const GemvParams& p, bf16_t* As, int a_stride, float* re
   float ss[8];
 #pragma unroll
   for (int m = 0; m < 8; ++m) ss[m] = 0.f;
+  const bool from_stat = NORM && p.nstat;  // sums of squares handed over by the producer
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
     if (m < M) {
       const uint4* src = reinterpret_cast<const uint4*>(p.A + (size_t)m * p.lda);
       uint4* dst = reinterpret_cast<uint4*>(As + (size_t)m * a_stride);
+      f32x2 acc = {0.f, 0.f};
       for (int v = tid; v < nvec; v += NT) {
         uint4 x = src[v];
         dst[v] = x;
-        if (NORM) {
-          uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float a = bflo(w[i]), b = bfhi(w[i]);
-            ss[m] += round_bf(a * a) + round_bf(b * b);
-          }
-        }
+        if (NORM && !from_stat) acc = sumsq8(__builtin_bit_cast(u32x4, x), acc);
       }
+      if (from_stat)
+        for (int q = tid; q < p.npart; q += NT) acc.x += p.nstat[(size_t)q * kNstRows + m];
+      ss[m] = acc.x + acc.y;
     }
   }
   if (!NORM) return;
@@ -271,8 +285,10 @@ template <int MB, bool NORM>
 struct APre {
   static constexpr int XR = MB == 1 ? (NORM ? 4 : 8) : 16;
   static constexpr int GR = NORM ? 4 : 1;
+  static constexpr int SR = NORM ? (MB == 1 ? 1 : 8) : 1;  // handed-over partials: rows per partial
   u32x4 x[XR];
   u32x4 g[GR];
+  float ns[2][SR];  // 2 partials per thread (scalar loads: a vector-element read of these miscompiled)
 };
 
 #ifndef LLJ_ABAR
@@ -299,6 +315,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   constexpr bool I8 = (WF == WF_I8);
   constexpr bool W4L = (WF == WF_W4 || WF == WF_W8);  // nibble-coded: offset removed with row sums
   constexpr bool ALDS = I8 || (AM != AM_GLOBAL);
+  // row sums of A for the nibble offset: an extra MFMA against a ones fragment for the global-A
+  // form and for batched norm-fused rows (LLJ_SACC_NORM; the VALU sums + 8 wave reductions of the
+  // prologue sit on its critical path), else summed while the LDS image is written
+  constexpr bool SACC = W4L && (!ALDS || (LLJ_SACC_NORM && AM == AM_NORM && MB > 1));
   constexpr int WV = (WF == WF_W4) ? 1 : (WF == WF_BF16 ? 4 : 2);  // 16-B loads per lane per chunk per matrix
   constexpr int NSTEP = I8 ? 2 : 4;
   const int lane = threadIdx.x & 63;
@@ -418,7 +438,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
           acc[j] = mfma_bf16(a, dequant_w4(r1[d][j][0][t], msk, mag), acc[j]);
           if (DUAL) acc2[j] = mfma_bf16(a, dequant_w4(r2[d][j][0][t], msk, mag), acc2[j]);
         }
-        if (!ALDS && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);  // else: row sums from the prologue / caller
+        if (SACC && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);  // else: row sums from the prologue / caller
       } else if constexpr (WF == WF_W8) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
@@ -430,7 +450,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
             acc2[j] = mfma_bf16(a, dequant_w4(r2[d][j][1][t], msk, mag_hi), acc2[j]);
           }
         }
-        if (!ALDS && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);
+        if (SACC && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);
       } else if constexpr (WF == WF_BF16) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
@@ -551,6 +571,17 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         const int v = tid + NT * j;
         ap.g[j] = g4[v < nvec ? v : nvec - 1];
       }
+      // the producer's partial sums of squares (thread: partials tid and tid + NT), branch-free:
+      // without a hand-off the loads read the norm weights and are never used
+      const bool st = p.nstat != nullptr;
+      const int np = st ? p.npart : 1;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int qi = tid + NT * q < np ? tid + NT * q : np - 1;
+        const float* src = st ? p.nstat + (size_t)qi * kNstRows : reinterpret_cast<const float*>(g4);
+#pragma unroll
+        for (int m = 0; m < (MR < AP::SR ? MR : AP::SR); ++m) ap.ns[q][m] = src[m];
+      }
     }
   };
   auto a_finish = [&](auto rsc, auto mrc) {
@@ -562,14 +593,18 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
 #pragma unroll
         for (int m = 0; m < MR; ++m) {
           float ss = 0.f;
+          if (p.nstat) {  // uniform: the producer's partials (rows >= M: unused)
 #pragma unroll
-          for (int j = 0; j < RS; ++j) {
-            const u32x4 xv = (m < M && tid + NT * j < nvec) ? ap.x[m * RS + j] : zero4;
+            for (int q = 0; q < 2; ++q)
+              if (tid + NT * q < p.npart) ss += ap.ns[q][m < AP::SR ? m : 0];
+          } else {
+            f32x2 acc = {0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float a = bflo(xv[i]), b = bfhi(xv[i]);
-              ss += round_bf(a * a) + round_bf(b * b);
+            for (int j = 0; j < RS; ++j) {
+              const u32x4 xv = (m < M && tid + NT * j < nvec) ? ap.x[m * RS + j] : zero4;
+              acc = sumsq8(xv, acc);
             }
+            ss = acc.x + acc.y;
           }
           ss = wave_sum(ss);
           if (lane == 0) redf[wave * 8 + m] = ss;
@@ -600,14 +635,15 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
               o = __builtin_bit_cast(u32x4, nv);
             }
             *reinterpret_cast<u32x4*>(As + (size_t)m * a_stride + 8 * v) = o;
-            if (W4L && !p.rowsum) {
-#pragma unroll
-              for (int i = 0; i < 4; ++i) rsum += bflo(o[i]) + bfhi(o[i]);
+            if (W4L && !SACC && !p.rowsum) {
+              f32x2 rp = unpk(o[0]) + unpk(o[1]);
+              rp += unpk(o[2]) + unpk(o[3]);
+              rsum += rp.x + rp.y;
             }
           }
         }
       }
-      if (W4L && m < M && !p.rowsum) {
+      if (W4L && !SACC && m < M && !p.rowsum) {
         rsum = wave_sum(rsum);
         if (lane == 0) tail[TL_RS + wave * 8 + m] = rsum;
       }
@@ -668,7 +704,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     if (rs == 0) {
       stage_a<NW, AM == AM_NORM>(p, reinterpret_cast<bf16_t*>(smem), a_stride, tail);
       __syncthreads();
-      if (W4L && !p.rowsum) {  // row sums of the staged rows (offset removal, see header)
+      if (W4L && !SACC && !p.rowsum) {  // row sums of the staged rows (offset removal, see header)
         const bf16_t* As = reinterpret_cast<const bf16_t*>(smem);
         for (int m = 0; m < M; ++m) {
           float rsum = 0.f;
@@ -765,7 +801,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         float sa = ys[r];
         if (p.rowsum) {
           sa = e_rs[r];  // rows >= M hold a clamped copy; their outputs are not stored
-        } else if constexpr (ALDS) {
+        } else if constexpr (ALDS && !SACC) {
           sa = 0.f;
           if (m < M) {
 #pragma unroll
@@ -836,6 +872,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         const uint32_t xb = (uint32_t)f2bf(xn);
         const uint32_t pr = lane_xor1(xb);
         if (m < M && !(row & 1)) st_out32(p.C + (size_t)m * p.ldc + n, xb | (pr << 16));
+        if (p.nstat_out) {  // uniform: the next RMSNorm's sum of squares over this tile's 16 columns
+          const float sq = row16_sum(m < M ? round_bf(xn * xn) : 0.f);
+          if (row == 0 && m < M) st_out32(p.nstat_out + (size_t)ntj[j] * kNstRows + m, __builtin_bit_cast(uint32_t, sq));
+        }
       } else {
         const uint32_t ob = (uint32_t)f2bf(out_value<EP>(y, y2));
         const uint32_t pr = lane_xor1(ob);

@@ -27,15 +27,16 @@ SIGNATURES = {
     "llj_w8_unpack": [_P, _P, _I, _I, _P],
     "llj_w8_scale_zero": [_P, _P, _I, _P, _I, _P],
     "llj_linear": [_I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
-    "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
+    "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I,
+                          _P],
     "llj_attention_split": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
     "llj_gptq_block": [_P, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P],
     "llj_colblock_pack": [_P, _I, _I, _P, _P, _I, _P, _P],
     "llj_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_attention_prefill": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
-    "llj_linear_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P],
-    "llj_norm_swiglu": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P],
-    "llj_norm_linear": [_I, _P, _P, _F, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
+    "llj_linear_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
+    "llj_norm_swiglu": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _I, _P],
+    "llj_norm_linear": [_I, _P, _P, _F, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P],
     "llj_i8_stats": [_P, _I, _I, _I, _F, _P, _P],
     "llj_i8_quant_weight": [_P, _I, _P, _P, _I, _I, _P],
     "llj_embedding": [_P, _P, _P, _I, _I, _P, _P],

@@ -109,6 +109,13 @@ def attn_splits(S: int) -> int:
 # instead of normalized inside every norm-fused GEMV workgroup
 PRE_NORM_ROWS = True
 PRE_NORM_MIN_M = 2  # smallest batch that takes the separate launch (measured best from bs=2 on)
+# batched decode rows (2 <= M <= HAND_NORM_MAX_M): the residual ops hand the next RMSNorm its sums
+# of squares (per-tile partials, llj_linear_resid's nstat_out) and the norm-fused GEMVs normalize
+# from them, so no separate RMSNorm launch remains after layer 0's rms_1. Measured 7B gptq.int4
+# ms/token, hand-off vs llj_rmsnorm_rows: bs=2 1.339 vs 1.384, bs=4 1.633 vs 1.539, bs=8 1.877 vs
+# 1.788 (every workgroup normalizes all rows: 768 of them at bs=4) -> bs=2 only
+HAND_NORM = True
+HAND_NORM_MAX_M = 2
 
 
 # prefill / no-cache calls with at least this many rows (B * T) run the MFMA-tiled GEMMs
@@ -155,6 +162,11 @@ class _Work:
         self.pre = M >= max(2, PRE_NORM_MIN_M) and not need_i8 and PRE_NORM_ROWS
         self.xn = torch.empty(M, C, dtype=bf, device=device) if (need_i8 or self.pre or gemm) else None
         self.rs = torch.empty(M, dtype=torch.float32, device=device) if self.pre else None
+        # norm statistics hand-off (HAND_NORM): partials [C / 16 tiles][16 rows]
+        self.hand = (HAND_NORM and not need_i8 and not gemm and 2 <= M <= HAND_NORM_MAX_M
+                     and C % 16 == 0 and C // 16 <= 512)
+        self.npart = C // 16
+        self.nst = torch.empty(self.npart * 16, dtype=torch.float32, device=device) if self.hand else None
         if need_i8:
             L = _hip.lib()
             nb = max(L.llj_i8_ws_bytes(M, C), L.llj_i8_ws_bytes(M, H))
@@ -374,6 +386,8 @@ class LLaMA(nn.Module):
                           M, C, st)
                 self._i8_prep(w.xn, M, C, w, st)
                 src, nw = w.xn, None
+            elif w.hand and i > 0:  # the previous mlp.c_proj handed over the sums of squares
+                src, nw = w.x, blk.rms_1.scale.data_ptr()
             elif w.pre:
                 rs = w.rs if fa in _ROWSUM_FMTS else None
                 _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
@@ -381,14 +395,15 @@ class LLaMA(nn.Module):
                 src, nw = w.xn, None
             else:
                 src, nw = w.x, blk.rms_1.scale.data_ptr()
+            nst = w.nst if (w.hand and i > 0 and fa != 2) else None
             for r0 in range(0, M, QKV_ROWS):
                 r = min(QKV_ROWS, M - r0)
                 _hip.call("llj_norm_qkv_rope", fa, src.data_ptr(), nw, blk.rms_1.eps, wa.data_ptr(), P(sa),
                           w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), B, T, C, nh,
-                          S, r0, r, P(w.i8ws), P(rs), st)
+                          S, r0, r, P(w.i8ws), P(rs), P(nst), w.npart, st)
             # 2. attention, 3. c_proj + residual
             self._attention(w, kc, vc, pos, B, T, S, st)
-            self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st)
+            self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst if w.hand else None)
             # 4. rms_2 + fc1/fc2 + silu*mul
             if f1 != f2:
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")
@@ -398,6 +413,8 @@ class LLaMA(nn.Module):
                           M, C, st)
                 self._i8_prep(w.xn, M, C, w, st)
                 src, nw, step = w.xn, None, I8_ROWS
+            elif w.hand:  # c_proj handed over the sums of squares
+                src, nw, step = w.x, blk.rms_2.scale.data_ptr(), QKV_ROWS
             elif w.pre:
                 rs = w.rs if f1 in _ROWSUM_FMTS else None
                 _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
@@ -405,29 +422,34 @@ class LLaMA(nn.Module):
                 src, nw, step = w.xn, None, QKV_ROWS
             else:
                 src, nw, step = w.x, blk.rms_2.scale.data_ptr(), QKV_ROWS
+            nst = w.nst if (w.hand and f1 != 2) else None
             for r0 in range(0, M, step):
                 r = min(step, M - r0)
                 _hip.call("llj_norm_swiglu", f1, src[r0].data_ptr(), nw, blk.rms_2.eps, w1.data_ptr(), P(s1),
                           w2.data_ptr(), P(s2), w.h[r0].data_ptr(), r, H, C, P(w.i8ws), r0,
-                          None if rs is None else rs[r0].data_ptr(), st)
+                          None if rs is None else rs[r0].data_ptr(), None if nst is None else nst[r0].data_ptr(),
+                          w.npart, st)
             # 5. mlp.c_proj + residual
-            self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st)
+            self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st, w.nst if w.hand else None)
 
-    def _resid(self, f, A, W, sz, x, M, N, K, w, st):
+    def _resid(self, f, A, W, sz, x, M, N, K, w, st, nst=None):
+        """x += A . W^T; with `nst` (the norm hand-off, N / 16 tiles x 16 rows) also the next
+        RMSNorm's partial sums of squares of the new x."""
         if f == 2:
             self._i8_prep(A, M, K, w, st)
         step = I8_ROWS if f == 2 else LIN_ROWS
         for r0 in range(0, M, step):
             r = min(step, M - r0)
             _hip.call("llj_linear_resid", f, A[r0].data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz),
-                      x[r0].data_ptr(), x.stride(0), r, N, K, _hip.ptr(w.i8ws), r0, st)
+                      x[r0].data_ptr(), x.stride(0), r, N, K, _hip.ptr(w.i8ws), r0,
+                      None if nst is None else nst[r0].data_ptr(), st)
 
     def _head(self, x, M, specs, out, st, w):
         cfg = self.config
         C, V = cfg.n_embd, cfg.padded_vocab_size
         f, W, sz = specs["head"]
         ln = self.transformer.ln_f
-        rs = None
+        rs = nst = None
         if f == 2:
             xn = torch.empty_like(x)
             _hip.call("llj_rmsnorm", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), M, C, st)
@@ -439,6 +461,9 @@ class LLaMA(nn.Module):
             _hip.call("llj_gemm_linear", f, xn.data_ptr(), C, W.data_ptr(), _hip.ptr(sz), out.data_ptr(), out.stride(0),
                       M, V, C, st)
             return
+        elif x is w.x and w.hand and f != 2 and len(self.transformer.h) > 0:  # the last mlp.c_proj's partials
+            nst = w.nst
+            src, nw = x, ln.scale.data_ptr()
         elif M >= 2 and w.pre:  # batched rows: normalize once (see _Work.pre)
             xn = torch.empty_like(x)
             rs = torch.empty(M, dtype=torch.float32, device=x.device) if f in _ROWSUM_FMTS else None
@@ -451,7 +476,8 @@ class LLaMA(nn.Module):
             r = min(QKV_ROWS, M - r0)
             _hip.call("llj_norm_linear", f, src[r0].data_ptr(), nw, ln.eps, W.data_ptr(), _hip.ptr(sz),
                       out[r0].data_ptr(), out.stride(0), r, V, C, _hip.ptr(w.i8ws), r0,
-                      None if rs is None else rs[r0].data_ptr(), st)
+                      None if rs is None else rs[r0].data_ptr(), None if nst is None else nst[r0].data_ptr(),
+                      w.npart, st)
 
 
 Linear8bitLtThreshold = 6.0  # reference quantization.py:45
@@ -569,7 +595,7 @@ class MLP(nn.Module):
         for r0 in range(0, M, step):
             r = min(step, M - r0)
             _hip.call("llj_norm_swiglu", f1, x2[r0].data_ptr(), None, 0.0, w1.data_ptr(), _hip.ptr(s1), w2.data_ptr(),
-                      _hip.ptr(s2), h[r0].data_ptr(), r, H, K, _hip.ptr(ws), r0, None, st)
+                      _hip.ptr(s2), h[r0].data_ptr(), r, H, K, _hip.ptr(ws), r0, None, None, 0, st)
         out = torch.empty(M, self.c_proj.out_features, dtype=torch.bfloat16, device=x.device)
         if fd == 2:
             _hip.call("llj_i8_stats", h.data_ptr(), H, M, H, Linear8bitLtThreshold, ws.data_ptr(), st)

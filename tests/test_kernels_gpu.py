@@ -319,7 +319,7 @@ def test_fused_qkv_rope_kv(hip, wfmt, B, T_):
         r = min(8, M - r0)
         call(hip, "llj_norm_qkv_rope", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, Wd.data_ptr(),
              None if szd is None else szd.data_ptr(), q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rd.data_ptr(),
-             pd.data_ptr(), B, T_, C, nh, S, r0, r, None, None, st())
+             pd.data_ptr(), B, T_, C, nh, S, r0, r, None, None, None, 0, st())
     torch.cuda.synchronize()
     h = bf16(O.rmsnorm(x, g))
     qkv = bf16(h @ Wref.T)
@@ -353,9 +353,9 @@ def test_fused_swiglu_and_resid(hip, wfmt):
     P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
     xd, gd = T(x, torch.bfloat16), T(g, torch.bfloat16)
     call(hip, "llj_norm_swiglu", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, W1d.data_ptr(), P(s1), W2d.data_ptr(),
-         P(s2), h.data_ptr(), M, H, C, None, 0, None, st())
+         P(s2), h.data_ptr(), M, H, C, None, 0, None, None, 0, st())
     xr = xd.clone()
-    call(hip, "llj_linear_resid", wfmt, h.data_ptr(), H, Wdd.data_ptr(), P(sd), xr.data_ptr(), C, M, C, H, None, 0,
+    call(hip, "llj_linear_resid", wfmt, h.data_ptr(), H, Wdd.data_ptr(), P(sd), xr.data_ptr(), C, M, C, H, None, 0, None,
          st())
     torch.cuda.synchronize()
     hn = bf16(O.rmsnorm(x, g))
@@ -366,6 +366,97 @@ def test_fused_swiglu_and_resid(hip, wfmt):
     assert_bf16_close(h.float().cpu().numpy(), hexp, "swiglu", rel=3e-2)
     hg = h.float().cpu().numpy()
     assert_bf16_close(xr.float().cpu().numpy(), x + bf16(hg @ Wd_.T), "resid")
+
+
+@pytest.mark.parametrize("wfmt", [0, 1, 3])
+@pytest.mark.parametrize("M", [2, 8, 13])
+def test_norm_statistics_handoff(hip, wfmt, M):
+    """Batched decode's RMSNorm hand-off: llj_linear_resid writes, per 16-column tile of the new x,
+    the partial sums of its bf16-rounded squares (nstat_out); the norm-fused ops that follow
+    (rms_2 + SwiGLU, rms_1 + QKV, ln_f + lm_head) take those partials instead of recomputing the
+    sums from x. The partials must add up to the sum of squares of the stored x, and the fused
+    ops must give what they give without the hand-off (only the fp32 summation order differs)."""
+    rng = np.random.default_rng(300 + 7 * wfmt + M)
+    C, H, nh, hs, S, V = 512, 768, 4, 128, 16, 1024
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    x0 = bf16(rng.standard_normal((M, C)))
+    hin = bf16(rng.standard_normal((M, H)))
+    g = bf16(rng.uniform(0.5, 1.5, C))
+    Wd_, Wdd, sd = quant_operands(hip, rng, wfmt, C, H)
+    npart = C // 16
+    nst = torch.full((npart * 16,), float("nan"), dtype=torch.float32, device=dev)
+    xd, hd, gd = T(x0, torch.bfloat16), T(hin, torch.bfloat16), T(g, torch.bfloat16)
+    for r0 in range(0, M, 16):
+        r = min(16, M - r0)
+        call(hip, "llj_linear_resid", wfmt, hd[r0].data_ptr(), H, Wdd.data_ptr(), P(sd), xd[r0].data_ptr(), C, r, C,
+             H, None, 0, nst[r0:].data_ptr(), st())
+    torch.cuda.synchronize()
+    xn = xd.float().cpu().numpy()
+    part = nst.cpu().numpy().reshape(npart, 16)[:, :M]
+    assert np.isfinite(part).all()
+    sq = bf16(xn * xn).astype(np.float64)  # x * x in bf16 (model.py:281)
+    np.testing.assert_allclose(part.sum(0), sq.sum(1), rtol=1e-5)
+    for t in range(npart):  # every tile's partial is its own 16 columns
+        np.testing.assert_allclose(part[t], sq[:, 16 * t:16 * t + 16].sum(1), rtol=1e-5, atol=1e-6)
+
+    def both(run):
+        a = run(None)
+        b = run(nst)
+        torch.cuda.synchronize()
+        return a.float().cpu().numpy(), b.float().cpu().numpy()
+
+    W1, W1d, s1 = quant_operands(hip, rng, wfmt, H, C)
+    W2, W2d, s2 = quant_operands(hip, rng, wfmt, H, C)
+
+    def swiglu(ns):
+        h = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+        for r0 in range(0, M, 8):
+            r = min(8, M - r0)
+            call(hip, "llj_norm_swiglu", wfmt, xd[r0].data_ptr(), gd.data_ptr(), 1e-5, W1d.data_ptr(), P(s1),
+                 W2d.data_ptr(), P(s2), h[r0].data_ptr(), r, H, C, None, 0, None,
+                 None if ns is None else ns[r0:].data_ptr(), npart, st())
+        return h
+
+    a, b = both(swiglu)
+    hn = bf16(O.rmsnorm(xn, g))
+    hexp = bf16(bf16(O.silu(bf16(hn @ W1.T))) * bf16(hn @ W2.T))
+    assert_bf16_close(a, hexp, "swiglu", rel=3e-2)
+    assert_bf16_close(b, hexp, "swiglu hand-off", rel=3e-2)
+    assert np.mean(a == b) > 0.999, np.mean(a == b)
+    Wq, Wqd, sqd = quant_operands(hip, rng, wfmt, 3 * C, C)
+    rope, pos = T(O.build_rope_cache(32, hs)), T(np.array([5], np.int32))
+
+    def qkv(ns):
+        q = torch.zeros(M, C, dtype=torch.bfloat16, device=dev)
+        kc = torch.zeros(M, nh, S, hs, dtype=torch.bfloat16, device=dev)
+        vc = torch.zeros_like(kc)
+        for r0 in range(0, M, 8):
+            r = min(8, M - r0)
+            call(hip, "llj_norm_qkv_rope", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, Wqd.data_ptr(), P(sqd),
+                 q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), M, 1, C, nh, S, r0, r,
+                 None, None, P(ns), npart, st())
+        return torch.cat([q.reshape(M, -1), kc.reshape(M, -1), vc.reshape(M, -1)], 1)
+
+    a, b = both(qkv)
+    assert np.mean(a == b) > 0.999, np.mean(a == b)
+    Wh, Whd, shd = quant_operands(hip, rng, wfmt, V, C)
+
+    def head(ns):
+        lg = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
+        for r0 in range(0, M, 8):
+            r = min(8, M - r0)
+            call(hip, "llj_norm_linear", wfmt, xd[r0].data_ptr(), gd.data_ptr(), 1e-5, Whd.data_ptr(), P(shd),
+                 lg[r0].data_ptr(), V, r, V, C, None, 0, None, None if ns is None else ns[r0:].data_ptr(), npart,
+                 st())
+        return lg
+
+    a, b = both(head)
+    assert np.mean(a == b) > 0.999, np.mean(a == b)
+    # the hand-off is refused where it is not defined: int8, more rows than the partial stride
+    bad = torch.zeros(64, dtype=torch.bfloat16, device=dev)
+    assert hip.llj_norm_swiglu(wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, W1d.data_ptr(), P(s1),
+                               W2d.data_ptr(), P(s2), bad.data_ptr(), M, H, C, None, 0, None, nst.data_ptr(), 10000,
+                               st()) == 1000
 
 
 def test_rmsnorm_rows_rowsum_and_int4_rowsum_operand(hip, golden):
@@ -425,16 +516,16 @@ def test_multi_tile_workgroups_equal_single_tile(hip, wfmt, M):
         kc = torch.zeros(M, nh, S, 128, dtype=torch.bfloat16, device=dev)
         vc = torch.zeros_like(kc)
         call(hip, "llj_norm_qkv_rope", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, Wqd.data_ptr(), P(sq), q.data_ptr(),
-             kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), M, 1, C, nh, S, 0, M, None, None, st())
+             kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), M, 1, C, nh, S, 0, M, None, None, None, 0, st())
         h = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
         call(hip, "llj_norm_swiglu", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, W1d.data_ptr(), P(s1), W2d.data_ptr(),
-             P(s2), h.data_ptr(), M, H, C, None, 0, None, st())
+             P(s2), h.data_ptr(), M, H, C, None, 0, None, None, 0, st())
         lg = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
         call(hip, "llj_norm_linear", wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, Whd.data_ptr(), P(sh), lg.data_ptr(),
-             V, M, V, C, None, 0, None, st())
+             V, M, V, C, None, 0, None, None, 0, st())
         xr = xr0.clone()
         call(hip, "llj_linear_resid", wfmt, hxd.data_ptr(), H13, Wrd.data_ptr(), P(sr), xr.data_ptr(), C13, M, C13,
-             H13, None, 0, st())
+             H13, None, 0, None, st())
         torch.cuda.synchronize()
         return q, kc, vc, h, lg, xr
 
@@ -464,7 +555,7 @@ def test_long_k_residual_eight_waves_m1(hip, wfmt):
     x0 = bf16(rng.standard_normal((1, N)))
     xd = T(x0, torch.bfloat16)
     call(hip, "llj_linear_resid", wfmt, T(h, torch.bfloat16).data_ptr(), K, Wd.data_ptr(), szd.data_ptr(),
-         xd.data_ptr(), N, 1, N, K, None, 0, st())
+         xd.data_ptr(), N, 1, N, K, None, 0, None, st())
     torch.cuda.synchronize()
     assert_bf16_close(xd.float().cpu().numpy(), x0 + bf16(h @ W.T), "resid K=11008 M=1")
 
@@ -532,18 +623,18 @@ def test_int8_fused_ops_7b_shapes(hip, M):
     vc = torch.zeros_like(kc)
     rd, pd = T(rope), T(pos)
     call(hip, "llj_norm_qkv_rope", 2, xn.data_ptr(), None, 1e-5, cbqd.data_ptr(), scbqd.data_ptr(), q.data_ptr(),
-         kc.data_ptr(), vc.data_ptr(), rd.data_ptr(), pd.data_ptr(), M, 1, C, nh, S, 0, M, ws.data_ptr(), None, st())
+         kc.data_ptr(), vc.data_ptr(), rd.data_ptr(), pd.data_ptr(), M, 1, C, nh, S, 0, M, ws.data_ptr(), None, None, 0, st())
     # SwiGLU
     (cb1, scb1), cb1d, scb1d = wq(H, C)
     (cb2, scb2), cb2d, scb2d = wq(H, C)
     h = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
     call(hip, "llj_norm_swiglu", 2, xn.data_ptr(), None, 1e-5, cb1d.data_ptr(), scb1d.data_ptr(), cb2d.data_ptr(),
-         scb2d.data_ptr(), h.data_ptr(), M, H, C, ws.data_ptr(), 0, None, st())
+         scb2d.data_ptr(), h.data_ptr(), M, H, C, ws.data_ptr(), 0, None, None, 0, st())
     # lm_head
     (cbh, scbh), cbhd, scbhd = wq(V, C)
     lg = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
     call(hip, "llj_norm_linear", 2, xn.data_ptr(), None, 1e-5, cbhd.data_ptr(), scbhd.data_ptr(), lg.data_ptr(), V,
-         M, V, C, ws.data_ptr(), 0, None, st())
+         M, V, C, ws.data_ptr(), 0, None, None, 0, st())
     torch.cuda.synchronize()
     # oracle on the same normalized rows
     qkv = bf16(O.int8_linear(xnh, cbq, scbq))
@@ -566,7 +657,7 @@ def test_int8_fused_ops_7b_shapes(hip, M):
     call(hip, "llj_i8_stats", h.data_ptr(), H, M, H, 6.0, ws.data_ptr(), st())
     xr = xd.clone()
     call(hip, "llj_linear_resid", 2, h.data_ptr(), H, cbdd.data_ptr(), scbdd.data_ptr(), xr.data_ptr(), C, M, C, H,
-         ws.data_ptr(), 0, st())
+         ws.data_ptr(), 0, None, st())
     torch.cuda.synchronize()
     assert_bf16_close(xr.float().cpu().numpy(), x + bf16(O.int8_linear(hh, cbd_, scbd_)), f"int8 resid M={M}")
 

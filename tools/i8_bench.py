@@ -42,7 +42,7 @@ def main():
                     c = cbs[it[0] % NC]
                     it[0] += 1
                     _hip.call("llj_linear_resid", 2, x.data_ptr(), K, c.data_ptr(), scb.data_ptr(), y.data_ptr(), N,
-                              M, N, K, ws.data_ptr(), 0, st)
+                              M, N, K, ws.data_ptr(), 0, None, st)
                 for _ in range(5):
                     run()
                 torch.cuda.synchronize()
