@@ -10,8 +10,12 @@
 // and the softmax statistics are per-lane; P^T goes straight from the S^T accumulators into the
 // B operand of O^T = V^T . P^T (the 32-key MFMA step's k order is chosen as
 // key = 4 g + (j & 3) + 16 (j >> 2) in each of its two 16-key halves, which is exactly what lane
-// group g holds), with V^T staged in LDS at load time. Keys are the cache slots 0 .. p of a query
-// at position p (no ring wrap: p0 + T <= S, checked by the caller), masked on the diagonal tile.
+// group g holds). V is staged row-major like K (16-B stores) and its V^T fragments are read with
+// gfx950's transposing LDS read (ds_read_b64_tr_b16: 4 keys x 16 head dims per 16-lane group,
+// delivered column-major); staging V^T with 2-byte scattered stores cost 8-way bank conflicts
+// and 32 LDS writes per thread per tile (7B T = 2048: 357 us per layer). Keys are the cache slots
+// 0 .. p of a query at position p (no ring wrap: p0 + T <= S, checked by the caller), masked on
+// the diagonal tile.
 #include "common.h"
 #include "lit_llama_amd.h"
 
@@ -19,18 +23,19 @@ namespace llj {
 
 constexpr int kFQ = 64;   // queries per workgroup
 constexpr int kFK = 64;   // keys per tile
-constexpr int kVtP = 72;  // V^T LDS row pitch (keys): 144 B, 8-B aligned, spreads the d rows over banks
+typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 template <int HS>
 __global__ __launch_bounds__(256) void flash_prefill_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                             const int* __restrict__ pos, int T, int S, int nh,
                                                             float sl2) {
-  constexpr int KP = HS + 8;  // K tile pitch (elements)
+  constexpr int KP = HS + 8;   // K tile pitch (elements): 16-B row reads
+  constexpr int VP = HS + 16;  // V tile pitch: 8 rows x 4 lanes x 8 B of a transposed read on distinct banks
   constexpr int KS = HS / 32;  // MFMA k-steps over the head dim
   constexpr int DB = HS / 16;  // 16-row output blocks of O^T
   __shared__ __attribute__((aligned(16))) bf16_t Ks[kFK * KP];
-  __shared__ __attribute__((aligned(16))) bf16_t Vt[HS * kVtP];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[kFK * VP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, g = lane >> 4;
   const int qb = gridDim.x - 1 - blockIdx.x;  // long (late) query blocks first
@@ -76,12 +81,7 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(const bf16_t* __rest
       const int piece = tid + 256 * i;
       const int key = piece / (HS / 8), v8 = piece % (HS / 8);
       *reinterpret_cast<u32x4*>(Ks + key * KP + 8 * v8) = kreg[i];
-      const u32x4 vv = vreg[i];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {  // V^T: element (key, d) at Vt[d * kVtP + key]
-        Vt[(8 * v8 + 2 * e) * kVtP + key] = (bf16_t)(vv[e] & 0xFFFFu);
-        Vt[(8 * v8 + 2 * e + 1) * kVtP + key] = (bf16_t)(vv[e] >> 16);
-      }
+      *reinterpret_cast<u32x4*>(Vs + key * VP + 8 * v8) = vreg[i];
     }
     __syncthreads();
     if (kt + 1 < ntile) load_tile(kt + 1);  // in flight during this tile's MFMAs
@@ -149,10 +149,13 @@ __global__ __launch_bounds__(256) void flash_prefill_kernel(const bf16_t* __rest
       const bf16x8 bfrag = __builtin_bit_cast(bf16x8, bw);
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
-        const bf16_t* vr = Vt + (16 * d + col) * kVtP + 32 * u + 4 * g;
-        const uint2 lo = *reinterpret_cast<const uint2*>(vr);
-        const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
-        const u32x4 aw = {lo.x, lo.y, hi.x, hi.y};
+        // lane 4q + p of group g addresses keys 32u + 4g + q (+16), dims 16d + 4p .. +3; lane col
+        // receives dim 16d + col of those 4 keys
+        const bf16_t* vr = Vs + (32 * u + 4 * g + ((lane >> 2) & 3)) * VP + 16 * d + 4 * (lane & 3);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)vr);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr + 16 * VP));
+        const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
+        const u32x4 aw = {l2.x, l2.y, h2.x, h2.y};
         acc_o[d] = mfma_bf16(__builtin_bit_cast(bf16x8, aw), bfrag, acc_o[d]);
       }
     }

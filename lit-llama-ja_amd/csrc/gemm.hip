@@ -7,14 +7,19 @@
 // elementwise work in the epilogue: model.py:204-228 (c_attn split, RoPE, KV-cache write),
 // :172-173 (residual adds), :258 (silu(c_fc1) * c_fc2).
 //
-// Tiling: a 256-thread workgroup owns a 128 x 128 output tile and walks K in 128-deep chunks;
-// the chunk's A tile (128 rows x 128 k bf16) and B tile (W4P: the eight 1 KiB W4P tiles of its
-// 128 columns; bf16: 128 rows x 128 k) are staged through double-buffered LDS (one barrier per
-// chunk: the loads of chunk c + 1 are in flight while chunk c is multiplied). The 4 waves form
-// a 2 x 2 grid of 64 x 64 sub-tiles = 4 x 4 MFMA 16x16x32 bf16 accumulators each. int4 codes
-// are dequantized from LDS into bf16 (128 + q) with one v_and_or_b32 per pair (the W4P lane
-// layout is the MFMA B fragment, as in the GEMV); the 128 + zero offset is removed in the
-// epilogue with the row sums of A, accumulated while the A tile is staged:
+// Tiling: a 256-thread workgroup owns a 128 x 128 output tile and walks K in 64-deep chunks;
+// the chunk's A tile (128 rows x 64 k bf16) and B tile (W4P: the half of each of the eight 1 KiB
+// W4P tiles of its 128 columns that holds these 64 k; bf16: 128 rows x 64 k) are staged through
+// double-buffered LDS (one barrier per chunk: the loads of chunk c + 1 are in flight while chunk
+// c is multiplied). 22.5 KiB (W4) / 36 KiB (bf16) per stage, so 3 / 2 workgroups share a CU and
+// one's barrier or load wait is covered by another's MFMAs (128-deep chunks with 86 / 139 KiB of
+// LDS held one workgroup per CU and left the chunk loads exposed: 0.17 of the MFMA peak). The 4
+// waves form a 2 x 2 grid of 64 x 64 sub-tiles = 4 x 4 MFMA 16x16x32 bf16 accumulators each.
+// MFMA step s of a chunk: lane group g supplies k = 32 s + 8 g + [0, 8) (A from LDS rows); for W4
+// those 8 codes are word g of the W4P lane (16 (2 h + s) + column) of the chunk's half h, so a B
+// fragment is one 4-byte LDS read + the GEMV's v_and_or_b32 dequant into bf16 (128 + q); the
+// 128 + zero offset is removed in the epilogue with the row sums of A, accumulated while the A
+// tile is staged:
 //   y[m,n] = s[n] * (sum_k A[m,k] (128 + q[k,n]) - (128 + z[n]) * sum_k A[m,k]).
 // Tile order is XCD-aware: the 8 XCDs take contiguous ranges of tiles, n fastest inside a
 // range, so an XCD's L2 keeps one 128-row A panel while it sweeps the weight columns.
@@ -43,8 +48,11 @@ struct GemmParams {
   int n_head, head_size, S, T;
 };
 
-constexpr int kGBM = 128, kGBN = 128, kGBK = 128, kGNT = 256;
-constexpr int kAP = kGBK + 8;  // A / bf16-B LDS row pitch (elements): 272 B, conflict-free 16-B reads
+constexpr int kGBM = 128, kGBN = 128, kGBK = 64, kGNT = 256;
+#ifndef LLJ_GDEPTH
+#define LLJ_GDEPTH 2  // W4: chunks in flight per thread (register ring); bf16 keeps 1 (registers)
+#endif
+constexpr int kAP = kGBK + 8;  // A / bf16-B LDS row pitch (elements): 144 B
 
 template <int WF>
 constexpr size_t gemm_b_bytes() { return WF == GWF_W4 ? (size_t)kGBN * kGBK / 2 : (size_t)kGBN * kAP * 2; }
@@ -59,7 +67,7 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave & 1, wc = wave >> 1;
   const int row = lane & 15, g = lane >> 4;
-  const int M = p.M, K = p.K, KC = K / kGBK;
+  const int M = p.M, K = p.K, KC = K / kGBK, KC128 = K / 128;
   const int mtiles = (M + kGBM - 1) / kGBM, ntiles = p.N / kGBN;
   const int total = mtiles * ntiles;
   int t = blockIdx.x;
@@ -73,45 +81,46 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   auto Bs = [&](int b) { return smem + 2 * kAB + b * kBB; };
   float* rs_lds = reinterpret_cast<float*>(smem + 2 * (kAB + kBB));
 
-  // ---- staging: thread -> (A row, half of the 256-B chunk row); B: W4 2 x 16 B, bf16 8 x 16 B
+  // ---- staging: thread -> (A row, half of the 128-B chunk row) = 4 x 16 B; B: W4 1 x 16 B
+  // (tile tid / 32, W4P lane 32 h + tid % 32), bf16 4 x 16 B (row, half) like A
   const int ar = tid >> 1, ah = tid & 1;
   const int agm = m0 + ar < M ? m0 + ar : M - 1;  // rows past M: a clamped copy, never stored
-  const bf16_t* asrc = p.A + (size_t)agm * p.lda + ah * 64;
-  u32x4 areg[8], breg[8];
-  auto load_chunk = [&](int c) {
+  const bf16_t* asrc = p.A + (size_t)agm * p.lda + ah * 32;
+  // register ring of GDEPTH chunks in flight (chunk c lives in slot c % GDEPTH)
+  constexpr int GDEPTH = WF == GWF_W4 ? LLJ_GDEPTH : 1;
+  constexpr int BV = WF == GWF_W4 ? 1 : 4;
+  u32x4 areg[GDEPTH][4], breg[GDEPTH][BV];
+  auto load_chunk = [&](int slot, int c) {
+    c = c < KC ? c : KC - 1;  // past the end: a valid duplicate, never stored
 #pragma unroll
-    for (int v = 0; v < 8; ++v) areg[v] = *reinterpret_cast<const u32x4*>(asrc + (size_t)c * kGBK + 8 * v);
+    for (int v = 0; v < 4; ++v) areg[slot][v] = *reinterpret_cast<const u32x4*>(asrc + (size_t)c * kGBK + 8 * v);
     if constexpr (WF == GWF_W4) {
-      // the 8 W4P tiles (16 columns x 128 k, 1 KiB each) of columns n0 .. n0 + 127, chunk c
       const u32x4* w = reinterpret_cast<const u32x4*>(p.W);
-#pragma unroll
-      for (int v = 0; v < 2; ++v) {
-        const int idx = tid + kGNT * v;  // 0..511: tile idx >> 6, lane idx & 63
-        const size_t nt = (size_t)(n0 / 16 + (idx >> 6));
-        breg[v] = __builtin_nontemporal_load(w + (nt * KC + c) * 64 + (idx & 63));
-      }
+      const size_t nt = (size_t)(n0 / 16 + (tid >> 5));
+      breg[slot][0] = __builtin_nontemporal_load(w + (nt * KC128 + (c >> 1)) * 64 + 32 * (c & 1) + (tid & 31));
     } else {
-      const bf16_t* w = reinterpret_cast<const bf16_t*>(p.W) + (size_t)(n0 + ar) * K + (size_t)c * kGBK + ah * 64;
+      const bf16_t* w = reinterpret_cast<const bf16_t*>(p.W) + (size_t)(n0 + ar) * K + (size_t)c * kGBK + ah * 32;
 #pragma unroll
-      for (int v = 0; v < 8; ++v) breg[v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w + 8 * v));
+      for (int v = 0; v < 4; ++v) breg[slot][v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w + 8 * v));
     }
   };
-  float rsum = 0.f;  // this thread's share of sum_k A[ar, k]
-  auto store_chunk = [&](int buf) {
-    bf16_t* a = As(buf) + ar * kAP + ah * 64;
+  f32x2 rsum2 = {0.f, 0.f};  // this thread's share of sum_k A[ar, k]
+  auto store_chunk = [&](int slot, int buf) {
+    bf16_t* a = As(buf) + ar * kAP + ah * 32;
 #pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      *reinterpret_cast<u32x4*>(a + 8 * v) = areg[v];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) rsum += bflo(areg[v][i]) + bfhi(areg[v][i]);
+    for (int v = 0; v < 4; ++v) {
+      *reinterpret_cast<u32x4*>(a + 8 * v) = areg[slot][v];
+      if constexpr (WF == GWF_W4) {
+        rsum2 += unpk(areg[slot][v][0]) + unpk(areg[slot][v][1]);
+        rsum2 += unpk(areg[slot][v][2]) + unpk(areg[slot][v][3]);
+      }
     }
     if constexpr (WF == GWF_W4) {
-#pragma unroll
-      for (int v = 0; v < 2; ++v) reinterpret_cast<u32x4*>(Bs(buf))[tid + kGNT * v] = breg[v];
+      reinterpret_cast<u32x4*>(Bs(buf))[tid] = breg[slot][0];
     } else {
-      bf16_t* b = reinterpret_cast<bf16_t*>(Bs(buf)) + ar * kAP + ah * 64;
+      bf16_t* b = reinterpret_cast<bf16_t*>(Bs(buf)) + ar * kAP + ah * 32;
 #pragma unroll
-      for (int v = 0; v < 8; ++v) *reinterpret_cast<u32x4*>(b + 8 * v) = breg[v];
+      for (int v = 0; v < 4; ++v) *reinterpret_cast<u32x4*>(b + 8 * v) = breg[slot][v];
     }
   };
 
@@ -124,27 +133,25 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_chunk(0);
-  for (int c = 0; c < KC; ++c) {
+  auto step = [&](int slot, int c) {  // chunk c: stage it, refill its slot with c + GDEPTH, multiply
     const int buf = c & 1;
-    store_chunk(buf);
+    store_chunk(slot, buf);
     __syncthreads();  // chunk c staged; every wave is done with chunk c - 1's buffer
-    if (c + 1 < KC) load_chunk(c + 1);
+    load_chunk(slot, c + GDEPTH);
     const bf16_t* a = As(buf);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {  // MFMA k-steps of the chunk
+    for (int s = 0; s < 2; ++s) {  // MFMA k-steps of the chunk: k = 32 s + 8 g + [0, 8)
       bf16x8 af[4], bfr[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = wr * 64 + 16 * i + row;
-        const int k = WF == GWF_W4 ? 32 * g + 8 * s : 32 * s + 8 * g;  // W4P k order, as the GEMV
-        af[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(a + r * kAP + k));
+        af[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(a + r * kAP + 32 * s + 8 * g));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if constexpr (WF == GWF_W4) {
-          const u32x4 wv = reinterpret_cast<const u32x4*>(Bs(buf))[(wc * 4 + j) * 64 + lane];
-          const uint32_t w = wv[s];
+          // word g of W4P lane 16 (2h + s) + column of tile wc * 4 + j (the chunk's half)
+          const uint32_t w = reinterpret_cast<const uint32_t*>(Bs(buf))[((wc * 4 + j) * 32 + 16 * s + row) * 4 + g];
           const uint4 d = make_uint4(and_or(w, msk, mag), and_or(w >> 4, msk, mag), and_or(w >> 8, msk, mag),
                                      and_or(w >> 12, msk, mag));
           bfr[j] = __builtin_bit_cast(bf16x8, d);
@@ -159,7 +166,18 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
     }
+  };
+#pragma unroll
+  for (int d = 0; d < GDEPTH; ++d) load_chunk(d, d);
+  int c = 0;  // KC is a multiple of 2 (K % 128 == 0); the ring slots are static inside the unrolled body
+  for (; c + GDEPTH <= KC; c += GDEPTH) {
+#pragma unroll
+    for (int d = 0; d < GDEPTH; ++d) step(d, c + d);
   }
+#pragma unroll
+  for (int d = 0; d < GDEPTH; ++d)
+    if (c + d < KC) step(d, c + d);
+  float rsum = rsum2.x + rsum2.y;
   // row sums of A (both halves of a row are adjacent lanes)
   rsum += lane_xor1(rsum);
   if (!ah) rs_lds[ar] = rsum;

@@ -19,6 +19,12 @@ REPO = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(REPO))
 import bench  # noqa: E402
 
+if __import__("os").environ.get("LLJ_LIB"):  # an experiment build of the library (same ABI)
+    sys.path.insert(0, str(REPO / "lit-llama-ja_amd"))
+    from lit_llama import _hip  # noqa: E402
+
+    _hip.LIB_PATH = Path(__import__("os").environ["LLJ_LIB"]).resolve()
+
 
 def main():
     ap = argparse.ArgumentParser()
