@@ -45,6 +45,14 @@ int llj_w8_repack(const void* qweight_ref, void* packed, int N, int K, void* str
 int llj_w8_unpack(const void* packed, void* qweight_ref, int N, int K, void* stream);
 int llj_w8_scale_zero(const void* scales, const void* zeros, int dtype, void* sz, int N, void* stream);
 
+/* ---------------------------------------------------------------- LLM.int8() weight layout
+ * Linear8bitLt's CB (N, K) int8 row-major (quantization.py:36-75; llj_i8_quant_weight) <-> "I8P",
+ * the tiling the int8 GEMV (wfmt 2) consumes: per 16 columns x 128 k, 2 KiB = two 1-KiB blocks (the
+ * two 64-deep MFMA steps), lane l of a block holding row 16 nt + (l & 15), k = 64 t + 16 (l >> 4)
+ * + 0 .. 15 of the chunk. packed and cb are distinct N*K-byte buffers. */
+int llj_i8_repack(const void* cb, void* packed, int N, int K, void* stream);
+int llj_i8_unpack(const void* packed, void* cb, int N, int K, void* stream);
+
 /* Host-side tuning knob (no device work): at most `tiles` 16-column tiles per workgroup in the
  * int4 / gptq.int8 GEMVs (default 4; 1 = one tile per workgroup). Results do not depend on it
  * (tested bitwise). Returns the previous value. */
@@ -52,7 +60,7 @@ int llj_set_tpw_max(int tiles);
 
 /* ---------------------------------------------------------------- linear layers
  * wfmt: 0 = int4 W4P (sz = (scale, 128+zero) pairs required), 1 = bf16 (N, K) row-major
- * (torch.nn.Linear.weight), 2 = LLM.int8() CB (N, K) int8 with sz = SCB (N) fp32,
+ * (torch.nn.Linear.weight), 2 = LLM.int8() CB in the I8P tiling (llj_i8_repack) with sz = SCB (N) fp32,
  * 3 = gptq.int8 W8P (sz = (scale, 2176+zero) pairs, llj_w8_scale_zero); for
  * wfmt 2, `i8ws` is the statistics workspace llj_i8_stats filled for the whole activation
  * and `i8_row0` the index of this call's first row in it (NULL / 0 otherwise).

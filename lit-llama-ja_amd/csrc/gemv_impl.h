@@ -29,7 +29,8 @@
 //      sum_k A (128 + lo) + A (2048 + 16 hi) = sum_k A q + 2176 sum_k A,
 //    so y = s * (acc - (2176 + z) * sum_k A), the W4 epilogue with offset 2176.
 //  * WF_BF16 — torch.nn.Linear weight (N, K) row-major bf16, read in place.
-//  * WF_I8 — LLM.int8(): CB (N, K) int8 row-quantized weight + SCB (N) fp32. A is quantized
+//  * WF_I8 — LLM.int8(): CB (N, K) int8 row-quantized weight in the I8P tiling (per (tile,
+//    chunk) 2 KiB, one contiguous KiB per MFMA step: llj_i8_repack) + SCB (N) fp32. A is quantized
 //    per row in the prologue (absmax over non-outlier elements, outlier columns zeroed,
 //    statistics from llj_i8_stats in int8.hip), int32 MFMA accumulation, dequant by
 //    SCA*SCB/127^2, plus the fp16 side product over the outlier columns.
@@ -242,7 +243,10 @@ __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float*
     }
     __syncthreads();
     for (int i = g; i < len; i += NG) {
-      const float w = (float)(_Float16)((float)CB[(size_t)n * p.K + s_k[i]] * scb);
+      const int k = s_k[i], kk = k & 127;  // byte of (n, k) in the I8P tiling
+      const size_t off = (((size_t)(n >> 4) * (p.K >> 7) + (k >> 7)) * 2 + (kk >> 6)) * 1024 +
+                         (16 * ((kk >> 4) & 3) + (n & 15)) * 16 + (kk & 15);
+      const float w = (float)(_Float16)((float)CB[off] * scb);
 #pragma unroll
       for (int m = 0; m < 8; ++m) acc[m] += s_a[m * kSideChunk + i] * w;
     }
@@ -384,11 +388,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       w1[j] = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.W) + off);
       if (DUAL) w2[j] = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.W2) + off);
       wstep = 16; vstride = 4;  // chunk = 256 B of a row; step t at +64 B
-    } else {
-      const size_t off = (size_t)(n0 + row) * K + 16 * grp;  // bytes
-      w1[j] = reinterpret_cast<const u32x4*>(reinterpret_cast<const int8_t*>(p.W) + off);
-      if (DUAL) w2[j] = reinterpret_cast<const u32x4*>(reinterpret_cast<const int8_t*>(p.W2) + off);
-      wstep = 8; vstride = 4;  // chunk = 128 B of a row; step t at +64 B
+    } else {  // I8P tiles (llj_i8_repack): per (tile, chunk) 2 KiB, step t at +1 KiB
+      w1[j] = reinterpret_cast<const u32x4*>(p.W) + (size_t)nt * KC * 128 + lane;
+      if (DUAL) w2[j] = reinterpret_cast<const u32x4*>(p.W2) + (size_t)nt * KC * 128 + lane;
+      wstep = 128; vstride = 64;
     }
   }
 

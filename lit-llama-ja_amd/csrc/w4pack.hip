@@ -99,6 +99,25 @@ __global__ void w8_unpack_kernel(const uint32_t* __restrict__ in, uint8_t* __res
 // sz[n] = (scale[n], off + zero[n]) in fp32 from the module's scale/zero buffers (any of
 // fp32 / bf16 / fp16, given by dtype code 0/1/2; one group per row: tile_cols = -1); off is the
 // magic-exponent offset of the format (W4P 128, W8P 128 + 2048).
+// LLM.int8() CB (N, K) int8 row-major <-> "I8P": per (16-column tile nt, 128-deep chunk c) 2 KiB,
+// [step t = 0: 64 lanes x 16 B][step t = 1: 64 lanes x 16 B]; lane l of step t holds
+// CB[16 nt + (l & 15)][128 c + 64 t + 16 (l >> 4) + 0 .. 15] (the int8 MFMA 16x16x64 B fragment),
+// so a wave reads 1 KiB contiguous per step (row-major CB: 16 rows x 64 B per wave load).
+// One thread per 16-byte piece.
+__global__ void i8_tile_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int N, int K, int unpack) {
+  const size_t total = (size_t)N * K / 16;
+  const int KC = K / 128;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int l = (int)(i & 63), t = (int)((i >> 6) & 1);
+    const size_t tc = i >> 7;  // (tile, chunk)
+    const int c = (int)(tc % KC), nt = (int)(tc / KC);
+    const int n = 16 * nt + (l & 15), k = 128 * c + 64 * t + 16 * (l >> 4);
+    const size_t rm = ((size_t)n * K + k) / 16;  // row-major piece
+    if (unpack) dst[rm] = src[i];
+    else dst[i] = src[rm];
+  }
+}
+
 __global__ void w4_sz_kernel(const void* scales, const void* zeros, int dtype, float2* sz, int N, float off) {
   int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
@@ -163,6 +182,26 @@ int llj_w8_unpack(const void* packed, void* qweight_ref, int N, int K, void* str
   int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
   hipLaunchKernelGGL(w8_unpack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint32_t*)packed,
                      (uint8_t*)qweight_ref, N, K);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_i8_repack(const void* cb, void* packed, int N, int K, void* stream) {
+  LLJ_REQUIRE(N > 0 && K > 0 && N % 16 == 0 && K % 128 == 0 && cb != packed);
+  const size_t total = (size_t)N * K / 16;
+  int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  hipLaunchKernelGGL(i8_tile_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4*)cb, (uint4*)packed,
+                     N, K, 0);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_i8_unpack(const void* packed, void* cb, int N, int K, void* stream) {
+  LLJ_REQUIRE(N > 0 && K > 0 && N % 16 == 0 && K % 128 == 0 && cb != packed);
+  const size_t total = (size_t)N * K / 16;
+  int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  hipLaunchKernelGGL(i8_tile_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4*)packed, (uint4*)cb,
+                     N, K, 1);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

@@ -25,6 +25,8 @@ SIGNATURES = {
     "llj_w4_scale_zero": [_P, _P, _I, _P, _I, _P],
     "llj_w8_repack": [_P, _P, _I, _I, _P],
     "llj_w8_unpack": [_P, _P, _I, _I, _P],
+    "llj_i8_repack": [_P, _P, _I, _I, _P],
+    "llj_i8_unpack": [_P, _P, _I, _I, _P],
     "llj_w8_scale_zero": [_P, _P, _I, _P, _I, _P],
     "llj_linear": [_I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
     "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I,

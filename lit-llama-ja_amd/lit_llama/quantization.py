@@ -208,7 +208,8 @@ def qlinear_4bit_weight(inp, weight, scales, zeros):
 
 
 def int8_linear(x: torch.Tensor, CB: torch.Tensor, SCB: torch.Tensor, bias, threshold: float = 6.0):
-    """LLM.int8() matmul of bf16 x (..., K) with the row-quantized (CB, SCB) weight."""
+    """LLM.int8() matmul of bf16 x (..., K) with the row-quantized (CB, SCB) weight; CB in the I8P
+    tiling (Linear8bitLt keeps its weight that way, llj_i8_repack)."""
     K = x.shape[-1]
     N = CB.shape[0]
     x2 = _as_rows(x, K)
@@ -235,6 +236,7 @@ class Linear8bitLt(torch.nn.Module):
         super().__init__()
         self.in_features = in_features
         self.out_features = out_features
+        self._ikey = None  # (data_ptr, version) of weight right after its in-place I8P tiling
         w = torch.empty((out_features, in_features), device=device, dtype=dtype)
         torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5))
         self.weight = torch.nn.Parameter(w, requires_grad=False)
@@ -281,17 +283,60 @@ class Linear8bitLt(torch.nn.Module):
             if k in missing_keys:
                 missing_keys.remove(k)
 
-    def _wspec(self):
-        if self.SCB is None:
+    # ---- CB storage: the int8 GEMV reads the I8P tiling (llj_i8_repack: one contiguous KiB per
+    # wave and MFMA step instead of 16 rows x 64 B), so `weight` is re-tiled IN PLACE the first
+    # time it is used on the GPU; the state dict, `.to()` and `cb_reference()` see the row-major CB
+    def _is_tiled(self) -> bool:
+        w = self.weight
+        return self._ikey is not None and self._ikey == (w.data_ptr(), w._version)
+
+    def cb_reference(self) -> torch.Tensor:
+        """CB (N, K) int8 row-major: the weight itself, or an un-tiled copy."""
+        w = self.weight
+        if not self._is_tiled():
+            return w.detach()
+        cb = torch.empty_like(w)
+        _hip.call("llj_i8_unpack", w.data_ptr(), cb.data_ptr(), w.shape[0], w.shape[1], _hip.stream())
+        return cb
+
+    def _prepare(self):
+        if self.SCB is None or self.weight.dtype != torch.int8:
             self._quantize_weight(self.weight)
+        if self._is_tiled():
+            return
+        w = self.weight
+        _hip.require_device(w, "Linear8bitLt weight")
+        N, K = w.shape
+        if N % 16 or K % 128:
+            raise NotImplementedError(f"Linear8bitLt ({N}, {K}): the int8 kernels need N % 16 == 0 and K % 128 == 0")
+        tiled = torch.empty_like(w)
+        _hip.call("llj_i8_repack", w.data_ptr(), tiled.data_ptr(), N, K, _hip.stream())
+        with torch.no_grad():
+            w.copy_(tiled)
+        self._ikey = (w.data_ptr(), w._version)
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+        if self._is_tiled():  # the state dict carries the row-major CB
+            destination[prefix + "weight"] = self.cb_reference()
+
+    def _apply(self, fn, *args, **kwargs):
+        if self._is_tiled():  # moving / casting: put the row-major CB back first
+            cb = self.cb_reference()
+            with torch.no_grad():
+                self.weight.copy_(cb)
+            self._ikey = None
+        return super()._apply(fn, *args, **kwargs)
+
+    def _wspec(self):
+        self._prepare()
         return 2, self.weight, self.SCB
 
     def forward(self, x):
         _hip.require_device(x, "input")
         if x.dtype != torch.bfloat16:
             raise TypeError(f"Linear8bitLt HIP path computes in bfloat16, got {x.dtype}")
-        if self.SCB is None:
-            self._quantize_weight(self.weight)
+        self._prepare()
         bias = None if self.bias is None else self.bias.to(torch.bfloat16)
         return int8_linear(x, self.weight, self.SCB, bias, self.threshold)
 

@@ -200,6 +200,16 @@ def test_int8_linear_vs_restatement(hip, M, outliers):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(cb.cpu().numpy(), cb_ref)
     np.testing.assert_allclose(scb.cpu().numpy(), scb_ref, rtol=0, atol=0)
+    # the GEMV reads CB in the I8P tiling; the round trip restores it byte for byte
+    cbt = torch.empty_like(cb)
+    call(hip, "llj_i8_repack", cb.data_ptr(), cbt.data_ptr(), N, K, st())
+    back = torch.empty_like(cb)
+    call(hip, "llj_i8_unpack", cbt.data_ptr(), back.data_ptr(), N, K, st())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(back.cpu().numpy(), cb_ref)
+    tiles = cbt.cpu().numpy().reshape(N // 16, K // 128, 2, 4, 16, 16)  # (nt, c, t, grp, row, byte)
+    np.testing.assert_array_equal(tiles[1, 2, 1, 3, 5], cb_ref[16 + 5, 256 + 64 + 48:256 + 64 + 64])
+    cb = cbt
     xd = T(x, torch.bfloat16)
     ws = torch.empty(hip.llj_i8_ws_bytes(M, K), dtype=torch.uint8, device=dev)
     call(hip, "llj_i8_stats", xd.data_ptr(), K, M, K, 6.0, ws.data_ptr(), st())
@@ -609,8 +619,10 @@ def test_int8_fused_ops_7b_shapes(hip, M):
         cb = torch.empty(N, K, dtype=torch.int8, device=dev)
         scb = torch.empty(N, dtype=torch.float32, device=dev)
         call(hip, "llj_i8_quant_weight", Wd.data_ptr(), 1, cb.data_ptr(), scb.data_ptr(), N, K, st())
+        cbt = torch.empty_like(cb)
+        call(hip, "llj_i8_repack", cb.data_ptr(), cbt.data_ptr(), N, K, st())
         torch.cuda.synchronize()
-        return O.int8_quantize_weight(W), cb, scb
+        return O.int8_quantize_weight(W), cbt, scb
 
     ws = torch.empty(max(hip.llj_i8_ws_bytes(M, C), hip.llj_i8_ws_bytes(M, H)), dtype=torch.uint8, device=dev)
     call(hip, "llj_i8_stats", xn.data_ptr(), C, M, C, 6.0, ws.data_ptr(), st())

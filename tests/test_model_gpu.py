@@ -228,6 +228,29 @@ def test_colblock_state_dict_contract(golden):
     np.testing.assert_allclose(y0, zref, rtol=2e-2, atol=2e-2)
 
 
+def test_linear8bitlt_tiling_is_invisible():
+    """Linear8bitLt re-tiles its CB in place (I8P) on first use; state_dict(), cb_reference() and
+    .cpu() still give the row-major CB of llj_i8_quant_weight, a reload re-tiles, and outputs agree."""
+    from lit_llama.quantization import Linear8bitLt
+
+    torch.manual_seed(3)
+    lin = Linear8bitLt(512, 256, bias=False, device="cuda", dtype=torch.bfloat16)
+    cb0 = lin.weight.detach().clone()
+    sd0 = {k: v.clone() for k, v in lin.state_dict().items()}
+    x = torch.randn(3, 512, device="cuda", dtype=torch.bfloat16)
+    y1 = lin(x)
+    assert lin._is_tiled() and not torch.equal(lin.weight, cb0)  # the storage now holds the tiling
+    sd1 = lin.state_dict()
+    assert set(sd1) == set(sd0) and torch.equal(sd1["weight"], cb0) and torch.equal(sd1["SCB"], sd0["SCB"])
+    assert torch.equal(lin.cb_reference(), cb0)
+    lin2 = Linear8bitLt(512, 256, bias=False, device="cuda", dtype=torch.bfloat16)
+    lin2.load_state_dict(sd1)
+    assert torch.equal(lin2(x), y1)
+    assert torch.equal(lin(x), y1)
+    lin.cpu()
+    assert torch.equal(lin.weight, cb0.cpu()) and not lin._is_tiled()
+
+
 def test_int8_model_vs_restatement():
     """llm.int8 (unpinned: no reference fixture exists) against the oracle's LLM.int8()
     restatement on the same weights: logits close, greedy ids margin-guarded."""

@@ -24,6 +24,8 @@ def main():
         cb = torch.empty(N, K, dtype=torch.int8, device=dev)
         scb = torch.empty(N, dtype=torch.float32, device=dev)
         _hip.call("llj_i8_quant_weight", W.data_ptr(), 1, cb.data_ptr(), scb.data_ptr(), N, K, st)
+        cbr = cb.clone()
+        _hip.call("llj_i8_repack", cbr.data_ptr(), cb.data_ptr(), N, K, st)  # the GEMV reads the I8P tiling
         cbs = [cb] + [cb.clone() for _ in range(NC - 1)]
         del W
         for M in (1, 8):

@@ -1,4 +1,4 @@
-"""int8 GEMV layout probe (profiling aid): the LLM.int8 GEMV (CB row-major, wfmt 2) vs the gptq.int8
+"""int8 GEMV layout probe (profiling aid): the LLM.int8 GEMV (CB in I8P tiles, wfmt 2) vs the gptq.int8
 GEMV (W8P tiles, wfmt 3) on the same shapes, cold weights (8 copies > MALL), M = 1 / 8, no
 outlier columns. python tools/w8_vs_i8.py"""
 from __future__ import annotations
@@ -38,6 +38,8 @@ def main():
         cb = torch.empty(N, K, dtype=torch.int8, device=dev)
         scb = torch.empty(N, dtype=torch.float32, device=dev)
         _hip.call("llj_i8_quant_weight", W.data_ptr(), 1, cb.data_ptr(), scb.data_ptr(), N, K, st)
+        cbr = cb.clone()
+        _hip.call("llj_i8_repack", cbr.data_ptr(), cb.data_ptr(), N, K, st)  # the GEMV reads the I8P tiling
         cbs = [cb.clone() for _ in range(NC)]
         # gptq.int8: random codes in the reference layout -> W8P
         qref = torch.randint(0, 256, (K, N), dtype=torch.uint8, device=dev, generator=g)
@@ -67,7 +69,7 @@ def main():
                 it[0] += 1
                 _hip.call("llj_linear", 3, x.data_ptr(), K, c.data_ptr(), sz.data_ptr(), None, y.data_ptr(), N, M, N,
                           K, None, 0, None, st)
-            for name, run in (("llm.int8 CB row-major", run_i8), ("gptq.int8 W8P", run_w8)):
+            for name, run in (("llm.int8 CB (I8P tiles)", run_i8), ("gptq.int8 W8P", run_w8)):
                 us = timed(run)
                 print(json.dumps({"N": N, "K": K, "M": M, "kernel": name, "us": round(us, 2),
                                   "GBps": round(N * K / us / 1e3, 1)}), flush=True)
