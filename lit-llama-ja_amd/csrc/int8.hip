@@ -50,14 +50,50 @@ __global__ __launch_bounds__(256) void i8_stats_kernel(const bf16_t* __restrict_
   }
 }
 
-// Pass 2, one block per row: SCA = max over the k-blocks, then the row quantized once:
-// q = round(A16 * 127 / SCA) clamped to +-127, outlier columns 0 (their contribution is the
-// fp16 side product).
+// q = round(A16 * 127 / SCA) clamped to +-127, outlier columns 0, for 8 columns
+__device__ __forceinline__ uint2 quant8(uint4 x, uint2 fl, float inv) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  const uint32_t fw[2] = {fl.x, fl.y};
+  uint32_t o[2] = {0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = to_f16f(bflo(w[i])), bb = to_f16f(bfhi(w[i]));
+    int qa = (int)fminf(fmaxf(rintf(a * inv), -127.f), 127.f);
+    int qb = (int)fminf(fmaxf(rintf(bb * inv), -127.f), 127.f);
+    if ((fw[i >> 1] >> (16 * (i & 1))) & 0xFF) qa = 0;
+    if ((fw[i >> 1] >> (16 * (i & 1) + 8)) & 0xFF) qb = 0;
+    o[i >> 1] |= ((uint32_t)(qa & 0xFF) | ((uint32_t)(qb & 0xFF) << 8)) << (16 * (i & 1));
+  }
+  return make_uint2(o[0], o[1]);
+}
+
+// Pass 2, one block per row: SCA = max over the k-blocks, then the row quantized once (outlier
+// columns 0: their contribution is the fp16 side product). The row and its flags (up to QV
+// vectors of 8 per thread, K <= 8 * 256 * QV) are loaded BEFORE the k-block maxima are reduced, so
+// both reads share one memory latency.
+constexpr int QV = 8;
 __global__ __launch_bounds__(256) void i8_quant_act_kernel(const bf16_t* __restrict__ A, int lda, int M, int K,
                                                            char* __restrict__ ws) {
   __shared__ float s_sca;
   const int m = blockIdx.x, tid = threadIdx.x;
   const I8Layout L = i8_layout(ws, M, K);
+  const bf16_t* ar = A + (size_t)m * lda;
+  int8_t* qr = L.aq + (size_t)m * K;
+  const int nv = K / 8;
+  uint4 xs[QV];
+  uint2 fs[QV];
+  const bool pre = nv <= QV * 256;
+  const int jn = (nv + 255) / 256;  // uniform
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < QV; ++j) {
+      if (j < jn) {
+        const int v = tid + 256 * j < nv ? tid + 256 * j : nv - 1;  // clamped: always valid
+        xs[j] = *reinterpret_cast<const uint4*>(ar + 8 * v);
+        fs[j] = *reinterpret_cast<const uint2*>(L.flag + 8 * v);
+      }
+    }
+  }
   if (tid < 64) {
     float mx = tid < kNSB ? L.part[(size_t)tid * M + m] : 0.f;
     mx = wave_max(mx);
@@ -69,24 +105,18 @@ __global__ __launch_bounds__(256) void i8_quant_act_kernel(const bf16_t* __restr
   __syncthreads();
   const float s = s_sca;
   const float inv = s > 0.f ? 127.f / s : 0.f;
-  const bf16_t* ar = A + (size_t)m * lda;
-  int8_t* qr = L.aq + (size_t)m * K;
-  for (int v = tid; v < K / 8; v += 256) {
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < QV; ++j) {
+      const int v = tid + 256 * j;
+      if (j < jn && v < nv) *reinterpret_cast<uint2*>(qr + 8 * v) = quant8(xs[j], fs[j], inv);
+    }
+    return;
+  }
+  for (int v = tid; v < nv; v += 256) {
     const uint4 x = *reinterpret_cast<const uint4*>(ar + 8 * v);
     const uint2 fl = *reinterpret_cast<const uint2*>(L.flag + 8 * v);
-    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-    const uint32_t fw[2] = {fl.x, fl.y};
-    uint32_t o[2] = {0, 0};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float a = to_f16f(bflo(w[i])), bb = to_f16f(bfhi(w[i]));
-      int qa = (int)fminf(fmaxf(rintf(a * inv), -127.f), 127.f);
-      int qb = (int)fminf(fmaxf(rintf(bb * inv), -127.f), 127.f);
-      if ((fw[i >> 1] >> (16 * (i & 1))) & 0xFF) qa = 0;
-      if ((fw[i >> 1] >> (16 * (i & 1) + 8)) & 0xFF) qb = 0;
-      o[i >> 1] |= ((uint32_t)(qa & 0xFF) | ((uint32_t)(qb & 0xFF) << 8)) << (16 * (i & 1));
-    }
-    *reinterpret_cast<uint2*>(qr + 8 * v) = make_uint2(o[0], o[1]);
+    *reinterpret_cast<uint2*>(qr + 8 * v) = quant8(x, fl, inv);
   }
 }
 
