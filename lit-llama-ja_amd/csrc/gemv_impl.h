@@ -242,13 +242,28 @@ __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float*
         s_a[m * kSideChunk + i] = m < M ? (float)(_Float16)bf2f(p.A[(size_t)m * p.lda + k]) : 0.f;
     }
     __syncthreads();
-    for (int i = g; i < len; i += NG) {
-      const int k = s_k[i], kk = k & 127;  // byte of (n, k) in the I8P tiling
-      const size_t off = (((size_t)(n >> 4) * (p.K >> 7) + (k >> 7)) * 2 + (kk >> 6)) * 1024 +
-                         (16 * ((kk >> 4) & 3) + (n & 15)) * 16 + (kk & 15);
-      const float w = (float)(_Float16)((float)CB[off] * scb);
+    // the CB bytes of SB outlier columns are loaded together (independent loads, one latency),
+    // then accumulated in the same column order as one at a time
+    constexpr int SB = 8;
+    for (int i0 = g; i0 < len; i0 += NG * SB) {
+      int cbv[SB];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) acc[m] += s_a[m * kSideChunk + i] * w;
+      for (int u = 0; u < SB; ++u) {
+        const int i = i0 + NG * u < len ? i0 + NG * u : i0;
+        const int k = s_k[i], kk = k & 127;  // byte of (n, k) in the I8P tiling
+        const size_t off = (((size_t)(n >> 4) * (p.K >> 7) + (k >> 7)) * 2 + (kk >> 6)) * 1024 +
+                           (16 * ((kk >> 4) & 3) + (n & 15)) * 16 + (kk & 15);
+        cbv[u] = CB[off];
+      }
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int i = i0 + NG * u;
+        if (i < len) {
+          const float w = (float)(_Float16)((float)cbv[u] * scb);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) acc[m] += s_a[m * kSideChunk + i] * w;
+        }
+      }
     }
     __syncthreads();
   }
