@@ -98,7 +98,7 @@ def _oracle_steps(orc, ids):
     return np.stack(outs, 1)
 
 
-@pytest.mark.parametrize("B", [1, 8])
+@pytest.mark.parametrize("B", [1, 2, 8])  # 2: the batched RMSNorm hand-off (nstat)
 @pytest.mark.parametrize("mode", ["gptq.int4", None, "llm.int8"])
 def test_7b_width_decode_vs_oracle(mode, B):
     key = ("setup", mode)
