@@ -50,6 +50,9 @@ struct GemmParams {
 };
 
 constexpr int kGBM = 128, kGBN = 128, kGBK = 64, kGNT = 256;
+#ifndef LLJ_GEMM_PRIO
+#define LLJ_GEMM_PRIO 0
+#endif
 #ifndef LLJ_GEMM_MFAST
 #define LLJ_GEMM_MFAST 1
 #endif
@@ -170,10 +173,12 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
               bf16x8, *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(Bs(buf)) + n * kAP + 32 * s + 8 * g));
         }
       }
+      if (LLJ_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);  // the MFMA cluster ahead of the other waves' staging
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+      if (LLJ_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
     }
   };
 #pragma unroll
