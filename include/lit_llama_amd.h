@@ -61,7 +61,11 @@ int llj_set_tpw_max(int tiles);
 /* ---------------------------------------------------------------- linear layers
  * wfmt: 0 = int4 W4P (sz = (scale, 128+zero) pairs required), 1 = bf16 (N, K) row-major
  * (torch.nn.Linear.weight), 2 = LLM.int8() CB in the I8P tiling (llj_i8_repack) with sz = SCB (N) fp32,
- * 3 = gptq.int8 W8P (sz = (scale, 2176+zero) pairs, llj_w8_scale_zero); for
+ * 3 = gptq.int8 W8P (sz = (scale, 2176+zero) pairs, llj_w8_scale_zero),
+ * 4 | (g / 128) << 8 = grouped int4 (ColBlockQuantizedLinear tile_cols = g, g % 128 == 0,
+ * quantization.py:338-409 with scales (N, ceil(K / g))): W4P tiles with sz = (scale, 128+zero)
+ * pairs per (group, column), group-major (ceil(K / g), N) (llj_w4_scale_zero over the transposed
+ * buffers); the fused ops below take the same wfmt; for
  * wfmt 2, `i8ws` is the statistics workspace llj_i8_stats filled for the whole activation
  * and `i8_row0` the index of this call's first row in it (NULL / 0 otherwise).
  * C[M, N] = A[M, K] . W^T (+ bias), bf16 in/out, fp32 (int8: int32) accumulation,

@@ -13,12 +13,16 @@ static int dispatch(int wf, int am, const GemvParams& p, hipStream_t s) {
     case WF_BF16: return gemv_launch_bf16(am, EP, p, s);
     case WF_W8: return gemv_launch_w8(am, EP, p, s);
     case WF_I8: return gemv_launch_i8(am, EP, p, s);
+    case WF_W4G: return gemv_launch_w4g(am, EP, p, s);
   }
   return LLJ_EINVAL;
 }
 
 template <int EP>
-static int run(int wf, GemvParams& p, void* stream) {
+static int run(int wfmt, GemvParams& p, void* stream) {
+  // wfmt: weight format in bits [0, 8); WF_W4G carries its group size (in 128-deep chunks) above
+  const int wf = wfmt & 0xff;
+  p.gch = wfmt >> 8;
   if (int e = check_shape(wf, p)) return e;
   // norm statistics hand-off: partial sums of squares [npart][16] (row slot = row of the call),
   // written by a residual op, read by the next norm-fused op; at most 16 rows, 2 partials per thread

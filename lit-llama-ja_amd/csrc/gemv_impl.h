@@ -34,6 +34,11 @@
 //    per row in the prologue (absmax over non-outlier elements, outlier columns zeroed,
 //    statistics from llj_i8_stats in int8.hip), int32 MFMA accumulation, dequant by
 //    SCA*SCB/127^2, plus the fp16 side product over the outlier columns.
+//  * WF_W4G — grouped int4 (ColBlock bits=4, tile_cols = g, g % 128 == 0; reference
+//    quantization.py:338-409 with scales (N, ceil(K / g))): the W4P tiles of WF_W4 plus one
+//    (scale, 128 + zero) pair per (group, column), group-major (G, N). Each 128-deep chunk lies in
+//    one group, so a wave accumulates the chunk into a fresh accumulator (and its A row sums
+//    through a ones fragment) and adds s_g * (acc_c - (128 + z_g) * sum_c A) to the running sum.
 #pragma once
 #include <algorithm>
 
@@ -44,7 +49,7 @@
 
 namespace llj {
 
-enum : int { WF_W4 = 0, WF_BF16 = 1, WF_I8 = 2, WF_W8 = 3 };
+enum : int { WF_W4 = 0, WF_BF16 = 1, WF_I8 = 2, WF_W8 = 3, WF_W4G = 4 };
 enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2 };
 enum : int { EP_STORE = 0, EP_RESID = 1, EP_QKV = 2, EP_SWIGLU = 3 };
 
@@ -81,6 +86,7 @@ struct GemvParams {
   const float* nstat;
   int npart;
   float* nstat_out;
+  int gch;  // WF_W4G: group size in 128-deep chunks (tile_cols / 128)
 };
 constexpr int kNstRows = 16;
 #ifndef LLJ_SACC_NORM
@@ -192,7 +198,7 @@ __device__ __forceinline__ bf16x8 dequant_w4(uint32_t w, uint32_t msk, uint32_t 
 template <int WF>
 __device__ __forceinline__ int kofs(int t, int grp) {
   // k offset inside a 128-deep chunk of the elements lane-group `grp` feeds at MFMA step t
-  return (WF == WF_W4 || WF == WF_W8) ? 32 * grp + 8 * t : WF == WF_BF16 ? 32 * t + 8 * grp : 64 * t + 16 * grp;
+  return (WF == WF_W4 || WF == WF_W8 || WF == WF_W4G) ? 32 * grp + 8 * t : WF == WF_BF16 ? 32 * t + 8 * grp : 64 * t + 16 * grp;
 }
 
 // fp16 side product of LLM.int8() over the outlier columns, for this workgroup's 16 columns
@@ -333,12 +339,13 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   constexpr bool DUAL = (EP == EP_SWIGLU);
   constexpr bool I8 = (WF == WF_I8);
   constexpr bool W4L = (WF == WF_W4 || WF == WF_W8);  // nibble-coded: offset removed with row sums
+  constexpr bool GRP = (WF == WF_W4G);  // grouped int4: offset and scale removed per chunk
   constexpr bool ALDS = I8 || (AM != AM_GLOBAL);
   // row sums of A for the nibble offset: an extra MFMA against a ones fragment for the global-A
   // form and for batched norm-fused rows (LLJ_SACC_NORM; the VALU sums + 8 wave reductions of the
   // prologue sit on its critical path), else summed while the LDS image is written
   constexpr bool SACC = W4L && (!ALDS || (LLJ_SACC_NORM && AM == AM_NORM && MB > 1));
-  constexpr int WV = (WF == WF_W4) ? 1 : (WF == WF_BF16 ? 4 : 2);  // 16-B loads per lane per chunk per matrix
+  constexpr int WV = (WF == WF_W4 || GRP) ? 1 : (WF == WF_BF16 ? 4 : 2);  // 16-B loads per lane per chunk per matrix
   constexpr int NSTEP = I8 ? 2 : 4;
   const int lane = threadIdx.x & 63;
   const int wave = uniform(threadIdx.x >> 6);
@@ -390,7 +397,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   for (int j = 0; j < TPW; ++j) {
     const int nt = ntj[j], n0 = nt * 16;
     w2[j] = nullptr;
-    if (WF == WF_W4) {
+    if (WF == WF_W4 || GRP) {
       w1[j] = reinterpret_cast<const u32x4*>(p.W) + (size_t)nt * KC * 64 + lane;
       if (DUAL) w2[j] = reinterpret_cast<const u32x4*>(p.W2) + (size_t)nt * KC * 64 + lane;
       wstep = 64; vstride = 0;
@@ -418,9 +425,18 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
 
   u32x4 r1[D][TPW][WV], r2[D][TPW][WV];
   u32x4 ra[D][4];
+  float2 rg[D][TPW], rg2[D][TPW];  // WF_W4G: (scale, 128 + zero) of the chunk's group, this lane's column
   auto load = [&](int d, int i) {
     int c = wave + NW * (i < nmy ? i : nmy - 1);
     c = c < 0 ? 0 : (c >= KC ? KC - 1 : c);  // always a valid chunk (loads past the end are unused)
+    if constexpr (GRP) {
+      const size_t go = (size_t)(c / p.gch) * p.N + row;
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        rg[d][j] = p.sz[go + ntj[j] * 16];
+        if (DUAL) rg2[d][j] = p.sz2[go + ntj[j] * 16];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TPW; ++j)
 #pragma unroll
@@ -444,6 +460,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       }
       return;
     }
+    f32x4 gt[TPW], gt2[TPW], gs = {0, 0, 0, 0};  // WF_W4G: this chunk's sums
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) gt[j] = gt2[j] = gs;
 #pragma unroll
     for (int t = 0; t < NSTEP; ++t) {
       // LDS lanes of rows >= M read row 0 (abase clamped): their output rows are never stored, and
@@ -457,6 +476,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
           if (DUAL) acc2[j] = mfma_bf16(a, dequant_w4(r2[d][j][0][t], msk, mag), acc2[j]);
         }
         if (SACC && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);  // else: row sums from the prologue / caller
+      } else if constexpr (GRP) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          gt[j] = mfma_bf16(a, dequant_w4(r1[d][j][0][t], msk, mag), gt[j]);
+          if (DUAL) gt2[j] = mfma_bf16(a, dequant_w4(r2[d][j][0][t], msk, mag), gt2[j]);
+        }
+        gs = mfma_bf16(a, ones, gs);
       } else if constexpr (WF == WF_W8) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
@@ -481,6 +508,15 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         iacc = mfma_i8(a, __builtin_bit_cast(i32x4, r1[d][0][t]), iacc);
         if (DUAL) iacc2 = mfma_i8(a, __builtin_bit_cast(i32x4, r2[d][0][t]), iacc2);
       }
+    }
+    if constexpr (GRP) {  // s_g * (sum_c A (128 + q) - (128 + z_g) * sum_c A)
+#pragma unroll
+      for (int j = 0; j < TPW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc[j][r] += rg[d][j].x * (gt[j][r] - rg[d][j].y * gs[r]);
+          if (DUAL) acc2[j][r] += rg2[d][j].x * (gt2[j][r] - rg2[d][j].y * gs[r]);
+        }
     }
   };
 
@@ -828,7 +864,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         }
         y = s1 * (ya[r] - o1 * sa);
         if (DUAL) y2 = s2 * (yb[r] - o2 * sa);
-      } else if (WF == WF_BF16) {
+      } else if (WF == WF_BF16 || GRP) {
         y = ya[r];
         y2 = yb[r];
       } else {
@@ -1081,7 +1117,8 @@ static int pick_am(int wf, const GemvParams& p) {
 
 static int check_shape(int wf, const GemvParams& p) {
   if (p.M < 1 || p.M > 16 || p.N % 16 || p.K % 128 || p.K < 128) return LLJ_EINVAL;
-  if (wf != WF_W4 && wf != WF_BF16 && wf != WF_I8 && wf != WF_W8) return LLJ_EINVAL;
+  if (wf != WF_W4 && wf != WF_BF16 && wf != WF_I8 && wf != WF_W8 && wf != WF_W4G) return LLJ_EINVAL;
+  if (wf == WF_W4G && p.gch < 1) return LLJ_EINVAL;
   if (wf != WF_BF16 && !p.sz) return LLJ_EINVAL;
   if (p.C && (p.ldc & 1)) return LLJ_EINVAL;  // epilogues store column pairs as 4-byte words
   return 0;
@@ -1093,6 +1130,7 @@ int gemv_launch_w4(int am, int ep, const GemvParams& p, hipStream_t s);
 int gemv_launch_bf16(int am, int ep, const GemvParams& p, hipStream_t s);
 int gemv_launch_w8(int am, int ep, const GemvParams& p, hipStream_t s);
 int gemv_launch_i8(int am, int ep, const GemvParams& p, hipStream_t s);
+int gemv_launch_w4g(int am, int ep, const GemvParams& p, hipStream_t s);
 
 template <int WF, int AM>
 static int launch_ep(int ep, const GemvParams& p, hipStream_t s) {

@@ -103,9 +103,16 @@ class ColBlockQuantizedLinear(torch.nn.Module):
         return weight
 
     # ---- HIP path ---------------------------------------------------------------------
+    def _groups(self) -> int:
+        return self.scales.shape[1]
+
     def _supported(self) -> bool:
-        return self.bits in (4, 8) and self.scales.shape[1] == 1 and self.out_features % 16 == 0 \
-            and self.in_features % 128 == 0
+        if self.out_features % 16 or self.in_features % 128 or self.bits not in (4, 8):
+            return False
+        if self._groups() == 1:
+            return True
+        # grouped (tile_cols = g): int4 with every 128-deep k-chunk inside one group
+        return self.bits == 4 and self.tile_cols % 128 == 0
 
     def _is_packed(self) -> bool:
         """quant_weight currently holds the streaming tiling (not the reference layout)."""
@@ -133,9 +140,9 @@ class ColBlockQuantizedLinear(torch.nn.Module):
         _hip.require_device(qw, "ColBlockQuantizedLinear.quant_weight")
         if not self._supported():
             raise NotImplementedError(
-                f"ColBlockQuantizedLinear(bits={self.bits}, groups={self.scales.shape[1]}, "
-                f"{self.in_features}->{self.out_features}) has no HIP kernel yet "
-                "(gptq.int4 / gptq.int8 with tile_cols=-1, N % 16 == 0, K % 128 == 0 is supported)")
+                f"ColBlockQuantizedLinear(bits={self.bits}, tile_cols={self.tile_cols}, groups={self._groups()}, "
+                f"{self.in_features}->{self.out_features}) has no HIP kernel yet (supported: N % 16 == 0, "
+                "K % 128 == 0; gptq.int4 / gptq.int8 with tile_cols=-1, int4 with tile_cols % 128 == 0)")
         N, K = self.out_features, self.in_features
         s = _hip.stream()
         if not self._is_packed():
@@ -149,13 +156,15 @@ class ColBlockQuantizedLinear(torch.nn.Module):
             del tmp
             self._qkey = (qw.data_ptr(), qw._version)
         if szkey != self._szkey or self._sz is None or self._sz.device != qw.device:
-            if self._sz is None or self._sz.device != qw.device:
-                self._sz = torch.empty(N, 2, dtype=torch.float32, device=qw.device)
-            sc1, zr1 = sc.reshape(N).contiguous(), zr.reshape(N).contiguous()
+            G = self._groups()
+            if self._sz is None or self._sz.device != qw.device or self._sz.shape[0] != G * N:
+                self._sz = torch.empty(G * N, 2, dtype=torch.float32, device=qw.device)
+            # (scale, offset + zero) pairs; grouped: group-major (G, N), one row of pairs per group
+            sc1, zr1 = sc.t().contiguous().reshape(G * N), zr.t().contiguous().reshape(G * N)
             if sc1.dtype not in _DTYPE_CODE or zr1.dtype != sc1.dtype:
                 sc1, zr1 = sc1.float(), zr1.float()
             _hip.call("llj_w4_scale_zero" if self.bits == 4 else "llj_w8_scale_zero", sc1.data_ptr(), zr1.data_ptr(),
-                      _DTYPE_CODE[sc1.dtype], self._sz.data_ptr(), N, s)
+                      _DTYPE_CODE[sc1.dtype], self._sz.data_ptr(), G * N, s)
             self._szkey = szkey
 
     def _save_to_state_dict(self, destination, prefix, keep_vars):
@@ -180,7 +189,10 @@ class ColBlockQuantizedLinear(torch.nn.Module):
 
     @property
     def wfmt(self) -> int:
-        """C-ABI weight format: 0 = W4P (bits=4), 3 = W8P (bits=8)."""
+        """C-ABI weight format: 0 = W4P (bits=4), 3 = W8P (bits=8), grouped int4 (tile_cols = g):
+        4 (W4P tiles + per-group pairs) | (g / 128) << 8."""
+        if self._groups() > 1:
+            return 4 | ((self.tile_cols // 128) << 8)
         return 0 if self.bits == 4 else 3
 
     def forward(self, inp):
@@ -347,17 +359,22 @@ class GPTQQuantizer:
     error)`. The calibration Hessian, the Cholesky factors and the trailing block update are
     library work on the device (torch GEMM / rocSOLVER); the sequential 128-column loop and the
     ColBlock packing are the HIP kernels `llj_gptq_block` / `llj_colblock_pack` (csrc/gptq.hip).
-    Supported: the configuration quantize/gptq.py uses (per-channel, asymmetric, groupsize -1,
-    blocksize 128), in_features % 128 == 0. fp32 weights reproduce the reference's op order;
+    Supported: per-channel, asymmetric, blocksize 128 (the configuration quantize/gptq.py uses),
+    groupsize -1 or a multiple of 128 (grouped scales: each group's (scale, zero) is found when the
+    column loop reaches its first column, from the weights as updated so far (reference 571-577);
+    with groupsize % 128 == 0 that is the start of a 128-column block), in_features % 128 == 0.
+    fp32 weights reproduce the reference's op order;
     other weight dtypes are quantized from their fp32 value (the reference would round the
     packing step in that dtype). No CPU path."""
 
     def __init__(self, linear_module, *, bits, perchannel=True, sym=False, blocksize=128, percdamp=0.01,
                  groupsize=-1, actorder=False):
         assert isinstance(linear_module, torch.nn.Linear)
-        if not perchannel or sym or groupsize != -1 or blocksize != 128:
-            raise NotImplementedError("GPTQQuantizer HIP path: perchannel=True, sym=False, groupsize=-1, "
-                                      "blocksize=128 (the gptq.int4 / gptq.int8 producer configuration)")
+        if not perchannel or sym or blocksize != 128 or (groupsize != -1 and (groupsize <= 0 or groupsize % 128)):
+            raise NotImplementedError("GPTQQuantizer HIP path: perchannel=True, sym=False, blocksize=128, "
+                                      "groupsize -1 or a multiple of 128 (the gptq.int4 / gptq.int8 producer "
+                                      "configuration)")
+        assert not (actorder and groupsize != -1), "The permutation trick does not work for grouped quantization"
         self.linear_module = linear_module
         self.dev = linear_module.weight.device
         self.rows, self.columns = linear_module.weight.shape
@@ -369,8 +386,9 @@ class GPTQQuantizer:
         self.maxq = 2 ** bits - 1
         self.perchannel, self.sym, self.blocksize = perchannel, sym, blocksize
         self.percdamp, self.groupsize, self.actorder = percdamp, groupsize, actorder
-        self.tile_cols = self.columns
-        self.scales = torch.zeros((self.rows, 1), dtype=linear_module.weight.dtype, device=self.dev)
+        self.tile_cols = self.columns if groupsize == -1 else groupsize
+        self.scales = torch.zeros((self.rows, (self.columns + self.tile_cols - 1) // self.tile_cols),
+                                  dtype=linear_module.weight.dtype, device=self.dev)
         self.zeros = torch.zeros_like(self.scales)
 
     def find_params_weight(self, x):
@@ -433,13 +451,24 @@ class GPTQQuantizer:
         # the stored (scale, zero) -- rounded to the buffers' dtype, e.g. bf16 -- are what decode
         # dequantizes with, so the column loop's reconstructions and error feedback use them too
         # (fp32 buffers: the reference's values exactly)
-        sc = self.scales.reshape(-1).float().contiguous()
-        zr = self.zeros.reshape(-1).float().contiguous()
+        g = self.tile_cols
+        G = self.scales.shape[1]
         s = _hip.stream()
+        scg, zrg = [None] * G, [None] * G  # per group: the stored (scale, zero) as fp32 columns
+        if G == 1:
+            scg[0] = self.scales.reshape(-1).float().contiguous()
+            zrg[0] = self.zeros.reshape(-1).float().contiguous()
         for i1 in range(0, K, B):
             i2 = i1 + B
-            _hip.call("llj_gptq_block", Hinv.data_ptr(), K, i1, Wt.data_ptr(), N, sc.data_ptr(), zr.data_ptr(),
-                      self.bits, Qt.data_ptr(), Err.data_ptr(), loss.data_ptr(), s)
+            gi = i1 // g
+            if G > 1 and i1 % g == 0:  # reference 571-577: the group's params from W as updated so far
+                gs, gz = self.find_params_weight(Wt[i1:i1 + g].t())
+                self.scales[:, gi] = gs.reshape(-1)
+                self.zeros[:, gi] = gz.reshape(-1)
+                scg[gi] = self.scales[:, gi].float().contiguous()
+                zrg[gi] = self.zeros[:, gi].float().contiguous()
+            _hip.call("llj_gptq_block", Hinv.data_ptr(), K, i1, Wt.data_ptr(), N, scg[gi].data_ptr(),
+                      zrg[gi].data_ptr(), self.bits, Qt.data_ptr(), Err.data_ptr(), loss.data_ptr(), s)
             if i2 < K:  # W[:, i2:] -= Err1 @ Hinv[i1:i2, i2:] (596), transposed
                 Wt[i2:] -= Hinv[i1:i2, i2:].t().matmul(Err)
         if perm is not None:
@@ -452,7 +481,10 @@ class GPTQQuantizer:
         q_module.zeros = self.zeros
         # pack_weight (374-388) into quant_weight's column-major storage ((K/epb, N) bytes)
         assert q_module.quant_weight.stride() == (1, N)
-        _hip.call("llj_colblock_pack", Qt.data_ptr(), K, N, sc.data_ptr(), zr.data_ptr(), self.bits,
-                  q_module.quant_weight.data_ptr(), s)
+        epb = 8 // self.bits
+        for gi in range(G):  # group gi's columns are the contiguous bytes [g0 / epb, g1 / epb) x N
+            g0, g1 = gi * g, min(K, (gi + 1) * g)
+            _hip.call("llj_colblock_pack", Qt[g0].data_ptr(), g1 - g0, N, scg[gi].data_ptr(), zrg[gi].data_ptr(),
+                      self.bits, q_module.quant_weight.data_ptr() + (g0 // epb) * N, s)
         q_module.bias = self.linear_module.bias
         return q_module, error

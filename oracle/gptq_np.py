@@ -2,7 +2,12 @@
 
 Follows /root/reference/lit_llama/quantization.py:424-614 (GPTQQuantizer, the IST-DASLab GPTQ
 algorithm, arXiv:2210.17323) for the configuration quantize/gptq.py:84-90 uses for gptq.int4 /
-gptq.int8: per-channel, asymmetric, blocksize 128, percdamp 0.01, groupsize -1, actorder True.
+gptq.int8: per-channel, asymmetric, blocksize 128, percdamp 0.01, groupsize -1, actorder True;
+and grouped scales (groupsize g, actorder off; 571-577). The reference's own grouped column loop
+raises (576 assigns the (N, 1) scale into the (N,) column scales[:, j]), so the grouped case
+restates the algorithm as written there (a group's (scale, zero) from find_params_weight on the
+group's columns of W as updated by the earlier blocks, at the group's first column) and its
+parity is UNPINNED: no reference output exists (tests/golden/make_golden.py gen_gptq_grouped).
 Every step is fp32 like the reference's torch CPU run; the column loop is the reference's op
 order with each fp32 op rounded on its own (numpy does not contract to FMA), so it is bitwise
 the reference's loop given the same W1 / Hinv1. The Cholesky factors come from LAPACK in fp32 as
@@ -65,8 +70,9 @@ def hinv_upper(H: np.ndarray, actorder: bool = True, percdamp: float = 0.01):
 
 
 def gptq_block(W1: np.ndarray, Hinv1: np.ndarray, scale, zero, bits: int):
-    """quantization.py:568-596 for one block (groupsize -1), in place on a copy of W1 (N, count).
-    Returns (Q1 reconstructions, Err1, Losses1) — each op fp32, the reference's order."""
+    """quantization.py:568-596 for one block, in place on a copy of W1 (N, count). scale / zero:
+    (N,) for the whole block, or (N, count) per column (grouped). Returns (Q1 reconstructions,
+    Err1, Losses1) — each op fp32, the reference's order."""
     maxq = F32(2 ** bits - 1)
     W1 = W1.astype(F32).copy()
     N, count = W1.shape
@@ -76,8 +82,10 @@ def gptq_block(W1: np.ndarray, Hinv1: np.ndarray, scale, zero, bits: int):
     for i in range(count):
         w = W1[:, i].copy()
         d = Hinv1[i, i]
-        q = np.clip(np.round(w / scale).astype(F32) + zero, F32(0), maxq).astype(F32)  # 470-473
-        q = (scale * (q - zero)).astype(F32)
+        sc = scale if np.ndim(scale) == 1 else scale[:, i]
+        zr = zero if np.ndim(zero) == 1 else zero[:, i]
+        q = np.clip(np.round(w / sc).astype(F32) + zr, F32(0), maxq).astype(F32)  # 470-473
+        q = (sc * (q - zr)).astype(F32)
         Q1[:, i] = q
         dq = (w - q).astype(F32)
         L1[:, i] = (dq * dq).astype(F32) / F32(d * d)
@@ -88,11 +96,18 @@ def gptq_block(W1: np.ndarray, Hinv1: np.ndarray, scale, zero, bits: int):
 
 
 def gptq_quantize(W: np.ndarray, H: np.ndarray, bits: int, blocksize: int = 128, actorder: bool = True,
-                  percdamp: float = 0.01):
-    """GPTQQuantizer.quantize (quantization.py:532-614) for groupsize -1. W (N, K) fp32, H (K, K).
-    Returns (Q reconstructions (N, K), scale (N,), zero (N,), error)."""
+                  percdamp: float = 0.01, groupsize: int = -1):
+    """GPTQQuantizer.quantize (quantization.py:532-614). W (N, K) fp32, H (K, K). Returns
+    (Q reconstructions (N, K), scale, zero, error) with scale / zero (N,) for groupsize -1, else
+    (N, ceil(K / groupsize)) (see the module header: grouped parity unpinned)."""
+    assert not (actorder and groupsize != -1)  # 465-467
     W = W.astype(F32).copy()
     scale, zero = find_params_weight(W, bits)
+    K0 = W.shape[1]
+    if groupsize != -1:
+        G = (K0 + groupsize - 1) // groupsize
+        scales = np.repeat(scale[:, None], G, 1)  # self.scales[:] = scale (533)
+        zeros = np.repeat(zero[:, None], G, 1)
     Hinv, perm, dead = hinv_upper(H, actorder, percdamp)
     W[:, dead] = 0
     if perm is not None:
@@ -100,23 +115,41 @@ def gptq_quantize(W: np.ndarray, H: np.ndarray, bits: int, blocksize: int = 128,
     N, K = W.shape
     Q = np.zeros_like(W)
     Losses = np.zeros_like(W)
+    cur = (scale, zero)
     for i1 in range(0, K, blocksize):
         i2 = min(i1 + blocksize, K)
-        Q1, Err1, L1 = gptq_block(W[:, i1:i2], Hinv[i1:i2, i1:i2], scale, zero, bits)
+        bs, bz = scale, zero
+        if groupsize != -1:  # 571-577: params at each group's first column, from W before this block's loop
+            bs, bz = np.empty((N, i2 - i1), F32), np.empty((N, i2 - i1), F32)
+            for i in range(i2 - i1):
+                c = i1 + i
+                if c % groupsize == 0:
+                    cur = find_params_weight(W[:, c:c + groupsize], bits)
+                    scales[:, c // groupsize], zeros[:, c // groupsize] = cur
+                bs[:, i], bz[:, i] = cur
+        Q1, Err1, L1 = gptq_block(W[:, i1:i2], Hinv[i1:i2, i1:i2], bs, bz, bits)
         Q[:, i1:i2] = Q1
         Losses[:, i1:i2] = L1 / F32(2)
         W[:, i2:] = (W[:, i2:] - (Err1 @ Hinv[i1:i2, i2:]).astype(F32)).astype(F32)
     if perm is not None:
         Q = Q[:, np.argsort(perm)]
+    if groupsize != -1:
+        return Q, scales, zeros, float(Losses.sum())
     return Q, scale, zero, float(Losses.sum())
 
 
-def pack_weight(Q: np.ndarray, scale, zero, bits: int) -> np.ndarray:
+def pack_weight(Q: np.ndarray, scale, zero, bits: int, tile_cols: int = -1) -> np.ndarray:
     """ColBlockQuantizedLinear.pack_weight (quantization.py:374-388): codes =
     uint8(clamp(Q / scale + zero, 0, 2^bits - 1)) (truncating), packed entries_per_byte per byte,
-    column epb*j + nr at bit nr*bits. Returns quant_weight as its logical (N, K/epb) array."""
+    column epb*j + nr at bit nr*bits; scale / zero (N,) or (N, groups) with tile_cols columns per
+    group. Returns quant_weight as its logical (N, K/epb) array."""
     epb = 8 // bits
-    c = np.clip((Q / scale[:, None]).astype(F32) + zero[:, None], 0, 2 ** bits - 1).astype(F32)
+    K = Q.shape[1]
+    if np.ndim(scale) == 1:
+        scale, zero, tile_cols = scale[:, None], zero[:, None], K
+    tc = K if tile_cols == -1 else tile_cols
+    col = np.arange(K) // tc
+    c = np.clip((Q / scale[:, col]).astype(F32) + zero[:, col], 0, 2 ** bits - 1).astype(F32)
     codes = c.astype(np.uint8)
     out = np.zeros((Q.shape[0], Q.shape[1] // epb), np.uint8)
     for nr in range(epb):

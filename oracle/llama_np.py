@@ -185,7 +185,8 @@ class LinearSpec:
             return (x.astype(F32) @ self.w.T).astype(F32)
         if self.kind == "colblock":
             if not hasattr(self, "_wdeq"):
-                self._wdeq = colblock_get_weight(self.qw, self.scales, self.zeros, self.bits)
+                self._wdeq = colblock_get_weight(self.qw, self.scales, self.zeros, self.bits,
+                                                 getattr(self, "tile_cols", -1))
             return (x.astype(F32) @ self._wdeq.T).astype(F32)
         if self.kind == "int8":
             return int8_linear(x, self.cb, self.scb)

@@ -267,6 +267,56 @@ def gen_gptq():
     save("gptq", **out)
 
 
+def gen_gptq_grouped():
+    """Grouped ColBlockQuantizedLinear (tile_cols = g; pack_weight / get_weight / forward =
+    get_weight + F.linear, quantization.py:374-421) with per-group (scale, zero) from the
+    reference's own GPTQQuantizer.find_params_weight on each group's columns. Cases: g = 128 over
+    K = 384 (3 groups), g = 256 over K = 640 (a ragged last group of 128 columns).
+    The reference's grouped GPTQ column loop itself raises (quantization.py:576 assigns the
+    (N, 1) scale from find_params_weight into the (N,) column scales[:, j]: "expand ... the number
+    of sizes provided (1) must be greater or equal to the number of dimensions"), so the grouped
+    PRODUCER has no reference output: it is checked against oracle/gptq_np.py only (parity
+    unpinned), on the W / X recorded here."""
+    out = {}
+    cases = {"g1": (96, 384, 128, 21), "g2": (64, 640, 256, 22)}
+    for tag, (N, K, g, seed) in cases.items():
+        rng = np.random.default_rng(seed)
+        W = (rng.standard_normal((N, K)) * 0.05).astype(np.float32)
+        W[:, :8] *= 4.0
+        W[:, K // 2: K // 2 + 8] *= 3.0  # wide columns inside a later group
+        X = rng.standard_normal((4, 32, K)).astype(np.float32) * rng.uniform(0.2, 2.0, K).astype(np.float32)
+        lin = torch.nn.Linear(K, N, bias=False)
+        lin.weight.data = torch.from_numpy(W.copy())
+        gq = rq.GPTQQuantizer(lin, bits=4, groupsize=g, actorder=False)
+        G = (K + g - 1) // g
+        qm = rq.ColBlockQuantizedLinear(K, N, False, bits=4, tile_cols=g)
+        Wt = torch.from_numpy(W.copy())
+        Wrec = torch.empty_like(Wt)
+        for j in range(G):
+            sl = slice(j * g, min(K, (j + 1) * g))
+            sc, zr = gq.find_params_weight(Wt[:, sl])
+            qm.scales[:, j] = sc[:, 0]
+            qm.zeros[:, j] = zr[:, 0]
+            q = torch.clamp(torch.round(Wt[:, sl] / sc) + zr, 0, 15)
+            Wrec[:, sl] = sc * (q - zr)
+        qm.pack_weight(Wrec)
+        out.update({f"{tag}_W": W, f"{tag}_X": X, f"{tag}_g": np.int64(g),
+                    f"{tag}_quant_weight": qm.quant_weight.contiguous().numpy(),
+                    f"{tag}_scales": qm.scales.numpy(), f"{tag}_zeros": qm.zeros.numpy(),
+                    f"{tag}_wdeq": qm.get_weight(torch.float).numpy(),
+                    f"{tag}_wdeq_bf16": qm.get_weight(torch.bfloat16).float().numpy()})
+        for M in (1, 5):
+            x = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32))
+            with torch.no_grad():
+                out[f"{tag}_x{M}"] = x.numpy()
+                out[f"{tag}_y{M}"] = qm(x).numpy()
+        try:
+            gq.quantize()  # recorded: the reference's grouped column loop raises
+            out[f"{tag}_ref_quantize_raises"] = np.int64(0)
+        except RuntimeError:
+            out[f"{tag}_ref_quantize_raises"] = np.int64(1)
+    save("gptq_grouped", **out)
+
 def gen_hf_convert():
     """The reference's scripts/convert_hf_checkpoint.py on a tiny synthetic HF LLaMA checkpoint
     (two .bin shards, layer 1's q / k / v split across them, rotary inv_freq buffers), written to
@@ -501,6 +551,6 @@ def gen_bf16_init():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq", "hf_convert",
-                             "meta_convert", "bf16_init", "sampled", "ppl"]
+                             "meta_convert", "bf16_init", "sampled", "ppl", "gptq_grouped"]
     for w in which:
         globals()[f"gen_{w}"]()

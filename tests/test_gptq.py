@@ -282,3 +282,125 @@ def test_gptq_cli_writes_a_checkpoint_generate_loads(hip, tmp_path):
     qm.reset_cache()
     y = G.generate(qm, idx[0], 8, top_k=1)
     assert y.shape[0] == 24
+
+
+# ------------------------------------------------------------------ grouped scales (tile_cols = g)
+GG = np.load(Path(__file__).parent / "golden" / "gptq_grouped.npz")
+GCASES = ["g1", "g2"]
+
+
+def gcase(t):
+    return {k[len(t) + 1:]: GG[k] for k in GG.files if k.startswith(t + "_")}
+
+
+@pytest.mark.parametrize("t", GCASES)
+def test_oracle_grouped_colblock_matches_reference(t):
+    """The reference's grouped ColBlockQuantizedLinear (tile_cols = g): per-group find_params_weight,
+    pack_weight and get_weight reproduced exactly by the oracle. The fixture also records that the
+    reference's own grouped GPTQ column loop raises (quantization.py:576), which is why the grouped
+    producer below is checked against the oracle only (parity unpinned)."""
+    c = gcase(t)
+    W, g, sc, zr = c["W"], int(c["g"]), c["scales"], c["zeros"]
+    K = W.shape[1]
+    assert sc.shape == (W.shape[0], (K + g - 1) // g) and int(c["ref_quantize_raises"]) == 1
+    col = np.arange(K) // g
+    for j in range(sc.shape[1]):
+        s, z = G.find_params_weight(W[:, j * g:(j + 1) * g], 4)
+        np.testing.assert_array_equal(s, sc[:, j])
+        np.testing.assert_array_equal(z, zr[:, j])
+    q = np.clip(np.round(W / sc[:, col]).astype(np.float32) + zr[:, col], 0, 15)
+    Wrec = (sc[:, col] * (q - zr[:, col])).astype(np.float32)
+    np.testing.assert_array_equal(G.pack_weight(Wrec, sc, zr, 4, g), c["quant_weight"])
+    from oracle import llama_np as O
+    np.testing.assert_array_equal(O.colblock_get_weight(c["quant_weight"], sc, zr, 4, tile_cols=g), c["wdeq"])
+
+
+@pytest.mark.parametrize("t", GCASES)
+def test_oracle_grouped_gptq_properties(t):
+    """Grouped GPTQ restatement: one group spanning all columns is the ungrouped algorithm exactly;
+    group 0's params are find_params_weight of the untouched first columns; grouping lowers the loss."""
+    c = gcase(t)
+    W, X, g = c["W"], c["X"], int(c["g"])
+    K = W.shape[1]
+    H, n = np.zeros((K, K), np.float32), 0
+    for j in range(X.shape[0]):
+        H, n = G.collect_input_stats(H, n, X[j:j + 1])
+    Qg, sg, zg, eg = G.gptq_quantize(W, H, 4, actorder=False, groupsize=g)
+    QK, sK, zK, eK = G.gptq_quantize(W, H, 4, actorder=False, groupsize=K)
+    Q1, s1, z1, e1 = G.gptq_quantize(W, H, 4, actorder=False)
+    np.testing.assert_array_equal(QK, Q1)
+    np.testing.assert_array_equal(sK[:, 0], s1)
+    assert eK == e1
+    s0, z0 = G.find_params_weight(W[:, :g], 4)
+    np.testing.assert_array_equal(sg[:, 0], s0)
+    assert eg < e1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t", GCASES)
+def test_grouped_colblock_module_vs_reference(hip, t):
+    """Our ColBlockQuantizedLinear(tile_cols = g) loaded with the reference's grouped buffers:
+    forward on the grouped int4 GEMV (wfmt 4) vs the reference's fp32 forward and the oracle's
+    bf16-input product; get_weight and the state dict give the reference's buffers back after the
+    in-place repack."""
+    from lit_llama.quantization import ColBlockQuantizedLinear
+    from tests.helpers import assert_bf16_close, bf16
+    c = gcase(t)
+    N, K, g = c["W"].shape[0], c["W"].shape[1], int(c["g"])
+    m = ColBlockQuantizedLinear(K, N, False, bits=4, tile_cols=g).to(dev)
+    m.load_state_dict({"quant_weight": torch.from_numpy(c["quant_weight"]), "scales": torch.from_numpy(c["scales"]),
+                       "zeros": torch.from_numpy(c["zeros"])})
+    assert m.wfmt == 4 | ((g // 128) << 8)
+    for M in (1, 5):
+        x = c[f"x{M}"]
+        with torch.no_grad():
+            y = m(torch.from_numpy(x).to(dev, torch.bfloat16)).float().cpu().numpy()
+        assert_bf16_close(y, bf16(x).astype(np.float64) @ c["wdeq"].T.astype(np.float64), f"{t} M={M} vs oracle")
+        ref = c[f"y{M}"]
+        assert np.linalg.norm(y - ref) / np.linalg.norm(ref) < 1e-2  # bf16 input rounding vs the fp32 reference
+    sd = m.state_dict()
+    np.testing.assert_array_equal(sd["quant_weight"].cpu().numpy(), c["quant_weight"])
+    np.testing.assert_array_equal(m.get_weight(torch.float).cpu().numpy(), c["wdeq"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t", GCASES)
+def test_grouped_gptq_quantizer_vs_oracle(hip, t):
+    """Device GPTQQuantizer(groupsize = g, actorder off) against the oracle's grouped restatement
+    (parity unpinned: the reference's grouped loop raises). Group 0's params are exact; later groups
+    are found on weights the device GEMM / Cholesky updated, so at least 97 % of the (row, group)
+    params agree, and where they do every code is within one step and at most 1 % differ."""
+    from lit_llama.quantization import GPTQQuantizer
+    c = gcase(t)
+    W, X, g = c["W"], c["X"], int(c["g"])
+    N, K = W.shape
+    lin = torch.nn.Linear(K, N, bias=False).to(dev)
+    lin.weight.data = torch.from_numpy(W).to(dev)
+    gq = GPTQQuantizer(lin, bits=4, groupsize=g, actorder=False)
+    h = lin.register_forward_hook(gq.collect_input_stats)
+    with torch.no_grad():
+        for j in range(X.shape[0]):
+            lin(torch.from_numpy(X[j:j + 1]).to(dev))
+    h.remove()
+    H = gq.H.cpu().numpy()
+    qm, e = gq.quantize()
+    Q, sg, zg, eo = G.gptq_quantize(W, H, 4, actorder=False, groupsize=g)
+    assert qm.scales.shape == (N, (K + g - 1) // g) and qm.tile_cols == g
+    got_s, got_z = qm.scales.cpu().numpy(), qm.zeros.cpu().numpy()
+    np.testing.assert_array_equal(got_s[:, 0], sg[:, 0])
+    np.testing.assert_array_equal(got_z[:, 0], zg[:, 0])
+    # a code flipped by one in an earlier block (allowed below) feeds a different error into the
+    # later columns, which can move a later group's min / max: such (row, group) params may differ
+    same = (np.abs(got_s - sg) <= 1e-5 * np.abs(sg)) & (got_z == zg)
+    assert same.mean() >= 0.97, same.mean()
+    got = codes_of(qm.quant_weight.cpu().numpy(), 4)
+    ref = codes_of(G.pack_weight(Q, sg, zg, 4, g), 4)
+    keep = same[:, np.arange(K) // g]  # codes of the (row, group) pairs with the same params
+    assert np.abs(got - ref)[keep].max() <= 1
+    assert (got != ref)[keep].mean() <= 1e-2
+    assert e == pytest.approx(eo, rel=1e-2)
+    x = torch.randn(3, K, device=dev, dtype=torch.bfloat16)
+    with torch.no_grad():
+        y = qm(x).float()
+        yr = x.float() @ qm.get_weight(torch.float).t()
+    assert (y - yr).norm() / yr.norm() < 1e-2

@@ -72,8 +72,29 @@ def repack8(hip, qw):
     return out
 
 
+def rand_w4g(rng, N, K, g):
+    G = (K + g - 1) // g
+    qw = rng.integers(0, 256, size=(N, K // 2), dtype=np.uint8)
+    scales = rng.uniform(0.5, 1.5, size=(N, G)).astype(np.float32) * np.float32(0.02 / 7)
+    zeros = rng.integers(0, 16, size=(N, G)).astype(np.float32)
+    return qw, scales, zeros
+
+
+def sz_grouped(hip, scales, zeros):
+    """(scale, 128 + zero) pairs of a grouped int4 weight, group-major (G, N) (wfmt 4)."""
+    return sz_of(hip, np.ascontiguousarray(scales.T).reshape(-1, 1), np.ascontiguousarray(zeros.T).reshape(-1, 1))
+
+
+W4G_128 = 4 | (1 << 8)  # wfmt of grouped int4 with tile_cols = 128
+
+
 def quant_operands(hip, rng, wfmt, N, K):
-    """(reference fp32 weight (N, K), device weight operand, device sz) for wfmt 0 / 1 / 3."""
+    """(reference fp32 weight (N, K), device weight operand, device sz) for wfmt 0 / 1 / 3 and
+    grouped int4 (wfmt 4 | (g / 128) << 8)."""
+    if wfmt & 0xFF == 4:
+        g = 128 * (wfmt >> 8)
+        qw, sc, z = rand_w4g(rng, N, K, g)
+        return O.colblock_get_weight(qw, sc, z, 4, tile_cols=g), repack(hip, qw), sz_grouped(hip, sc, z)
     if wfmt == 0:
         qw, sc, z = rand_w4(rng, N, K)
         return O.colblock_get_weight(qw, sc, z, 4), repack(hip, qw), sz_of(hip, sc, z)
@@ -102,6 +123,31 @@ def _linear(hip, wfmt, x, W, sz, N, K, bias=None):
          None if bias is None else bias.data_ptr(), out.data_ptr(), N, M, N, K, None, 0, None, st())
     torch.cuda.synchronize()
     return out.float().cpu().numpy()
+
+
+@pytest.mark.parametrize("g,M,N,K", [(g, M, 64, 640) for g in (128, 256, 512) for M in (1, 4, 8, 16)]
+                         + [(128, 1, 4096, 4096), (128, 8, 4096, 4096), (256, 1, 4096, 11008), (128, 8, 11008, 4096)])
+def test_w4_grouped_linear_shapes(hip, g, M, N, K):
+    """Grouped int4 (tile_cols = g: 1, 2 and 4 chunks per group; K = 640 / 11008 leave a ragged last
+    group) against the oracle's get_weight (quantization.py:390-409) at decode and 7B shapes."""
+    rng = np.random.default_rng(g + M + N + K)
+    qw, sc, z = rand_w4g(rng, N, K, g)
+    Wref = O.colblock_get_weight(qw, sc, z, 4, tile_cols=g)
+    x = bf16(rng.standard_normal((M, K)))
+    got = _linear(hip, 4 | ((g // 128) << 8), T(x, torch.bfloat16), repack(hip, qw), sz_grouped(hip, sc, z), N, K)
+    assert_bf16_close(got, x.astype(np.float64) @ Wref.T.astype(np.float64), f"w4g g={g}")
+
+
+def test_w4_grouped_rejects_bad_group(hip):
+    """wfmt 4 needs a group size of at least one 128-deep chunk (EINVAL otherwise)."""
+    N, K = 32, 256
+    x = torch.zeros(1, K, dtype=torch.bfloat16, device=dev)
+    w = torch.zeros(N * K // 2, dtype=torch.uint8, device=dev)
+    sz = torch.zeros(2 * N, 2, dtype=torch.float32, device=dev)
+    out = torch.empty(1, N, dtype=torch.bfloat16, device=dev)
+    rc = hip.llj_linear(4, x.data_ptr(), K, w.data_ptr(), sz.data_ptr(), None, out.data_ptr(), N, 1, N, K, None, 0,
+                        None, st())
+    assert rc == 1000
 
 
 def test_w4_linear_reference_fixture(hip, golden):
@@ -309,7 +355,7 @@ def test_embedding_and_pos_inc(hip):
     assert int(pos) == 8
 
 
-@pytest.mark.parametrize("wfmt", [0, 1, 3])
+@pytest.mark.parametrize("wfmt", [0, 1, 3, W4G_128])
 @pytest.mark.parametrize("B,T_", [(1, 1), (8, 1), (2, 5)])
 def test_fused_qkv_rope_kv(hip, wfmt, B, T_):
     rng = np.random.default_rng(wfmt * 10 + B + T_)
@@ -346,7 +392,7 @@ def test_fused_qkv_rope_kv(hip, wfmt, B, T_):
     assert not kcn[:, :, untouched].any() and not vcn[:, :, untouched].any()
 
 
-@pytest.mark.parametrize("wfmt", [0, 1, 3])
+@pytest.mark.parametrize("wfmt", [0, 1, 3, W4G_128])
 def test_fused_swiglu_and_resid(hip, wfmt):
     rng = np.random.default_rng(11 + wfmt)
     M, C, H = 3, 256, 768
@@ -378,7 +424,7 @@ def test_fused_swiglu_and_resid(hip, wfmt):
     assert_bf16_close(xr.float().cpu().numpy(), x + bf16(hg @ Wd_.T), "resid")
 
 
-@pytest.mark.parametrize("wfmt", [0, 1, 3])
+@pytest.mark.parametrize("wfmt", [0, 1, 3, W4G_128])
 @pytest.mark.parametrize("M", [2, 8, 13])
 def test_norm_statistics_handoff(hip, wfmt, M):
     """Batched decode's RMSNorm hand-off: llj_linear_resid writes, per 16-column tile of the new x,
@@ -554,7 +600,7 @@ def test_multi_tile_workgroups_equal_single_tile(hip, wfmt, M):
     assert_bf16_close(multi[5].float().cpu().numpy(), xr0.float().cpu().numpy() + bf16(hx @ Wr.T), "resid 13B")
 
 
-@pytest.mark.parametrize("wfmt", [0, 3])
+@pytest.mark.parametrize("wfmt", [0, 3, W4G_128])
 def test_long_k_residual_eight_waves_m1(hip, wfmt):
     """mlp.c_proj at 7B (K = 11008 >= 8192: 8-wave workgroups, M = 1 register prologue): every
     wave's A row sum lands in the LDS tail (the int4 / int8 offset removal needs all eight)."""

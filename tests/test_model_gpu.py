@@ -311,6 +311,47 @@ def test_gptq_int8_model_vs_oracle():
     assert rel < 3e-2, rel
 
 
+def test_grouped_int4_model_vs_oracle():
+    """Grouped int4 (ColBlockQuantizedLinear tile_cols = 128: per-group (scale, zero), the form
+    GPTQQuantizer(groupsize=128) returns) in every Linear of a model: the fused decode launches
+    (norm + QKV + RoPE, SwiGLU, residual, ln_f + lm_head) take wfmt 4; logits and margin-guarded
+    greedy ids (graph replays) against the oracle running the reference's get_weight."""
+    from lit_llama.quantization import ColBlockQuantizedLinear
+    cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=2048)
+    p = make_params(cfg, 41)
+    g = 128
+    m = build(cfg, p, mode="gptq.int4")
+    lin = {}
+    for name, mod in list(m.named_modules()):
+        if not isinstance(mod, ColBlockQuantizedLinear):
+            continue
+        w = p[name + ".weight"].astype(np.float32)
+        N, K = w.shape
+        col = np.arange(K) // g
+        wg = w.reshape(N, K // g, g)
+        xmin, xmax = np.minimum(wg.min(2), 0), np.maximum(wg.max(2), 0)
+        sc = bf16(((xmax - xmin) / 15).astype(np.float32))  # (N, G), the module's bf16 buffers
+        z = np.round(-xmin / sc).astype(np.float32)
+        q = np.clip(np.round(w / sc[:, col]) + z[:, col], 0, 15)
+        qw = O.colblock_pack(sc[:, col] * (q - z[:, col]), sc, z, 4, tile_cols=g)
+        gm = ColBlockQuantizedLinear(K, N, False, bits=4, tile_cols=g).to("cuda", torch.bfloat16)
+        gm.load_state_dict({"quant_weight": torch.from_numpy(qw), "scales": torch.from_numpy(sc),
+                            "zeros": torch.from_numpy(z)})
+        parent, _, leaf = name.rpartition(".")
+        setattr(m.get_submodule(parent) if parent else m, leaf, gm)
+        lin[name] = O.LinearSpec("colblock", qw=qw, scales=sc, zeros=z, bits=4, tile_cols=g)
+    assert m.lm_head.wfmt == 4 | (1 << 8)
+    prompt = np.random.default_rng(19).integers(3, 2048, 8).astype(np.int32)
+    orc = O.OracleLLaMA(cfg, {k: bf16(v) for k, v in p.items()}, linears=lin, act_bf16=True)
+    oids, olog = O.generate_greedy(orc, prompt, 12, return_logits=True)
+    ids = gen(m, prompt, 12)
+    top = np.sort(olog, -1)[:, ::-1][:, :2]
+    assert guarded(ids, oids, top, len(prompt), tol=0.3) >= 8
+    out = m(torch.from_numpy(prompt[None].astype(np.int64)).cuda()).float().cpu().numpy()[0, -1]
+    rel = np.linalg.norm(out - olog[0]) / np.linalg.norm(olog[0])
+    assert rel < 3e-2, rel
+
+
 def test_bf16_vs_int4_module_forward_paths(golden):
     """ColBlockQuantizedLinear.forward, qlinear_4bit_weight and the fused model path agree."""
     from lit_llama.quantization import qlinear_4bit_weight
