@@ -377,7 +377,7 @@ def test_fused_qkv_rope_kv(hip, wfmt, B, T_):
              None if szd is None else szd.data_ptr(), q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rd.data_ptr(),
              pd.data_ptr(), B, T_, C, nh, S, r0, r, None, None, None, 0, st())
     torch.cuda.synchronize()
-    h = bf16(O.rmsnorm(x, g))
+    h = O.rmsnorm_bf16(x, g)  # the kernels round where the reference does on bf16 tensors
     qkv = bf16(h @ Wref.T)
     qe = O.apply_rope(qkv[:, :C].reshape(B, T_, nh, hs), rope[pos]).reshape(M, C)
     ke = O.apply_rope(qkv[:, C:2 * C].reshape(B, T_, nh, hs), rope[pos])
@@ -414,7 +414,7 @@ def test_fused_swiglu_and_resid(hip, wfmt):
     call(hip, "llj_linear_resid", wfmt, h.data_ptr(), H, Wdd.data_ptr(), P(sd), xr.data_ptr(), C, M, C, H, None, 0, None,
          st())
     torch.cuda.synchronize()
-    hn = bf16(O.rmsnorm(x, g))
+    hn = O.rmsnorm_bf16(x, g)
     a1, a2 = bf16(hn @ W1.T), bf16(hn @ W2.T)
     hexp = bf16(bf16(O.silu(a1)) * a2)
     # a1, a2, silu(a1) and the product are each rounded to bf16 on the reference path

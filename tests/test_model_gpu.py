@@ -320,10 +320,10 @@ def test_grouped_int4_model_vs_oracle():
     cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=2048)
     p = make_params(cfg, 41)
     g = 128
-    m = build(cfg, p, mode="gptq.int4")
+    m = build(cfg, p)  # dense bf16, every nn.Linear then replaced by its grouped int4 form
     lin = {}
     for name, mod in list(m.named_modules()):
-        if not isinstance(mod, ColBlockQuantizedLinear):
+        if not isinstance(mod, torch.nn.Linear):
             continue
         w = p[name + ".weight"].astype(np.float32)
         N, K = w.shape
