@@ -162,6 +162,12 @@ size_t llj_i8_ws_bytes(int M, int K);
 /* Outlier columns (any row |A16| >= threshold) and per-row absmax of the other elements of
  * A (M, K) bf16 into ws (bitsandbytes double_quant(A, threshold) as used by MatMul8bitLt). */
 int llj_i8_stats(const void* A, int lda, int M, int K, float threshold, void* ws, void* stream);
+/* The RMSNorm before an int8 Linear and llj_i8_stats of its output in two launches instead of
+ * three: xn (M, K) = RMSNorm(x; norm_w, eps) bit-identical to llj_rmsnorm (model.py:276-283 on
+ * bf16 tensors), then ws as llj_i8_stats(xn, K, M, K, threshold, ws). One-launch form for
+ * M <= 16, K <= 8192 and M * (k-block width / 8) <= 256; otherwise the two ops it replaces. */
+int llj_i8_norm_stats(const void* x, const void* norm_w, float eps, void* xn, int M, int K, float threshold, void* ws,
+                      void* stream);
 /* CB = round(W16 * 127 / SCB), SCB = row absmax of W16 = W.half() (Linear8bitLt._quantize_weight,
  * quantization.py:67-75). W (N, K) of dtype 0 fp32 / 1 bf16 / 2 fp16. */
 int llj_i8_quant_weight(const void* W, int dtype, void* CB, void* SCB, int N, int K, void* stream);

@@ -141,6 +141,11 @@ __device__ __forceinline__ void lane_halves(float v, float& lo, float& hi) {
 }
 // Sum / max over the 64 lanes of the wave, the same value (bitwise) in every lane: DPP inside
 // each 16-lane row, then rows (0+1, 2+3) and halves (lo+hi), in one order for all lanes.
+// RMSNorm output pair g * bf16(x * r), each product rounded to bf16 (model.py:283 on bf16 tensors)
+__device__ __forceinline__ uint32_t norm_pair(uint32_t a, uint32_t g, float r) {
+  return pack2bf(round_bf(bflo(g) * round_bf(bflo(a) * r)), round_bf(bfhi(g) * round_bf(bfhi(a) * r)));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
   float lo, hi;
   v = row16_sum(v);

@@ -9,6 +9,7 @@
 //                SCA[m] = max over the row's elements with |A16| < threshold
 #include "common.h"
 #include "i8ws.h"
+#include "lit_llama_amd.h"
 
 namespace llj {
 
@@ -37,6 +38,100 @@ __global__ __launch_bounds__(256) void i8_stats_kernel(const bf16_t* __restrict_
     if (lane == 0) L.part[(size_t)b * M + m] = mx;
   }
   __syncthreads();
+  for (int k = k0 + tid; k < k1; k += 256) L.flag[k] = (uint8_t)flag[k - k0];
+  if (wave == 0) {  // compact the flags into the list, 64 columns per ballot
+    int c = 0;
+    for (int i0 = 0; i0 < k1 - k0; i0 += 64) {
+      const bool f = i0 + lane < k1 - k0 && flag[i0 + lane];
+      const unsigned long long bal = __ballot(f);
+      if (f) L.list[b * kb + c + __popcll(bal & ((1ull << lane) - 1ull))] = k0 + i0 + lane;
+      c += __popcll(bal);
+    }
+    if (lane == 0) L.cnt[b] = c;
+  }
+}
+
+// Pass 1 fused with the RMSNorm before it (decode rows, M <= MR): every block reduces the
+// sums of squares of all M rows itself -- the rmsnorm_kernel's summation order exactly (thread t:
+// vectors t, t + 256, ... in order; wave sums; the 4 wave partials in order), so r is bit-identical
+// to llj_rmsnorm's --, writes the normalized rows of its own k-range (xn) and takes the outlier
+// flags / row maxima of those values (the i8_stats_kernel rule). One launch instead of two.
+template <int MR, int VPT>
+__global__ __launch_bounds__(256) void i8_norm_stats_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                            float eps, bf16_t* __restrict__ xn, int M, int K, float thr,
+                                                            char* __restrict__ ws, int kb) {
+  constexpr int RG = 4;  // rows whose vectors are in flight together
+  __shared__ int flag[1024];
+  __shared__ float red[4][MR];
+  __shared__ float rr[MR];
+  __shared__ int rmax[MR];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const I8Layout L = i8_layout(ws, M, K);
+  if (b == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb};
+  const int k0 = b * kb;
+  const int k1 = min(K, k0 + kb);
+  const int nvec = K >> 3;
+  const int vpr = k1 > k0 ? (k1 - k0) >> 3 : 0;  // vectors of 8 per row in this block's range
+  // this thread's (row, vector) of the own range (M * vpr <= 256 on this path), loaded first
+  const bool own = tid < M * vpr;
+  const int om = own ? tid / vpr : 0, ov = own ? (k0 >> 3) + tid % vpr : 0;
+  const uint4 oa = reinterpret_cast<const uint4*>(x + (size_t)om * K)[ov];
+  const uint4 og = reinterpret_cast<const uint4*>(w)[ov];
+  for (int i = tid; i < kb; i += 256) flag[i] = 0;
+  if (tid < MR) rmax[tid] = 0;
+  float ss[MR];
+#pragma unroll
+  for (int m0 = 0; m0 < MR; m0 += RG) {
+    uint4 xa[RG][VPT];
+#pragma unroll
+    for (int r = 0; r < RG; ++r)
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int m = m0 + r < M ? m0 + r : M - 1, v = tid + 256 * j < nvec ? tid + 256 * j : nvec - 1;
+        xa[r][j] = reinterpret_cast<const uint4*>(x + (size_t)m * K)[v];
+      }
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        if (tid + 256 * j < nvec) {
+          const uint32_t aw[4] = {xa[r][j].x, xa[r][j].y, xa[r][j].z, xa[r][j].w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a += round_bf(bflo(aw[i]) * bflo(aw[i])) + round_bf(bfhi(aw[i]) * bfhi(aw[i]));
+        }
+      }
+      ss[m0 + r] = a;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    const float t = wave_sum(ss[m]);
+    if (lane == 0) red[wave][m] = t;
+  }
+  __syncthreads();
+  if (tid < MR) {
+    const float tot = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    rr[tid] = round_bf(rsqrtf(round_bf(round_bf(tot / (float)K) + eps)));
+  }
+  __syncthreads();
+  if (own) {  // normalize, store, statistics of the own (row, vector)
+    const float r = rr[om];
+    const uint4 o = make_uint4(norm_pair(oa.x, og.x, r), norm_pair(oa.y, og.y, r), norm_pair(oa.z, og.z, r),
+                               norm_pair(oa.w, og.w, r));
+    reinterpret_cast<uint4*>(xn + (size_t)om * K)[ov] = o;
+    const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float av = fabsf(to_f16f((i & 1) ? bfhi(ow[i >> 1]) : bflo(ow[i >> 1])));
+      if (av >= thr) flag[8 * ov + i - k0] = 1;
+      else mx = fmaxf(mx, av);
+    }
+    atomicMax(&rmax[om], __float_as_int(mx));  // non-negative floats order as their bits
+  }
+  __syncthreads();
+  if (tid < M && tid < MR) L.part[(size_t)b * M + tid] = __int_as_float(rmax[tid]);
   for (int k = k0 + tid; k < k1; k += 256) L.flag[k] = (uint8_t)flag[k - k0];
   if (wave == 0) {  // compact the flags into the list, 64 columns per ballot
     int c = 0;
@@ -158,6 +253,31 @@ int llj_i8_stats(const void* A, int lda, int M, int K, float threshold, void* ws
   LLJ_CHECK_LAUNCH();
   hipLaunchKernelGGL(i8_quant_act_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)A, lda, M, K,
                      (char*)ws);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_i8_norm_stats(const void* x, const void* norm_w, float eps, void* xn, int M, int K, float threshold, void* ws,
+                      void* stream) {
+  const int kb = i8_kb(K), nvec = K / 8, vpt = (nvec + 255) / 256;
+  LLJ_REQUIRE(M > 0 && K > 0 && K % 16 == 0 && kb <= 1024);
+  if (M > 16 || vpt > 4 || M * (kb / 8) > 256) {  // outside the one-launch form: the two ops
+    if (int e = llj_rmsnorm(x, norm_w, eps, xn, M, K, stream)) return e;
+    return llj_i8_stats(xn, K, M, K, threshold, ws, stream);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const bf16_t *xb = (const bf16_t*)x, *wb = (const bf16_t*)norm_w;
+#define LLJ_NS(MR, VPT) \
+  hipLaunchKernelGGL((i8_norm_stats_kernel<MR, VPT>), dim3(kNSB), dim3(256), 0, s, xb, wb, eps, (bf16_t*)xn, M, K, \
+                     threshold, (char*)ws, kb)
+  if (M <= 8) {
+    if (vpt <= 2) LLJ_NS(8, 2); else LLJ_NS(8, 4);
+  } else {
+    if (vpt <= 2) LLJ_NS(16, 2); else LLJ_NS(16, 4);
+  }
+#undef LLJ_NS
+  LLJ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(i8_quant_act_kernel, dim3(M), dim3(256), 0, s, (const bf16_t*)xn, K, M, K, (char*)ws);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

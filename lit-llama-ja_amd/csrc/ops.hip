@@ -20,9 +20,7 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ 
 // ---- RMSNorm with the bf16 rounding points of model.py:281-283 on bf16 tensors. One block
 // per row; rows up to 8192 wide are loaded once into registers (x and the scale together,
 // before any use), so the kernel is one memory round trip.
-__device__ __forceinline__ uint32_t norm_pair(uint32_t a, uint32_t g, float r) {
-  return pack2bf(round_bf(bflo(g) * round_bf(bflo(a) * r)), round_bf(bfhi(g) * round_bf(bfhi(a) * r)));
-}
+// (norm_pair: common.h)
 
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                       float eps, bf16_t* __restrict__ y, int C,

@@ -40,6 +40,7 @@ SIGNATURES = {
     "llj_norm_swiglu": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _I, _P],
     "llj_norm_linear": [_I, _P, _P, _F, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P],
     "llj_i8_stats": [_P, _I, _I, _I, _F, _P, _P],
+    "llj_i8_norm_stats": [_P, _P, _F, _P, _I, _I, _F, _P, _P],
     "llj_i8_quant_weight": [_P, _I, _P, _P, _I, _I, _P],
     "llj_embedding": [_P, _P, _P, _I, _I, _P, _P],
     "llj_rmsnorm": [_P, _P, _F, _P, _I, _I, _P],

@@ -123,6 +123,9 @@ HAND_NORM_MAX_M = 2
 # the model is int4 W4P or bf16 and the shapes tile by 128 (LLM.int8 and gptq.int8 keep the
 # GEMV slices)
 GEMM_MIN_ROWS = 32
+
+# int8 decode: RMSNorm + LLM.int8() statistics in one launch pair up to this many rows
+I8_NORM_STATS_MAX_M = 16
 _GEMM_FMTS = (0, 1)
 
 # weight formats whose kernels remove the nibble offset with the row sums of A (W4P, W8P)
@@ -315,6 +318,16 @@ class LLaMA(nn.Module):
     def _i8_prep(self, A, M, K, w, st):
         _hip.call("llj_i8_stats", A.data_ptr(), A.stride(0), M, K, Linear8bitLtThreshold, w.i8ws.data_ptr(), st)
 
+    def _i8_norm_prep(self, x, norm, xn, M, K, w, st):
+        """RMSNorm of x into xn + the int8 statistics of xn: one fused launch pair for decode rows
+        (llj_i8_norm_stats, M <= 16), else llj_rmsnorm then llj_i8_stats."""
+        if M <= I8_NORM_STATS_MAX_M and x.stride(0) == K:  # (the library falls back by itself past its envelope)
+            _hip.call("llj_i8_norm_stats", x.data_ptr(), norm.scale.data_ptr(), norm.eps, xn.data_ptr(), M, K,
+                      Linear8bitLtThreshold, w.i8ws.data_ptr(), st)
+            return
+        _hip.call("llj_rmsnorm", x.data_ptr(), norm.scale.data_ptr(), norm.eps, xn.data_ptr(), M, K, st)
+        self._i8_prep(xn, M, K, w, st)
+
     def _flash_ok(self, pos, T, S):
         """prompt rows attend through the flash kernel: T >= FLASH_MIN_T, head_size 64 / 128,
         positions contiguous and inside the cache without wrapping (one host read of pos; prompts
@@ -382,9 +395,7 @@ class LLaMA(nn.Module):
             # 1. rms_1 + c_attn + rope + kv write
             rs = None
             if fa == 2:
-                _hip.call("llj_rmsnorm", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps, w.xn.data_ptr(),
-                          M, C, st)
-                self._i8_prep(w.xn, M, C, w, st)
+                self._i8_norm_prep(w.x, blk.rms_1, w.xn, M, C, w, st)
                 src, nw = w.xn, None
             elif w.hand and i > 0:  # the previous mlp.c_proj handed over the sums of squares
                 src, nw = w.x, blk.rms_1.scale.data_ptr()
@@ -409,9 +420,7 @@ class LLaMA(nn.Module):
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")
             rs = None
             if f1 == 2:
-                _hip.call("llj_rmsnorm", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(),
-                          M, C, st)
-                self._i8_prep(w.xn, M, C, w, st)
+                self._i8_norm_prep(w.x, blk.rms_2, w.xn, M, C, w, st)
                 src, nw, step = w.xn, None, I8_ROWS
             elif w.hand:  # c_proj handed over the sums of squares
                 src, nw, step = w.x, blk.rms_2.scale.data_ptr(), QKV_ROWS
@@ -452,8 +461,7 @@ class LLaMA(nn.Module):
         rs = nst = None
         if f == 2:
             xn = torch.empty_like(x)
-            _hip.call("llj_rmsnorm", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), M, C, st)
-            self._i8_prep(xn, M, C, w, st)
+            self._i8_norm_prep(x, ln, xn, M, C, w, st)
             src, nw = xn, None
         elif M >= GEMM_MIN_ROWS and f in _GEMM_FMTS and C % 128 == 0 and V % 128 == 0:  # many rows: GEMM
             xn = torch.empty_like(x)

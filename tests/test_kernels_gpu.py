@@ -600,6 +600,31 @@ def test_multi_tile_workgroups_equal_single_tile(hip, wfmt, M):
     assert_bf16_close(multi[5].float().cpu().numpy(), xr0.float().cpu().numpy() + bf16(hx @ Wr.T), "resid 13B")
 
 
+@pytest.mark.parametrize("M,K", [(1, 4096), (8, 4096), (13, 4096), (3, 256), (8, 5120), (16, 5120), (20, 4096)])
+def test_i8_norm_stats_equals_separate_launches(hip, M, K):
+    """llj_i8_norm_stats (RMSNorm + LLM.int8() pass 1 in one launch, then the row quantization) is
+    bit-identical to llj_rmsnorm followed by llj_i8_stats: the normalized rows and every byte of
+    the statistics workspace (outlier flags / lists / counts, row maxima, SCA, quantized rows)."""
+    rng = np.random.default_rng(M * 7 + K)
+    x = bf16(rng.standard_normal((M, K)))
+    x[:, rng.choice(K, 5, replace=False)] *= 40.0  # outlier columns after the norm
+    g = bf16(rng.uniform(0.5, 1.5, K))
+    xd, gd = T(x, torch.bfloat16), T(g, torch.bfloat16)
+    nb = hip.llj_i8_ws_bytes(M, K)
+    ws1 = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    ws2 = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    xn1 = torch.zeros(M, K, dtype=torch.bfloat16, device=dev)
+    xn2 = torch.zeros(M, K, dtype=torch.bfloat16, device=dev)
+    call(hip, "llj_rmsnorm", xd.data_ptr(), gd.data_ptr(), 1e-5, xn1.data_ptr(), M, K, st())
+    call(hip, "llj_i8_stats", xn1.data_ptr(), K, M, K, 6.0, ws1.data_ptr(), st())
+    call(hip, "llj_i8_norm_stats", xd.data_ptr(), gd.data_ptr(), 1e-5, xn2.data_ptr(), M, K, 6.0, ws2.data_ptr(), st())
+    torch.cuda.synchronize()
+    assert torch.equal(xn1.view(torch.int16), xn2.view(torch.int16))
+    assert torch.equal(ws1, ws2)
+    flags = ws1.cpu().numpy()  # the case has outliers to find
+    assert (np.abs(bf16(xn1.float().cpu().numpy())) >= 6.0).any()
+
+
 @pytest.mark.parametrize("wfmt", [0, 3, W4G_128])
 def test_long_k_residual_eight_waves_m1(hip, wfmt):
     """mlp.c_proj at 7B (K = 11008 >= 8192: 8-wave workgroups, M = 1 register prologue): every
