@@ -162,6 +162,140 @@ __device__ __forceinline__ uint2 quant8(uint4 x, uint2 fl, float inv) {
   return make_uint2(o[0], o[1]);
 }
 
+// The whole activation preparation in ONE launch for decode batches (M <= 8 rows): one 1024-thread
+// block per k-block (kNSB blocks). Every block reads all M rows (four 256-thread groups, group g
+// taking rows g and g + 4 with llj_rmsnorm's thread-to-vector map, so with norm_w the sums of
+// squares -- and xn -- are bit-identical to llj_rmsnorm's) and reduces each row's SCA = max of the
+// elements below the threshold itself (redundant across blocks, no grid-wide dependency); then it
+// finishes its own k-block: outlier flags, the list, part, the normalized rows (xn) and the
+// quantized rows (aq). Block 0 writes the header and SCA.
+template <bool NORM, int VPT>
+__global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restrict__ x, int lda,
+                                                           const bf16_t* __restrict__ w, float eps,
+                                                           bf16_t* __restrict__ xn, int M, int K, float thr,
+                                                           char* __restrict__ ws, int kb) {
+  constexpr int MR = 8;
+  __shared__ int flag[1024];
+  __shared__ float red[MR][4];
+  __shared__ float rr[MR];
+  __shared__ float mred[16][MR];
+  __shared__ int pmax[MR];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int grp = tid >> 8, lt = tid & 255, gw = lt >> 6;  // row group, thread / wave within it
+  const I8Layout L = i8_layout(ws, M, K);
+  const int nvec = K >> 3;
+  const int k0 = b * kb, k1 = min(K, k0 + kb);
+  const int vpr = k1 > k0 ? (k1 - k0) >> 3 : 0;
+  // own k-block item (row, vector), loaded first (M * vpr <= 1024 on this path)
+  const bool own = tid < M * vpr;
+  const int om = own ? tid / vpr : 0, ov = own ? (k0 >> 3) + tid % vpr : 0;
+  const uint4 oa = reinterpret_cast<const uint4*>(x + (size_t)om * lda)[ov];
+  uint4 og = oa;
+  if (NORM) og = reinterpret_cast<const uint4*>(w)[ov];
+  // rows grp and grp + 4, vectors lt + 256 j
+  uint4 xa[2][VPT], ga[VPT];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int m = grp + 4 * r < M ? grp + 4 * r : M - 1, v = lt + 256 * j < nvec ? lt + 256 * j : nvec - 1;
+      xa[r][j] = reinterpret_cast<const uint4*>(x + (size_t)m * lda)[v];
+    }
+  if (NORM) {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) ga[j] = reinterpret_cast<const uint4*>(w)[lt + 256 * j < nvec ? lt + 256 * j : nvec - 1];
+  }
+  for (int i = tid; i < kb; i += 1024) flag[i] = 0;
+  if (tid < MR) pmax[tid] = 0;
+  if (NORM) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        if (lt + 256 * j < nvec) {
+          const uint32_t aw[4] = {xa[r][j].x, xa[r][j].y, xa[r][j].z, xa[r][j].w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a += round_bf(bflo(aw[i]) * bflo(aw[i])) + round_bf(bfhi(aw[i]) * bfhi(aw[i]));
+        }
+      }
+      a = wave_sum(a);
+      if (lane == 0) red[grp + 4 * r][gw] = a;
+    }
+    __syncthreads();
+    if (tid < MR) rr[tid] = round_bf(rsqrtf(round_bf(round_bf((red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3]) / (float)K) + eps)));
+    __syncthreads();
+  }
+  // each row's maximum of the (normalized) elements below the threshold
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const float rn = NORM ? rr[grp + 4 * r < M ? grp + 4 * r : M - 1] : 1.f;
+    float mx = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      if (lt + 256 * j < nvec) {
+        uint32_t aw[4] = {xa[r][j].x, xa[r][j].y, xa[r][j].z, xa[r][j].w};
+        if (NORM) {
+          aw[0] = norm_pair(aw[0], ga[j].x, rn); aw[1] = norm_pair(aw[1], ga[j].y, rn);
+          aw[2] = norm_pair(aw[2], ga[j].z, rn); aw[3] = norm_pair(aw[3], ga[j].w, rn);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float av = fabsf(to_f16f((i & 1) ? bfhi(aw[i >> 1]) : bflo(aw[i >> 1])));
+          mx = av < thr ? fmaxf(mx, av) : mx;
+        }
+      }
+    }
+    mx = wave_max(mx);
+    if (lane == 0) mred[tid >> 6][r] = mx;  // wave (grp, gw): slot r <-> row grp + 4 r
+  }
+  if (!NORM) __syncthreads();  // flag / pmax zeroed before any thread sets them (NORM: synced above)
+  // own k-block: normalize, flags, per-row maximum
+  uint4 on = oa;
+  if (NORM && own) {
+    const float rn = rr[om];
+    on = make_uint4(norm_pair(oa.x, og.x, rn), norm_pair(oa.y, og.y, rn), norm_pair(oa.z, og.z, rn),
+                    norm_pair(oa.w, og.w, rn));
+  }
+  if (own) {
+    if (NORM) reinterpret_cast<uint4*>(xn + (size_t)om * K)[ov] = on;
+    const uint32_t ow[4] = {on.x, on.y, on.z, on.w};
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float av = fabsf(to_f16f((i & 1) ? bfhi(ow[i >> 1]) : bflo(ow[i >> 1])));
+      if (av >= thr) flag[8 * ov + i - k0] = 1;
+      else mx = fmaxf(mx, av);
+    }
+    atomicMax(&pmax[om], __float_as_int(mx));  // non-negative floats order as their bits
+  }
+  __syncthreads();
+  // SCA of row m: max over the 4 waves of its group (slot m >> 2)
+  if (own) {
+    const int g = om & 3, r = om >> 2;
+    const float sca = fmaxf(fmaxf(mred[4 * g][r], mred[4 * g + 1][r]), fmaxf(mred[4 * g + 2][r], mred[4 * g + 3][r]));
+    const float inv = sca > 0.f ? 127.f / sca : 0.f;
+    const int c = 8 * ov - k0;
+    const uint2 fb = make_uint2(flag[c] | (flag[c + 1] << 8) | (flag[c + 2] << 16) | (flag[c + 3] << 24),
+                                flag[c + 4] | (flag[c + 5] << 8) | (flag[c + 6] << 16) | (flag[c + 7] << 24));
+    reinterpret_cast<uint2*>(L.aq + (size_t)om * K)[ov] = quant8(on, fb, inv);
+    if (om == 0) reinterpret_cast<uint2*>(L.flag)[ov] = fb;
+    if (b == 0 && ov == (k0 >> 3)) L.sca[om] = sca;
+  }
+  if (tid < M) L.part[(size_t)b * M + tid] = __int_as_float(pmax[tid]);
+  if (b == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb};
+  if (tid < 64) {  // compact the flags into the list, 64 columns per ballot
+    int c = 0;
+    for (int i0 = 0; i0 < k1 - k0; i0 += 64) {
+      const bool f = i0 + lane < k1 - k0 && flag[i0 + lane];
+      const unsigned long long bal = __ballot(f);
+      if (f) L.list[b * kb + c + __popcll(bal & ((1ull << lane) - 1ull))] = k0 + i0 + lane;
+      c += __popcll(bal);
+    }
+    if (lane == 0) L.cnt[b] = c;
+  }
+}
+
 // Pass 2, one block per row: SCA = max over the k-blocks, then the row quantized once (outlier
 // columns 0: their contribution is the fp16 side product). The row and its flags (up to QV
 // vectors of 8 per thread, K <= 8 * 256 * QV) are loaded BEFORE the k-block maxima are reduced, so
@@ -237,6 +371,26 @@ __global__ __launch_bounds__(256) void i8_quant_weight_kernel(const void* __rest
   if (tid == 0) SCB[n] = mx;
 }
 
+
+// i8_prep_one_kernel for M <= 8, K <= 6 * 2048 (with the norm 4 * 2048), M * (k-block width / 8) <= 1024: returns 0 after the
+// launch (or -hipError), 1 when the shape is outside that envelope (nothing launched)
+static int i8_prep_one(bool norm, const bf16_t* x, int lda, const bf16_t* w, float eps, bf16_t* xn, int M, int K,
+                       float thr, void* ws, void* stream) {
+  const int kb = i8_kb(K), vpt = (K / 8 + 255) / 256;
+  if (M > 8 || vpt > (norm ? 4 : 6) || M * (kb / 8) > 1024 || lda % 8) return 1;
+  hipStream_t s = (hipStream_t)stream;
+#define LLJ_P1(N, V) \
+  hipLaunchKernelGGL((i8_prep_one_kernel<N, V>), dim3(kNSB), dim3(1024), 0, s, x, lda, w, eps, xn, M, K, thr, (char*)ws, kb)
+  if (norm) {
+    if (vpt <= 2) LLJ_P1(true, 2); else LLJ_P1(true, 4);
+  } else {
+    if (vpt <= 2) LLJ_P1(false, 2); else if (vpt <= 4) LLJ_P1(false, 4); else LLJ_P1(false, 6);
+  }
+#undef LLJ_P1
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
 }  // namespace llj
 
 using namespace llj;
@@ -248,6 +402,8 @@ size_t llj_i8_ws_bytes(int M, int K) { return i8_offsets(M, K).total; }
 
 int llj_i8_stats(const void* A, int lda, int M, int K, float threshold, void* ws, void* stream) {
   LLJ_REQUIRE(M > 0 && K > 0 && K % 16 == 0 && lda % 8 == 0 && i8_kb(K) <= 1024);
+  if (int e = i8_prep_one(false, (const bf16_t*)A, lda, nullptr, 0.f, nullptr, M, K, threshold, ws, stream); e <= 0)
+    return -e;  // one launch (decode batches), or past its envelope (> 0): the two passes
   hipLaunchKernelGGL(i8_stats_kernel, dim3(kNSB), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)A, lda, M, K,
                      threshold, (char*)ws, i8_kb(K));
   LLJ_CHECK_LAUNCH();
@@ -267,6 +423,7 @@ int llj_i8_norm_stats(const void* x, const void* norm_w, float eps, void* xn, in
   }
   hipStream_t s = (hipStream_t)stream;
   const bf16_t *xb = (const bf16_t*)x, *wb = (const bf16_t*)norm_w;
+  if (int e = i8_prep_one(true, xb, K, wb, eps, (bf16_t*)xn, M, K, threshold, ws, stream); e <= 0) return -e;
 #define LLJ_NS(MR, VPT) \
   hipLaunchKernelGGL((i8_norm_stats_kernel<MR, VPT>), dim3(kNSB), dim3(256), 0, s, xb, wb, eps, (bf16_t*)xn, M, K, \
                      threshold, (char*)ws, kb)

@@ -600,11 +600,12 @@ def test_multi_tile_workgroups_equal_single_tile(hip, wfmt, M):
     assert_bf16_close(multi[5].float().cpu().numpy(), xr0.float().cpu().numpy() + bf16(hx @ Wr.T), "resid 13B")
 
 
-@pytest.mark.parametrize("M,K", [(1, 4096), (8, 4096), (13, 4096), (3, 256), (8, 5120), (16, 5120), (20, 4096)])
+@pytest.mark.parametrize("M,K", [(1, 4096), (8, 4096), (13, 4096), (3, 256), (8, 5120), (16, 5120), (20, 4096), (5, 11008)])
 def test_i8_norm_stats_equals_separate_launches(hip, M, K):
-    """llj_i8_norm_stats (RMSNorm + LLM.int8() pass 1 in one launch, then the row quantization) is
-    bit-identical to llj_rmsnorm followed by llj_i8_stats: the normalized rows and every byte of
-    the statistics workspace (outlier flags / lists / counts, row maxima, SCA, quantized rows)."""
+    """llj_i8_norm_stats (one launch for M <= 8, K <= 4096; RMSNorm + pass 1, then the row
+    quantization up to 16 rows; the two ops beyond) is bit-identical to llj_rmsnorm followed by
+    llj_i8_stats (itself one launch for M <= 8, K <= 4096, else two passes): the normalized rows
+    and every byte of the statistics workspace, which also matches the numpy restatement."""
     rng = np.random.default_rng(M * 7 + K)
     x = bf16(rng.standard_normal((M, K)))
     x[:, rng.choice(K, 5, replace=False)] *= 40.0  # outlier columns after the norm
@@ -621,8 +622,46 @@ def test_i8_norm_stats_equals_separate_launches(hip, M, K):
     torch.cuda.synchronize()
     assert torch.equal(xn1.view(torch.int16), xn2.view(torch.int16))
     assert torch.equal(ws1, ws2)
-    flags = ws1.cpu().numpy()  # the case has outliers to find
-    assert (np.abs(bf16(xn1.float().cpu().numpy())) >= 6.0).any()
+    assert (np.abs(xn1.float().cpu().numpy()) >= 6.0).any()  # the case has outlier columns
+    _check_i8_ws(ws1.cpu().numpy(), xn1.float().cpu().numpy(), M, K)
+
+
+def _check_i8_ws(ws, a, M, K, thr=6.0):
+    """The statistics workspace (csrc/i8ws.h) against a numpy restatement of the LLM.int8() rules
+    (oracle/llama_np.py int8_linear): A16 = A.half(); outlier columns = any row |A16| >= thr, listed
+    ascending per k-block; SCA = row max of the other elements; aq = round(A16 * 127 / SCA),
+    outlier columns 0; part = the per-(k-block, row) maxima."""
+    nsb = 32
+    kb = ((K + nsb - 1) // nsb + 15) & ~15
+    a16 = np.abs(a.astype(np.float16).astype(np.float32))
+    out = a16 >= thr
+    flag = out.any(0)
+    small = np.where(out, 0.0, a16)
+    al = lambda x: (x + 15) & ~15  # noqa: E731
+    o_part = 16
+    o_cnt = o_part + 4 * nsb * M
+    o_list = o_cnt + 4 * nsb
+    o_sca = o_list + 4 * nsb * kb
+    o_flag = al(o_sca + 4 * M)
+    o_aq = al(o_flag + K)
+    hdr = ws[:16].view(np.int32)
+    assert list(hdr) == [M, K, nsb, kb]
+    part = ws[o_part:o_cnt].view(np.float32).reshape(nsb, M)
+    cnt = ws[o_cnt:o_list].view(np.int32)
+    lst = ws[o_list:o_sca].view(np.int32).reshape(nsb, kb)
+    sca = ws[o_sca:o_sca + 4 * M].view(np.float32)
+    np.testing.assert_array_equal(ws[o_flag:o_flag + K], flag.astype(np.uint8))
+    np.testing.assert_array_equal(sca, small.max(1))
+    for b in range(nsb):
+        cols = np.nonzero(flag[b * kb:(b + 1) * kb])[0] + b * kb
+        assert cnt[b] == len(cols)
+        np.testing.assert_array_equal(lst[b, :len(cols)], cols)
+        blk = small[:, b * kb:(b + 1) * kb]
+        np.testing.assert_array_equal(part[b], blk.max(1) if blk.size else np.zeros(M, np.float32))
+    inv = np.where(sca > 0, np.float32(127) / sca, np.float32(0)).astype(np.float32)
+    q = np.clip(np.rint(a.astype(np.float16).astype(np.float32) * inv[:, None]), -127, 127)
+    q[:, flag] = 0
+    np.testing.assert_array_equal(ws[o_aq:o_aq + M * K].view(np.int8).reshape(M, K), q.astype(np.int8))
 
 
 @pytest.mark.parametrize("wfmt", [0, 3, W4G_128])
