@@ -210,7 +210,7 @@ __device__ __forceinline__ int kofs(int t, int grp) {
 constexpr int kSideChunk = 256;
 template <int NW>
 __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float* SCB, int n0, float* part,
-                             unsigned char* stage) {
+                             unsigned char* stage, int cnt_lane) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nl = tid & 15, g = tid >> 4;
   constexpr int NG = NW * 4, NT = NW * 64;
@@ -221,8 +221,8 @@ __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float*
   float* s_a = reinterpret_cast<float*>(s_k + kSideChunk);  // [8][kSideChunk] f16(A) values
   const int n = n0 + nl, M = p.M;
   const float scb = SCB[n] / 127.f;
-  if (tid < 64) {  // prefix sum of the per-block outlier counts (kNSB <= 64)
-    int c = tid < h.nsb ? L.cnt[tid] : 0;
+  if (tid < 64) {  // prefix sum of the per-block outlier counts (kNSB <= 64; cnt_lane = cnt[lane], loaded early)
+    int c = tid < h.nsb ? cnt_lane : 0;
     int x = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -737,6 +737,13 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
 #endif
 #pragma unroll
   for (int d = 0; d < D; ++d) load(d, d);  // the weight stream starts before any A wait
+  // int8: the per-k-block outlier counts the side product starts from, loaded now (one memory
+  // latency less in the tail; needed once the stream is done)
+  int i8cnt = 0;
+  if constexpr (I8) {
+    const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
+    i8cnt = i8_layout(p.i8ws, h.mtot, h.K).cnt[lane < kNSB ? lane : 0];
+  }
   LLJ_STAMP(1);
   float2 e_cs[TPW][4];
   if constexpr (EP == EP_QKV) {  // RoPE rows of the rows' positions (needs e_ps: waits for it only)
@@ -807,10 +814,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     if (ALDS) __syncthreads();  // every wave is done reading the A image it aliases
     if constexpr (I8) {
       i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W), reinterpret_cast<const float*>(p.sz), ntj[0] * 16,
-                       side, smem);
+                       side, smem, i8cnt);
       if (DUAL)
         i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W2), reinterpret_cast<const float*>(p.sz2),
-                         ntj[0] * 16, side + NW * 8 * 16, smem);
+                         ntj[0] * 16, side + NW * 8 * 16, smem, i8cnt);
     }
     if constexpr (I8) {
       int* mine = reinterpret_cast<int*>(red) + (size_t)(wave * 64 + lane) * NV;
