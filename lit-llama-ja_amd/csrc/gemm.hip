@@ -21,6 +21,10 @@
 // 128 + zero offset is removed in the epilogue with the row sums of A, accumulated while the A
 // tile is staged:
 //   y[m,n] = s[n] * (sum_k A[m,k] (128 + q[k,n]) - (128 + z[n]) * sum_k A[m,k]).
+// gptq.int8 (W8P: per 16 columns x 128 k the W4P tile of the low nibbles, then that of the high
+// nibbles) stages both planes' halves (8 KiB per chunk) and feeds both to the same accumulator,
+// the high plane dequantized to bf16 2048 + 16 hi (exponent 0x45): the epilogue is the int4 one
+// with the offset 2176 + zero (llj_w8_scale_zero).
 // Tile order is XCD-aware: the 8 XCDs take contiguous ranges of tiles; inside a range bf16 weights
 // go m fastest (the row tiles of one weight panel run together on one XCD and share it through its
 // L2), int4 weights n fastest (one 128-row A panel shared while the XCD sweeps the columns).
@@ -29,15 +33,15 @@
 
 namespace llj {
 
-enum : int { GWF_W4 = 0, GWF_BF16 = 1 };
+enum : int { GWF_W4 = 0, GWF_BF16 = 1, GWF_W8 = 3 };
 enum : int { GEP_STORE = 0, GEP_RESID = 1, GEP_QKV = 2, GEP_SILU_MUL = 3 };
 
 struct GemmParams {
   const bf16_t* A;  // (M, K) rows with stride lda
   int lda;
   int M, N, K;
-  const void* W;      // GWF_W4: W4P tiles; GWF_BF16: (N, K) bf16 row-major
-  const float2* sz;   // GWF_W4: per column (scale, 128 + zero)
+  const void* W;      // GWF_W4: W4P tiles; GWF_W8: W8P tiles; GWF_BF16: (N, K) bf16 row-major
+  const float2* sz;   // GWF_W4 / GWF_W8: per column (scale, 128 / 2176 + zero)
   bf16_t* C;          // STORE: out; RESID: residual (updated); SILU_MUL: h (holds bf16 fc1 output)
   int ldc;
   // GEP_QKV
@@ -62,7 +66,9 @@ constexpr int kGBM = 128, kGBN = 128, kGBK = 64, kGNT = 256;
 constexpr int kAP = kGBK + 8;  // A / bf16-B LDS row pitch (elements): 144 B
 
 template <int WF>
-constexpr size_t gemm_b_bytes() { return WF == GWF_W4 ? (size_t)kGBN * kGBK / 2 : (size_t)kGBN * kAP * 2; }
+constexpr size_t gemm_b_bytes() {
+  return WF == GWF_W4 ? (size_t)kGBN * kGBK / 2 : WF == GWF_W8 ? (size_t)kGBN * kGBK : (size_t)kGBN * kAP * 2;
+}
 template <int WF>
 constexpr size_t gemm_lds_bytes() {
   return 2 * ((size_t)kGBM * kAP * 2 + gemm_b_bytes<WF>()) + kGBM * sizeof(float);
@@ -71,6 +77,7 @@ constexpr size_t gemm_lds_bytes() {
 template <int WF, int EP>
 __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr bool NIB = WF == GWF_W4 || WF == GWF_W8;  // nibble-coded: offset removed with the A row sums
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave & 1, wc = wave >> 1;
   const int row = lane & 15, g = lane >> 4;
@@ -99,8 +106,8 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   const int agm = m0 + ar < M ? m0 + ar : M - 1;  // rows past M: a clamped copy, never stored
   const bf16_t* asrc = p.A + (size_t)agm * p.lda + ah * 32;
   // register ring of GDEPTH chunks in flight (chunk c lives in slot c % GDEPTH)
-  constexpr int GDEPTH = WF == GWF_W4 ? LLJ_GDEPTH : 1;
-  constexpr int BV = WF == GWF_W4 ? 1 : 4;
+  constexpr int GDEPTH = NIB ? LLJ_GDEPTH : 1;
+  constexpr int BV = WF == GWF_W4 ? 1 : WF == GWF_W8 ? 2 : 4;
   u32x4 areg[GDEPTH][4], breg[GDEPTH][BV];
   auto load_chunk = [&](int slot, int c) {
     c = c < KC ? c : KC - 1;  // past the end: a valid duplicate, never stored
@@ -110,6 +117,12 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
       const u32x4* w = reinterpret_cast<const u32x4*>(p.W);
       const size_t nt = (size_t)(n0 / 16 + (tid >> 5));
       breg[slot][0] = __builtin_nontemporal_load(w + (nt * KC128 + (c >> 1)) * 64 + 32 * (c & 1) + (tid & 31));
+    } else if constexpr (WF == GWF_W8) {  // the same W4P lane of the low plane and of the high plane
+      const u32x4* w = reinterpret_cast<const u32x4*>(p.W);
+      const size_t nt = (size_t)(n0 / 16 + (tid >> 5));
+      const size_t o = (nt * KC128 + (c >> 1)) * 128 + 32 * (c & 1) + (tid & 31);
+      breg[slot][0] = __builtin_nontemporal_load(w + o);
+      breg[slot][1] = __builtin_nontemporal_load(w + o + 64);
     } else {
       const bf16_t* w = reinterpret_cast<const bf16_t*>(p.W) + (size_t)(n0 + ar) * K + (size_t)c * kGBK + ah * 32;
 #pragma unroll
@@ -122,13 +135,16 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       *reinterpret_cast<u32x4*>(a + 8 * v) = areg[slot][v];
-      if constexpr (WF == GWF_W4) {
+      if constexpr (NIB) {
         rsum2 += unpk(areg[slot][v][0]) + unpk(areg[slot][v][1]);
         rsum2 += unpk(areg[slot][v][2]) + unpk(areg[slot][v][3]);
       }
     }
     if constexpr (WF == GWF_W4) {
       reinterpret_cast<u32x4*>(Bs(buf))[tid] = breg[slot][0];
+    } else if constexpr (WF == GWF_W8) {  // [low plane halves 4 KiB][high plane halves 4 KiB]
+      reinterpret_cast<u32x4*>(Bs(buf))[tid] = breg[slot][0];
+      reinterpret_cast<u32x4*>(Bs(buf))[kGNT + tid] = breg[slot][1];
     } else {
       bf16_t* b = reinterpret_cast<bf16_t*>(Bs(buf)) + ar * kAP + ah * 32;
 #pragma unroll
@@ -136,9 +152,10 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
     }
   };
 
-  uint32_t msk = 0x000F000Fu, mag = 0x43004300u;
+  uint32_t msk = 0x000F000Fu, mag = 0x43004300u, mag_hi = 0x45004500u;  // mag_hi: W8 high nibbles, 2048 + 16 hi
   asm volatile("" : "+s"(msk));
   asm volatile("" : "+v"(mag));
+  if constexpr (WF == GWF_W8) asm volatile("" : "+v"(mag_hi));
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -153,7 +170,7 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
     const bf16_t* a = As(buf);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {  // MFMA k-steps of the chunk: k = 32 s + 8 g + [0, 8)
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[4], bfr[4], bhi[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = wr * 64 + 16 * i + row;
@@ -167,6 +184,14 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
           const uint4 d = make_uint4(and_or(w, msk, mag), and_or(w >> 4, msk, mag), and_or(w >> 8, msk, mag),
                                      and_or(w >> 12, msk, mag));
           bfr[j] = __builtin_bit_cast(bf16x8, d);
+        } else if constexpr (WF == GWF_W8) {
+          const uint32_t* b32 = reinterpret_cast<const uint32_t*>(Bs(buf));
+          const int wi = ((wc * 4 + j) * 32 + 16 * s + row) * 4 + g;
+          const uint32_t wl = b32[wi], wh = b32[kGNT * 4 + wi];
+          bfr[j] = __builtin_bit_cast(bf16x8, make_uint4(and_or(wl, msk, mag), and_or(wl >> 4, msk, mag),
+                                                         and_or(wl >> 8, msk, mag), and_or(wl >> 12, msk, mag)));
+          bhi[j] = __builtin_bit_cast(bf16x8, make_uint4(and_or(wh, msk, mag_hi), and_or(wh >> 4, msk, mag_hi),
+                                                         and_or(wh >> 8, msk, mag_hi), and_or(wh >> 12, msk, mag_hi)));
         } else {
           const int n = wc * 64 + 16 * j + row;
           bfr[j] = __builtin_bit_cast(
@@ -177,7 +202,10 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+          if constexpr (WF == GWF_W8) acc[i][j] = mfma_bf16(af[i], bhi[j], acc[i][j]);
+        }
       if (LLJ_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
     }
   };
@@ -203,7 +231,7 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   for (int j = 0; j < 4; ++j) {
     const int n = n0 + wc * 64 + 16 * j + row;
     float2 szn = make_float2(1.f, 0.f);
-    if constexpr (WF == GWF_W4) szn = p.sz[n];
+    if constexpr (NIB) szn = p.sz[n];
     const int nblk = n0 + wc * 64 + 16 * j;  // first column of this 16-column block
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -212,7 +240,7 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
         const int ml = wr * 64 + 16 * i + 4 * g + r;
         const int m = m0 + ml;
         float y = acc[i][j][r];
-        if constexpr (WF == GWF_W4) y = szn.x * (y - szn.y * rs_lds[ml]);
+        if constexpr (NIB) y = szn.x * (y - szn.y * rs_lds[ml]);
         const bool live = m < M;
         if constexpr (EP == GEP_QKV) {
           const float v = round_bf(y);  // c_attn output in bf16 (model.py:204), RoPE in fp32
@@ -285,6 +313,7 @@ static int gemm_run(int wfmt, GemmParams& p, void* stream) {
   if (EP != GEP_QKV && (!p.C || (p.ldc & 1))) return LLJ_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   if (wfmt == GWF_W4) return p.sz ? gemm_launch<GWF_W4, EP>(p, s) : LLJ_EINVAL;
+  if (wfmt == GWF_W8) return p.sz ? gemm_launch<GWF_W8, EP>(p, s) : LLJ_EINVAL;
   if (wfmt == GWF_BF16) return gemm_launch<GWF_BF16, EP>(p, s);
   return LLJ_EINVAL;
 }

@@ -120,13 +120,13 @@ HAND_NORM_MAX_M = 2
 
 # prefill / no-cache calls with at least this many rows (B * T) run the MFMA-tiled GEMMs
 # (llj_gemm_*) instead of the weight-streaming GEMVs in 8 / 16-row slices, when every Linear of
-# the model is int4 W4P or bf16 and the shapes tile by 128 (LLM.int8 and gptq.int8 keep the
-# GEMV slices)
+# the model is int4 W4P, gptq.int8 W8P or bf16 and the shapes tile by 128 (LLM.int8 and grouped
+# int4 keep the GEMV slices)
 GEMM_MIN_ROWS = 32
+_GEMM_FMTS = (0, 1, 3)
 
 # int8 decode: RMSNorm + LLM.int8() statistics in one launch pair up to this many rows
 I8_NORM_STATS_MAX_M = 16
-_GEMM_FMTS = (0, 1)
 
 # weight formats whose kernels remove the nibble offset with the row sums of A (W4P, W8P)
 _ROWSUM_FMTS = (0, 3)

@@ -379,8 +379,11 @@ def _random_int4_model(n_embd, n_head, n_layer=2, vocab=2048, seed=0, mode="gptq
             if hasattr(mod, "quant_weight"):
                 mod.quant_weight.copy_(torch.randint(0, 256, mod.quant_weight.shape, device=dev, dtype=torch.uint8,
                                                      generator=g))
-                mod.scales.copy_((torch.rand(mod.scales.shape, device=dev, generator=g) + 0.5) * (0.5 / 7))
-                mod.zeros.copy_(torch.randint(6, 10, mod.zeros.shape, device=dev, generator=g).to(mod.zeros.dtype))
+                q8 = getattr(mod, "bits", 4) == 8  # 8-bit codes: zero near 128, 16x finer steps
+                mod.scales.copy_((torch.rand(mod.scales.shape, device=dev, generator=g) + 0.5) * (0.5 / 7)
+                                 / (16 if q8 else 1))
+                lo, hi = (120, 136) if q8 else (6, 10)
+                mod.zeros.copy_(torch.randint(lo, hi, mod.zeros.shape, device=dev, generator=g).to(mod.zeros.dtype))
             elif isinstance(mod, torch.nn.Linear):
                 mod.weight.normal_(0.0, 1.0 / mod.in_features ** 0.5, generator=g)
             elif isinstance(mod, torch.nn.Embedding):
@@ -552,7 +555,7 @@ def test_generate_main_end_to_end(tmp_path, capsys):
     assert err.count("tokens/sec") == 2 and "Time to load model" in err and "Memory used" in err
 
 
-@pytest.mark.parametrize("mode", ["gptq.int4", None])
+@pytest.mark.parametrize("mode", ["gptq.int4", "gptq.int8", None])
 def test_prefill_gemm_path_equals_gemv_path(mode):
     """A 96-token prompt through the prefill GEMMs (model.GEMM_MIN_ROWS) gives the logits of the
     GEMV row-slice path within bf16 summation-order noise, and the KV caches it leaves behind
