@@ -140,8 +140,9 @@ int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, cons
 /* ---------------------------------------------------------------- prefill GEMMs (many rows)
  * The same Linear layers for M >> 16 rows (a prompt, a perplexity window: LLaMA.forward over
  * T tokens, model.py:84-128), MFMA-tiled 128 x 128 per workgroup with the chunk tiles staged
- * through LDS (csrc/gemm.hip). wfmt 0 (int4 W4P, sz = (scale, 128 + zero)), 1 (bf16 (N, K)) or
- * 3 (gptq.int8 W8P, sz = (scale, 2176 + zero)).
+ * through LDS (csrc/gemm.hip). wfmt 0 (int4 W4P, sz = (scale, 128 + zero)), 1 (bf16 (N, K)),
+ * 3 (gptq.int8 W8P, sz = (scale, 2176 + zero)) or 4 | (g / 128) << 8 (grouped int4, sz per
+ * (group, column) as for llj_linear; B fragments dequantized to bf16((q - z) * s)).
  * N % 128 == 0, K % 128 == 0, lda % 8 == 0; any M >= 1. Same epilogue semantics as the GEMVs. */
 int llj_gemm_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, void* C, int ldc, int M, int N,
                     int K, void* stream);

@@ -25,6 +25,10 @@
 // nibbles) stages both planes' halves (8 KiB per chunk) and feeds both to the same accumulator,
 // the high plane dequantized to bf16 2048 + 16 hi (exponent 0x45): the epilogue is the int4 one
 // with the offset 2176 + zero (llj_w8_scale_zero).
+// Grouped int4 (ColBlock tile_cols = g, g % 128 == 0) stages the W4P tiles like int4 and
+// dequantizes each B fragment to bf16((q - z_g) * s_g) with its chunk's group pair -- exactly the
+// weights of the reference's grouped forward, F.linear over get_weight(bf16)
+// (quantization.py:390-421) -- so its epilogue takes the accumulator as is.
 // Tile order is XCD-aware: the 8 XCDs take contiguous ranges of tiles; inside a range bf16 weights
 // go m fastest (the row tiles of one weight panel run together on one XCD and share it through its
 // L2), int4 weights n fastest (one 128-row A panel shared while the XCD sweeps the columns).
@@ -33,7 +37,7 @@
 
 namespace llj {
 
-enum : int { GWF_W4 = 0, GWF_BF16 = 1, GWF_W8 = 3 };
+enum : int { GWF_W4 = 0, GWF_BF16 = 1, GWF_W8 = 3, GWF_W4G = 4 };
 enum : int { GEP_STORE = 0, GEP_RESID = 1, GEP_QKV = 2, GEP_SILU_MUL = 3 };
 
 struct GemmParams {
@@ -51,6 +55,7 @@ struct GemmParams {
   const float* rope;
   const int* pos;
   int n_head, head_size, S, T;
+  int gch;  // GWF_W4G: group size in 128-deep chunks; sz = (scale, 128 + zero) per (group, column), (G, N)
 };
 
 constexpr int kGBM = 128, kGBN = 128, kGBK = 64, kGNT = 256;
@@ -67,7 +72,8 @@ constexpr int kAP = kGBK + 8;  // A / bf16-B LDS row pitch (elements): 144 B
 
 template <int WF>
 constexpr size_t gemm_b_bytes() {
-  return WF == GWF_W4 ? (size_t)kGBN * kGBK / 2 : WF == GWF_W8 ? (size_t)kGBN * kGBK : (size_t)kGBN * kAP * 2;
+  return (WF == GWF_W4 || WF == GWF_W4G) ? (size_t)kGBN * kGBK / 2 : WF == GWF_W8 ? (size_t)kGBN * kGBK
+                                                                                 : (size_t)kGBN * kAP * 2;
 }
 template <int WF>
 constexpr size_t gemm_lds_bytes() {
@@ -78,6 +84,7 @@ template <int WF, int EP>
 __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool NIB = WF == GWF_W4 || WF == GWF_W8;  // nibble-coded: offset removed with the A row sums
+  constexpr bool GRP = WF == GWF_W4G;                  // grouped int4: dequantized to the weight values
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave & 1, wc = wave >> 1;
   const int row = lane & 15, g = lane >> 4;
@@ -106,17 +113,23 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   const int agm = m0 + ar < M ? m0 + ar : M - 1;  // rows past M: a clamped copy, never stored
   const bf16_t* asrc = p.A + (size_t)agm * p.lda + ah * 32;
   // register ring of GDEPTH chunks in flight (chunk c lives in slot c % GDEPTH)
-  constexpr int GDEPTH = NIB ? LLJ_GDEPTH : 1;
-  constexpr int BV = WF == GWF_W4 ? 1 : WF == GWF_W8 ? 2 : 4;
+  constexpr int GDEPTH = (NIB || GRP) ? LLJ_GDEPTH : 1;
+  constexpr int BV = (WF == GWF_W4 || GRP) ? 1 : WF == GWF_W8 ? 2 : 4;
   u32x4 areg[GDEPTH][4], breg[GDEPTH][BV];
+  float2 szr[GDEPTH][4];  // GWF_W4G: (scale, 128 + zero) of the chunk's group for the lane's column of tile j
   auto load_chunk = [&](int slot, int c) {
     c = c < KC ? c : KC - 1;  // past the end: a valid duplicate, never stored
 #pragma unroll
     for (int v = 0; v < 4; ++v) areg[slot][v] = *reinterpret_cast<const u32x4*>(asrc + (size_t)c * kGBK + 8 * v);
-    if constexpr (WF == GWF_W4) {
+    if constexpr (WF == GWF_W4 || GRP) {
       const u32x4* w = reinterpret_cast<const u32x4*>(p.W);
       const size_t nt = (size_t)(n0 / 16 + (tid >> 5));
       breg[slot][0] = __builtin_nontemporal_load(w + (nt * KC128 + (c >> 1)) * 64 + 32 * (c & 1) + (tid & 31));
+      if constexpr (GRP) {
+        const size_t go = (size_t)((c >> 1) / p.gch) * p.N + n0 + wc * 64 + row;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) szr[slot][j] = p.sz[go + 16 * j];
+      }
     } else if constexpr (WF == GWF_W8) {  // the same W4P lane of the low plane and of the high plane
       const u32x4* w = reinterpret_cast<const u32x4*>(p.W);
       const size_t nt = (size_t)(n0 / 16 + (tid >> 5));
@@ -140,7 +153,7 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
         rsum2 += unpk(areg[slot][v][2]) + unpk(areg[slot][v][3]);
       }
     }
-    if constexpr (WF == GWF_W4) {
+    if constexpr (WF == GWF_W4 || GRP) {
       reinterpret_cast<u32x4*>(Bs(buf))[tid] = breg[slot][0];
     } else if constexpr (WF == GWF_W8) {  // [low plane halves 4 KiB][high plane halves 4 KiB]
       reinterpret_cast<u32x4*>(Bs(buf))[tid] = breg[slot][0];
@@ -164,6 +177,9 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
 
   auto step = [&](int slot, int c) {  // chunk c: stage it, refill its slot with c + GDEPTH, multiply
     const int buf = c & 1;
+    float2 gsz[4];  // GWF_W4G: this chunk's group pairs (the slot is refilled below)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gsz[j] = szr[slot][j];
     store_chunk(slot, buf);
     __syncthreads();  // chunk c staged; every wave is done with chunk c - 1's buffer
     load_chunk(slot, c + GDEPTH);
@@ -184,6 +200,15 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
           const uint4 d = make_uint4(and_or(w, msk, mag), and_or(w >> 4, msk, mag), and_or(w >> 8, msk, mag),
                                      and_or(w >> 12, msk, mag));
           bfr[j] = __builtin_bit_cast(bf16x8, d);
+        } else if constexpr (GRP) {
+          // bf16((q - z) s): (128 + q) - (128 + z) is exact and so is its product with the bf16 scale,
+          // so the fma rounds once (to fp32, exactly) and the conversion once (to bf16)
+          const uint32_t w = reinterpret_cast<const uint32_t*>(Bs(buf))[((wc * 4 + j) * 32 + 16 * s + row) * 4 + g];
+          const f32x2 sc = {gsz[j].x, gsz[j].x}, nb = {-gsz[j].y * gsz[j].x, -gsz[j].y * gsz[j].x};
+          uint32_t o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = cvt_pk(unpk(and_or(w >> (4 * e), msk, mag)) * sc + nb);
+          bfr[j] = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
         } else if constexpr (WF == GWF_W8) {
           const uint32_t* b32 = reinterpret_cast<const uint32_t*>(Bs(buf));
           const int wi = ((wc * 4 + j) * 32 + 16 * s + row) * 4 + g;
@@ -314,6 +339,10 @@ static int gemm_run(int wfmt, GemmParams& p, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (wfmt == GWF_W4) return p.sz ? gemm_launch<GWF_W4, EP>(p, s) : LLJ_EINVAL;
   if (wfmt == GWF_W8) return p.sz ? gemm_launch<GWF_W8, EP>(p, s) : LLJ_EINVAL;
+  if ((wfmt & 0xff) == GWF_W4G) {  // grouped int4: group size (128-deep chunks) in the bits above
+    p.gch = wfmt >> 8;
+    return (p.sz && p.gch >= 1 && p.K % 128 == 0) ? gemm_launch<GWF_W4G, EP>(p, s) : LLJ_EINVAL;
+  }
   if (wfmt == GWF_BF16) return gemm_launch<GWF_BF16, EP>(p, s);
   return LLJ_EINVAL;
 }

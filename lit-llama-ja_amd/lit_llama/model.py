@@ -120,10 +120,14 @@ HAND_NORM_MAX_M = 2
 
 # prefill / no-cache calls with at least this many rows (B * T) run the MFMA-tiled GEMMs
 # (llj_gemm_*) instead of the weight-streaming GEMVs in 8 / 16-row slices, when every Linear of
-# the model is int4 W4P, gptq.int8 W8P or bf16 and the shapes tile by 128 (LLM.int8 and grouped
-# int4 keep the GEMV slices)
+# the model is int4 W4P (per-row or grouped scales), gptq.int8 W8P or bf16 and the shapes tile by
+# 128 (LLM.int8 keeps the GEMV slices)
 GEMM_MIN_ROWS = 32
-_GEMM_FMTS = (0, 1, 3)
+_GEMM_FMTS = (0, 1, 3, 4)  # weight formats (low byte of wfmt; 4 = grouped int4) the prefill GEMMs take
+
+
+def _gemm_fmt(wfmt: int) -> bool:
+    return (wfmt & 0xFF) in _GEMM_FMTS
 
 # int8 decode: RMSNorm + LLM.int8() statistics in one launch pair up to this many rows
 I8_NORM_STATS_MAX_M = 16
@@ -355,8 +359,8 @@ class LLaMA(nn.Module):
         cfg = self.config
         C, H = cfg.n_embd, MLP.hidden(cfg)
         fmts = {s[0] for layer in specs["layers"] for s in layer}
-        return (M >= GEMM_MIN_ROWS and fmts <= set(_GEMM_FMTS) and C % 128 == 0 and H % 128 == 0
-                and specs["head"][0] in _GEMM_FMTS)
+        return (M >= GEMM_MIN_ROWS and all(_gemm_fmt(f) for f in fmts) and C % 128 == 0 and H % 128 == 0
+                and _gemm_fmt(specs["head"][0]))
 
     def _blocks_gemm(self, w, specs, kv, pos, B, T, S, st):
         """The n_layer blocks for many rows through the prefill GEMMs (csrc/gemm.hip): per layer
@@ -463,7 +467,7 @@ class LLaMA(nn.Module):
             xn = torch.empty_like(x)
             self._i8_norm_prep(x, ln, xn, M, C, w, st)
             src, nw = xn, None
-        elif M >= GEMM_MIN_ROWS and f in _GEMM_FMTS and C % 128 == 0 and V % 128 == 0:  # many rows: GEMM
+        elif M >= GEMM_MIN_ROWS and _gemm_fmt(f) and C % 128 == 0 and V % 128 == 0:  # many rows: GEMM
             xn = torch.empty_like(x)
             _hip.call("llj_rmsnorm_rows", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), None, M, C, st)
             _hip.call("llj_gemm_linear", f, xn.data_ptr(), C, W.data_ptr(), _hip.ptr(sz), out.data_ptr(), out.stride(0),

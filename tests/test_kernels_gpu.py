@@ -843,7 +843,7 @@ def test_sample_device_rng_distribution(hip):
     assert (out2.cpu().numpy() != draws).mean() > 0.3
 
 
-@pytest.mark.parametrize("wfmt", [0, 1, 3])
+@pytest.mark.parametrize("wfmt", [0, 1, 3, W4G_128, 4 | (2 << 8)])
 @pytest.mark.parametrize("M,N,K", [(17, 256, 128), (100, 4096, 4096), (300, 11008, 4096), (256, 4096, 11008),
                                    (129, 384, 1024)])
 def test_gemm_linear_and_resid(hip, wfmt, M, N, K):
@@ -869,7 +869,7 @@ def test_gemm_linear_and_resid(hip, wfmt, M, N, K):
     assert_bf16_close(xr.float().cpu().numpy(), x0 + bf16(y), f"gemm resid wfmt={wfmt}")
 
 
-@pytest.mark.parametrize("wfmt", [0, 1, 3])
+@pytest.mark.parametrize("wfmt", [0, 1, 3, W4G_128, 4 | (2 << 8)])
 def test_gemm_swiglu_two_pass(hip, wfmt):
     """c_fc1 into h (llj_gemm_linear), then c_fc2 with the silu * mul epilogue in place
     (llj_gemm_silu_mul): model.py:258 with the reference's bf16 rounding points."""
@@ -888,7 +888,7 @@ def test_gemm_swiglu_two_pass(hip, wfmt):
     assert_bf16_close(h.float().cpu().numpy(), hexp, f"gemm swiglu wfmt={wfmt}", rel=3e-2)
 
 
-@pytest.mark.parametrize("wfmt", [0, 1, 3])
+@pytest.mark.parametrize("wfmt", [0, 1, 3, W4G_128, 4 | (2 << 8)])
 @pytest.mark.parametrize("B,T_,nh,hs", [(1, 200, 32, 128), (3, 40, 4, 64)])
 def test_gemm_qkv_rope_kv(hip, wfmt, B, T_, nh, hs):
     """llj_gemm_qkv_rope: c_attn + RoPE + KV-cache write for a whole prompt (ring slots p % S)."""

@@ -350,6 +350,15 @@ def test_grouped_int4_model_vs_oracle():
     out = m(torch.from_numpy(prompt[None].astype(np.int64)).cuda()).float().cpu().numpy()[0, -1]
     rel = np.linalg.norm(out - olog[0]) / np.linalg.norm(olog[0])
     assert rel < 3e-2, rel
+    # a 40-token prompt takes the prefill GEMMs (grouped int4 B fragments): logits vs the oracle
+    from lit_llama import model as MD
+    p40 = np.random.default_rng(23).integers(3, 2048, 40).astype(np.int32)
+    assert 40 >= MD.GEMM_MIN_ROWS
+    out40 = m(torch.from_numpy(p40[None].astype(np.int64)).cuda()).float().cpu().numpy()[0]
+    orc.reset_cache()
+    ref40 = orc.forward(p40[None].astype(np.int64))[0]
+    rel40 = np.linalg.norm(out40 - ref40) / np.linalg.norm(ref40)
+    assert rel40 < 3e-2, rel40
 
 
 def test_bf16_vs_int4_module_forward_paths(golden):
