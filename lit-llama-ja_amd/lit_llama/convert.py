@@ -7,13 +7,17 @@ from HF's half-split rotary layout back to the interleaved pairs `apply_rope` us
 (model.py:312-329; the inverse of transformers' convert_llama_weights_to_hf permute), every other
 tensor renamed by the reference's weight map, `rotary_emb.inv_freq` dropped. Shards are opened
 memory-mapped with `torch.load(weights_only=True, mmap=True)` (nothing in a checkpoint is
-executed) and the output written once with `torch.save`; `load_lit_checkpoint` streams a
+executed); every converted tensor is spilled into a file-backed (memory-mapped) storage next to
+the output as soon as it exists, so the final `torch.save` streams from the page cache and the
+process never holds more than one converted tensor in anonymous memory (the reference gets the
+same bound from its incremental_save, lit_llama/utils.py). `load_lit_checkpoint` streams a
 lit-llama.pth straight into a model's (device) parameters.
 """
 from __future__ import annotations
 
 import json
 import shutil
+import tempfile
 from pathlib import Path
 
 import torch
@@ -44,8 +48,39 @@ def unpermute_rotary(w: torch.Tensor, n_head: int) -> torch.Tensor:
     return w.view(n_head, 2, dim // n_head // 2, dim).transpose(1, 2).reshape(dim, dim)
 
 
-def convert_hf_state_dict(hf: dict, config: LLaMAConfig, dtype=torch.float32) -> dict:
-    """Map one HF LLaMA state dict (possibly merged from all shards) to lit-llama keys."""
+class _Spill:
+    """Sink for converted tensors: each one is copied into its own memory-mapped file in `dir` and
+    the file-backed tensor is kept instead (its pages are the kernel's to write back and drop)."""
+
+    def __init__(self, dir: Path):
+        self.dir = Path(tempfile.mkdtemp(prefix=".lit-convert-", dir=dir))
+        self.n = 0
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        t = t.contiguous()
+        f = self.dir / f"{self.n}.bin"
+        self.n += 1
+        m = torch.from_file(str(f), shared=True, size=t.numel(), dtype=t.dtype).view(t.shape)
+        m.copy_(t)
+        return m
+
+    def close(self):
+        shutil.rmtree(self.dir, ignore_errors=True)
+
+
+def _save_spilled(make, out_path: Path) -> None:
+    """torch.save of the state dict make(sink) builds, every tensor spilled as it is made."""
+    sink = _Spill(out_path.parent)
+    try:
+        torch.save(make(sink), out_path)
+    finally:
+        sink.close()
+
+
+def convert_hf_state_dict(hf: dict, config: LLaMAConfig, dtype=torch.float32, sink=None) -> dict:
+    """Map one HF LLaMA state dict (possibly merged from all shards) to lit-llama keys; `sink`
+    (optional) receives each converted tensor and returns what the result dict keeps."""
+    keep = sink if sink is not None else (lambda t: t)
     out, qkv = {}, {}
     for name, t in hf.items():
         if "rotary_emb.inv_freq" in name:
@@ -58,13 +93,13 @@ def convert_hf_state_dict(hf: dict, config: LLaMAConfig, dtype=torch.float32) ->
                 qkv.setdefault(key, {})[proj] = t
                 if len(qkv[key]) == 3:
                     parts3 = qkv.pop(key)
-                    out[key] = torch.cat([unpermute_rotary(parts3["q_proj"].to(dtype), config.n_head),
-                                          unpermute_rotary(parts3["k_proj"].to(dtype), config.n_head),
-                                          parts3["v_proj"].to(dtype)], 0)
+                    out[key] = keep(torch.cat([unpermute_rotary(parts3["q_proj"].to(dtype), config.n_head),
+                                               unpermute_rotary(parts3["k_proj"].to(dtype), config.n_head),
+                                               parts3["v_proj"].to(dtype)], 0))
                 continue
-            out[key] = t.to(dtype)
+            out[key] = keep(t.to(dtype))
         else:
-            out[WEIGHT_MAP[name]] = t.to(dtype)
+            out[WEIGHT_MAP[name]] = keep(t.to(dtype))
     if qkv:  # reference convert_hf_checkpoint.py:137
         raise AssertionError(f"unexpected partial weights {list(qkv)}")
     return out
@@ -93,7 +128,7 @@ def convert_hf_checkpoint(*, output_dir: Path = Path("checkpoints/lit-llama/7B")
     hf = {}
     for b in bin_files:  # memory-mapped: tensors are read when converted
         hf.update(torch.load(b, map_location="cpu", weights_only=True, mmap=True))
-    torch.save(convert_hf_state_dict(hf, config, dt), output_dir / "lit-llama.pth")
+    _save_spilled(lambda sink: convert_hf_state_dict(hf, config, dt, sink), output_dir / "lit-llama.pth")
 
 
 def load_lit_checkpoint(model: torch.nn.Module, path: Path, strict: bool = True):
@@ -105,23 +140,25 @@ def load_lit_checkpoint(model: torch.nn.Module, path: Path, strict: bool = True)
 
 
 # ----------------------------------------------------------------------- Meta (consolidated.*.pth)
-def convert_meta_state_dict(state_dict: dict, dtype=torch.float32) -> dict:
+def convert_meta_state_dict(state_dict: dict, dtype=torch.float32, sink=None) -> dict:
     """reference scripts/convert_checkpoint.py:20-53: Meta names -> lit-llama names, wq / wk / wv
-    stacked into c_attn (Meta's rotary layout is already the interleaved one)."""
-    out = {"transformer.wte.weight": state_dict["tok_embeddings.weight"].to(dtype),
-           "lm_head.weight": state_dict["output.weight"].to(dtype),
-           "transformer.ln_f.scale": state_dict["norm.weight"].to(dtype)}
+    stacked into c_attn (Meta's rotary layout is already the interleaved one). `sink` as in
+    convert_hf_state_dict."""
+    keep = sink if sink is not None else (lambda t: t)
+    out = {"transformer.wte.weight": keep(state_dict["tok_embeddings.weight"].to(dtype)),
+           "lm_head.weight": keep(state_dict["output.weight"].to(dtype)),
+           "transformer.ln_f.scale": keep(state_dict["norm.weight"].to(dtype))}
     layers = sorted({k.split(".")[1] for k in state_dict if k.startswith("layers")})
     for i in layers:
         p, q = f"layers.{i}.", f"transformer.h.{i}."
-        out[q + "attn.c_attn.weight"] = torch.cat([state_dict[p + f"attention.{w}.weight"].to(dtype)
-                                                   for w in ("wq", "wk", "wv")])
-        out[q + "attn.c_proj.weight"] = state_dict[p + "attention.wo.weight"].to(dtype)
-        out[q + "mlp.c_fc1.weight"] = state_dict[p + "feed_forward.w1.weight"].to(dtype)
-        out[q + "mlp.c_proj.weight"] = state_dict[p + "feed_forward.w2.weight"].to(dtype)
-        out[q + "mlp.c_fc2.weight"] = state_dict[p + "feed_forward.w3.weight"].to(dtype)
-        out[q + "rms_1.scale"] = state_dict[p + "attention_norm.weight"].to(dtype)
-        out[q + "rms_2.scale"] = state_dict[p + "ffn_norm.weight"].to(dtype)
+        out[q + "attn.c_attn.weight"] = keep(torch.cat([state_dict[p + f"attention.{w}.weight"].to(dtype)
+                                                        for w in ("wq", "wk", "wv")]))
+        out[q + "attn.c_proj.weight"] = keep(state_dict[p + "attention.wo.weight"].to(dtype))
+        out[q + "mlp.c_fc1.weight"] = keep(state_dict[p + "feed_forward.w1.weight"].to(dtype))
+        out[q + "mlp.c_proj.weight"] = keep(state_dict[p + "feed_forward.w2.weight"].to(dtype))
+        out[q + "mlp.c_fc2.weight"] = keep(state_dict[p + "feed_forward.w3.weight"].to(dtype))
+        out[q + "rms_1.scale"] = keep(state_dict[p + "attention_norm.weight"].to(dtype))
+        out[q + "rms_2.scale"] = keep(state_dict[p + "ffn_norm.weight"].to(dtype))
     return out
 
 
@@ -130,23 +167,23 @@ SHARD_DIMS = {"lm_head.weight": 0, "wte.weight": 1, "attn.c_attn.weight": 0, "at
               "mlp.c_fc1.weight": 0, "mlp.c_fc2.weight": 0, "mlp.c_proj.weight": 1}
 
 
-def merge_meta_shards(converted: list) -> dict:
+def merge_meta_shards(converted: list, sink=None) -> dict:
     """Concatenate the model-parallel parts (convert_checkpoint.py:95-113; unsharded tensors are
     taken from the first part) and regroup c_attn from [Q1 K1 V1 Q2 K2 V2 ...] to
-    [Q1 Q2 ... K1 K2 ... V1 V2 ...] (115-131)."""
+    [Q1 Q2 ... K1 K2 ... V1 V2 ...] (115-131). Tensor by tensor, each merged result handed to
+    `sink` (as in convert_hf_state_dict) before the next is built."""
+    keep = sink if sink is not None else (lambda t: t)
     n = len(converted)
-    combined = dict(converted[0])
-    for part in converted[1:]:
-        for name, t in part.items():
-            dim = next((d for k, d in SHARD_DIMS.items() if k in name), None)
-            if dim is not None:
-                combined[name] = torch.cat((combined[name], t), dim=dim)
-    for name, t in combined.items():
-        if "c_attn" not in name:
-            continue
-        src = t.shape[0] // n
-        mat = src // 3
-        combined[name] = torch.cat([t[i * src + j * mat: i * src + (j + 1) * mat] for j in range(3) for i in range(n)])
+    combined = {}
+    for name, t0 in converted[0].items():
+        dim = next((d for k, d in SHARD_DIMS.items() if k in name), None)
+        t = torch.cat([part[name] for part in converted], dim=dim) if (dim is not None and n > 1) else t0
+        if "c_attn" in name:
+            src = t.shape[0] // n
+            mat = src // 3
+            t = torch.cat([t[i * src + j * mat: i * src + (j + 1) * mat] for j in range(3) for i in range(n)])
+        combined[name] = keep(t)
+        del t
     return combined
 
 
@@ -165,6 +202,10 @@ def meta_weights_for_nano_model(*, output_dir: Path = Path("checkpoints/lit-llam
     if not files:
         raise RuntimeError(f"No checkpoints were found at checkpoint_dir {checkpoint_dir}. "
                            "`consolidated.0*.pth` files expected at that location.")
-    parts = [convert_meta_state_dict(torch.load(f, map_location="cpu", weights_only=True, mmap=True), dt)
-             for f in files]
-    torch.save(merge_meta_shards(parts), output_dir / "lit-llama.pth")
+    def make(sink):
+        # every part converted into spilled (file-backed) tensors, then merged tensor by tensor
+        parts = [convert_meta_state_dict(torch.load(f, map_location="cpu", weights_only=True, mmap=True), dt, sink)
+                 for f in files]
+        return merge_meta_shards(parts, sink)
+
+    _save_spilled(make, output_dir / "lit-llama.pth")

@@ -51,6 +51,8 @@ def test_file_conversion_matches_reference(tiny_config, tmp_path):
     assert set(sd) == set(LIT)
     for k, v in sd.items():
         np.testing.assert_array_equal(v.numpy(), LIT[k], err_msg=k)
+    # the converted tensors were spilled to memory-mapped files beside the output, removed after the save
+    assert sorted(p.name for p in out.iterdir()) == ["lit-llama.pth"]
     with pytest.raises(ValueError):
         CV.convert_hf_checkpoint(output_dir=out, checkpoint_dir=ck, model_size="tinyhf", dtype="float33")
 
