@@ -68,12 +68,14 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def spawn_replicas(n: int, argv) -> int:
+def spawn_replicas(n: int, argv, timeout_s: float = 3000.0, poll_s: float = 0.2) -> int:
     """`bench.py --gpus N` started without a launcher: start N child processes of this script
     with the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), one per GPU
     (LOCAL_RANK i -> cuda:i), BEFORE this process touches the GPU (it never does: only the
-    children initialise HIP), wait for all of them and return the worst exit code. Rank 0's
-    stdout carries the JSON line."""
+    children initialise HIP). All children are polled together: the first non-zero exit
+    terminates the others (a replica that died would otherwise leave its siblings blocked in the
+    gloo barrier) and is returned; past `timeout_s` every child is terminated and 124 returned.
+    Rank 0's stdout carries the JSON line."""
     import subprocess
 
     port = _free_port()
@@ -82,9 +84,33 @@ def spawn_replicas(n: int, argv) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    t_end = time.monotonic() + timeout_s
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            print(f"[bench] a replica exited with {bad[0]}: stopping the others", file=sys.stderr)
+            stop_all()
+            return bad[0]
+        if all(rc == 0 for rc in rcs):
+            return 0
+        if time.monotonic() > t_end:
+            print(f"[bench] replicas still running after {timeout_s:.0f} s: stopping them", file=sys.stderr)
+            stop_all()
+            return 124
+        time.sleep(poll_s)
 
 
 def barrier(ws):
@@ -390,6 +416,8 @@ def main():
                     help="profiling aid: decode steps launched one by one instead of graph replays (PMC passes)")
     ap.add_argument("--stub", action="store_true",
                     help="CPU rehearsal of the replica launch / timing / aggregation (no GPU, no measurement)")
+    ap.add_argument("--stub-fail-rank", type=int, default=-1,
+                    help="with --stub: this rank exits 3 before the barrier (launcher failure test)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -400,6 +428,8 @@ def main():
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {ws}", file=sys.stderr)
 
     if args.stub:
+        if args.stub_fail_rank == rank:  # launcher test: this replica dies before the barrier
+            sys.exit(3)
         r = time_stub(args.steps, args.warmup, ws)
         t_max, tokens = aggregate(r["seconds"], r["tokens"], ws)
         if rank == 0:

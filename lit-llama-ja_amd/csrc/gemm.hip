@@ -201,13 +201,15 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
                                      and_or(w >> 12, msk, mag));
           bfr[j] = __builtin_bit_cast(bf16x8, d);
         } else if constexpr (GRP) {
-          // bf16((q - z) s): (128 + q) - (128 + z) is exact and so is its product with the bf16 scale,
-          // so the fma rounds once (to fp32, exactly) and the conversion once (to bf16)
+          // bf16(fp32(q - z) * s), the reference's get_weight(bf16) (quantization.py:402-408: the bf16
+          // weight times the scale in the scale's precision, then stored to bf16): (128 + q) - (128 + z)
+          // is an exact small integer, its product with s rounds once to fp32 (exact for bf16 / fp16
+          // scales, the reference's fp32 product for fp32 scales), the conversion once to bf16
           const uint32_t w = reinterpret_cast<const uint32_t*>(Bs(buf))[((wc * 4 + j) * 32 + 16 * s + row) * 4 + g];
-          const f32x2 sc = {gsz[j].x, gsz[j].x}, nb = {-gsz[j].y * gsz[j].x, -gsz[j].y * gsz[j].x};
+          const f32x2 sc = {gsz[j].x, gsz[j].x}, zz = {gsz[j].y, gsz[j].y};
           uint32_t o[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = cvt_pk(unpk(and_or(w >> (4 * e), msk, mag)) * sc + nb);
+          for (int e = 0; e < 4; ++e) o[e] = cvt_pk((unpk(and_or(w >> (4 * e), msk, mag)) - zz) * sc);
           bfr[j] = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
         } else if constexpr (WF == GWF_W8) {
           const uint32_t* b32 = reinterpret_cast<const uint32_t*>(Bs(buf));

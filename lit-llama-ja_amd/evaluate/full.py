@@ -21,6 +21,7 @@ wd = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(wd))
 
 from lit_llama import LLaMA  # noqa: E402
+from lit_llama.checkpoint import read_checkpoint  # noqa: E402
 from lit_llama.utils import EmptyInitOnDevice  # noqa: E402
 
 WINDOW = 2048  # reference evaluate/full.py:117 ("for compat with gptq")
@@ -56,7 +57,7 @@ def main(text_path: str, *, checkpoint_path: Optional[Path] = None,
         print("Loading model ...", file=sys.stderr)
         t0 = time.time()
         model = LLaMA.from_name(model_size)
-        model.load_state_dict(torch.load(checkpoint_path, map_location="cpu", mmap=True, weights_only=True))
+        model.load_state_dict(read_checkpoint(checkpoint_path))  # weights only, memory-mapped
         print(f"Time to load model: {time.time() - t0:.02f} seconds.", file=sys.stderr)
     model.eval()
     tokenizer = tokenizer_for(tokenizer_path)

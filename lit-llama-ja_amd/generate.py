@@ -24,6 +24,7 @@ wd = Path(__file__).resolve().parent
 sys.path.insert(0, str(wd))
 
 from lit_llama import LLaMA, HFTokenizer  # noqa: E402
+from lit_llama.checkpoint import read_checkpoint  # noqa: E402
 from lit_llama.engine import DecodeSession  # noqa: E402
 from lit_llama.utils import EmptyInitOnDevice, llama_model_lookup  # noqa: E402
 
@@ -101,7 +102,7 @@ def main(prompt: str = "Hello, my name is", *, num_samples: int = 1, max_new_tok
         raise SystemExit("this generate.py runs on a ROCm GPU (MI355X) only")
     print("Loading model ...", file=sys.stderr)
     t0 = time.time()
-    checkpoint = torch.load(checkpoint_path, map_location="cpu", mmap=True, weights_only=True)
+    checkpoint = read_checkpoint(checkpoint_path)  # weights only, memory-mapped (incremental_save files too)
     name = llama_model_lookup(checkpoint)
     with EmptyInitOnDevice(device=torch.device("cuda"), dtype=torch.bfloat16, quantization_mode=quantize):
         model = LLaMA.from_name(name)

@@ -551,6 +551,9 @@ class _OneBlock:
     def _i8_prep(self, A, M, K, w, st):
         LLaMA._i8_prep(self, A, M, K, w, st)
 
+    def _i8_norm_prep(self, *a):
+        LLaMA._i8_norm_prep(self, *a)
+
     def _resid(self, *a):
         LLaMA._resid(self, *a)
 

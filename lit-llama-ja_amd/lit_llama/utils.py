@@ -11,6 +11,8 @@ from contextlib import contextmanager
 import torch
 import torch.utils._device
 
+from .checkpoint import incremental_save, lazy_load  # noqa: F401  (reference utils.py:364-376, 492-531)
+
 llama_model_sizes = {  # reference utils.py:19-27
     512: "19M",
     640: "49M",

@@ -24,6 +24,7 @@ if __name__ == "__main__":
 import torch
 import torch.nn.functional as F
 
+from lit_llama.checkpoint import read_checkpoint
 from lit_llama.model import apply_rope
 from lit_llama.quantization import GPTQQuantizer
 
@@ -160,7 +161,7 @@ def main(*, checkpoint_path: Path = Path("checkpoints/lit-llama/7B/lit-llama.pth
 
     print("Loading model ...", file=sys.stderr)
     t0 = time.time()
-    checkpoint = torch.load(checkpoint_path, map_location="cpu", mmap=True, weights_only=True)
+    checkpoint = read_checkpoint(checkpoint_path)  # weights only, memory-mapped (incremental_save files too)
     with EmptyInitOnDevice(device=torch.device("cuda"), dtype=dt):
         model = LLaMA.from_name(llama_model_lookup(checkpoint))
     model.load_state_dict(checkpoint)

@@ -549,8 +549,63 @@ def gen_bf16_init():
     save("bf16_init", seed=np.int64(seed), tokens=tokens, expected=expected.astype(np.float32))
 
 
+def gen_ref_ckpt():
+    """A lit-llama.pth exactly as the reference writes it: its scripts/convert_hf_checkpoint.py
+    (which streams through its incremental_save, protocol 5, lit_llama/utils.py:492-531) run with
+    dtype="bfloat16" on a synthetic HF checkpoint of a shape the gfx950 kernels take (n_embd 128,
+    2 heads of 64, n_hidden 512, vocab 256, 2 layers; O(1) activations like oracle.weights). The
+    .pth file itself is the fixture (ref_lit_llama_bf16.pth, data written by the reference), with
+    digests of the tensors the reference's own lazy_load reads back from it (ref_ckpt.npz)."""
+    import json
+    import shutil
+    import tempfile
+
+    from lit_llama import model as rmodel
+    from scripts.convert_hf_checkpoint import convert_hf_checkpoint
+
+    C, nh, H, V, L = 128, 2, 512, 256, 2
+    rmodel.llama_configs["tinyref"] = dict(n_layer=L, n_head=nh, n_embd=C, vocab_size=V, block_size=64)
+    rng = np.random.default_rng(79)
+    t = lambda *sh: torch.from_numpy((rng.standard_normal(sh) / np.sqrt(sh[-1])).astype(np.float32))  # noqa: E731
+    u = lambda n: torch.from_numpy(rng.uniform(0.5, 1.5, n).astype(np.float32))  # noqa: E731
+    hf = {"model.embed_tokens.weight": torch.from_numpy(rng.standard_normal((V, C)).astype(np.float32)),
+          "model.norm.weight": u(C), "lm_head.weight": t(V, C) * 2}
+    for i in range(L):
+        p = f"model.layers.{i}."
+        hf.update({p + "self_attn.q_proj.weight": t(C, C), p + "self_attn.k_proj.weight": t(C, C),
+                   p + "self_attn.v_proj.weight": t(C, C), p + "self_attn.o_proj.weight": t(C, C),
+                   p + "mlp.gate_proj.weight": t(H, C), p + "mlp.up_proj.weight": t(H, C),
+                   p + "mlp.down_proj.weight": t(C, H), p + "input_layernorm.weight": u(C),
+                   p + "post_attention_layernorm.weight": u(C)})
+    with tempfile.TemporaryDirectory() as td:
+        ck, out = Path(td) / "hf" / "tinyref", Path(td) / "lit" / "tinyref"
+        ck.mkdir(parents=True)
+        (ck / "tokenizer.model").write_bytes(b"placeholder")
+        torch.save(hf, ck / "pytorch_model-00001-of-00001.bin")
+        wm = {k: "pytorch_model-00001-of-00001.bin" for k in hf}
+        (ck / "pytorch_model.bin.index.json").write_text(json.dumps({"metadata": {}, "weight_map": wm}))
+        with contextlib.redirect_stdout(io.StringIO()):
+            convert_hf_checkpoint(output_dir=out, checkpoint_dir=ck, model_size="tinyref", dtype="bfloat16")
+        from lit_llama.utils import lazy_load  # the reference's own reader of its incremental_save format
+        with lazy_load(out / "lit-llama.pth") as sd:
+            lit = {k: v._load_tensor() for k, v in sd.items()}
+        shutil.copy(out / "lit-llama.pth", HERE / "ref_lit_llama_bf16.pth")
+        print(f"wrote tests/golden/ref_lit_llama_bf16.pth ({(HERE / 'ref_lit_llama_bf16.pth').stat().st_size} B)")
+    import hashlib
+
+    # per tensor: sha256 of the bytes the reference's lazy_load returns (C order), shape, dtype
+    arrays = {}
+    for k, v in lit.items():
+        b = v.contiguous().view(torch.int16).numpy().tobytes()
+        arrays["sha/" + k] = np.array(hashlib.sha256(b).hexdigest())
+        arrays["shape/" + k] = np.array(v.shape, np.int64)
+        arrays["dtype/" + k] = np.array(str(v.dtype))
+    arrays["config"] = np.array([C, nh, V, L, 64], np.int64)
+    save("ref_ckpt", **arrays)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq", "hf_convert",
-                             "meta_convert", "bf16_init", "sampled", "ppl", "gptq_grouped"]
+                             "meta_convert", "bf16_init", "sampled", "ppl", "gptq_grouped", "ref_ckpt"]
     for w in which:
         globals()[f"gen_{w}"]()

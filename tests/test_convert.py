@@ -51,7 +51,7 @@ def test_file_conversion_matches_reference(tiny_config, tmp_path):
     assert set(sd) == set(LIT)
     for k, v in sd.items():
         np.testing.assert_array_equal(v.numpy(), LIT[k], err_msg=k)
-    # the converted tensors were spilled to memory-mapped files beside the output, removed after the save
+    # the converted tensors were written straight into the output zip: it is the only file written
     assert sorted(p.name for p in out.iterdir()) == ["lit-llama.pth"]
     with pytest.raises(ValueError):
         CV.convert_hf_checkpoint(output_dir=out, checkpoint_dir=ck, model_size="tinyhf", dtype="float33")
@@ -118,3 +118,80 @@ def test_meta_conversion_matches_reference(tmp_path):
     with pytest.raises(RuntimeError, match="No checkpoints"):
         CV.meta_weights_for_nano_model(output_dir=tmp_path / "lit", checkpoint_dir=tmp_path / "llama",
                                        model_size="missing")
+
+
+# ------------------------------------------------------------------ checkpoints the reference wrote
+REF_PTH = Path(__file__).parent / "golden" / "ref_lit_llama_bf16.pth"
+REF_SUM = np.load(Path(__file__).parent / "golden" / "ref_ckpt.npz")
+
+
+def _sha(t: torch.Tensor) -> str:
+    import hashlib
+
+    return hashlib.sha256(t.contiguous().view(torch.int16).numpy().tobytes()).hexdigest()
+
+
+def test_reference_incremental_save_file_reads_bitwise():
+    """A lit-llama.pth written by the reference's own converter (scripts/convert_hf_checkpoint.py:88
+    through its incremental_save, pickle protocol 5; tests/golden/make_golden.py gen_ref_ckpt) reads
+    through lazy_load / read_checkpoint with every tensor bit-identical to what the reference's
+    lazy_load returned (sha256 per tensor), while torch.load(weights_only=True) refuses it."""
+    from lit_llama.checkpoint import read_checkpoint
+    from lit_llama.utils import lazy_load
+
+    names = {k[4:] for k in REF_SUM.files if k.startswith("sha/")}
+    with lazy_load(REF_PTH) as sd:
+        assert set(sd) == names
+        for k, v in sd.items():
+            assert v.dtype == torch.bfloat16 and str(REF_SUM["dtype/" + k]) == "torch.bfloat16", k
+            assert tuple(v.shape) == tuple(REF_SUM["shape/" + k]), k
+            assert _sha(v) == str(REF_SUM["sha/" + k]), k
+    sd2 = read_checkpoint(REF_PTH)
+    assert torch.equal(sd2["lm_head.weight"].view(torch.int16), sd["lm_head.weight"].view(torch.int16))
+    import pickle
+
+    with pytest.raises(pickle.UnpicklingError):
+        torch.load(REF_PTH, weights_only=True)
+
+
+def test_lazy_load_refuses_code_in_a_checkpoint(tmp_path):
+    """A checkpoint whose pickle names anything but tensors, storages and OrderedDict is refused
+    before anything from it runs."""
+    import os
+    import pickle
+
+    from lit_llama.checkpoint import read_checkpoint
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("touch " + str(tmp_path / "pwned"),))
+
+    p = tmp_path / "evil.pth"
+    w = torch._C.PyTorchFileWriter(str(p))
+    data = pickle.dumps({"x": Evil()}, protocol=2)
+    w.write_record("data.pkl", data, len(data))
+    w.write_end_of_file()
+    with pytest.raises(pickle.UnpicklingError, match="posix.system|os.system|refused"):
+        read_checkpoint(p)
+    assert not (tmp_path / "pwned").exists()
+
+
+def test_incremental_save_roundtrip(tmp_path):
+    """incremental_save (the converters' writer): every dtype / a strided view / an empty tensor,
+    written one by one, read back equal by read_checkpoint and by torch.load(weights_only=True)."""
+    from lit_llama.checkpoint import incremental_save, read_checkpoint
+
+    base = torch.randn(8, 6)
+    tensors = {"f32": torch.randn(3, 5), "bf16": torch.randn(4, 4).to(torch.bfloat16),
+               "fp16": torch.randn(7).half(), "u8": torch.randint(0, 255, (5, 3), dtype=torch.uint8),
+               "i64": torch.arange(9), "view": base[2:6, 1:4], "empty": torch.empty(0, 3)}
+    with incremental_save(tmp_path / "o.pth") as saver:
+        saver.save({k: saver.store_early(v) for k, v in tensors.items()})
+    for sd in (read_checkpoint(tmp_path / "o.pth"), torch.load(tmp_path / "o.pth", weights_only=True)):
+        assert set(sd) == set(tensors)
+        for k, v in tensors.items():
+            assert sd[k].dtype == v.dtype and torch.equal(sd[k], v), k
+    with pytest.raises(RuntimeError):
+        with incremental_save(tmp_path / "p.pth") as saver:
+            saver.save({})
+            saver.save({})

@@ -935,3 +935,24 @@ def test_attention_prefill_flash(hip, hs, nh, B, T_, S, p0):
     torch.cuda.synchronize()
     # P is rounded to bf16 before the P.V MFMA (as flash kernels do): ~1 bf16 ulp on the weights
     assert_bf16_close(y.float().cpu().numpy(), _attn_oracle(q, kc, vc, pos, S, T_, nh, hs), "flash prefill", rel=2e-2)
+
+
+@pytest.mark.parametrize("scale_kind", ["fp32", "bf16"])
+def test_gemm_grouped_dequant_equals_get_weight_bf16(hip, scale_kind):
+    """The grouped-int4 prefill GEMM dequantizes every B fragment to the reference's
+    get_weight(bfloat16) value (quantization.py:390-409: (q - z) in bf16, times the scale in the
+    scale's precision, stored to bf16) bit for bit, with fp32 scales (the fp32 GPTQ calibration's)
+    as well as bf16 ones: an identity A makes the GEMM output the dequantized weight itself
+    (one nonzero product per output, exact in the fp32 accumulator)."""
+    rng = np.random.default_rng(11)
+    N, K, g = 256, 384, 128
+    qw, sc, z = rand_w4g(rng, N, K, g)
+    if scale_kind == "bf16":
+        sc = bf16(sc)
+    x = np.eye(K, dtype=np.float32)
+    out = torch.empty(K, N, dtype=torch.bfloat16, device=dev)
+    call(hip, "llj_gemm_linear", 4 | (1 << 8), T(x, torch.bfloat16).data_ptr(), K, repack(hip, qw).data_ptr(),
+         sz_grouped(hip, sc, z).data_ptr(), out.data_ptr(), N, K, N, K, st())
+    torch.cuda.synchronize()
+    wref = O.colblock_get_weight(qw, sc, z, 4, tile_cols=g, bf16=True)
+    np.testing.assert_array_equal(out.float().cpu().numpy().T, wref)

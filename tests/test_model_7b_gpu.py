@@ -1,20 +1,29 @@
-"""Every production kernel instantiation at the exact LLaMA-7B layer shapes (C = 4096, 32 heads
-of 128, n_hidden = 11008, vocab 32000; 2 layers so the numpy oracle stays fast), for the three
---quantize modes of BASELINE.json (gptq.int4 = C2, bf16 = C1, llm.int8 = C3) at batch 1 and 8:
-prefill + teacher-forced decode steps through LLaMA.forward against the oracle (bf16-emulating,
-oracle/llama_np.py) on the same weights. This is where the bs=1 M == 1 instantiations
-(gemv_kernel<W4, NORM, SWIGLU, 4, 4, 1, 1> etc.), the bs=8 multi-tile forms and the int8
-fused launches meet an independent check at their real shapes.
+"""Every production kernel instantiation at the exact LLaMA-7B and LLaMA-13B layer shapes (7B:
+C = 4096, 32 heads of 128, n_hidden = 11008; 13B: C = 5120, 40 heads of 128, n_hidden = 13824
+(reference lit_llama/model.py:52-53, 249-251); vocab 32000; 2 layers so the numpy oracle stays
+fast), for the --quantize modes of BASELINE.json (gptq.int4 = C2 / C4, bf16 = C1, llm.int8 = C3)
+at batch 1 and 8: prefill + teacher-forced decode steps through LLaMA.forward against the oracle
+(bf16-emulating, oracle/llama_np.py) on the same weights. This is where the bs=1 M == 1
+instantiations (gemv_kernel<W4, NORM, SWIGLU, 4, 4, 1, 1> etc.), the bs=8 multi-tile forms, the
+int8 fused launches and, with a 64-token prompt, the prefill GEMMs + flash attention meet an
+independent check at their real shapes.
 
 Tolerance (written here), per step and row: ||logits - oracle|| / ||oracle|| < REL[mode], and
 the argmax equals the oracle's wherever the oracle's top-1 / top-2 margin exceeds 4 % of
 max|logit|. The oracle rounds to bf16 at the reference's points (incl. every op of the bf16
-RMSNorm); what remains is fp32 summation order and 1-ulp flips that propagate through two
-layers of O(1) activations: measured on MI355X 0.6-1.0e-2 for bf16 / gptq.int4 -> REL 1.5e-2.
+RMSNorm); what remains is fp32 summation order and 1-ulp bf16 flips that propagate through two
+layers of O(1) activations. That is a floor no implementation can go under: the oracle against
+ITSELF with the Linears summed in another valid fp32 order (tools/noise_floor.py,
+profiles/r03_noise_floor.json) differs by the same order of magnitude as this path does, so
+north_star's 1e-3 is below what any bf16 implementation of the reference can meet here. REL is set
+at about twice that measured floor: gptq.int4 floor max 5.0e-3 (7B) / 6.2e-3 (13B) -> REL 1.2e-2,
+bf16 floor max 6.4e-3 -> REL 1.3e-2 (7B decode measured 6.4-9.3e-3 on MI355X in round 2).
 llm.int8 re-quantizes every Linear's input to int8 per row, which turns those flips into
 whole-step differences of the int8 codes (a 0.3 % input difference moves ~10 % of the codes by
-one step of absmax/127): measured 2.8-3.2e-2 -> REL 5e-2. The int8 kernels themselves are held to
-a tight bound on identical inputs in tests/test_kernels_gpu.py::test_int8_fused_ops_7b_shapes."""
+one step of absmax/127): the order-only floor is 1.2e-2 (max), and the GPU's own fp32 rounding of
+the activation quantization adds flips of the same kind (measured 2.8-3.2e-2) -> REL 5e-2. The int8
+kernels themselves are held to a tight bound on identical inputs in
+tests/test_kernels_gpu.py::test_int8_fused_ops_7b_shapes."""
 import numpy as np
 import pytest
 import torch
@@ -25,17 +34,21 @@ from tests.helpers import bf16
 
 pytestmark = pytest.mark.gpu
 
-C7 = Cfg(block_size=64, n_layer=2, n_head=32, n_embd=4096, vocab_size=32000)
-REL = {"gptq.int4": 1.5e-2, None: 1.5e-2, "llm.int8": 5e-2}
+C7 = Cfg(block_size=128, n_layer=2, n_head=32, n_embd=4096, vocab_size=32000)
+C13 = Cfg(block_size=128, n_layer=2, n_head=40, n_embd=5120, vocab_size=32000)
+SEEDS = {4096: 4096, 5120: 5120}
+REL = {"gptq.int4": 1.2e-2, None: 1.3e-2, "llm.int8": 5e-2}
 T_PROMPT, STEPS, S = 6, 4, 32
 _cache = {}
 
 
-def _params():
-    if "p" not in _cache:
-        _cache["p"] = make_params(C7, 4096)
-    _cache.setdefault("order", 0)
-    return _cache["p"]
+def _params(cfg: Cfg):
+    key = ("p", cfg.n_embd)
+    if key not in _cache:
+        for k in [k for k in _cache if k[0] == "p"]:  # one width's weights at a time (13B: 2.6 GB fp32)
+            del _cache[k]
+        _cache[key] = make_params(cfg, SEEDS[cfg.n_embd])
+    return _cache[key]
 
 
 def _quant4(w):
@@ -50,12 +63,8 @@ def _quant4(w):
     return qw, sc, z
 
 
-def _setup(mode):
-    """(model, oracle) for `mode` on the shared 7B-width weights."""
-    from lit_llama import LLaMA, LLaMAConfig
-    from lit_llama.utils import EmptyInitOnDevice
-
-    p = _params()
+def oracle_linears(p: dict, mode):
+    """(state dict for the module, oracle Linear specs) of `mode` on the fp32 weights `p`."""
     pb = {k: bf16(v) for k, v in p.items()}
     lin, sd = {}, dict(pb)
     for k, v in p.items():
@@ -70,55 +79,103 @@ def _setup(mode):
         elif mode == "llm.int8":
             cb, scb = O.int8_quantize_weight(pb[k])
             lin[name] = O.LinearSpec("int8", cb=cb, scb=scb)
+    return pb, sd, lin
+
+
+def _setup(cfg: Cfg, mode):
+    """(model, oracle) for `mode` on the shared weights of this width."""
+    from lit_llama import LLaMA, LLaMAConfig
+    from lit_llama.utils import EmptyInitOnDevice
+
+    pb, sd, lin = oracle_linears(_params(cfg), mode)
     with EmptyInitOnDevice(device=torch.device("cuda"), dtype=torch.bfloat16, quantization_mode=mode):
-        m = LLaMA(LLaMAConfig(block_size=C7.block_size, vocab_size=C7.vocab_size, n_layer=C7.n_layer,
-                              n_head=C7.n_head, n_embd=C7.n_embd))
+        m = LLaMA(LLaMAConfig(block_size=cfg.block_size, vocab_size=cfg.vocab_size, n_layer=cfg.n_layer,
+                              n_head=cfg.n_head, n_embd=cfg.n_embd))
     m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()})
-    orc = O.OracleLLaMA(C7, pb, linears=lin, act_bf16=True)
+    orc = O.OracleLLaMA(cfg, pb, linears=lin, act_bf16=True)
     return m.eval(), orc
 
 
-def _gpu_steps(model, ids):
+def _get(cfg, mode):
+    key = ("setup", cfg.n_embd, mode)
+    if key not in _cache:  # one model + oracle kept at a time
+        for k in [k for k in _cache if k[0] == "setup"]:
+            del _cache[k]
+        torch.cuda.empty_cache()
+        _cache[key] = _setup(cfg, mode)
+    return _cache[key]
+
+
+def _gpu_steps(model, ids, t_prompt=T_PROMPT, steps=STEPS, s=S, all_rows=False):
     B = ids.shape[0]
     x = torch.from_numpy(ids).cuda().long()
     model.reset_cache()
-    outs = [model(x[:, :T_PROMPT], S, torch.arange(T_PROMPT).cuda())[:, -1].float()]
-    for p in range(T_PROMPT, T_PROMPT + STEPS):
-        outs.append(model(x[:, p:p + 1], S, torch.tensor([p]).cuda())[:, -1].float())
+    first = model(x[:, :t_prompt], s, torch.arange(t_prompt).cuda()).float()
+    outs = [first[:, -1]]
+    for p in range(t_prompt, t_prompt + steps):
+        outs.append(model(x[:, p:p + 1], s, torch.tensor([p]).cuda())[:, -1].float())
     model.reset_cache()
-    return torch.stack(outs, 1).cpu().numpy()  # (B, steps + 1, V)
+    res = torch.stack(outs, 1).cpu().numpy()  # (B, steps + 1, V)
+    return (res, first.cpu().numpy()) if all_rows else res
 
 
-def _oracle_steps(orc, ids):
+def _oracle_steps(orc, ids, t_prompt=T_PROMPT, steps=STEPS, s=S, all_rows=False):
     orc.reset_cache()
-    outs = [orc.forward(ids[:, :T_PROMPT], S, np.arange(T_PROMPT))[:, -1]]
-    for p in range(T_PROMPT, T_PROMPT + STEPS):
-        outs.append(orc.forward(ids[:, p:p + 1], S, np.array([p]))[:, -1])
+    first = orc.forward(ids[:, :t_prompt], s, np.arange(t_prompt))
+    outs = [first[:, -1]]
+    for p in range(t_prompt, t_prompt + steps):
+        outs.append(orc.forward(ids[:, p:p + 1], s, np.array([p]))[:, -1])
     orc.reset_cache()
-    return np.stack(outs, 1)
+    res = np.stack(outs, 1)
+    return (res, first) if all_rows else res
+
+
+def _check(got, ref, rel_max, what):
+    B, n = got.shape[:2]
+    rels = [float(np.linalg.norm(got[b, s] - ref[b, s]) / np.linalg.norm(ref[b, s])) for b in range(B) for s in range(n)]
+    print(f"[{what}] rel err max {max(rels):.3e} mean {np.mean(rels):.3e}")
+    for b in range(B):
+        for s in range(n):
+            g, r = got[b, s], ref[b, s]
+            rel = float(np.linalg.norm(g - r) / np.linalg.norm(r))
+            assert rel < rel_max, f"{what} row {b} step {s}: rel err {rel:.3e}"
+            top2 = np.sort(r)[-2:]
+            if top2[1] - top2[0] > 4e-2 * np.abs(r).max():
+                assert int(g.argmax()) == int(r.argmax()), f"{what} row {b} step {s}: argmax"
+    return max(rels)
 
 
 @pytest.mark.parametrize("B", [1, 2, 8])  # 2: the batched RMSNorm hand-off (nstat)
 @pytest.mark.parametrize("mode", ["gptq.int4", None, "llm.int8"])
 def test_7b_width_decode_vs_oracle(mode, B):
-    key = ("setup", mode)
-    if key not in _cache:  # one mode's model + oracle kept at a time
-        for k in [k for k in _cache if k[0] == "setup"]:
-            del _cache[k]
-        torch.cuda.empty_cache()
-        _cache[key] = _setup(mode)
-    model, orc = _cache[key]
+    model, orc = _get(C7, mode)
     ids = np.random.default_rng(B + 17).integers(3, C7.vocab_size, (B, T_PROMPT + STEPS + 1))
-    got = _gpu_steps(model, ids)
-    ref = _oracle_steps(orc, ids)
-    rels = [float(np.linalg.norm(got[b, s] - ref[b, s]) / np.linalg.norm(ref[b, s]))
-            for b in range(B) for s in range(STEPS + 1)]
-    print(f"[7b] {mode} B={B} rel err max {max(rels):.3e} mean {np.mean(rels):.3e}")
-    for b in range(B):
-        for s in range(STEPS + 1):
-            g, r = got[b, s], ref[b, s]
-            rel = float(np.linalg.norm(g - r) / np.linalg.norm(r))
-            assert rel < REL[mode], f"{mode} B={B} row {b} step {s}: rel err {rel:.3e}"
-            top2 = np.sort(r)[-2:]
-            if top2[1] - top2[0] > 4e-2 * np.abs(r).max():
-                assert int(g.argmax()) == int(r.argmax()), f"{mode} B={B} row {b} step {s}: argmax"
+    _check(_gpu_steps(model, ids), _oracle_steps(orc, ids), REL[mode], f"7b {mode} B={B}")
+
+
+@pytest.mark.parametrize("B", [1, 8])
+def test_13b_width_decode_vs_oracle(B):
+    """C4's shapes (LLaMA-13B gptq.int4, reference model.py:53): every M = 1 and batched
+    instantiation at C = 5120, n_hidden = 13824, 40 heads (QKV N = 15360, K = 5120; SwiGLU
+    13824 x 5120; mlp.c_proj K = 13824 on the eight-wave residual form; 40-head attention)."""
+    model, orc = _get(C13, "gptq.int4")
+    ids = np.random.default_rng(B + 31).integers(3, C13.vocab_size, (B, T_PROMPT + STEPS + 1))
+    _check(_gpu_steps(model, ids), _oracle_steps(orc, ids), REL["gptq.int4"], f"13b gptq.int4 B={B}")
+
+
+@pytest.mark.parametrize("mode", ["gptq.int4", None])
+def test_7b_width_prefill_gemm_flash_vs_oracle(mode):
+    """A 64-token prompt at 7B width through LLaMA.forward takes the prefill path (>= GEMM_MIN_ROWS
+    rows: rmsnorm_rows -> MFMA GEMM QKV + RoPE + KV write -> flash attention -> GEMM residual ->
+    GEMM SwiGLU (two passes) -> GEMM residual, lm_head GEMM): every prompt row's logits against the
+    oracle, then decode steps from the caches it wrote."""
+    from lit_llama import model as MD
+
+    t = 64
+    assert t >= MD.GEMM_MIN_ROWS and t >= MD.FLASH_MIN_T
+    model, orc = _get(C7, mode)
+    ids = np.random.default_rng(64).integers(3, C7.vocab_size, (1, t + 3))
+    got, got_rows = _gpu_steps(model, ids, t_prompt=t, steps=2, s=96, all_rows=True)
+    ref, ref_rows = _oracle_steps(orc, ids, t_prompt=t, steps=2, s=96, all_rows=True)
+    _check(got_rows, ref_rows, REL[mode], f"7b prefill {mode} rows")
+    _check(got, ref, REL[mode], f"7b prefill {mode} steps")

@@ -73,3 +73,21 @@ def test_bench_spawns_its_own_replicas():
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["stub"] is True and line["steps"] == 3
     assert line["value"] > 0
+
+
+def test_bench_replica_failure_stops_siblings():
+    """One replica dying (here rank 1 exits 3 before the barrier) must not leave rank 0 blocked in
+    the gloo barrier until the driver's time limit: the launcher polls every child, terminates the
+    others on the first non-zero exit and returns that exit code (advisor finding, round 2)."""
+    import subprocess
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    t0 = time.monotonic()
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--stub", "--stub-fail-rank", "1",
+                          "--steps", "3", "--warmup", "1"], env=env, capture_output=True, text=True, timeout=240)
+    took = time.monotonic() - t0
+    assert out.returncode == 3, (out.returncode, out.stderr[-2000:])
+    assert "stopping the others" in out.stderr
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert took < 120, took  # gloo's own barrier timeout is 30 min
