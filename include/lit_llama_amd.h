@@ -218,6 +218,48 @@ int llj_argmax(const void* logits, int ldl, int M, int V, int* out_idx, int* tok
 int llj_sample(const void* logits, int ldl, int M, int V, float temperature, int top_k, const float* u,
                unsigned long long seed, int* out_idx, int* tokens_out, int tok_stride, const int* pos, void* stream);
 
+/* ---------------------------------------------------------------- persistent decode engine
+ * One launch per decode token (batch 1, every Linear int4 W4P with per-row (scale, zero); head
+ * size 64 / 128): the whole of LLaMA.forward for the token at position *pos + 1 (model.py:84-128)
+ * plus, with flags bit 0, the greedy next-token choice (generate.py:66-74, top_k = 1). Weights
+ * stream through an LDS ring by LDS-DMA across op boundaries; op outputs travel between CUs as
+ * 8-byte {tag, data} granules in `arena` (csrc/engine.hip). Same results as the launch chain
+ * (llj_embedding + the fused ops + llj_norm_linear + llj_argmax) up to fp32 summation order.
+ * At the end of a step: logits (V bf16) written, *pos advanced by one; greedy: *cur = next token and
+ * tokens[*pos + 1] = next (tokens may be NULL). The plan is passed by host pointer and copied into
+ * the launch (graph-capturable); every pointer inside it is a device pointer. `arena` holds
+ * llj_engine_arena_bytes(C, H) bytes, zeroed once before the first step; its control words carry
+ * an error bit (word 2 of the 16 behind the granules) that a step sets on a timed-out wait. */
+#define LLJ_ENGINE_MAX_CUS 1024
+typedef struct llj_engine_layer {
+  const void* w_qkv; const void* sz_qkv;   /* attn.c_attn: W4P codes, (scale, 128 + zero) fp32 pairs */
+  const void* w_o; const void* sz_o;       /* attn.c_proj */
+  const void* w_fc1; const void* sz_fc1;   /* mlp.c_fc1 */
+  const void* w_fc2; const void* sz_fc2;   /* mlp.c_fc2 */
+  const void* w_down; const void* sz_down; /* mlp.c_proj */
+  const void* rms1; const void* rms2;      /* RMSNorm scales, bf16 (C) */
+  void* kcache; void* vcache;              /* bf16 (1, n_head, S, head_size), slot p % S */
+  float eps1, eps2;
+} llj_engine_layer;
+typedef struct llj_engine_plan {
+  const llj_engine_layer* layers;          /* device array of n_layer entries */
+  int n_layer, C, H, V, n_head, S;         /* V: lm_head rows (padded vocab), < 65536 */
+  const void* wte;                         /* bf16 (V, C) embedding */
+  const void* ln_f; float eps_f;           /* bf16 (C) */
+  const void* w_head; const void* sz_head; /* lm_head W4P + pairs */
+  const float* rope;                       /* (block_size, hs / 2, 2) fp32 */
+  int* pos; int* cur; int* tokens;         /* device step state (int32) */
+  void* logits;                            /* bf16 (V) */
+  void* arena;
+  int flags;                               /* bit 0: greedy token choice inside the step */
+  int grid;                                /* workgroups (0 = every CU) */
+  int ring_blocks;                         /* LDS ring slots (1 KiB), <= llj_engine_ring_blocks() */
+  unsigned long long* trace;               /* profiling only: NULL, or grid x 128 phase stamps (s_memrealtime) */
+} llj_engine_plan;
+size_t llj_engine_arena_bytes(int C, int H);
+int llj_engine_ring_blocks(int C, int H, int n_head);
+int llj_engine_step(const llj_engine_plan* plan, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,911 @@
+// Persistent decode engine: ONE launch per decode token for batch 1 with int4 (W4P) weights.
+//
+// Replaces, for a whole decode step, the launch chain of LLaMA.forward (reference
+// lit_llama/model.py:84-128: embedding, n_layer x Block.forward 162-175 = rms_1 + c_attn + RoPE +
+// KV write + SDPA + c_proj + residual, rms_2 + c_fc1/c_fc2 + silu*mul + c_proj + residual, then
+// ln_f + lm_head) and the greedy next-token choice of generate.py:66-74 (top_k = 1).
+//
+// Why: a launch boundary costs 1.2-1.9 us and every launch re-ramps its weight stream behind the
+// activation it waits for. Here the weight stream never stops at an op edge
+// (MI355X_MICROARCH.md price list: ldsdma-fill, prefetch-credit, allgather, engine-vs-launches):
+//  * grid = one 256-thread workgroup per CU, resident for the whole step (LDS > half a CU).
+//  * wave 3 of every workgroup is a LOADER: it streams this CU's weight blocks (1 KiB W4P tiles =
+//    16 columns x 128 k) into an LDS ring by LDS-DMA (global_load_lds_dwordx4 ... nt) in the order
+//    the CU consumes them, across op and layer boundaries -- weights do not depend on
+//    activations, so the next op's blocks land while the consumers wait for that op's input. It
+//    publishes `landed` (blocks in LDS) and waits on the consumers' `freed` counts before reusing a
+//    slot. Its DMAs never sit in a consumer's vmcnt queue.
+//  * waves 0-2 CONSUME: block b of the CU stream goes to wave b % 3 (bf16 MFMA 16x16x32 on the
+//    dequantized codes, as the GEMVs), partial sums meet in LDS, one wave runs each tile's epilogue.
+//    They synchronise through an LDS counter barrier (the loader never joins a barrier).
+//  * op outputs travel between CUs as 8-byte {tag, payload} granules written by one agent-scope
+//    (sc1) store each and read by sc1 polling loads: the data is its own flag, no fence, no grid
+//    barrier. tag = epoch * 128 + layer + 1 (epoch advanced on the device once per step), never 0.
+//  * each op's tiles are dealt round-robin over the CUs (tile t on CU t % G).
+// Per layer: gather x -> rms_1 -> QKV tiles (RoPE, KV-cache write, publish q/k/v) -> attention of
+// head h on CU h * (G / n_head) (gathers its q/k/v, reads the cache rows of earlier positions) ->
+// gather y -> c_proj tile + residual (publish x_mid) -> gather x_mid -> rms_2 -> SwiGLU tiles
+// (publish h) -> gather h -> down tile + residual (publish x). After the last layer: ln_f +
+// lm_head tiles (logits to HBM, per-CU argmax publish); the last CU to arrive picks the token,
+// writes it and advances the device position and the epoch.
+// Numerics follow the GEMV path (gemv_impl.h): bf16 rounding points of the reference, int4 offset
+// removed with the row sum of the normalized input, RoPE / softmax in fp32.
+// Every spin is bounded (kSpinTicks from the step's start); a timeout sets ctl[2] and turns every
+// later wait into a pass-through, so a faulty step still terminates (the host checks ctl[2]).
+#include "common.h"
+#include "lit_llama_amd.h"
+
+namespace llj {
+namespace eng {
+
+#ifndef LLJ_ENG_NC
+#define LLJ_ENG_NC 7       // consumer waves
+#endif
+constexpr int NWV = LLJ_ENG_NC + 1;  // waves per workgroup (two per SIMD at 8)
+constexpr int NC = LLJ_ENG_NC;  // consumer waves (0 .. NC-1); wave NC is the loader
+static_assert(NC >= 3 && NC <= 15, "consumer waves");
+constexpr int NTH = 64 * NWV;
+constexpr int TG = 4;      // tiles per partial-sum group (accumulators per wave: TG x 2 matrices)
+#ifndef LLJ_ENG_D
+#define LLJ_ENG_D 48       // DMAs the loader keeps in flight (vmcnt immediate)
+#endif
+constexpr int D = LLJ_ENG_D;
+static_assert(D >= 1 && D <= 62, "vmcnt immediate");
+constexpr int GKC = 16;    // granules per lane per gather batch of a C-sized vector (x, y, x_mid)
+constexpr int GKH = 32;    // ... of the SwiGLU output h
+constexpr int GN = 22;     // RMSNorm gain pairs per lane (C / 2 <= GN * 64 * NC: C <= 8448)
+constexpr unsigned long long kSpinTicks = 5000000ull;  // 50 ms of s_memrealtime (100 MHz)
+constexpr int kMaxCUs = LLJ_ENGINE_MAX_CUS;
+
+enum : int { OP_QKV = 0, OP_O = 1, OP_SW = 2, OP_DOWN = 3, OP_HEAD = 4, OP_END = 5 };
+enum : unsigned { ERR_TIMEOUT = 1u };
+
+// granule arena (u64 units) and the control words behind it
+struct Arena {
+  unsigned long long *gx, *gqkv, *gy, *gxm, *gh, *garg;
+  unsigned* ctl;  // [0] epoch, [1] end-of-step arrivals, [2] error bits
+};
+__host__ __device__ inline size_t arena_granules(int C, int H) {
+  return (size_t)3 * (C / 2) + (size_t)3 * C / 2 + (size_t)H / 2 + (size_t)kMaxCUs;  // x, y, x_mid | qkv | h | argmax
+}
+__device__ inline Arena arena_of(const llj_engine_plan& P) {
+  Arena a;
+  unsigned long long* b = reinterpret_cast<unsigned long long*>(P.arena);
+  const int C = P.C, H = P.H;
+  a.gx = b;
+  a.gqkv = a.gx + C / 2;
+  a.gy = a.gqkv + 3 * C / 2;
+  a.gxm = a.gy + C / 2;
+  a.gh = a.gxm + C / 2;
+  a.garg = a.gh + H / 2;
+  a.ctl = reinterpret_cast<unsigned*>(a.garg + kMaxCUs);
+  return a;
+}
+
+__device__ __forceinline__ unsigned long long ld_gran(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load_dwordx2 sc1
+}
+__device__ __forceinline__ void st_gran(unsigned long long* p, unsigned tag, uint32_t v) {
+  __hip_atomic_store(p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// LDS-DMA of one 16-byte piece per lane into LDS byte address lds (wave-uniform) + 16 * lane,
+// non-temporal (weights are read once per step). Invisible to the compiler's wait counting: the
+// loader counts its own DMAs (wait_vm). Its LDS reads are done first (lgkmcnt(0)).
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds)
+               : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ unsigned lds_ld(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void lds_st(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+__device__ __forceinline__ bf16x8 dequant(uint32_t w, uint32_t msk, uint32_t mag) {
+  uint4 b = make_uint4(and_or(w, msk, mag), and_or(w >> 4, msk, mag), and_or(w >> 8, msk, mag), and_or(w >> 12, msk, mag));
+  return __builtin_bit_cast(bf16x8, b);
+}
+__device__ __forceinline__ float rstd_bf16(float ss_over_k, float eps) {
+  return round_bf(rsqrtf(round_bf(round_bf(ss_over_k) + eps)));  // model.py:281-282 on bf16 tensors
+}
+__device__ __forceinline__ uint32_t bf_key(uint32_t b) { return (b & 0x8000u) ? (~b & 0xFFFFu) : (b | 0x8000u); }
+
+// profiling stamps (plan.trace != NULL): [g][128]; consumers: 0 start, per layer l at 2 + 12 l:
+// +0 x staged, +1 QKV done, +2 attention done, +3 y staged, +4 c_proj done, +5 x_mid staged,
+// +6 SwiGLU done, +7 h staged, +8 down done; the loader: 100 + op index of its last DMA of each op
+// (per layer, layers 0..1 only: 100..107), 120 stream end; 126 head staged, 127 head done
+__device__ __forceinline__ void stamp(const llj_engine_plan& P, int lane, int k) {
+  if (P.trace && lane == 0 && k < 128) P.trace[(size_t)blockIdx.x * 128 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// a pointer loaded by a vector load, moved to SGPRs: the compiler waits for the load HERE (once),
+// not at its first use inside a DMA loop, where that wait would also drain every DMA in flight
+__device__ __forceinline__ const char* sgpr_ptr(const char* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const char*>(((uint64_t)hi << 32) | lo);
+}
+
+// ------------------------------------------------------------------------------------ schedule
+struct Shape {
+  int C, H, V, nh, hs, S, L, G, g;
+};
+__device__ __forceinline__ int op_ntiles(const Shape& s, int op) {
+  return op == OP_QKV ? 3 * s.C / 16 : op == OP_SW ? s.H / 16 : op == OP_HEAD ? s.V / 16 : s.C / 16;
+}
+__device__ __forceinline__ int op_kc(const Shape& s, int op) { return (op == OP_DOWN ? s.H : s.C) >> 7; }
+__device__ __forceinline__ int op_nmat(int op) { return op == OP_SW ? 2 : 1; }
+__device__ __forceinline__ int tiles_of_cu(const Shape& s, int op) {
+  const int n = op_ntiles(s, op);
+  return s.g < n ? (n - s.g + s.G - 1) / s.G : 0;
+}
+__device__ __forceinline__ int op_blocks(const Shape& s, int op) { return tiles_of_cu(s, op) * op_kc(s, op) * op_nmat(op); }
+__device__ __forceinline__ const char* op_weight(const llj_engine_plan& P, int l, int op, int m) {
+  if (op == OP_HEAD) return reinterpret_cast<const char*>(P.w_head);
+  const llj_engine_layer& Ly = P.layers[l];
+  const void* w = op == OP_QKV ? Ly.w_qkv : op == OP_O ? Ly.w_o : op == OP_SW ? (m ? Ly.w_fc2 : Ly.w_fc1) : Ly.w_down;
+  return reinterpret_cast<const char*>(w);
+}
+
+// ------------------------------------------------------------------------------------ LDS
+// carve (bytes, 16-aligned): ctl words | A (max(C, H) bf16) | xres[2] (C bf16) | red[2][NC][TG][2][16]
+// f32 | eop[2] (epilogue operands) | misc[64] f32 ([0, NC) sums of squares, [16, 16 + NC) row sums,
+// [32, 32 + NC) argmax, [48] last-arriver flag) | attention scratch | ring (nb x 1 KiB)
+constexpr int kCtlWords = 32;  // [0] landed, [1 .. NC] freed per consumer, [16] consumer barrier
+struct Lds {
+  unsigned* ctl;
+  unsigned char* ring;
+  bf16_t* A;
+  bf16_t* xres[2];
+  float* red;
+  float2* eop;  // [2][kEopTiles][2][16]
+  float* misc;
+  float* att;
+  int nb;
+};
+__host__ __device__ inline size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
+// epilogue operands staged per op: (scale, 128 + zero) of both matrices for every tile of the CU
+// (at most kEopTiles), or the RoPE (cos, sin) pairs of the QKV tiles
+constexpr int kEopTiles = 16;
+__host__ __device__ inline size_t lds_fixed(int C, int H, int hs) {
+  const int K = C > H ? C : H;
+  return (size_t)kCtlWords * 4 + al16((size_t)K * 2) + 2 * al16((size_t)C * 2) + (size_t)2 * NC * TG * 2 * 16 * 4 +
+         (size_t)2 * kEopTiles * 2 * 16 * 8 + 64 * 4 + al16((size_t)(3 * hs + 2 * NC + NC * hs) * 4);
+}
+// ring blocks that fit next to the fixed part in `budget` bytes
+__host__ __device__ inline int ring_blocks(int C, int H, int hs, size_t budget) {
+  const size_t f = lds_fixed(C, H, hs);
+  return f >= budget ? 0 : (int)((budget - f) / 1024);
+}
+
+// ------------------------------------------------------------------------------------ state
+struct Ctx {
+  Shape s;
+  int wave, lane;
+  unsigned* gctl;     // global control words
+  unsigned long long t0;
+  bool aborted;
+  unsigned bar_gen;   // consumer barriers passed
+  int n_used;         // CU-stream index of the next block of this op (consumers)
+};
+
+// bounded spin bookkeeping: true = give up (a timeout here or anywhere in the grid). Global polls
+// sleep a little between passes; LDS spins only look at the clock every 256 passes.
+__device__ __forceinline__ bool spin_timeout(unsigned* gctl, unsigned long long t0, int lane) {
+  const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+  if (now - t0 > kSpinTicks || __hip_atomic_load(gctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+    if (lane == 0) __hip_atomic_fetch_or(gctl + 2, ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  }
+  return false;
+}
+__device__ __forceinline__ bool spin_check(Ctx& X) {
+  if (spin_timeout(X.gctl, X.t0, X.lane)) X.aborted = true;
+  return X.aborted;
+}
+__device__ __forceinline__ bool spin_fail(Ctx& X, unsigned& it) {
+  if (X.aborted) return true;
+  __builtin_amdgcn_s_sleep(1);
+  return (++it & 15u) == 0u && spin_check(X);
+}
+__device__ __forceinline__ bool spin_fail_lds(Ctx& X, unsigned& it) {
+  if (X.aborted) return true;
+  return (++it & 255u) == 0u && spin_check(X);
+}
+
+// barrier of the NC consumer waves (an LDS counter: the loader wave never takes part)
+__device__ __forceinline__ void cbarrier(Ctx& X, const Lds& L) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes are done
+  if (X.lane == 0) __hip_atomic_fetch_add(L.ctl + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const unsigned target = (X.bar_gen + 1) * NC;
+  unsigned it = 0;
+  while (lds_ld(L.ctl + 16) < target) {
+    if (spin_fail_lds(X, it)) break;
+  }
+  ++X.bar_gen;
+}
+
+// Gather granules [0, n) of `g` tagged `tag`: consumer wave w takes indices lane + 64 (w + NC k);
+// every load of a batch of GK per lane is in flight before any tag is checked; a batch is re-read
+// until every tag matches. sink(idx, payload) for each.
+template <int GK, typename F>
+__device__ __forceinline__ void gather(Ctx& X, const unsigned long long* g, int n, unsigned tag, F&& sink) {
+  const int first = X.lane + 64 * X.wave;
+  constexpr int STEP = 64 * NC;
+  for (int b0 = 0; b0 < n; b0 += STEP * GK) {
+    unsigned long long v[GK];
+    unsigned it = 0;
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < GK; ++k) {
+        const int idx = b0 + first + STEP * k;
+        v[k] = ld_gran(g + (idx < n ? idx : 0));
+      }
+#pragma unroll
+      for (int k = 0; k < GK; ++k) {
+        const int idx = b0 + first + STEP * k;
+        ok &= idx >= n || (unsigned)(v[k] >> 32) == tag;
+      }
+      if (__all(ok)) break;
+      if (spin_fail(X, it)) break;
+    }
+#pragma unroll
+    for (int k = 0; k < GK; ++k) {
+      const int idx = b0 + first + STEP * k;
+      if (idx < n) sink(idx, (uint32_t)v[k]);
+    }
+  }
+}
+
+// Stage the epilogue operands of op into eop (one of two LDS buffers, alternating per op: the
+// previous op's epilogue may still read the other): per tile slot j (< kEopTiles) and matrix m, the
+// (scale, 128 + zero) of column 16 tile + c at eop[(j * 2 + m) * 16 + c]. Loaded by the consumers
+// ahead of the gather they are about to wait in, so the epilogue reads LDS only.
+__device__ __forceinline__ void stage_sz(Ctx& X, float2* eop, const llj_engine_plan& P, int l, int op) {
+  const Shape& s = X.s;
+  const int nt = tiles_of_cu(s, op) < kEopTiles ? tiles_of_cu(s, op) : kEopTiles;
+  const int nm = op_nmat(op);
+  const llj_engine_layer* Ly = op == OP_HEAD ? nullptr : &P.layers[l];
+  for (int i = X.lane + 64 * X.wave; i < nt * nm * 16; i += 64 * NC) {
+    const int c = i & 15, m = (i >> 4) % nm, j = (i >> 4) / nm;
+    const float2* sz = op == OP_HEAD ? reinterpret_cast<const float2*>(P.sz_head)
+                       : op == OP_QKV ? reinterpret_cast<const float2*>(Ly->sz_qkv)
+                       : op == OP_O   ? reinterpret_cast<const float2*>(Ly->sz_o)
+                       : op == OP_SW  ? reinterpret_cast<const float2*>(m ? Ly->sz_fc2 : Ly->sz_fc1)
+                                      : reinterpret_cast<const float2*>(Ly->sz_down);
+    eop[(j * 2 + m) * 16 + c] = sz[16 * (s.g + j * s.G) + c];
+  }
+}
+
+// input of a norm-fused op: x (gathered, or the embedding row at layer 0) -> xres[buf] raw and
+// A = RMSNorm(x) * gain (model.py:276-283, bf16 rounding points); returns sum_k A[k]
+__device__ __forceinline__ float stage_norm(Ctx& X, const Lds& L, int buf, const unsigned long long* g, unsigned tag,
+                            const bf16_t* direct, const bf16_t* gain, float eps, int C) {
+  uint32_t* xr2 = reinterpret_cast<uint32_t*>(L.xres[buf]);
+  const uint32_t* g2 = reinterpret_cast<const uint32_t*>(gain);
+  // this wave's gain pairs, loaded before the wait (C / 2 / (64 NC) <= GN per lane)
+  uint32_t gv[GN];
+#pragma unroll
+  for (int k = 0; k < GN; ++k) {
+    const int idx = X.lane + 64 * X.wave + 64 * NC * k;
+    gv[k] = g2[idx < C / 2 ? idx : 0];
+  }
+  float ss = 0.f;
+  auto sink = [&](int idx, uint32_t v) {
+    xr2[idx] = v;
+    const f32x2 f = unpk(v);
+    ss += round_bf(f.x * f.x) + round_bf(f.y * f.y);  // model.py:281: x * x in bf16
+  };
+  if (direct) {  // layer 0: the embedding row wte[cur] (model.py:110), read by every CU
+    const uint32_t* d2 = reinterpret_cast<const uint32_t*>(direct);
+    for (int idx = X.lane + 64 * X.wave; idx < C / 2; idx += 64 * NC) sink(idx, d2[idx]);
+  } else {
+    gather<GKC>(X, g, C / 2, tag, sink);
+  }
+  ss = wave_sum(ss);
+  if (X.lane == 0) L.misc[X.wave] = ss;
+  cbarrier(X, L);
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < NC; ++w) tot += L.misc[w];
+  const float r = rstd_bf16(tot / (float)C, eps);
+  uint32_t* a2 = reinterpret_cast<uint32_t*>(L.A);
+  float asum = 0.f;
+#pragma unroll
+  for (int k = 0; k < GN; ++k) {
+    const int idx = X.lane + 64 * X.wave + 64 * NC * k;
+    if (idx < C / 2) {
+      const uint32_t o = norm_pair(xr2[idx], gv[k], r);
+      a2[idx] = o;
+      asum += bflo(o) + bfhi(o);
+    }
+  }
+  asum = wave_sum(asum);
+  if (X.lane == 0) L.misc[16 + X.wave] = asum;
+  cbarrier(X, L);
+  float a = 0.f;
+#pragma unroll
+  for (int w = 0; w < NC; ++w) a += L.misc[16 + w];
+  return a;
+}
+// input of a plain op: gathered vector -> A; returns sum_k A[k]
+template <int GK>
+__device__ __forceinline__ float stage_plain(Ctx& X, const Lds& L, const unsigned long long* g, unsigned tag, int K) {
+  uint32_t* a2 = reinterpret_cast<uint32_t*>(L.A);
+  float asum = 0.f;
+  gather<GK>(X, g, K / 2, tag, [&](int idx, uint32_t v) {
+    a2[idx] = v;
+    asum += bflo(v) + bfhi(v);
+  });
+  asum = wave_sum(asum);
+  if (X.lane == 0) L.misc[16 + X.wave] = asum;
+  cbarrier(X, L);
+  float a = 0.f;
+#pragma unroll
+  for (int w = 0; w < NC; ++w) a += L.misc[16 + w];
+  return a;
+}
+
+// Consume this CU's blocks of `op` (its tiles x chunks x matrices, in stream order, block b on
+// consumer b % NC), TG tiles per partial-sum group; epi(slot, tile, n, y1, y2) runs on lanes 0..15
+// (column 16 tile + lane) of consumer (slot % NC) with the fp32 outputs of both matrices (int4
+// offset removed).
+template <typename E>
+__device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop, int op, float asum, int& red_par, E&& epi) {
+  const Shape& s = X.s;
+  const int nt = tiles_of_cu(s, op), kc = op_kc(s, op), nm = op_nmat(op);
+  const int per_tile = kc * nm;
+  const int lane = X.lane, grp = lane >> 4;
+  uint32_t msk = 0x000F000Fu, mag = 0x43004300u;  // bf16 128 + q via one v_and_or_b32 per pair
+  asm volatile("" : "+s"(msk));
+  asm volatile("" : "+v"(mag));
+  const int base = X.n_used;  // CU-stream index of this op's first block
+  for (int j0 = 0; j0 < nt; j0 += TG) {
+    const int ng = nt - j0 < TG ? nt - j0 : TG;
+    f32x4 acc[TG][2];
+#pragma unroll
+    for (int a = 0; a < TG; ++a) acc[a][0] = acc[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int jj = 0; jj < TG; ++jj) {
+      if (jj >= ng) break;
+      const int t_lo = base + (j0 + jj) * per_tile, t_hi = t_lo + per_tile;
+      int b = t_lo + ((X.wave - t_lo % NC) + NC) % NC;  // this consumer's first block of the tile
+      int slot = b % L.nb;
+      int landed = 0;
+      unsigned it = 0;
+      for (; b < t_hi; b += NC) {
+        const int r = b - t_lo;
+        const int c = r >> (nm - 1), m = r & (nm - 1);
+        while (landed <= b) {  // the loader's count of blocks in LDS
+          landed = (int)lds_ld(L.ctl + 0);
+          if (landed > b || spin_fail_lds(X, it)) break;
+        }
+        const u32x4 wv = *reinterpret_cast<const u32x4*>(L.ring + (size_t)slot * 1024 + 16 * lane);
+        const bf16_t* arow = L.A + 128 * c + 32 * grp;
+        bf16x8 av[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) av[t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(arow + 8 * t));
+        if (m == 0) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[jj][0] = mfma_bf16(av[t], dequant(wv[t], msk, mag), acc[jj][0]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[jj][1] = mfma_bf16(av[t], dequant(wv[t], msk, mag), acc[jj][1]);
+        }
+        // the slot may be refilled once its bytes are in registers: this consumer's blocks taken so far
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) lds_st(L.ctl + 1 + X.wave, (unsigned)(b / NC + 1));
+        slot += NC;
+        if (slot >= L.nb) slot -= L.nb;
+      }
+    }
+    // partial sums of output row 0 (lanes 0..15, register 0) -> red[parity][wave][jj][m][col]
+    float* red = L.red + (size_t)red_par * NC * TG * 2 * 16;
+    if (lane < 16) {
+#pragma unroll
+      for (int jj = 0; jj < TG; ++jj)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) red[((X.wave * TG + jj) * 2 + m) * 16 + lane] = acc[jj][m][0];
+    }
+    cbarrier(X, L);
+#pragma unroll
+    for (int jj = 0; jj < TG; ++jj) {
+      if (jj >= ng || jj % NC != X.wave) continue;
+      const int slot = j0 + jj;
+      const int tile = s.g + slot * s.G;
+      const int col = lane & 15;
+      const int n = 16 * tile + col;
+      float y1 = 0.f, y2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NC; ++w) {
+        y1 += red[((w * TG + jj) * 2 + 0) * 16 + col];
+        y2 += red[((w * TG + jj) * 2 + 1) * 16 + col];
+      }
+      const int es = slot < kEopTiles ? slot : kEopTiles - 1;
+      const float2 e1 = eop[(es * 2 + 0) * 16 + col], e2 = eop[(es * 2 + 1) * 16 + col];
+      y1 = e1.x * (y1 - e1.y * asum);  // s * (sum A (128 + q) - (128 + z) sum A)
+      y2 = e2.x * (y2 - e2.y * asum);
+      epi(slot, tile, n, y1, y2);
+    }
+    red_par ^= 1;
+  }
+  X.n_used = base + nt * per_tile;
+}
+
+// publish the bf16 pair (column n even: lanes 2i, 2i + 1 of a tile's 16) as one granule
+__device__ __forceinline__ void publish_pair(unsigned long long* g, int n, unsigned tag, float v, int lane) {
+  const uint32_t b = (uint32_t)f2bf(v);
+  const uint32_t pr = lane_xor1(b);
+  if (lane < 16 && !(lane & 1)) st_gran(g + n / 2, tag, b | (pr << 16));
+}
+
+// Attention of head h on this CU (model.py:237 for the token at position p) by the NC consumer
+// waves: q / k / v of the head from the QKV granules, keys of earlier positions from the cache
+// (slots written by earlier steps; slot p % S is being written by this step and is skipped), the
+// current key from the granules. 16 lanes per key, online softmax per 16-lane group, groups merged
+// by lane swaps, waves through LDS. y_h published as granules.
+template <int HS>
+__device__ __forceinline__ void attention_head(Ctx& X, const Lds& L, const llj_engine_plan& P, const Arena& ar, int l, int h, int p,
+                               unsigned tag) {
+  const Shape& s = X.s;
+  constexpr int DPL = HS / 16;
+  constexpr int NG = NC * 4;  // 16-lane key groups
+  constexpr int U = 8;
+  const int C = s.C, Sc = s.S;
+  float* sq = L.att;            // [HS] q (fp32, pre-scaled by log2(e) / sqrt(hs))
+  float* sk = sq + HS;          // [HS] current k
+  float* sv = sk + HS;          // [HS] current v
+  float* s_m = sv + HS;         // [NC]
+  float* s_l = s_m + NC;        // [NC]
+  float* s_o = s_l + NC;        // [NC][HS]
+  const float scale_log2 = 1.4426950408889634f / sqrtf((float)HS);
+  if (X.wave < 3) {  // wave 0: q, 1: k, 2: v of head h (HS / 2 granules each)
+    const unsigned long long* src = ar.gqkv + (X.wave * C + h * HS) / 2;
+    float* dst = X.wave == 0 ? sq : X.wave == 1 ? sk : sv;
+    const float mul = X.wave == 0 ? scale_log2 : 1.f;
+    for (int b0 = 0; b0 < HS / 2; b0 += 64) {
+      const int idx = b0 + X.lane;
+      unsigned long long v;
+      unsigned it = 0;
+      for (;;) {
+        v = ld_gran(src + (idx < HS / 2 ? idx : 0));
+        if (__all(idx >= HS / 2 || (unsigned)(v >> 32) == tag)) break;
+        if (spin_fail(X, it)) break;
+      }
+      if (idx < HS / 2) {
+        dst[2 * idx] = bflo((uint32_t)v) * mul;
+        dst[2 * idx + 1] = bfhi((uint32_t)v) * mul;
+      }
+    }
+  }
+  cbarrier(X, L);
+  const int sub = X.lane & 15, kg = (X.wave * 64 + X.lane) >> 4;
+  const int nprev = p < Sc ? p : Sc - 1;  // earlier positions still in the window
+  const int cur_slot = p % Sc;
+  const bf16_t* kc = reinterpret_cast<const bf16_t*>(P.layers[l].kcache) + (size_t)h * Sc * HS + sub * DPL;
+  const bf16_t* vc = reinterpret_cast<const bf16_t*>(P.layers[l].vcache) + (size_t)h * Sc * HS + sub * DPL;
+  float qf[DPL];
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) qf[i] = sq[sub * DPL + i];
+  float mx = -INFINITY, lsum = 0.f, o[DPL];
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) o[i] = 0.f;
+  auto step = [&](float sc, const float* vv) {
+    const float mn = fmaxf(mx, sc);
+    const float corr = exp2f(mx - mn);
+    const float pj = exp2f(sc - mn);
+    lsum = lsum * corr + pj;
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) o[i] = o[i] * corr + pj * vv[i];
+    mx = mn;
+  };
+  for (int j0 = kg; j0 < nprev; j0 += NG * U) {
+    uint32_t kw[U][DPL / 2], vw[U][DPL / 2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + NG * u < nprev ? j0 + NG * u : 0;
+      const int slot = p < Sc ? j : (j < cur_slot ? j : j + 1);
+      const size_t eo = (size_t)slot * HS;
+#pragma unroll
+      for (int i = 0; i < DPL / 2; ++i) {
+        kw[u][i] = reinterpret_cast<const uint32_t*>(kc + eo)[i];
+        vw[u][i] = reinterpret_cast<const uint32_t*>(vc + eo)[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float sc = 0.f;
+#pragma unroll
+      for (int i = 0; i < DPL / 2; ++i) sc += qf[2 * i] * bflo(kw[u][i]) + qf[2 * i + 1] * bfhi(kw[u][i]);
+      sc = row16_sum(sc);
+      if (j0 + NG * u >= nprev) continue;
+      float vv[DPL];
+#pragma unroll
+      for (int i = 0; i < DPL / 2; ++i) {
+        vv[2 * i] = bflo(vw[u][i]);
+        vv[2 * i + 1] = bfhi(vw[u][i]);
+      }
+      step(sc, vv);
+    }
+  }
+  if (kg == NG - 1) {  // the current key (this step's k / v: not yet readable from the cache)
+    float sc = 0.f;
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) sc += qf[i] * sk[sub * DPL + i];
+    sc = row16_sum(sc);
+    float vv[DPL];
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) vv[i] = sv[sub * DPL + i];
+    step(sc, vv);
+  }
+  {  // merge the 4 groups of a wave (rows 0+1 and 2+3, then the halves)
+    float mlo, mhi, llo, lhi, olo[DPL], ohi[DPL];
+    auto merge = [&]() {
+      const float M = fmaxf(mlo, mhi);
+      const float flo = mlo == -INFINITY ? 0.f : exp2f(mlo - M);
+      const float fhi = mhi == -INFINITY ? 0.f : exp2f(mhi - M);
+      mx = M;
+      lsum = llo * flo + lhi * fhi;
+#pragma unroll
+      for (int i = 0; i < DPL; ++i) o[i] = olo[i] * flo + ohi[i] * fhi;
+    };
+    lane_halves<false>(mx, mlo, mhi);
+    lane_halves<false>(lsum, llo, lhi);
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) lane_halves<false>(o[i], olo[i], ohi[i]);
+    merge();
+    lane_halves<true>(mx, mlo, mhi);
+    lane_halves<true>(lsum, llo, lhi);
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) lane_halves<true>(o[i], olo[i], ohi[i]);
+    merge();
+  }
+  if (X.lane < 16) {
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) s_o[X.wave * HS + sub * DPL + i] = o[i];
+    if (sub == 0) {
+      s_m[X.wave] = mx;
+      s_l[X.wave] = lsum;
+    }
+  }
+  cbarrier(X, L);
+  const int d = X.wave * 64 + X.lane;
+  if (d < HS) {
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NC; ++w) M = fmaxf(M, s_m[w]);
+    float Ls = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < NC; ++w) {
+      const float f = s_m[w] == -INFINITY ? 0.f : exp2f(s_m[w] - M);
+      Ls += s_l[w] * f;
+      O += s_o[w * HS + d] * f;
+    }
+    const uint32_t ob = (uint32_t)f2bf(O / Ls);
+    const uint32_t pr = lane_xor1(ob);
+    if (!(d & 1)) st_gran(ar.gy + (h * HS + d) / 2, tag, ob | (pr << 16));
+  }
+  cbarrier(X, L);  // the scratch is free again
+}
+
+// ------------------------------------------------------------------------------------ loader
+// Streams every block of this CU's step into the ring, in consumption order. Slot b % nb is
+// reused once its previous block (b - nb) has been taken by its consumer ((b - nb) % NC).
+__device__ __forceinline__ void loader(Ctx& X, const Lds& L, const llj_engine_plan& P) {
+  const Shape& s = X.s;
+  const uint32_t ring = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)L.ring);
+  const int nb = L.nb;
+  int b = 0, slot = 0;
+  int pub = 0;    // blocks published as landed
+  int limit = nb; // blocks that may be issued before the consumers' counts are read again
+  int opi = 0;
+  for (int l = 0; l <= s.L; ++l) {
+    for (int op = (l == s.L ? OP_HEAD : OP_QKV); op <= (l == s.L ? OP_HEAD : OP_DOWN); ++op) {
+      const int nt = tiles_of_cu(s, op), kc = op_kc(s, op), nm = op_nmat(op);
+      const char* w0 = sgpr_ptr(op_weight(P, l, op, 0));
+      const char* w1 = sgpr_ptr(op_weight(P, l, op, nm - 1));
+      for (int j = 0; j < nt; ++j) {
+        const size_t tile_off = (size_t)(s.g + j * s.G) * kc * 1024 + 16 * X.lane;
+        for (int c = 0; c < kc; ++c) {
+          for (int m = 0; m < nm; ++m) {
+            if (b == limit) {
+              // every block below F = min over consumers of their next block has been taken:
+              // slots of blocks < F are free, so blocks < F + nb may be issued
+              unsigned it = 0;
+              for (;;) {
+                int F = 0x7fffffff;
+#pragma unroll
+                for (int w = 0; w < NC; ++w) {
+                  const int f = (int)lds_ld(L.ctl + 1 + w) * NC + w;
+                  F = f < F ? f : F;
+                }
+                limit = F + nb;
+                if (limit > b) break;
+                if (pub < b) {  // nothing to issue: publish everything in flight first
+                  wait_vm<0>();
+                  pub = b;
+                  if (X.lane == 0) lds_st(L.ctl + 0, (unsigned)pub);
+                }
+                if (spin_fail_lds(X, it)) { limit = b + nb; break; }
+              }
+            }
+            unsigned keep;
+            const char* src = (m ? w1 : w0) + tile_off + (size_t)c * 1024;
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)slot * 1024u);
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+                         "s_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(src), "s"(dst)
+                         : "memory");
+            ++b;
+            if (++slot == nb) slot = 0;
+            if ((b & 7) == 0 && b - pub > D) {  // publish in batches of 8 landings
+              wait_vm<D>();
+              pub = b - D;
+              if (X.lane == 0) lds_st(L.ctl + 0, (unsigned)pub);
+            }
+          }
+        }
+      }
+      if (opi < 8) stamp(P, X.lane, 100 + opi);
+      ++opi;
+    }
+  }
+  wait_vm<0>();
+  if (X.lane == 0) lds_st(L.ctl + 0, (unsigned)b);
+  stamp(P, X.lane, 120);
+}
+
+// ------------------------------------------------------------------------------------ kernel
+__global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Ctx X;
+  Shape& s = X.s;
+  s.C = P.C; s.H = P.H; s.V = P.V; s.nh = P.n_head; s.hs = P.C / P.n_head; s.S = P.S; s.L = P.n_layer;
+  s.G = gridDim.x; s.g = blockIdx.x;
+  X.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  X.lane = threadIdx.x & 63;
+  X.aborted = false;
+  X.bar_gen = 0;
+  X.n_used = 0;
+  X.t0 = __builtin_amdgcn_s_memrealtime();
+  const int C = s.C, H = s.H;
+  Lds L;
+  {
+    size_t o = 0;
+    L.ctl = reinterpret_cast<unsigned*>(smem);
+    o += kCtlWords * 4;
+    L.A = reinterpret_cast<bf16_t*>(smem + o);
+    o += al16((size_t)(C > H ? C : H) * 2);
+    L.xres[0] = reinterpret_cast<bf16_t*>(smem + o);
+    o += al16((size_t)C * 2);
+    L.xres[1] = reinterpret_cast<bf16_t*>(smem + o);
+    o += al16((size_t)C * 2);
+    L.red = reinterpret_cast<float*>(smem + o);
+    o += (size_t)2 * NC * TG * 2 * 16 * 4;
+    L.eop = reinterpret_cast<float2*>(smem + o);
+    o += (size_t)2 * kEopTiles * 2 * 16 * 8;
+    L.misc = reinterpret_cast<float*>(smem + o);
+    o += 64 * 4;
+    L.att = reinterpret_cast<float*>(smem + o);
+    o += al16((size_t)(3 * s.hs + 2 * NC + NC * s.hs) * 4);
+    L.ring = smem + o;
+    L.nb = P.ring_blocks;
+  }
+  const Arena ar = arena_of(P);
+  X.gctl = ar.ctl;
+  if (threadIdx.x < kCtlWords) L.ctl[threadIdx.x] = 0u;
+  __syncthreads();  // the only full-workgroup barrier: control words zeroed before any role starts
+  if (X.wave == NC) {
+    loader(X, L, P);
+    return;
+  }
+  // ---- consumers. Step state written by the previous step (an earlier launch).
+  if (X.wave == 0) stamp(P, X.lane, 0);
+  const unsigned epoch = ar.ctl[0];
+  const int p = P.pos[0] + 1;  // position of the token this step processes
+  const int tok = P.cur[0];
+  int red_par = 0;
+  const int hs = s.hs;
+  const int att_stride = s.G / s.nh;
+  const bool att_cu = (s.g % att_stride) == 0 && s.g / att_stride < s.nh;
+  const int att_h = s.g / att_stride;
+  // epilogue-operand buffers alternate per op (QKV 0, c_proj 1, SwiGLU 0, down 1, lm_head 0)
+  float2* eop0 = L.eop;
+  float2* eop1 = L.eop + kEopTiles * 2 * 16;
+  for (int l = 0; l < s.L; ++l) {
+    const llj_engine_layer& Ly = P.layers[l];
+    const unsigned tag = epoch * 128u + (unsigned)l + 1u;
+    const unsigned tag_prev = epoch * 128u + (unsigned)l;  // x from the previous layer's down tiles
+    // ---- rms_1(x) -> QKV + RoPE + KV write
+    stage_sz(X, eop0, P, l, OP_QKV);
+    const int slot = p % s.S;
+    float2* rcs = eop0 + kEopTiles * 2 * 16 - 8 * TG;  // RoPE (cos, sin) per tile slot (slots < TG; QKV has <= TG per CU)
+    {
+      const int nt = tiles_of_cu(s, OP_QKV);
+      for (int i = X.lane + 64 * X.wave; i < nt * 8 && i < 8 * TG; i += 64 * NC) {
+        const int j = i >> 3, pr = i & 7;
+        const int n = 16 * (s.g + j * s.G) + 2 * pr;
+        const int dd = (n % C) % hs;
+        rcs[i] = *reinterpret_cast<const float2*>(P.rope + ((size_t)p * (hs >> 1) + (dd >> 1)) * 2);
+      }
+    }
+    float asum = stage_norm(X, L, 0, ar.gx, tag_prev,
+                            l == 0 ? reinterpret_cast<const bf16_t*>(P.wte) + (size_t)tok * C : nullptr,
+                            reinterpret_cast<const bf16_t*>(Ly.rms1), Ly.eps1, C);
+    const int sb = 2 + 12 * l;  // this layer's stamps (profiling)
+    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 0);
+    {
+      bf16_t* kcache = reinterpret_cast<bf16_t*>(Ly.kcache);
+      bf16_t* vcache = reinterpret_cast<bf16_t*>(Ly.vcache);
+      consume(X, L, eop0, OP_QKV, asum, red_par, [&](int sl, int tile, int n, float y, float) {
+        const int region = (16 * tile) / C;  // 0 q, 1 k, 2 v (uniform per tile)
+        const int nc = n - region * C;
+        const int hh = nc / hs, dd = nc % hs;
+        const float v = round_bf(y);  // c_attn output in bf16 (model.py:204)
+        const float partner = lane_xor1(v);
+        float out = v;
+        if (region < 2) {  // RoPE in fp32 (model.py:318-329)
+          const float2 cs = rcs[(sl < TG ? sl : 0) * 8 + ((X.lane & 15) >> 1)];
+          out = (dd & 1) ? (v * cs.x + partner * cs.y) : (v * cs.x - partner * cs.y);
+        }
+        const uint32_t ob = (uint32_t)f2bf(out);
+        const uint32_t pr = lane_xor1(ob);
+        if (X.lane < 16 && !(X.lane & 1)) {
+          st_gran(ar.gqkv + n / 2, tag, ob | (pr << 16));
+          if (region > 0) {  // the cache row of this position, for later steps
+            bf16_t* dst = (region == 1 ? kcache : vcache) + ((size_t)hh * s.S + slot) * hs + dd;
+            *reinterpret_cast<uint32_t*>(dst) = ob | (pr << 16);
+          }
+        }
+      });
+    }
+    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 1);
+    // ---- attention of one head on the attention CUs
+    if (att_cu) {
+      if (hs == 128) attention_head<128>(X, L, P, ar, l, att_h, p, tag);
+      else attention_head<64>(X, L, P, ar, l, att_h, p, tag);
+    }
+    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 2);
+    // ---- c_proj + residual
+    stage_sz(X, eop1, P, l, OP_O);
+    asum = stage_plain<GKC>(X, L, ar.gy, tag, C);
+    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 3);
+    consume(X, L, eop1, OP_O, asum, red_par, [&](int, int, int n, float y, float) {
+      const float xn = round_bf(bf2f(L.xres[0][n]) + round_bf(y));  // x + attn(x) in bf16 (model.py:172)
+      publish_pair(ar.gxm, n, tag, xn, X.lane);
+    });
+    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 4);
+    // ---- rms_2 -> SwiGLU
+    stage_sz(X, eop0, P, l, OP_SW);
+    asum = stage_norm(X, L, 1, ar.gxm, tag, nullptr, reinterpret_cast<const bf16_t*>(Ly.rms2), Ly.eps2, C);
+    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 5);
+    consume(X, L, eop0, OP_SW, asum, red_par, [&](int, int, int n, float y1, float y2) {
+      const float a1 = round_bf(y1), a2 = round_bf(y2);
+      const float sl = round_bf(a1 / (1.f + __expf(-a1)));  // F.silu in bf16 (model.py:258)
+      publish_pair(ar.gh, n, tag, sl * a2, X.lane);
+    });
+    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 6);
+    // ---- down + residual
+    stage_sz(X, eop1, P, l, OP_DOWN);
+    asum = stage_plain<GKH>(X, L, ar.gh, tag, H);
+    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 7);
+    consume(X, L, eop1, OP_DOWN, asum, red_par, [&](int, int, int n, float y, float) {
+      const float xn = round_bf(bf2f(L.xres[1][n]) + round_bf(y));  // model.py:173
+      publish_pair(ar.gx, n, tag, xn, X.lane);
+    });
+    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 8);
+  }
+  // ---- ln_f + lm_head + argmax
+  const unsigned tag_last = epoch * 128u + (unsigned)s.L;
+  const unsigned tag_head = epoch * 128u + 127u;
+  stage_sz(X, eop0, P, 0, OP_HEAD);
+  float asum = stage_norm(X, L, 0, ar.gx, tag_last, nullptr, reinterpret_cast<const bf16_t*>(P.ln_f), P.eps_f, C);
+  if (X.wave == 0) stamp(P, X.lane, 126);
+  uint32_t best = 0;  // (order key of the bf16 logit << 16) | (0xFFFF - column): max = argmax, lowest index on ties
+  bf16_t* logits = reinterpret_cast<bf16_t*>(P.logits);
+  consume(X, L, eop0, OP_HEAD, asum, red_par, [&](int, int, int n, float y, float) {
+    const uint32_t b = (uint32_t)f2bf(y);
+    const uint32_t pr = lane_xor1(b);
+    if (X.lane < 16 && !(X.lane & 1)) *reinterpret_cast<uint32_t*>(logits + n) = b | (pr << 16);
+    const uint32_t key = X.lane < 16 ? ((bf_key(b) << 16) | (0xFFFFu - (uint32_t)n)) : 0u;
+    best = max(best, key);
+  });
+  if (X.wave == 0) stamp(P, X.lane, 127);
+  // CU best over its consumer waves -> one granule; the last CU to arrive picks the token
+  uint32_t b = best;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
+  unsigned* mb = reinterpret_cast<unsigned*>(L.misc) + 32;
+  if (X.lane == 0) mb[X.wave] = b;
+  cbarrier(X, L);
+  if (X.wave == 0 && X.lane == 0) {
+    uint32_t cb = 0;
+#pragma unroll
+    for (int w = 0; w < NC; ++w) cb = max(cb, mb[w]);
+    st_gran(ar.garg + s.g, tag_head, cb);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ar.ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mb[16] = (t + 1 == (unsigned)s.G) ? 1u : 0u;
+  }
+  if (X.wave != 0) return;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lds_ld(mb + 16) != 1u) return;
+  uint32_t tb = 0;
+  for (int b0 = 0; b0 < s.G; b0 += 64) {
+    const int idx = b0 + X.lane;
+    unsigned long long v;
+    unsigned it = 0;
+    for (;;) {
+      v = ld_gran(ar.garg + (idx < s.G ? idx : 0));
+      if (__all(idx >= s.G || (unsigned)(v >> 32) == tag_head)) break;
+      if (spin_fail(X, it)) break;
+    }
+    if (idx < s.G) tb = max(tb, (uint32_t)v);
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) tb = max(tb, (uint32_t)__shfl_xor((int)tb, o, 64));
+  if (X.lane == 0) {
+    const int next = (int)(0xFFFFu - (tb & 0xFFFFu));
+    if (P.flags & 1) {  // greedy (generate.py:66-74 with top_k = 1)
+      P.cur[0] = next;
+      if (P.tokens) P.tokens[p + 1] = next;
+    }
+    P.pos[0] = p;
+    ar.ctl[1] = 0u;
+    ar.ctl[0] = epoch + 1u;
+  }
+}
+
+}  // namespace eng
+}  // namespace llj
+
+using namespace llj;
+
+extern "C" {
+
+size_t llj_engine_arena_bytes(int C, int H) { return eng::arena_granules(C, H) * 8 + 64; }
+
+int llj_engine_ring_blocks(int C, int H, int n_head) {
+  if (n_head < 1 || C % n_head) return 0;
+  return eng::ring_blocks(C, H, C / n_head, 160 * 1024);
+}
+
+int llj_engine_step(const llj_engine_plan* plan, void* stream) {
+  if (!plan) return LLJ_EINVAL;
+  const llj_engine_plan& P = *plan;
+  const int hs = P.n_head > 0 ? P.C / P.n_head : 0;
+  LLJ_REQUIRE(P.layers && P.n_layer >= 1 && P.n_layer <= 126 && P.C % 128 == 0 && P.H % 128 == 0 && P.V % 16 == 0);
+  LLJ_REQUIRE(P.V <= 65536 && (hs == 64 || hs == 128) && P.S >= 1 && P.arena && P.pos && P.cur && P.logits);
+  LLJ_REQUIRE(P.C / 2 <= eng::GN * 64 * eng::NC);  // stage_norm's gain registers
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return LLJ_EINVAL;
+  const int G = P.grid > 0 ? P.grid : cus;
+  LLJ_REQUIRE(G >= 1 && G <= cus && G <= eng::kMaxCUs && P.n_head <= G);
+  // at most TG QKV tiles per CU (RoPE operands) and kEopTiles tiles per op
+  LLJ_REQUIRE((3 * P.C / 16 + G - 1) / G <= eng::TG && (P.V / 16 + G - 1) / G <= eng::kEopTiles &&
+              (P.H / 16 + G - 1) / G <= eng::kEopTiles);
+  const int nb = eng::ring_blocks(P.C, P.H, hs, 160 * 1024);
+  LLJ_REQUIRE(P.ring_blocks >= 2 * eng::D && P.ring_blocks <= nb);
+  const size_t lds = eng::lds_fixed(P.C, P.H, hs) + (size_t)P.ring_blocks * 1024;
+  LLJ_REQUIRE(lds <= 160 * 1024 && lds > 80 * 1024);  // one workgroup per CU, every one resident
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)eng::engine_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(eng::engine_step_kernel, dim3(G), dim3(eng::NTH), lds, (hipStream_t)stream, P);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -35,31 +35,47 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in list(CSRC.glob("*")) + [INCLUDE / "lit_llama_amd.h"])
 
 
+OBJ_CACHE = PKG.parent.parent / "build" / "obj"  # per-source objects of the in-tree library (git-ignored)
+
+
+def _stale(obj: Path, src: Path) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    deps = [src] + list(CSRC.glob("*.h")) + [INCLUDE / "lit_llama_amd.h", Path(__file__)]
+    return any(d.stat().st_mtime > t for d in deps)
+
+
 def build(force: bool = False, verbose: bool = False, out: Path | None = None, defines=()) -> Path:
     """Compile every csrc/*.hip for gfx950 and link `out` (default: the in-tree _lljamd.so).
-    `defines`: extra -D macros (profiling / experiment variants built next to the product)."""
+    `defines`: extra -D macros (profiling / experiment variants built next to the product).
+    The product build keeps one object per source under build/obj and recompiles only the sources
+    whose file (or any shared header) changed; force=True recompiles everything."""
     out = Path(out) if out is not None else OUT
     if out == OUT and not defines and not force and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     extra = [f"-D{d}" for d in defines]
     with tempfile.TemporaryDirectory(prefix="lljbuild") as td:
+        cache = OBJ_CACHE if (out == OUT and not defines) else Path(td)
+        cache.mkdir(parents=True, exist_ok=True)
         objs = []
         cmds = []
         for src in sources():
-            obj = Path(td) / (src.stem + ".o")
+            obj = cache / (src.stem + ".o")
             objs.append(obj)
-            cmds.append([hipcc, f"--offload-arch={ARCH}", *FLAGS, *FILE_FLAGS.get(src.name, []), *extra,
-                         f"-I{INCLUDE}", "-c", str(src),
-                         "-o", str(obj)])
+            if force or cache != OBJ_CACHE or _stale(obj, src):
+                cmds.append([hipcc, f"--offload-arch={ARCH}", *FLAGS, *FILE_FLAGS.get(src.name, []), *extra,
+                             f"-I{INCLUDE}", "-c", str(src), "-o", str(obj)])
 
         def run(cmd):
             if verbose:
                 print(" ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)
 
-        with ThreadPoolExecutor(max_workers=len(cmds)) as ex:
-            list(ex.map(run, cmds))
+        if cmds:
+            with ThreadPoolExecutor(max_workers=min(len(cmds), 8)) as ex:
+                list(ex.map(run, cmds))
         tmp = out.with_suffix(".so.tmp")
         link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs]
         run(link)

@@ -52,6 +52,8 @@ SIGNATURES = {
     "llj_gemm_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_silu_mul": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_qkv_rope": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "llj_engine_step": [_P, _P],
+    "llj_engine_ring_blocks": [_I, _I, _I],
 }
 
 _lib = None
@@ -77,6 +79,8 @@ def lib() -> ctypes.CDLL:
         L.llj_i8_ws_bytes.restype = ctypes.c_size_t
         L.llj_attention_ws_bytes.argtypes = [_I, _I, _I, _I]
         L.llj_attention_ws_bytes.restype = ctypes.c_size_t
+        L.llj_engine_arena_bytes.argtypes = [_I, _I]
+        L.llj_engine_arena_bytes.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
