@@ -51,9 +51,8 @@ constexpr int TG = 4;      // tiles per partial-sum group (accumulators per wave
 #endif
 constexpr int D = LLJ_ENG_D;
 static_assert(D >= 1 && D <= 62, "vmcnt immediate");
-constexpr int GKC = 16;    // granules per lane per gather batch of a C-sized vector (x, y, x_mid)
-constexpr int GKH = 32;    // ... of the SwiGLU output h
-constexpr int GN = 22;     // RMSNorm gain pairs per lane (C / 2 <= GN * 64 * NC: C <= 8448)
+constexpr int GK = 8;      // granules per lane per gather batch (x, y, x_mid: one batch at 7B; h: two)
+constexpr int GN = 6;      // RMSNorm gain pairs per lane (C / 2 <= GN * 64 * NC: C <= 5376)
 constexpr unsigned long long kSpinTicks = 5000000ull;  // 50 ms of s_memrealtime (100 MHz)
 constexpr int kMaxCUs = LLJ_ENGINE_MAX_CUS;
 
@@ -118,7 +117,7 @@ __device__ __forceinline__ uint32_t bf_key(uint32_t b) { return (b & 0x8000u) ? 
 // profiling stamps (plan.trace != NULL): [g][128]; consumers: 0 start, per layer l at 2 + 12 l:
 // +0 x staged, +1 QKV done, +2 attention done, +3 y staged, +4 c_proj done, +5 x_mid staged,
 // +6 SwiGLU done, +7 h staged, +8 down done; the loader: 100 + op index of its last DMA of each op
-// (per layer, layers 0..1 only: 100..107), 120 stream end; 126 head staged, 127 head done
+// (per layer, layers 0..1 only: 100..107), 120 stream end, 121 loader start; 126 head staged, 127 head done
 __device__ __forceinline__ void stamp(const llj_engine_plan& P, int lane, int k) {
   if (P.trace && lane == 0 && k < 128) P.trace[(size_t)blockIdx.x * 128 + k] = __builtin_amdgcn_s_memrealtime();
 }
@@ -145,11 +144,17 @@ __device__ __forceinline__ int tiles_of_cu(const Shape& s, int op) {
   return s.g < n ? (n - s.g + s.G - 1) / s.G : 0;
 }
 __device__ __forceinline__ int op_blocks(const Shape& s, int op) { return tiles_of_cu(s, op) * op_kc(s, op) * op_nmat(op); }
+// Weight pointer of (layer, op, matrix) for the loader wave, read by a scalar load (the layer table
+// is written by the host before the launch and only read here). A compiler-visible vector load
+// would be followed by s_waitcnt vmcnt(0) at its use -- a wait that also drains every LDS-DMA the
+// loader has in flight (the compiler does not see them), once per op edge.
 __device__ __forceinline__ const char* op_weight(const llj_engine_plan& P, int l, int op, int m) {
   if (op == OP_HEAD) return reinterpret_cast<const char*>(P.w_head);
-  const llj_engine_layer& Ly = P.layers[l];
-  const void* w = op == OP_QKV ? Ly.w_qkv : op == OP_O ? Ly.w_o : op == OP_SW ? (m ? Ly.w_fc2 : Ly.w_fc1) : Ly.w_down;
-  return reinterpret_cast<const char*>(w);
+  const llj_engine_layer* Ly = P.layers + l;
+  const void* const* f = op == OP_QKV ? &Ly->w_qkv : op == OP_O ? &Ly->w_o : op == OP_SW ? (m ? &Ly->w_fc2 : &Ly->w_fc1) : &Ly->w_down;
+  uint64_t v;
+  asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(f) : "memory");
+  return reinterpret_cast<const char*>(v);
 }
 
 // ------------------------------------------------------------------------------------ LDS
@@ -167,6 +172,7 @@ struct Lds {
   float* misc;
   float* att;
   int nb;
+  unsigned nb_magic;  // ceil(2^32 / nb): b % nb by one multiply-high
 };
 __host__ __device__ inline size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
 // epilogue operands staged per op: (scale, 128 + zero) of both matrices for every tile of the CU
@@ -216,6 +222,13 @@ __device__ __forceinline__ bool spin_fail(Ctx& X, unsigned& it) {
 __device__ __forceinline__ bool spin_fail_lds(Ctx& X, unsigned& it) {
   if (X.aborted) return true;
   return (++it & 255u) == 0u && spin_check(X);
+}
+// the loader's spins: its own clock only -- a vector load of the global error word would come with
+// a compiler s_waitcnt vmcnt(0) that drains the DMA window
+__device__ __forceinline__ bool spin_fail_loader(Ctx& X, unsigned& it) {
+  if (X.aborted) return true;
+  if ((++it & 255u) == 0u && __builtin_amdgcn_s_memrealtime() - X.t0 > kSpinTicks) X.aborted = true;
+  return X.aborted;
 }
 
 // barrier of the NC consumer waves (an LDS counter: the loader wave never takes part)
@@ -283,66 +296,58 @@ __device__ __forceinline__ void stage_sz(Ctx& X, float2* eop, const llj_engine_p
   }
 }
 
-// input of a norm-fused op: x (gathered, or the embedding row at layer 0) -> xres[buf] raw and
-// A = RMSNorm(x) * gain (model.py:276-283, bf16 rounding points); returns sum_k A[k]
-__device__ __forceinline__ float stage_norm(Ctx& X, const Lds& L, int buf, const unsigned long long* g, unsigned tag,
-                            const bf16_t* direct, const bf16_t* gain, float eps, int C) {
+// Stage the input of an op into A (one call site for every op, so its code is in the kernel once):
+// norm ops (QKV, SwiGLU, lm_head): x (gathered, or the embedding row at layer 0) -> xres[buf] raw
+// and A = RMSNorm(x) * gain (model.py:276-283, bf16 rounding points); plain ops (c_proj, down):
+// the gathered vector -> A. Returns sum_k A[k].
+__device__ __forceinline__ float stage(Ctx& X, const Lds& L, bool norm, int buf, const unsigned long long* g, unsigned tag,
+                                       const bf16_t* direct, const bf16_t* gain, float eps, int K) {
   uint32_t* xr2 = reinterpret_cast<uint32_t*>(L.xres[buf]);
+  uint32_t* a2 = reinterpret_cast<uint32_t*>(L.A);
   const uint32_t* g2 = reinterpret_cast<const uint32_t*>(gain);
-  // this wave's gain pairs, loaded before the wait (C / 2 / (64 NC) <= GN per lane)
+  // this wave's gain pairs, loaded before the wait (K / 2 / (64 NC) <= GN per lane)
   uint32_t gv[GN];
+  if (norm) {
 #pragma unroll
-  for (int k = 0; k < GN; ++k) {
-    const int idx = X.lane + 64 * X.wave + 64 * NC * k;
-    gv[k] = g2[idx < C / 2 ? idx : 0];
+    for (int k = 0; k < GN; ++k) {
+      const int idx = X.lane + 64 * X.wave + 64 * NC * k;
+      gv[k] = g2[idx < K / 2 ? idx : 0];
+    }
   }
-  float ss = 0.f;
+  // one accumulator: the sum of squares (norm) or of the values (plain) -- a select, not two
+  // variables (which the compiler turns into a scratch array indexed by `norm`)
+  float part = 0.f;
+  uint32_t* dst = norm ? xr2 : a2;
   auto sink = [&](int idx, uint32_t v) {
-    xr2[idx] = v;
+    dst[idx] = v;
     const f32x2 f = unpk(v);
-    ss += round_bf(f.x * f.x) + round_bf(f.y * f.y);  // model.py:281: x * x in bf16
+    part += norm ? round_bf(f.x * f.x) + round_bf(f.y * f.y) : f.x + f.y;  // model.py:281: x * x in bf16
   };
   if (direct) {  // layer 0: the embedding row wte[cur] (model.py:110), read by every CU
     const uint32_t* d2 = reinterpret_cast<const uint32_t*>(direct);
-    for (int idx = X.lane + 64 * X.wave; idx < C / 2; idx += 64 * NC) sink(idx, d2[idx]);
+    for (int idx = X.lane + 64 * X.wave; idx < K / 2; idx += 64 * NC) sink(idx, d2[idx]);
   } else {
-    gather<GKC>(X, g, C / 2, tag, sink);
+    gather<GK>(X, g, K / 2, tag, sink);
   }
-  ss = wave_sum(ss);
-  if (X.lane == 0) L.misc[X.wave] = ss;
-  cbarrier(X, L);
-  float tot = 0.f;
+  float asum = norm ? 0.f : part;
+  if (norm) {
+    const float ss = wave_sum(part);
+    if (X.lane == 0) L.misc[X.wave] = ss;
+    cbarrier(X, L);
+    float tot = 0.f;
 #pragma unroll
-  for (int w = 0; w < NC; ++w) tot += L.misc[w];
-  const float r = rstd_bf16(tot / (float)C, eps);
-  uint32_t* a2 = reinterpret_cast<uint32_t*>(L.A);
-  float asum = 0.f;
+    for (int w = 0; w < NC; ++w) tot += L.misc[w];
+    const float r = rstd_bf16(tot / (float)K, eps);
 #pragma unroll
-  for (int k = 0; k < GN; ++k) {
-    const int idx = X.lane + 64 * X.wave + 64 * NC * k;
-    if (idx < C / 2) {
-      const uint32_t o = norm_pair(xr2[idx], gv[k], r);
-      a2[idx] = o;
-      asum += bflo(o) + bfhi(o);
+    for (int k = 0; k < GN; ++k) {
+      const int idx = X.lane + 64 * X.wave + 64 * NC * k;
+      if (idx < K / 2) {
+        const uint32_t o = norm_pair(xr2[idx], gv[k], r);
+        a2[idx] = o;
+        asum += bflo(o) + bfhi(o);
+      }
     }
   }
-  asum = wave_sum(asum);
-  if (X.lane == 0) L.misc[16 + X.wave] = asum;
-  cbarrier(X, L);
-  float a = 0.f;
-#pragma unroll
-  for (int w = 0; w < NC; ++w) a += L.misc[16 + w];
-  return a;
-}
-// input of a plain op: gathered vector -> A; returns sum_k A[k]
-template <int GK>
-__device__ __forceinline__ float stage_plain(Ctx& X, const Lds& L, const unsigned long long* g, unsigned tag, int K) {
-  uint32_t* a2 = reinterpret_cast<uint32_t*>(L.A);
-  float asum = 0.f;
-  gather<GK>(X, g, K / 2, tag, [&](int idx, uint32_t v) {
-    a2[idx] = v;
-    asum += bflo(v) + bfhi(v);
-  });
   asum = wave_sum(asum);
   if (X.lane == 0) L.misc[16 + X.wave] = asum;
   cbarrier(X, L);
@@ -352,97 +357,182 @@ __device__ __forceinline__ float stage_plain(Ctx& X, const Lds& L, const unsigne
   return a;
 }
 
-// Consume this CU's blocks of `op` (its tiles x chunks x matrices, in stream order, block b on
-// consumer b % NC), TG tiles per partial-sum group; epi(slot, tile, n, y1, y2) runs on lanes 0..15
-// (column 16 tile + lane) of consumer (slot % NC) with the fp32 outputs of both matrices (int4
-// offset removed).
-template <typename E>
-__device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop, int op, float asum, int& red_par, E&& epi) {
-  const Shape& s = X.s;
-  const int nt = tiles_of_cu(s, op), kc = op_kc(s, op), nm = op_nmat(op);
-  const int per_tile = kc * nm;
-  const int lane = X.lane, grp = lane >> 4;
-  uint32_t msk = 0x000F000Fu, mag = 0x43004300u;  // bf16 128 + q via one v_and_or_b32 per pair
-  asm volatile("" : "+s"(msk));
-  asm volatile("" : "+v"(mag));
-  const int base = X.n_used;  // CU-stream index of this op's first block
-  for (int j0 = 0; j0 < nt; j0 += TG) {
-    const int ng = nt - j0 < TG ? nt - j0 : TG;
-    f32x4 acc[TG][2];
-#pragma unroll
-    for (int a = 0; a < TG; ++a) acc[a][0] = acc[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int jj = 0; jj < TG; ++jj) {
-      if (jj >= ng) break;
-      const int t_lo = base + (j0 + jj) * per_tile, t_hi = t_lo + per_tile;
-      int b = t_lo + ((X.wave - t_lo % NC) + NC) % NC;  // this consumer's first block of the tile
-      int slot = b % L.nb;
-      int landed = 0;
-      unsigned it = 0;
-      for (; b < t_hi; b += NC) {
-        const int r = b - t_lo;
-        const int c = r >> (nm - 1), m = r & (nm - 1);
-        while (landed <= b) {  // the loader's count of blocks in LDS
-          landed = (int)lds_ld(L.ctl + 0);
-          if (landed > b || spin_fail_lds(X, it)) break;
-        }
-        const u32x4 wv = *reinterpret_cast<const u32x4*>(L.ring + (size_t)slot * 1024 + 16 * lane);
-        const bf16_t* arow = L.A + 128 * c + 32 * grp;
-        bf16x8 av[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) av[t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(arow + 8 * t));
-        if (m == 0) {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) acc[jj][0] = mfma_bf16(av[t], dequant(wv[t], msk, mag), acc[jj][0]);
-        } else {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) acc[jj][1] = mfma_bf16(av[t], dequant(wv[t], msk, mag), acc[jj][1]);
-        }
-        // the slot may be refilled once its bytes are in registers: this consumer's blocks taken so far
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) lds_st(L.ctl + 1 + X.wave, (unsigned)(b / NC + 1));
-        slot += NC;
-        if (slot >= L.nb) slot -= L.nb;
-      }
-    }
-    // partial sums of output row 0 (lanes 0..15, register 0) -> red[parity][wave][jj][m][col]
-    float* red = L.red + (size_t)red_par * NC * TG * 2 * 16;
-    if (lane < 16) {
-#pragma unroll
-      for (int jj = 0; jj < TG; ++jj)
-#pragma unroll
-        for (int m = 0; m < 2; ++m) red[((X.wave * TG + jj) * 2 + m) * 16 + lane] = acc[jj][m][0];
-    }
-    cbarrier(X, L);
-#pragma unroll
-    for (int jj = 0; jj < TG; ++jj) {
-      if (jj >= ng || jj % NC != X.wave) continue;
-      const int slot = j0 + jj;
-      const int tile = s.g + slot * s.G;
-      const int col = lane & 15;
-      const int n = 16 * tile + col;
-      float y1 = 0.f, y2 = 0.f;
-#pragma unroll
-      for (int w = 0; w < NC; ++w) {
-        y1 += red[((w * TG + jj) * 2 + 0) * 16 + col];
-        y2 += red[((w * TG + jj) * 2 + 1) * 16 + col];
-      }
-      const int es = slot < kEopTiles ? slot : kEopTiles - 1;
-      const float2 e1 = eop[(es * 2 + 0) * 16 + col], e2 = eop[(es * 2 + 1) * 16 + col];
-      y1 = e1.x * (y1 - e1.y * asum);  // s * (sum A (128 + q) - (128 + z) sum A)
-      y2 = e2.x * (y2 - e2.y * asum);
-      epi(slot, tile, n, y1, y2);
-    }
-    red_par ^= 1;
-  }
-  X.n_used = base + nt * per_tile;
-}
+// what the epilogue of each op needs (one epilogue function, switch on the op)
+struct Epi {
+  Arena ar;
+  unsigned tag;
+  int slot;            // cache slot of this step's position
+  bf16_t *kcache, *vcache;
+  const float2* rcs;   // RoPE (cos, sin) per QKV tile slot
+  bf16_t* logits;
+  uint32_t best;       // lm_head: (order key << 16) | (0xFFFF - column), max = argmax, lowest index on ties
+};
 
 // publish the bf16 pair (column n even: lanes 2i, 2i + 1 of a tile's 16) as one granule
 __device__ __forceinline__ void publish_pair(unsigned long long* g, int n, unsigned tag, float v, int lane) {
   const uint32_t b = (uint32_t)f2bf(v);
   const uint32_t pr = lane_xor1(b);
   if (lane < 16 && !(lane & 1)) st_gran(g + n / 2, tag, b | (pr << 16));
+}
+
+// output column n (lanes 0..15 of the tile's 16) of tile slot sl of op: y1 (and y2 of SwiGLU's
+// second matrix) in fp32 with the int4 offset removed
+__device__ __forceinline__ void epilogue(Ctx& X, const Lds& L, int op, Epi& E, int sl, int tile, int n, float y1, float y2) {
+  const Shape& s = X.s;
+  const int lane = X.lane;
+  switch (op) {
+    case OP_QKV: {
+      const int C = s.C, hs = s.hs;
+      const int region = (16 * tile) / C;  // 0 q, 1 k, 2 v (uniform per tile)
+      const int nc = n - region * C;
+      const int hh = nc / hs, dd = nc % hs;
+      const float v = round_bf(y1);  // c_attn output in bf16 (model.py:204)
+      const float partner = lane_xor1(v);
+      float out = v;
+      if (region < 2) {  // RoPE in fp32 (model.py:318-329)
+        const float2 cs = E.rcs[(sl < TG ? sl : 0) * 8 + ((lane & 15) >> 1)];
+        out = (dd & 1) ? (v * cs.x + partner * cs.y) : (v * cs.x - partner * cs.y);
+      }
+      const uint32_t ob = (uint32_t)f2bf(out);
+      const uint32_t pr = lane_xor1(ob);
+      if (lane < 16 && !(lane & 1)) {
+        st_gran(E.ar.gqkv + n / 2, E.tag, ob | (pr << 16));
+        if (region > 0) {  // the cache row of this position, for later steps
+          bf16_t* dst = (region == 1 ? E.kcache : E.vcache) + ((size_t)hh * s.S + E.slot) * hs + dd;
+          *reinterpret_cast<uint32_t*>(dst) = ob | (pr << 16);
+        }
+      }
+      break;
+    }
+    case OP_O:  // x + attn(x) in bf16 (model.py:172)
+      publish_pair(E.ar.gxm, n, E.tag, round_bf(bf2f(L.xres[0][n]) + round_bf(y1)), lane);
+      break;
+    case OP_SW: {
+      const float a1 = round_bf(y1), a2 = round_bf(y2);
+      const float sl2 = round_bf(a1 / (1.f + __expf(-a1)));  // F.silu in bf16 (model.py:258)
+      publish_pair(E.ar.gh, n, E.tag, sl2 * a2, lane);
+      break;
+    }
+    case OP_DOWN:  // model.py:173
+      publish_pair(E.ar.gx, n, E.tag, round_bf(bf2f(L.xres[1][n]) + round_bf(y1)), lane);
+      break;
+    default: {  // lm_head: bf16 logits + this wave's argmax key
+      const uint32_t b = (uint32_t)f2bf(y1);
+      const uint32_t pr = lane_xor1(b);
+      if (lane < 16 && !(lane & 1)) *reinterpret_cast<uint32_t*>(E.logits + n) = b | (pr << 16);
+      const uint32_t key = lane < 16 ? ((bf_key(b) << 16) | (0xFFFFu - (uint32_t)n)) : 0u;
+      E.best = max(E.best, key);
+    }
+  }
+}
+
+// Consume this CU's blocks of `op`. Stream order (the loader's): tile groups of TG tiles, tile-major
+// inside a group -- for tile slot jj: for chunk c: for matrix m (contiguous 1 KiB blocks of a tile
+// for the DMA) -- and consumer w owns the chunks c = w (mod NC) of every tile. For K <= AREG_C * NC *
+// 128 the consumer holds the A fragments of all its chunks in registers for the whole op (one LDS
+// read per block: the weights); longer K (the down projection) reads them per chunk. After each
+// chunk a consumer publishes in ctl[1 + w] the stream index of its next block (every block of its
+// below that index is taken). Partial sums of output row 0 go to red per tile; after each group the
+// epilogue of tile slot jj runs on consumer jj % NC, lanes 0..15 (column 16 tile + lane).
+// Code size matters more than unrolling here: the whole step runs from a 64 KiB instruction cache
+// shared by two CUs, so this is the only instance of the block loop in the kernel.
+constexpr int AREG_C = 5;  // chunks per consumer whose A fragments stay in registers (K <= 4480 at NC 7)
+__device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop, int op, float asum, int& red_par, Epi& E) {
+  const Shape& s = X.s;
+  const int nt = tiles_of_cu(s, op), kc = op_kc(s, op), nm = op_nmat(op);
+  const int lane = X.lane, grp = lane >> 4, w = X.wave;
+  uint32_t msk = 0x000F000Fu, mag = 0x43004300u;  // bf16 128 + q via one v_and_or_b32 per pair
+  asm volatile("" : "+s"(msk));
+  asm volatile("" : "+v"(mag));
+  const bool areg = kc <= AREG_C * NC;
+  bf16x8 ar[AREG_C][4];
+  if (areg) {
+#pragma unroll
+    for (int ci = 0; ci < AREG_C; ++ci) {
+      const int c = w + ci * NC < kc ? w + ci * NC : 0;
+      const bf16_t* arow = L.A + 128 * c + 32 * grp;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) ar[ci][t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(arow + 8 * t));
+    }
+  }
+  const int per_tile = kc * nm;
+  int gbase = X.n_used;  // CU-stream index of the current group's first block
+  int landed = 0;
+  unsigned it = 0;
+  // block b's bytes from the ring, once the loader has published it as landed
+  auto take = [&](int b) -> u32x4 {
+    while (landed <= b) {
+      landed = (int)lds_ld(L.ctl + 0);
+      if (landed > b || spin_fail_lds(X, it)) break;
+    }
+    const unsigned q = __umulhi((unsigned)b, L.nb_magic);
+    return *reinterpret_cast<const u32x4*>(L.ring + (size_t)((unsigned)b - q * (unsigned)L.nb) * 1024 + 16 * lane);
+  };
+  auto chunk = [&](const bf16x8* av, int b, f32x4& a0, f32x4& a1) {
+    const u32x4 w0 = take(b);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) a0 = mfma_bf16(av[t], dequant(w0[t], msk, mag), a0);
+    if (nm == 2) {
+      const u32x4 w1 = take(b + 1);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a1 = mfma_bf16(av[t], dequant(w1[t], msk, mag), a1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slots' bytes are in registers
+  };
+  for (int j0 = 0; j0 < nt; j0 += TG) {
+    const int ng = nt - j0 < TG ? nt - j0 : TG;
+    float* red = L.red + (size_t)red_par * NC * TG * 2 * 16;
+    for (int jj = 0; jj < ng; ++jj) {
+      const int tb = gbase + jj * per_tile;  // the tile's first block
+      const int tnext = jj + 1 < ng ? tb + per_tile + w * nm : gbase + ng * per_tile;
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      if (areg) {
+#pragma unroll
+        for (int ci = 0; ci < AREG_C; ++ci) {
+          const int c = w + ci * NC;
+          if (c >= kc) break;
+          chunk(ar[ci], tb + c * nm, a0, a1);
+          if (lane == 0) lds_st(L.ctl + 1 + w, (unsigned)(c + NC < kc ? tb + (c + NC) * nm : tnext));
+        }
+      } else {
+        for (int c = w; c < kc; c += NC) {
+          const bf16_t* arow = L.A + 128 * c + 32 * grp;
+          bf16x8 av[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) av[t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(arow + 8 * t));
+          chunk(av, tb + c * nm, a0, a1);
+          if (lane == 0) lds_st(L.ctl + 1 + w, (unsigned)(c + NC < kc ? tb + (c + NC) * nm : tnext));
+        }
+      }
+      if (w >= kc && lane == 0) lds_st(L.ctl + 1 + w, (unsigned)tnext);  // no chunk of this tile
+      // partial sums of output row 0 (lanes 0..15, register 0) -> red[parity][wave][jj][m][col]
+      if (lane < 16) {
+        red[((w * TG + jj) * 2 + 0) * 16 + lane] = a0[0];
+        red[((w * TG + jj) * 2 + 1) * 16 + lane] = a1[0];
+      }
+    }
+    gbase += ng * per_tile;
+    cbarrier(X, L);
+    for (int jj = w; jj < ng; jj += NC) {
+      const int slot = j0 + jj;
+      const int tile = s.g + slot * s.G;
+      const int col = lane & 15;
+      const int n = 16 * tile + col;
+      float y1 = 0.f, y2 = 0.f;
+#pragma unroll
+      for (int v = 0; v < NC; ++v) {
+        y1 += red[((v * TG + jj) * 2 + 0) * 16 + col];
+        y2 += red[((v * TG + jj) * 2 + 1) * 16 + col];
+      }
+      const int es = slot < kEopTiles ? slot : kEopTiles - 1;
+      const float2 e1 = eop[(es * 2 + 0) * 16 + col], e2 = eop[(es * 2 + 1) * 16 + col];
+      y1 = e1.x * (y1 - e1.y * asum);  // s * (sum A (128 + q) - (128 + z) sum A)
+      y2 = e2.x * (y2 - e2.y * asum);
+      epilogue(X, L, op, E, slot, tile, n, y1, y2);
+    }
+    red_par ^= 1;
+  }
+  X.n_used = gbase;
 }
 
 // Attention of head h on this CU (model.py:237 for the token at position p) by the NC consumer
@@ -597,10 +687,61 @@ __device__ __forceinline__ void attention_head(Ctx& X, const Lds& L, const llj_e
 // ------------------------------------------------------------------------------------ loader
 // Streams every block of this CU's step into the ring, in consumption order. Slot b % nb is
 // reused once its previous block (b - nb) has been taken by its consumer ((b - nb) % NC).
+// DMAs are issued in groups of 8 with one flow-control check and at most one publish per group:
+// per-block bookkeeping held one loader wave to ~16 GB/s, groups of 8 sustain ~25 GB/s per CU
+// (tools/micro/loader_probe.hip: 6.5 TB/s chip-wide).
+constexpr int LG = 8;
+static_assert(D % LG == 0, "publish granularity");
+// wait until at most (n rounded down to a multiple of 8) DMAs of this wave are in flight
+__device__ __forceinline__ void wait_vm_le(int n) {
+  switch (n >> 3) {
+    case 0: wait_vm<0>(); break;
+    case 1: wait_vm<8>(); break;
+    case 2: wait_vm<16>(); break;
+    case 3: wait_vm<24>(); break;
+    case 4: wait_vm<32>(); break;
+    case 5: wait_vm<40>(); break;
+    case 6: wait_vm<48>(); break;
+    default: wait_vm<56>(); break;
+  }
+}
 __device__ __forceinline__ void loader(Ctx& X, const Lds& L, const llj_engine_plan& P) {
   const Shape& s = X.s;
   const uint32_t ring = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)L.ring);
   const int nb = L.nb;
+  const bool free_run = (P.flags & 2) != 0;  // profiling: stream the step with no consumers
+  stamp(P, X.lane, 121);
+  if (P.flags & 4) {  // profiling: the micro-benchmark's plain loop inside this kernel (bisecting the stream rate)
+    int slot = 0, cnt = 0, opi = 0;
+    for (int l = 0; l <= s.L; ++l) {
+      for (int op = (l == s.L ? OP_HEAD : OP_QKV); op <= (l == s.L ? OP_HEAD : OP_DOWN); ++op, ++opi) {
+        const int nt = tiles_of_cu(s, op), kc = op_kc(s, op), nm = op_nmat(op);
+        const char* w0 = op_weight(P, l, op, 0) + 16 * X.lane;
+        const char* w1 = op_weight(P, l, op, nm - 1) + 16 * X.lane;
+        for (int j = 0; j < nt; ++j) {
+          const size_t tile = (size_t)s.g + (size_t)j * s.G;
+          for (int c = 0; c < kc; ++c) {
+            for (int m = 0; m < nm; ++m) {
+              const char* src = (m ? w1 : w0) + (tile * kc + c) * 1024;
+              const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)slot * 1024u);
+              unsigned keep;
+              asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+                           "s_mov_b32 m0, %0"
+                           : "=&s"(keep)
+                           : "v"(src), "s"(dst)
+                           : "memory");
+              if (++slot == nb) slot = 0;
+              if ((++cnt & 7) == 0) wait_vm<D>();
+            }
+          }
+        }
+        if (opi < 8) stamp(P, X.lane, 100 + opi);
+      }
+    }
+    wait_vm<0>();
+    stamp(P, X.lane, 120);
+    return;
+  }
   int b = 0, slot = 0;
   int pub = 0;    // blocks published as landed
   int limit = nb; // blocks that may be issued before the consumers' counts are read again
@@ -608,48 +749,66 @@ __device__ __forceinline__ void loader(Ctx& X, const Lds& L, const llj_engine_pl
   for (int l = 0; l <= s.L; ++l) {
     for (int op = (l == s.L ? OP_HEAD : OP_QKV); op <= (l == s.L ? OP_HEAD : OP_DOWN); ++op) {
       const int nt = tiles_of_cu(s, op), kc = op_kc(s, op), nm = op_nmat(op);
-      const char* w0 = sgpr_ptr(op_weight(P, l, op, 0));
-      const char* w1 = sgpr_ptr(op_weight(P, l, op, nm - 1));
-      for (int j = 0; j < nt; ++j) {
-        const size_t tile_off = (size_t)(s.g + j * s.G) * kc * 1024 + 16 * X.lane;
-        for (int c = 0; c < kc; ++c) {
-          for (int m = 0; m < nm; ++m) {
-            if (b == limit) {
-              // every block below F = min over consumers of their next block has been taken:
-              // slots of blocks < F are free, so blocks < F + nb may be issued
-              unsigned it = 0;
-              for (;;) {
-                int F = 0x7fffffff;
+      const char* w0 = op_weight(P, l, op, 0) + 16 * X.lane;
+      const char* w1 = op_weight(P, l, op, nm - 1) + 16 * X.lane;
+      for (int j0 = 0; j0 < nt; j0 += TG) {
+        const int ng = nt - j0 < TG ? nt - j0 : TG;
+        const int per_chunk = ng * nm, total = kc * per_chunk;
+        const size_t tstride = (size_t)s.G * kc * 1024;  // tile slot j0 + jj sits at tile g + (j0 + jj) G
+        const size_t t00 = (size_t)(s.g + j0 * s.G) * kc * 1024;
+        int c = 0, jj = 0, m = 0;  // cursor of the group's next block (tile-major: jj, then c, then m)
+        for (int i0 = 0; i0 < total; i0 += LG) {
+          const int n = total - i0 < LG ? total - i0 : LG;
+          if (!free_run && b + n > limit) {
+            // every block below F = min over consumers of their next block has been taken:
+            // slots of blocks < F are free, so blocks < F + nb may be issued
+            unsigned it = 0;
+            for (;;) {
+              int F = 0x7fffffff, Fmax = 0;
 #pragma unroll
-                for (int w = 0; w < NC; ++w) {
-                  const int f = (int)lds_ld(L.ctl + 1 + w) * NC + w;
-                  F = f < F ? f : F;
-                }
-                limit = F + nb;
-                if (limit > b) break;
-                if (pub < b) {  // nothing to issue: publish everything in flight first
-                  wait_vm<0>();
-                  pub = b;
-                  if (X.lane == 0) lds_st(L.ctl + 0, (unsigned)pub);
-                }
-                if (spin_fail_lds(X, it)) { limit = b + nb; break; }
+              for (int w = 0; w < NC; ++w) {
+                const int f = (int)lds_ld(L.ctl + 1 + w);
+                F = f < F ? f : F;
+                Fmax = f > Fmax ? f : Fmax;
+              }
+              limit = F + nb;
+              if (limit >= b + n) break;
+              // ring full. A consumer waiting for an unpublished block gets the oldest group in
+              // flight published (a wait for just those DMAs); draining the whole window here
+              // instead would make every ring-bound phase stop-and-go at one DMA latency per group
+              if (Fmax >= pub && pub < b) {
+                const int keep_n = b - pub > LG ? b - pub - LG : 0;
+                const int kq = ((keep_n >> 3) << 3) < 56 ? ((keep_n >> 3) << 3) : 56;
+                wait_vm_le(kq);
+                pub = b - kq;
+                if (X.lane == 0) lds_st(L.ctl + 0, (unsigned)pub);
+              }
+              if (spin_fail_loader(X, it)) { limit = b + nb; break; }
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < LG; ++u) {
+            if (u < n) {
+              const char* src = (m ? w1 : w0) + t00 + (size_t)jj * tstride + (size_t)c * 1024;
+              const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)slot * 1024u);
+              unsigned keep;
+              asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+                           "s_mov_b32 m0, %0"
+                           : "=&s"(keep)
+                           : "v"(src), "s"(dst)
+                           : "memory");
+              if (++slot == nb) slot = 0;
+              if (++m == nm) {
+                m = 0;
+                if (++c == kc) { c = 0; ++jj; }
               }
             }
-            unsigned keep;
-            const char* src = (m ? w1 : w0) + tile_off + (size_t)c * 1024;
-            const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)slot * 1024u);
-            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
-                         "s_mov_b32 m0, %0"
-                         : "=&s"(keep)
-                         : "v"(src), "s"(dst)
-                         : "memory");
-            ++b;
-            if (++slot == nb) slot = 0;
-            if ((b & 7) == 0 && b - pub > D) {  // publish in batches of 8 landings
-              wait_vm<D>();
-              pub = b - D;
-              if (X.lane == 0) lds_st(L.ctl + 0, (unsigned)pub);
-            }
+          }
+          b += n;
+          if (b - pub >= D + LG) {  // publish: all but the newest D have landed
+            wait_vm<D>();
+            pub = b - D;
+            if (X.lane == 0) lds_st(L.ctl + 0, (unsigned)pub);
           }
         }
       }
@@ -697,6 +856,7 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
     o += al16((size_t)(3 * s.hs + 2 * NC + NC * s.hs) * 4);
     L.ring = smem + o;
     L.nb = P.ring_blocks;
+    L.nb_magic = (unsigned)((0x100000000ull + (unsigned)L.nb - 1) / (unsigned)L.nb);
   }
   const Arena ar = arena_of(P);
   X.gctl = ar.ctl;
@@ -706,6 +866,7 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
     loader(X, L, P);
     return;
   }
+  if (P.flags & 6) return;  // profiling (loader-only stream rate): no step state is touched
   // ---- consumers. Step state written by the previous step (an earlier launch).
   if (X.wave == 0) stamp(P, X.lane, 0);
   const unsigned epoch = ar.ctl[0];
@@ -716,110 +877,64 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
   const int att_stride = s.G / s.nh;
   const bool att_cu = (s.g % att_stride) == 0 && s.g / att_stride < s.nh;
   const int att_h = s.g / att_stride;
+  Epi E;
+  E.ar = ar;
+  E.slot = p % s.S;
+  E.logits = reinterpret_cast<bf16_t*>(P.logits);
+  E.best = 0;
   // epilogue-operand buffers alternate per op (QKV 0, c_proj 1, SwiGLU 0, down 1, lm_head 0)
-  float2* eop0 = L.eop;
-  float2* eop1 = L.eop + kEopTiles * 2 * 16;
-  for (int l = 0; l < s.L; ++l) {
-    const llj_engine_layer& Ly = P.layers[l];
-    const unsigned tag = epoch * 128u + (unsigned)l + 1u;
+  float2* rcs = L.eop + kEopTiles * 2 * 16 - 8 * TG;  // RoPE (cos, sin) per QKV tile slot (<= TG per CU)
+  E.rcs = rcs;
+  // One loop over (layer, op) -- every stage, consume and epilogue is in the code once (the
+  // instruction cache holds the whole step's working set).
+  for (int i = 0; i <= 4 * s.L; ++i) {
+    const int l = i >> 2;
+    const int op = i == 4 * s.L ? OP_HEAD : (i & 3);
+    const llj_engine_layer* Ly = op == OP_HEAD ? nullptr : &P.layers[l];
+    const unsigned tag = epoch * 128u + (unsigned)l + 1u;  // this layer's granules
     const unsigned tag_prev = epoch * 128u + (unsigned)l;  // x from the previous layer's down tiles
-    // ---- rms_1(x) -> QKV + RoPE + KV write
-    stage_sz(X, eop0, P, l, OP_QKV);
-    const int slot = p % s.S;
-    float2* rcs = eop0 + kEopTiles * 2 * 16 - 8 * TG;  // RoPE (cos, sin) per tile slot (slots < TG; QKV has <= TG per CU)
-    {
+    const int sb = 2 + 12 * l;                             // this layer's stamps (profiling)
+    E.tag = tag;
+    float2* eop = L.eop + (op & 1) * kEopTiles * 2 * 16;
+    if (op == OP_O) {
+      if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 1);
+      if (att_cu) {  // attention of one head on the attention CUs
+        if (hs == 128) attention_head<128>(X, L, P, ar, l, att_h, p, tag);
+        else attention_head<64>(X, L, P, ar, l, att_h, p, tag);
+      }
+      if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 2);
+    } else if (X.wave == 0 && l < 8 && op != OP_QKV) {
+      stamp(P, X.lane, sb + (op == OP_SW ? 4 : 6));
+    }
+    stage_sz(X, eop, P, l, op);
+    if (op == OP_QKV) {
+      E.kcache = reinterpret_cast<bf16_t*>(Ly->kcache);
+      E.vcache = reinterpret_cast<bf16_t*>(Ly->vcache);
       const int nt = tiles_of_cu(s, OP_QKV);
-      for (int i = X.lane + 64 * X.wave; i < nt * 8 && i < 8 * TG; i += 64 * NC) {
-        const int j = i >> 3, pr = i & 7;
+      for (int k = X.lane + 64 * X.wave; k < nt * 8 && k < 8 * TG; k += 64 * NC) {
+        const int j = k >> 3, pr = k & 7;
         const int n = 16 * (s.g + j * s.G) + 2 * pr;
         const int dd = (n % C) % hs;
-        rcs[i] = *reinterpret_cast<const float2*>(P.rope + ((size_t)p * (hs >> 1) + (dd >> 1)) * 2);
+        rcs[k] = *reinterpret_cast<const float2*>(P.rope + ((size_t)p * (hs >> 1) + (dd >> 1)) * 2);
       }
     }
-    float asum = stage_norm(X, L, 0, ar.gx, tag_prev,
-                            l == 0 ? reinterpret_cast<const bf16_t*>(P.wte) + (size_t)tok * C : nullptr,
-                            reinterpret_cast<const bf16_t*>(Ly.rms1), Ly.eps1, C);
-    const int sb = 2 + 12 * l;  // this layer's stamps (profiling)
-    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 0);
-    {
-      bf16_t* kcache = reinterpret_cast<bf16_t*>(Ly.kcache);
-      bf16_t* vcache = reinterpret_cast<bf16_t*>(Ly.vcache);
-      consume(X, L, eop0, OP_QKV, asum, red_par, [&](int sl, int tile, int n, float y, float) {
-        const int region = (16 * tile) / C;  // 0 q, 1 k, 2 v (uniform per tile)
-        const int nc = n - region * C;
-        const int hh = nc / hs, dd = nc % hs;
-        const float v = round_bf(y);  // c_attn output in bf16 (model.py:204)
-        const float partner = lane_xor1(v);
-        float out = v;
-        if (region < 2) {  // RoPE in fp32 (model.py:318-329)
-          const float2 cs = rcs[(sl < TG ? sl : 0) * 8 + ((X.lane & 15) >> 1)];
-          out = (dd & 1) ? (v * cs.x + partner * cs.y) : (v * cs.x - partner * cs.y);
-        }
-        const uint32_t ob = (uint32_t)f2bf(out);
-        const uint32_t pr = lane_xor1(ob);
-        if (X.lane < 16 && !(X.lane & 1)) {
-          st_gran(ar.gqkv + n / 2, tag, ob | (pr << 16));
-          if (region > 0) {  // the cache row of this position, for later steps
-            bf16_t* dst = (region == 1 ? kcache : vcache) + ((size_t)hh * s.S + slot) * hs + dd;
-            *reinterpret_cast<uint32_t*>(dst) = ob | (pr << 16);
-          }
-        }
-      });
-    }
-    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 1);
-    // ---- attention of one head on the attention CUs
-    if (att_cu) {
-      if (hs == 128) attention_head<128>(X, L, P, ar, l, att_h, p, tag);
-      else attention_head<64>(X, L, P, ar, l, att_h, p, tag);
-    }
-    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 2);
-    // ---- c_proj + residual
-    stage_sz(X, eop1, P, l, OP_O);
-    asum = stage_plain<GKC>(X, L, ar.gy, tag, C);
-    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 3);
-    consume(X, L, eop1, OP_O, asum, red_par, [&](int, int, int n, float y, float) {
-      const float xn = round_bf(bf2f(L.xres[0][n]) + round_bf(y));  // x + attn(x) in bf16 (model.py:172)
-      publish_pair(ar.gxm, n, tag, xn, X.lane);
-    });
-    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 4);
-    // ---- rms_2 -> SwiGLU
-    stage_sz(X, eop0, P, l, OP_SW);
-    asum = stage_norm(X, L, 1, ar.gxm, tag, nullptr, reinterpret_cast<const bf16_t*>(Ly.rms2), Ly.eps2, C);
-    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 5);
-    consume(X, L, eop0, OP_SW, asum, red_par, [&](int, int, int n, float y1, float y2) {
-      const float a1 = round_bf(y1), a2 = round_bf(y2);
-      const float sl = round_bf(a1 / (1.f + __expf(-a1)));  // F.silu in bf16 (model.py:258)
-      publish_pair(ar.gh, n, tag, sl * a2, X.lane);
-    });
-    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 6);
-    // ---- down + residual
-    stage_sz(X, eop1, P, l, OP_DOWN);
-    asum = stage_plain<GKH>(X, L, ar.gh, tag, H);
-    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 7);
-    consume(X, L, eop1, OP_DOWN, asum, red_par, [&](int, int, int n, float y, float) {
-      const float xn = round_bf(bf2f(L.xres[1][n]) + round_bf(y));  // model.py:173
-      publish_pair(ar.gx, n, tag, xn, X.lane);
-    });
-    if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 8);
+    const bool norm = op == OP_QKV || op == OP_SW || op == OP_HEAD;
+    const unsigned long long* g = op == OP_QKV || op == OP_HEAD ? ar.gx : op == OP_O ? ar.gy : op == OP_SW ? ar.gxm : ar.gh;
+    const unsigned gtag = op == OP_QKV || op == OP_HEAD ? tag_prev : tag;
+    const bf16_t* direct = op == OP_QKV && l == 0 ? reinterpret_cast<const bf16_t*>(P.wte) + (size_t)tok * C : nullptr;
+    const void* gain = op == OP_QKV ? Ly->rms1 : op == OP_SW ? Ly->rms2 : P.ln_f;
+    const float eps = op == OP_QKV ? Ly->eps1 : op == OP_SW ? Ly->eps2 : P.eps_f;
+    const float asum = stage(X, L, norm, op == OP_SW ? 1 : 0, g, gtag, direct, reinterpret_cast<const bf16_t*>(gain), eps,
+                             op == OP_DOWN ? H : C);
+    if (X.wave == 0 && l < 8 && op != OP_HEAD) stamp(P, X.lane, sb + 2 * op + (op == OP_QKV ? 0 : 1));
+    if (op == OP_HEAD && X.wave == 0) stamp(P, X.lane, 126);
+    consume(X, L, eop, op, asum, red_par, E);
+    if (X.wave == 0 && l < 8 && op == OP_DOWN) stamp(P, X.lane, sb + 8);
   }
-  // ---- ln_f + lm_head + argmax
-  const unsigned tag_last = epoch * 128u + (unsigned)s.L;
-  const unsigned tag_head = epoch * 128u + 127u;
-  stage_sz(X, eop0, P, 0, OP_HEAD);
-  float asum = stage_norm(X, L, 0, ar.gx, tag_last, nullptr, reinterpret_cast<const bf16_t*>(P.ln_f), P.eps_f, C);
-  if (X.wave == 0) stamp(P, X.lane, 126);
-  uint32_t best = 0;  // (order key of the bf16 logit << 16) | (0xFFFF - column): max = argmax, lowest index on ties
-  bf16_t* logits = reinterpret_cast<bf16_t*>(P.logits);
-  consume(X, L, eop0, OP_HEAD, asum, red_par, [&](int, int, int n, float y, float) {
-    const uint32_t b = (uint32_t)f2bf(y);
-    const uint32_t pr = lane_xor1(b);
-    if (X.lane < 16 && !(X.lane & 1)) *reinterpret_cast<uint32_t*>(logits + n) = b | (pr << 16);
-    const uint32_t key = X.lane < 16 ? ((bf_key(b) << 16) | (0xFFFFu - (uint32_t)n)) : 0u;
-    best = max(best, key);
-  });
   if (X.wave == 0) stamp(P, X.lane, 127);
   // CU best over its consumer waves -> one granule; the last CU to arrive picks the token
-  uint32_t b = best;
+  const unsigned tag_head = epoch * 128u + 127u;
+  uint32_t b = E.best;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
   unsigned* mb = reinterpret_cast<unsigned*>(L.misc) + 32;
@@ -883,7 +998,7 @@ int llj_engine_step(const llj_engine_plan* plan, void* stream) {
   const int hs = P.n_head > 0 ? P.C / P.n_head : 0;
   LLJ_REQUIRE(P.layers && P.n_layer >= 1 && P.n_layer <= 126 && P.C % 128 == 0 && P.H % 128 == 0 && P.V % 16 == 0);
   LLJ_REQUIRE(P.V <= 65536 && (hs == 64 || hs == 128) && P.S >= 1 && P.arena && P.pos && P.cur && P.logits);
-  LLJ_REQUIRE(P.C / 2 <= eng::GN * 64 * eng::NC);  // stage_norm's gain registers
+  LLJ_REQUIRE(P.C / 2 <= eng::GN * 64 * eng::NC);  // stage's gain registers
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return LLJ_EINVAL;

@@ -128,6 +128,17 @@ class _Engine:
         self.plan.trace = self.trace.data_ptr()
         return self.trace
 
+    def probe_stream(self, st, plain: bool = False) -> None:
+        """Profiling only: one launch in which the loader streams the whole step's weights with
+        no consumers (flow control off, no step state touched): the in-engine stream rate
+        (plain: a minimal issue loop instead of the loader's)."""
+        bit = 4 if plain else 2
+        self.plan.flags |= bit
+        try:
+            self.step(st)
+        finally:
+            self.plan.flags &= ~bit
+
     def step(self, st) -> None:
         rc = _hip.lib().llj_engine_step(ctypes.byref(self.plan), st)
         if rc != 0:

@@ -68,6 +68,49 @@ def main():
         if eng:
             assert s.engine.error_bits() == 0
             tr = s.engine.enable_trace()
+            st = torch.cuda.current_stream().cuda_stream
+            s.engine.probe_stream(st)  # loader alone: the raw in-engine stream rate
+            torch.cuda.synchronize()
+            t = tr.view(-1, 128).cpu().numpy().astype(np.float64)
+            G = int((t[:, 120] > 0).sum())
+            t = t[:G]
+            st0 = t[:, 121:122]
+            res["probe_loader_op_issued"] = [float(np.median((t[:, 100 + i] - st0[:, 0]) / 100.0)) for i in range(8)]
+            res["probe_stream_end_us"] = float(np.median((t[:, 120] - st0[:, 0]) / 100.0))
+            # the same probe with every layer's weights copied into ONE allocation (layer-major, op
+            # order): does the weights' placement set the stream rate?
+            from lit_llama.engine import _EngLayer
+            eng_ = s.engine
+            n_l = model.config.n_layer
+            lay = (_EngLayer * n_l).from_buffer_copy(bytes(eng_.layers.cpu().numpy().tobytes()))
+            ws = [eng_.keep[12 * i + k] for i in range(n_l) for k in (0, 2, 4, 6, 8)]
+            tot = sum(w.numel() * w.element_size() for w in ws)
+            big = torch.empty(tot + 4096 * len(ws), dtype=torch.uint8, device="cuda")
+            off, newp = 0, []
+            for w in ws:
+                nbytes = w.numel() * w.element_size()
+                big[off:off + nbytes].copy_(w.reshape(-1).view(torch.uint8))
+                newp.append(big.data_ptr() + off)
+                off += (nbytes + 4095) // 4096 * 4096
+            for i in range(n_l):
+                lay[i].w_qkv, lay[i].w_o, lay[i].w_fc1, lay[i].w_fc2, lay[i].w_down = newp[5 * i:5 * i + 5]
+            saved_layers = eng_.layers
+            eng_.layers = torch.frombuffer(bytearray(bytes(lay)), dtype=torch.uint8).to("cuda")
+            eng_.plan.layers = eng_.layers.data_ptr()
+            tr.zero_()
+            eng_.probe_stream(st)
+            torch.cuda.synchronize()
+            t = tr.view(-1, 128).cpu().numpy().astype(np.float64)[:G]
+            res["probe_one_alloc_stream_end_us"] = float(np.median((t[:, 120] - t[:, 121]) / 100.0))
+            tr.zero_()
+            eng_.probe_stream(st, plain=True)
+            torch.cuda.synchronize()
+            t = tr.view(-1, 128).cpu().numpy().astype(np.float64)[:G]
+            res["probe_plain_loop_stream_end_us"] = float(np.median((t[:, 120] - t[:, 121]) / 100.0))
+            eng_.layers = saved_layers
+            eng_.plan.layers = eng_.layers.data_ptr()
+            del big
+            tr.zero_()
             s.graph = None  # recapture with the trace pointer
             s.decode(2)
             torch.cuda.synchronize()
@@ -102,6 +145,10 @@ def main():
         prev = r["median_us"]
     for r in res["loader_op_issued"]:
         print(f"loader op {r['op']} last DMA issued: median {r['median_us']:.2f} max {r['max_us']:.2f}")
+    print("loader-only probe, last DMA of each op (us after the loader's start): " +
+          " ".join(f"{v:.2f}" for v in res["probe_loader_op_issued"]) + f"; stream end {res['probe_stream_end_us']:.1f}; "
+          f"weights in one allocation: stream end {res['probe_one_alloc_stream_end_us']:.1f}; "
+          f"plain issue loop: {res['probe_plain_loop_stream_end_us']:.1f}")
     print(f"loader end {res['loader_end_median_us']:.1f}; head staged {res['head_staged_median_us']:.1f}, "
           f"head done {res['head_done_median_us']:.1f} (max {res['head_done_max_us']:.1f})")
 

@@ -58,11 +58,11 @@ __global__ __launch_bounds__(64 * (NC + 1), 1) void ring_kernel(const char* __re
       }
     }
     if (acc[0] == 1234.5f) out[threadIdx.x] = acc[1];
-  } else if (wave == NC) {  // loader
+  } else if (wave == NC) {  // loader (the engine's: groups of 8 DMAs, one check / publish per group)
     const uint32_t rb = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ring);
     int pub = 0, limit = nb, slot = 0;
-    for (int b = 0; b < nblk;) {
-      if (MODE != 0 && b == limit) {
+    for (int b = 0; b < nblk; b += 8) {
+      if (MODE != 0 && b + 8 > limit) {
         for (;;) {
           int F = 0x7fffffff;
 #pragma unroll
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(64 * (NC + 1), 1) void ring_kernel(const char* __re
             F = f < F ? f : F;
           }
           limit = F + nb;
-          if (limit > b) break;
+          if (limit >= b + 8) break;
           if (pub < b) {
             wait_vm<0>();
             pub = b;
@@ -79,16 +79,18 @@ __global__ __launch_bounds__(64 * (NC + 1), 1) void ring_kernel(const char* __re
           }
         }
       }
-      unsigned keep;
-      const char* src = base + (size_t)b * 1024;
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(rb + (uint32_t)slot * 1024u);
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-      ++b;
-      if (++slot == nb) slot = 0;
-      if ((b & 7) == 0 && b - pub > D) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        unsigned keep;
+        const char* src = base + (size_t)(b + u) * 1024;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(rb + (uint32_t)slot * 1024u);
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+        if (++slot == nb) slot = 0;
+      }
+      if (b + 8 - pub >= D + 8) {
         wait_vm<D>();
-        pub = b - D;
+        pub = b + 8 - D;
         if (lane == 0) lds_st(ctl, (unsigned)pub);
       }
     }
@@ -117,6 +119,32 @@ __global__ __launch_bounds__(64 * (NC + 1), 1) void ring_kernel(const char* __re
       if (slot >= nb) slot -= nb;
     }
     if (acc[0] == 1234.5f) out[threadIdx.x] = acc[1];
+  } else if (MODE == 4) {  // consumers: blocks b and b + NC per trip, both reads issued first
+    f32x4 acc = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
+    const bf16x8 a = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+    int landed = 0, slot = wave;
+    for (int b = wave; b < nblk; b += 2 * NC) {
+      const int b2 = b + NC < nblk ? b + NC : b;
+      while (landed <= b2) landed = (int)lds_ld(ctl);
+      int slot2 = slot + NC;
+      if (slot2 >= nb) slot2 -= nb;
+      const u32x4 wv = *reinterpret_cast<const u32x4*>(ring + (size_t)slot * 1024 + 16 * lane);
+      const u32x4 wv2 = *reinterpret_cast<const u32x4*>(ring + (size_t)slot2 * 1024 + 16 * lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t x = wv[t], y = wv2[t];
+        const u32x4 d = {(x & 0x000F000Fu) | 0x43004300u, ((x >> 4) & 0x000F000Fu) | 0x43004300u,
+                         ((x >> 8) & 0x000F000Fu) | 0x43004300u, ((x >> 12) & 0x000F000Fu) | 0x43004300u};
+        const u32x4 e = {(y & 0x000F000Fu) | 0x43004300u, ((y >> 4) & 0x000F000Fu) | 0x43004300u,
+                         ((y >> 8) & 0x000F000Fu) | 0x43004300u, ((y >> 12) & 0x000F000Fu) | 0x43004300u};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, d), acc, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, e), acc2, 0, 0, 0);
+      }
+      if (lane == 0) lds_st(ctl + 1 + wave, (unsigned)(b2 / NC + 1));
+      slot = slot2 + NC;
+      if (slot >= nb) slot -= nb;
+    }
+    if (acc[0] + acc2[0] == 1234.5f) out[threadIdx.x] = acc[1];
   }
   if (threadIdx.x == 0) cycles[blockIdx.x] = __builtin_amdgcn_s_memtime() - t0;
 }
@@ -158,14 +186,12 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&cyc, 8 * 4096));
   const int nb = 100;
   printf("per CU %d KiB, %d CUs, ring %d KiB\n", kib, G, nb);
-  run<3, 40, 0>(w, nblk, nb, G, out, cyc, "loader only");
-  run<3, 56, 0>(w, nblk, nb, G, out, cyc, "loader only");
-  run<3, 16, 0>(w, nblk, nb, G, out, cyc, "loader only");
-  run<3, 40, 1>(w, nblk, nb, G, out, cyc, "loader + consumers");
-  run<7, 40, 1>(w, nblk, nb, G, out, cyc, "loader + consumers");
-  run<3, 40, 3>(w, nblk, nb, G, out, cyc, "loader + consumers (sleep in spin)");
-  run<7, 40, 3>(w, nblk, nb, G, out, cyc, "loader + consumers (sleep in spin)");
-  run<7, 56, 3>(w, nblk, nb, G, out, cyc, "loader + consumers (sleep in spin)");
+  run<3, 48, 0>(w, nblk, nb, G, out, cyc, "loader only");
+  run<3, 48, 1>(w, nblk, nb, G, out, cyc, "loader + consumers");
+  run<7, 48, 1>(w, nblk, nb, G, out, cyc, "loader + consumers");
+  run<7, 48, 3>(w, nblk, nb, G, out, cyc, "loader + consumers (sleep in spin)");
+  run<3, 48, 4>(w, nblk, nb, G, out, cyc, "loader + consumers (2 blocks / trip)");
+  run<7, 48, 4>(w, nblk, nb, G, out, cyc, "loader + consumers (2 blocks / trip)");
   run<3, 8, 2>(w, nblk, nb, G, out, cyc, "register stream (all waves)");
   run<7, 4, 2>(w, nblk, nb, G, out, cyc, "register stream (all waves)");
   return 0;
