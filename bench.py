@@ -291,6 +291,33 @@ def time_dominant_kernel(model, B, iters=10):
     return avg_s, abytes
 
 
+def achievable_read_gbs(gb: float = 4.0, iters: int = 5):
+    """The achievable HBM read rate: llj_stream_read (non-temporal 16 B loads, grid-stride) over a
+    `gb` GB buffer (16x the 256 MB MALL, so the reads come from HBM), best over a few grid sizes,
+    HIP events on the launch stream. The denominator beside the 8 TB/s spec."""
+    from lit_llama import _hip
+
+    n = int(gb * 1e9) // 16 * 16
+    buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    buf.fill_(1)
+    out = torch.empty(65536, dtype=torch.float32, device="cuda")
+    st = _hip.stream()
+    best = 0.0
+    for grid in (2048, 4096, 8192):
+        _hip.call("llj_stream_read", buf.data_ptr(), n, out.data_ptr(), grid, st)
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(iters):
+            _hip.call("llj_stream_read", buf.data_ptr(), n, out.data_ptr(), grid, st)
+        ev1.record()
+        torch.cuda.synchronize()
+        best = max(best, n * iters / (ev0.elapsed_time(ev1) / 1e3) / 1e9)
+    del buf
+    torch.cuda.empty_cache()
+    return best
+
+
 def pmc_traffic(kernel_prefix: str = "llj::gemv_kernel<0, 2, 3, 4, 4, 1, 1>"):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC summary:
     profiles/<round>_pmc_summary.json (tools/profile_summary.py over separate rocprofv3 --pmc
@@ -465,6 +492,7 @@ def main():
 
     k_s, k_bytes = time_dominant_kernel(model, args.batch)
     k_gbs = k_bytes / k_s / 1e9
+    ach = achievable_read_gbs()
 
     pmc = pmc_traffic()
     bs8 = None
@@ -512,12 +540,15 @@ def main():
                        "parallelism": f"replicas x{ws} (no collective on the data path)"},
             "roofline": {"bound": "hbm", "achieved": round(k_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(k_gbs / HBM_PEAK_GBS, 4),
+                         "achievable": round(ach, 1), "frac_of_achievable": round(k_gbs / ach, 4),
+                         "achievable_source": "llj_stream_read over 4 GB (measured in this run)",
                          "traffic": round(pmc[0]) if pmc and head7 else None,
                          "traffic_source": (f"profiles/{pmc[1]} (PMC FETCH_SIZE/WRITE_SIZE passes, "
                                             f"profiled {pmc[2]:.2f} us)" if pmc and head7 else None),
                          "kernel": "gemv_kernel<W4,NORM,SWIGLU> (rms_2 + c_fc1/c_fc2 + silu*mul)",
                          "bytes_per_launch": k_bytes, "avg_launch_us": round(k_s * 1e6, 2)},
-            "step_roofline": {"bytes_per_step": sb, "achieved": round(step_gbs, 1), "frac": round(step_gbs / HBM_PEAK_GBS, 4)},
+            "step_roofline": {"bytes_per_step": sb, "achieved": round(step_gbs, 1), "frac": round(step_gbs / HBM_PEAK_GBS, 4),
+                              "frac_of_achievable": round(step_gbs / ach, 4)},
             "reference_formula_tokens_per_s": round(r["tokens"] / (r["seconds"] + r["t_prefill"]), 2),
             "memory": mem,
             "cpu_baseline": cpu,

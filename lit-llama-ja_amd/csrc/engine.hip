@@ -186,7 +186,7 @@ __host__ __device__ inline size_t lds_fixed(int C, int H, int hs) {
 // ring blocks that fit next to the fixed part in `budget` bytes
 __host__ __device__ inline int ring_blocks(int C, int H, int hs, size_t budget) {
   const size_t f = lds_fixed(C, H, hs);
-  return f >= budget ? 0 : (int)((budget - f) / 1024);
+  return f >= budget ? 0 : (int)((budget - f) / 1024) & ~7;  // whole runs of 8 slots (the loader's DMA runs)
 }
 
 // ------------------------------------------------------------------------------------ state
@@ -685,11 +685,13 @@ __device__ __forceinline__ void attention_head(Ctx& X, const Lds& L, const llj_e
 }
 
 // ------------------------------------------------------------------------------------ loader
-// Streams every block of this CU's step into the ring, in consumption order. Slot b % nb is
-// reused once its previous block (b - nb) has been taken by its consumer ((b - nb) % NC).
-// DMAs are issued in groups of 8 with one flow-control check and at most one publish per group:
-// per-block bookkeeping held one loader wave to ~16 GB/s, groups of 8 sustain ~25 GB/s per CU
-// (tools/micro/loader_probe.hip: 6.5 TB/s chip-wide).
+// Streams every block of this CU's step into the ring, in consumption order (tile-major: for each
+// tile, its chunks, SwiGLU's two matrices interleaved per chunk). Slot b % nb is reused once every
+// consumer's next block is past b - nb. One wave issues everything, so the issue sequence IS the
+// stream rate: runs of 8 blocks go out as one asm block (saddr = matrix base, 32-bit VGPR offsets,
+// M0 stepped in place: ~4.5 instructions per 1 KiB DMA); a general
+// per-block sequence of ~25 dependent instructions held the wave to ~12 GB/s per CU where the
+// memory system gives ~25 (tools/engine_trace.py probes, tools/micro/loader_probe.hip).
 constexpr int LG = 8;
 static_assert(D % LG == 0, "publish granularity");
 // wait until at most (n rounded down to a multiple of 8) DMAs of this wave are in flight
@@ -705,43 +707,65 @@ __device__ __forceinline__ void wait_vm_le(int n) {
     default: wait_vm<56>(); break;
   }
 }
+// one 1 KiB block: base + voff (per lane 16 B) -> LDS dst
+__device__ __forceinline__ void dma1(const char* base, uint32_t voff, uint32_t dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(base), "s"(dst)
+               : "memory");
+}
+#define LLJ_DMA_NEXT "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+// 8 consecutive blocks of one matrix into 8 consecutive slots. Per-DMA VGPR offsets, no immediate
+// offsets: an LDS-DMA's immediate offset also moves its LDS destination (measured,
+// tools/micro/glds_offset_probe.hip), so M0 alone steps the slots.
+__device__ __forceinline__ void dma8_1(const char* base, uint32_t voff, uint32_t dst) {
+  unsigned keep, t1, t2, t3, t4, t5, t6, t7;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %10\n\t"
+               "v_add_u32 %1, 0x400, %8\n\tv_add_u32 %2, 0x800, %8\n\tv_add_u32 %3, 0xc00, %8\n\t"
+               "v_add_u32 %4, 0x1000, %8\n\tv_add_u32 %5, 0x1400, %8\n\tv_add_u32 %6, 0x1800, %8\n\t"
+               "v_add_u32 %7, 0x1c00, %8\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %8, %9 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %1, %9 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %2, %9 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %3, %9 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %4, %9 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %5, %9 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %6, %9 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %7, %9 nt\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6), "=&v"(t7)
+               : "v"(voff), "s"(base), "s"(dst)
+               : "memory", "scc");
+}
+// 4 consecutive chunks of two matrices, interleaved per chunk, into 8 consecutive slots
+__device__ __forceinline__ void dma8_2(const char* b0, const char* b1, uint32_t voff, uint32_t dst) {
+  unsigned keep, t1, t2, t3;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %7\n\t"
+               "v_add_u32 %1, 0x400, %4\n\tv_add_u32 %2, 0x800, %4\n\tv_add_u32 %3, 0xc00, %4\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %4, %5 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %4, %6 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %1, %5 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %1, %6 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %2, %5 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %2, %6 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %3, %5 nt\n\t" LLJ_DMA_NEXT
+               "global_load_lds_dwordx4 %3, %6 nt\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+               : "v"(voff), "s"(b0), "s"(b1), "s"(dst)
+               : "memory", "scc");
+}
+#undef LLJ_DMA_NEXT
+
 __device__ __forceinline__ void loader(Ctx& X, const Lds& L, const llj_engine_plan& P) {
   const Shape& s = X.s;
   const uint32_t ring = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)L.ring);
-  const int nb = L.nb;
+  const int nb = L.nb;  // a multiple of 8
   const bool free_run = (P.flags & 2) != 0;  // profiling: stream the step with no consumers
+  const uint32_t lane16 = 16u * (uint32_t)X.lane;
   stamp(P, X.lane, 121);
-  if (P.flags & 4) {  // profiling: the micro-benchmark's plain loop inside this kernel (bisecting the stream rate)
-    int slot = 0, cnt = 0, opi = 0;
-    for (int l = 0; l <= s.L; ++l) {
-      for (int op = (l == s.L ? OP_HEAD : OP_QKV); op <= (l == s.L ? OP_HEAD : OP_DOWN); ++op, ++opi) {
-        const int nt = tiles_of_cu(s, op), kc = op_kc(s, op), nm = op_nmat(op);
-        const char* w0 = op_weight(P, l, op, 0) + 16 * X.lane;
-        const char* w1 = op_weight(P, l, op, nm - 1) + 16 * X.lane;
-        for (int j = 0; j < nt; ++j) {
-          const size_t tile = (size_t)s.g + (size_t)j * s.G;
-          for (int c = 0; c < kc; ++c) {
-            for (int m = 0; m < nm; ++m) {
-              const char* src = (m ? w1 : w0) + (tile * kc + c) * 1024;
-              const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)slot * 1024u);
-              unsigned keep;
-              asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
-                           "s_mov_b32 m0, %0"
-                           : "=&s"(keep)
-                           : "v"(src), "s"(dst)
-                           : "memory");
-              if (++slot == nb) slot = 0;
-              if ((++cnt & 7) == 0) wait_vm<D>();
-            }
-          }
-        }
-        if (opi < 8) stamp(P, X.lane, 100 + opi);
-      }
-    }
-    wait_vm<0>();
-    stamp(P, X.lane, 120);
-    return;
-  }
   int b = 0, slot = 0;
   int pub = 0;    // blocks published as landed
   int limit = nb; // blocks that may be issued before the consumers' counts are read again
@@ -749,16 +773,13 @@ __device__ __forceinline__ void loader(Ctx& X, const Lds& L, const llj_engine_pl
   for (int l = 0; l <= s.L; ++l) {
     for (int op = (l == s.L ? OP_HEAD : OP_QKV); op <= (l == s.L ? OP_HEAD : OP_DOWN); ++op) {
       const int nt = tiles_of_cu(s, op), kc = op_kc(s, op), nm = op_nmat(op);
-      const char* w0 = op_weight(P, l, op, 0) + 16 * X.lane;
-      const char* w1 = op_weight(P, l, op, nm - 1) + 16 * X.lane;
-      for (int j0 = 0; j0 < nt; j0 += TG) {
-        const int ng = nt - j0 < TG ? nt - j0 : TG;
-        const int per_chunk = ng * nm, total = kc * per_chunk;
-        const size_t tstride = (size_t)s.G * kc * 1024;  // tile slot j0 + jj sits at tile g + (j0 + jj) G
-        const size_t t00 = (size_t)(s.g + j0 * s.G) * kc * 1024;
-        int c = 0, jj = 0, m = 0;  // cursor of the group's next block (tile-major: jj, then c, then m)
-        for (int i0 = 0; i0 < total; i0 += LG) {
-          const int n = total - i0 < LG ? total - i0 : LG;
+      const char* w0 = op_weight(P, l, op, 0);
+      const char* w1 = op_weight(P, l, op, nm - 1);
+      const int per_tile = kc * nm;
+      for (int j = 0; j < nt; ++j) {
+        const uint32_t toff = (uint32_t)(s.g + j * s.G) * (uint32_t)kc * 1024u;  // the tile's first chunk
+        for (int r0 = 0; r0 < per_tile; r0 += LG) {
+          const int n = per_tile - r0 < LG ? per_tile - r0 : LG;
           if (!free_run && b + n > limit) {
             // every block below F = min over consumers of their next block has been taken:
             // slots of blocks < F are free, so blocks < F + nb may be issued
@@ -786,22 +807,18 @@ __device__ __forceinline__ void loader(Ctx& X, const Lds& L, const llj_engine_pl
               if (spin_fail_loader(X, it)) { limit = b + nb; break; }
             }
           }
-#pragma unroll
-          for (int u = 0; u < LG; ++u) {
-            if (u < n) {
-              const char* src = (m ? w1 : w0) + t00 + (size_t)jj * tstride + (size_t)c * 1024;
-              const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)slot * 1024u);
-              unsigned keep;
-              asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
-                           "s_mov_b32 m0, %0"
-                           : "=&s"(keep)
-                           : "v"(src), "s"(dst)
-                           : "memory");
+          if (n == LG && slot + LG <= nb) {
+            const uint32_t dst = ring + (uint32_t)slot * 1024u;
+            if (nm == 1) dma8_1(w0, toff + (uint32_t)r0 * 1024u + lane16, dst);
+            else dma8_2(w0, w1, toff + (uint32_t)(r0 >> 1) * 1024u + lane16, dst);
+            slot += LG;
+            if (slot == nb) slot = 0;
+          } else {
+            for (int u = 0; u < n; ++u) {
+              const int r = r0 + u;
+              const int c = nm == 1 ? r : r >> 1;
+              dma1((nm == 2 && (r & 1)) ? w1 : w0, toff + (uint32_t)c * 1024u + lane16, ring + (uint32_t)slot * 1024u);
               if (++slot == nb) slot = 0;
-              if (++m == nm) {
-                m = 0;
-                if (++c == kc) { c = 0; ++jj; }
-              }
             }
           }
           b += n;
@@ -866,7 +883,7 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
     loader(X, L, P);
     return;
   }
-  if (P.flags & 6) return;  // profiling (loader-only stream rate): no step state is touched
+  if (P.flags & 2) return;  // profiling (loader-only stream rate): no step state is touched
   // ---- consumers. Step state written by the previous step (an earlier launch).
   if (X.wave == 0) stamp(P, X.lane, 0);
   const unsigned epoch = ar.ctl[0];
@@ -1008,7 +1025,7 @@ int llj_engine_step(const llj_engine_plan* plan, void* stream) {
   LLJ_REQUIRE((3 * P.C / 16 + G - 1) / G <= eng::TG && (P.V / 16 + G - 1) / G <= eng::kEopTiles &&
               (P.H / 16 + G - 1) / G <= eng::kEopTiles);
   const int nb = eng::ring_blocks(P.C, P.H, hs, 160 * 1024);
-  LLJ_REQUIRE(P.ring_blocks >= 2 * eng::D && P.ring_blocks <= nb);
+  LLJ_REQUIRE(P.ring_blocks >= 2 * eng::D && P.ring_blocks <= nb && P.ring_blocks % eng::LG == 0);
   const size_t lds = eng::lds_fixed(P.C, P.H, hs) + (size_t)P.ring_blocks * 1024;
   LLJ_REQUIRE(lds <= 160 * 1024 && lds > 80 * 1024);  // one workgroup per CU, every one resident
   static bool attr = false;

@@ -17,6 +17,15 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ 
   if (pos_inc && m == 0 && threadIdx.x == 0) *pos_inc += 1;
 }
 
+// any C (the any-shape path, csrc/generic.hip): bf16 elements
+__global__ __launch_bounds__(256) void embedding_any_kernel(const int* __restrict__ idx, const bf16_t* __restrict__ wte,
+                                                            bf16_t* __restrict__ out, int C, int* pos_inc) {
+  const int m = blockIdx.x;
+  const size_t r = (size_t)idx[m];
+  for (int v = threadIdx.x; v < C; v += blockDim.x) out[(size_t)m * C + v] = wte[r * C + v];
+  if (pos_inc && m == 0 && threadIdx.x == 0) *pos_inc += 1;
+}
+
 // ---- RMSNorm with the bf16 rounding points of model.py:281-283 on bf16 tensors. One block
 // per row; rows up to 8192 wide are loaded once into registers (x and the scale together,
 // before any use), so the kernel is one memory round trip.
@@ -343,6 +352,31 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const bf16_t* __restric
   }
 }
 
+// Streaming read of n16 16-byte words (the achievable HBM read rate the decode kernels are priced
+// against): grid-stride, 4 non-temporal loads in flight per thread, one float per workgroup out so
+// the loads stay live.
+__global__ __launch_bounds__(256) void stream_read_kernel(const uint4* __restrict__ p, size_t n16, float* out) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u* q = reinterpret_cast<const v4u*>(p);
+  uint32_t acc = 0;
+  const size_t stride = (size_t)gridDim.x * 256;
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const v4u a = __builtin_nontemporal_load(q + i), b = __builtin_nontemporal_load(q + i + stride);
+    const v4u c = __builtin_nontemporal_load(q + i + 2 * stride), d = __builtin_nontemporal_load(q + i + 3 * stride);
+    acc ^= a.x ^ b.y ^ c.z ^ d.w;
+  }
+  for (; i < n16; i += stride) acc ^= __builtin_nontemporal_load(q + i).x;
+  __shared__ uint32_t r[256];
+  r[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int k = 0; k < 256; ++k) t ^= r[k];
+    out[blockIdx.x] = (float)(t & 0xFFu);
+  }
+}
+
 }  // namespace llj
 
 using namespace llj;
@@ -350,8 +384,21 @@ using namespace llj;
 extern "C" {
 LLJ_TRACE_EXPORT(ops)
 
+int llj_stream_read(const void* p, size_t bytes, float* out, int grid, void* stream) {
+  LLJ_REQUIRE(p && out && bytes % 16 == 0 && grid > 0);
+  hipLaunchKernelGGL(stream_read_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4*)p, bytes / 16, out);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
 int llj_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, void* stream) {
-  LLJ_REQUIRE(M > 0 && C % 8 == 0);
+  LLJ_REQUIRE(M > 0 && C > 0);
+  if (C % 8) {
+    hipLaunchKernelGGL(embedding_any_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, idx, (const bf16_t*)wte,
+                       (bf16_t*)out, C, pos_inc);
+    LLJ_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(embedding_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, idx, (const uint4*)wte,
                      (uint4*)out, C / 8, pos_inc);
   LLJ_CHECK_LAUNCH();

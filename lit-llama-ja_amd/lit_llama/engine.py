@@ -128,16 +128,14 @@ class _Engine:
         self.plan.trace = self.trace.data_ptr()
         return self.trace
 
-    def probe_stream(self, st, plain: bool = False) -> None:
+    def probe_stream(self, st) -> None:
         """Profiling only: one launch in which the loader streams the whole step's weights with
-        no consumers (flow control off, no step state touched): the in-engine stream rate
-        (plain: a minimal issue loop instead of the loader's)."""
-        bit = 4 if plain else 2
-        self.plan.flags |= bit
+        no consumers (flow control off, no step state touched): the in-engine stream rate."""
+        self.plan.flags |= 2
         try:
             self.step(st)
         finally:
-            self.plan.flags &= ~bit
+            self.plan.flags &= ~2
 
     def step(self, st) -> None:
         rc = _hip.lib().llj_engine_step(ctypes.byref(self.plan), st)
@@ -215,8 +213,11 @@ class DecodeSession:
         self.steps_done = 1
         # decode-step operands (fixed for the session)
         self.specs = m._layer_specs()
-        need_i8 = any(s[0] == 2 for layer in self.specs["layers"] for s in layer) or self.specs["head"][0] == 2
-        self.work = _Work(m.config, B, self.dev, need_i8, self.S)
+        if m._generic():  # the any-shape kernels (csrc/generic.hip)
+            self.work = _Work(m.config, B, self.dev, False, self.S, generic=True)
+        else:
+            need_i8 = any(s[0] == 2 for layer in self.specs["layers"] for s in layer) or self.specs["head"][0] == 2
+            self.work = _Work(m.config, B, self.dev, need_i8, self.S)
         self.graph = None  # the caches / operands may have changed
         why = engine_supported(m, self.specs, B, self.S)
         self.engine = _Engine(m, self.specs, self, greedy=self.top_k == 1) if why is None else None

@@ -57,11 +57,13 @@ class LLaMAConfig:
         return cls(**llama_configs[name])
 
     def kernel_support(self) -> Optional[str]:
-        """None if the gfx950 kernels take this configuration, else why not. The GEMVs stream
-        128-deep K chunks and 16-column tiles (n_embd % 128 == 0; n_hidden, 3 n_embd and the padded
-        vocab are then multiples of 16), the fused RoPE / attention kernels take head_size 64 or
-        128. The JA fork's 19M / 49M configs (head 64), 7B / 13B / 30B / 65B (head 128) run; its
-        125M config (n_embd 780, head 78) and the reference test's n_embd 32 / head 2 do not."""
+        """None if the streaming gfx950 kernels take this configuration, else why not -- such a
+        model runs on the any-shape kernels (csrc/generic.hip) instead. The GEMVs stream 128-deep
+        K chunks and 16-column tiles (n_embd % 128 == 0; n_hidden, 3 n_embd and the padded vocab
+        are then multiples of 16), the fused RoPE / attention kernels take head_size 64 or 128. The
+        JA fork's 19M / 49M configs (head 64), 7B / 13B / 30B / 65B (head 128) take the streaming
+        path; its 125M config (n_embd 780, head 78) and the reference test's n_embd 32 / head 2 the
+        any-shape path."""
         hs = self.n_embd // self.n_head
         if self.n_embd % self.n_head:
             return f"n_embd {self.n_embd} is not a multiple of n_head {self.n_head}"
@@ -152,12 +154,43 @@ def _wspec(lin: nn.Module):
     raise TypeError(f"unsupported Linear class {type(lin).__name__}")
 
 
+def _gspec(lin: nn.Module):
+    """Operands of a Linear for the any-shape kernel llj_g_linear: (wkind, W, scales, zeros, bits,
+    group) -- wkind 1 dense bf16, 0 ColBlockQuantizedLinear on its reference buffers."""
+    if hasattr(lin, "_gspec"):
+        return lin._gspec()
+    if isinstance(lin, nn.Linear):
+        w = lin.weight
+        _hip.require_device(w, "Linear.weight")
+        if w.dtype != torch.bfloat16 or not w.is_contiguous():
+            raise TypeError("dense Linear weights must be contiguous bfloat16 on the GPU")
+        if lin.bias is not None:
+            raise NotImplementedError("biased dense Linear is not on the LLaMA path")
+        return 1, w, None, None, 16, w.shape[1]
+    raise NotImplementedError(f"{type(lin).__name__} has no any-shape kernel (LLM.int8 needs n_embd % 128 == 0 "
+                              "and head size 64 / 128)")
+
+
 class _Work:
     """Per-call scratch for M rows (allocated from torch's caching allocator)."""
 
-    def __init__(self, cfg: LLaMAConfig, M: int, device, need_i8: bool, S: int = 0, gemm: bool = False):
+    def __init__(self, cfg: LLaMAConfig, M: int, device, need_i8: bool, S: int = 0, gemm: bool = False,
+                 generic: bool = False):
         C, H = cfg.n_embd, MLP.hidden(cfg)
         bf = torch.bfloat16
+        self.generic = generic  # the any-shape kernels (LLaMA._blocks_generic)
+        if generic:
+            self.x = torch.empty(M, C, dtype=bf, device=device)
+            self.xn = torch.empty(M, C, dtype=bf, device=device)
+            self.qkv = torch.empty(M, 3 * C, dtype=bf, device=device)
+            self.q = torch.empty(M, C, dtype=bf, device=device)
+            self.y = torch.empty(M, C, dtype=bf, device=device)
+            self.a1 = torch.empty(M, H, dtype=bf, device=device)
+            self.a2 = torch.empty(M, H, dtype=bf, device=device)
+            self.h = torch.empty(M, H, dtype=bf, device=device)
+            self.gemm = self.flash = self.pre = self.hand = False
+            self.i8ws = self.att_ws = self.nst = self.rs = None
+            return
         self.gemm = gemm  # many rows: the prefill GEMMs (LLaMA._blocks_gemm)
         self.flash = False  # T-row prompt attention on the MFMA flash kernel (set by LLaMA._run)
         self.x = torch.empty(M, C, dtype=bf, device=device)
@@ -204,12 +237,6 @@ class LLaMA(nn.Module):
         self.rope_cache: Optional[RoPECache] = None
         self.mask_cache: Optional[MaskCache] = None
         self.kv_caches: List[KVCache] = []
-        # a model built on the GPU must be one the kernels take: fail here, with the reason, rather
-        # than with EINVAL in the middle of a forward (CPU / meta construction stays allowed for
-        # checkpoint conversion and state-dict work; forward is GPU-only anyway)
-        why = config.kernel_support()
-        if why is not None and self.lm_head.weight.device.type == "cuda":
-            raise NotImplementedError(f"LLaMAConfig not supported by the MI355X kernels: {why}")
 
     def _init_weights(self, module: nn.Module) -> None:
         """reference model.py:78-82"""
@@ -246,9 +273,6 @@ class LLaMA(nn.Module):
         assert max_seq_length <= block_size, f"Cannot attend to {max_seq_length}, block size is only {block_size}"
         assert T <= block_size, f"Cannot forward sequence of length {T}, block size is only {block_size}"
         _hip.require_device(idx, "idx")
-        why = self.config.kernel_support()
-        if why is not None:
-            raise NotImplementedError(f"LLaMAConfig not supported by the MI355X kernels: {why}")
         self._check_dtype()
         if self.rope_cache is None:
             self.rope_cache = self.build_rope_cache(idx)
@@ -291,9 +315,12 @@ class LLaMA(nn.Module):
         M = B * T
         dev = idx.device
         specs = self._layer_specs()
-        need_i8 = any(s[0] == 2 for layer in specs["layers"] for s in layer) or specs["head"][0] == 2
-        w = _Work(cfg, M, dev, need_i8, S, gemm=self._gemm_ok(specs, M))
-        w.flash = self._flash_ok(pos, T, S)
+        if self._generic():
+            w = _Work(cfg, M, dev, False, S, generic=True)
+        else:
+            need_i8 = any(s[0] == 2 for layer in specs["layers"] for s in layer) or specs["head"][0] == 2
+            w = _Work(cfg, M, dev, need_i8, S, gemm=self._gemm_ok(specs, M))
+            w.flash = self._flash_ok(pos, T, S)
         st = _hip.stream()
         ids = idx.reshape(-1).to(torch.int32)
         _hip.call("llj_embedding", ids.data_ptr(), self.transformer.wte.weight.data_ptr(), w.x.data_ptr(), M,
@@ -311,8 +338,17 @@ class LLaMA(nn.Module):
         self._head(w.x, M, specs, logits, st, w)
         return logits.view(B, T, V)
 
+    def _generic(self) -> bool:
+        """True when this configuration runs on the any-shape kernels (kernel_support)."""
+        return self.config.kernel_support() is not None
+
     # -- weight operands, gathered once per call
     def _layer_specs(self):
+        if self._generic():
+            return {"layers": [tuple(_gspec(m) for m in (blk.attn.c_attn, blk.attn.c_proj, blk.mlp.c_fc1,
+                                                         blk.mlp.c_fc2, blk.mlp.c_proj))
+                               for blk in self.transformer.h],
+                    "head": _gspec(self.lm_head)}
         layers = []
         for blk in self.transformer.h:
             layers.append((_wspec(blk.attn.c_attn), _wspec(blk.attn.c_proj), _wspec(blk.mlp.c_fc1),
@@ -385,12 +421,46 @@ class LLaMA(nn.Module):
             _hip.call("llj_gemm_silu_mul", f2, w.xn.data_ptr(), C, w2.data_ptr(), P(s2), w.h.data_ptr(), H, M, H, C, st)
             _hip.call("llj_gemm_resid", fd, w.h.data_ptr(), H, wd.data_ptr(), P(sd), w.x.data_ptr(), C, M, C, H, st)
 
+    @staticmethod
+    def _glinear(spec, A, M, K, N, out, resid, st):
+        kind, W, sc, zr, bits, group = spec
+        _hip.call("llj_g_linear", kind, A.data_ptr(), A.stride(0), M, K, W.data_ptr(), _hip.ptr(sc), _hip.ptr(zr), bits,
+                  group, N, out.data_ptr(), out.stride(0), None if resid is None else resid.data_ptr(),
+                  0 if resid is None else resid.stride(0), st)
+
+    def _blocks_generic(self, w, specs, kv, pos, B, T, S, st):
+        """The blocks on the any-shape kernels (csrc/generic.hip), per layer (model.py:162-175):
+        rms_1 -> c_attn -> split + RoPE + KV write -> attention -> c_proj + residual -> rms_2 ->
+        c_fc1, c_fc2 -> silu * mul -> mlp.c_proj + residual."""
+        cfg = self.config
+        C, H, nh = cfg.n_embd, MLP.hidden(cfg), cfg.n_head
+        M = B * T
+        for i, blk in enumerate(self.transformer.h):
+            sa, sp, s1, s2, sd = specs["layers"][i]
+            kc, vc = kv[i]
+            _hip.call("llj_g_rmsnorm", w.x.data_ptr(), C, blk.rms_1.scale.data_ptr(), blk.rms_1.eps, w.xn.data_ptr(), C,
+                      M, C, st)
+            self._glinear(sa, w.xn, M, C, 3 * C, w.qkv, None, st)
+            _hip.call("llj_g_rope_kv", w.qkv.data_ptr(), w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                      self.rope_cache.data_ptr(), pos.data_ptr(), B, T, C, nh, S, st)
+            _hip.call("llj_g_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(), pos.data_ptr(),
+                      B, T, C, nh, S, st)
+            self._glinear(sp, w.y, M, C, C, w.x, w.x, st)
+            _hip.call("llj_g_rmsnorm", w.x.data_ptr(), C, blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(), C,
+                      M, C, st)
+            self._glinear(s1, w.xn, M, C, H, w.a1, None, st)
+            self._glinear(s2, w.xn, M, C, H, w.a2, None, st)
+            _hip.call("llj_g_silu_mul", w.a1.data_ptr(), w.a2.data_ptr(), w.h.data_ptr(), M * H, st)
+            self._glinear(sd, w.h, M, H, C, w.x, w.x, st)
+
     def _blocks(self, w, specs, kv, pos, B, T, S, st):
         cfg = self.config
         C, H, nh = cfg.n_embd, MLP.hidden(cfg), cfg.n_head
         M = B * T
         rope = self.rope_cache
         P = _hip.ptr
+        if w.generic:
+            return self._blocks_generic(w, specs, kv, pos, B, T, S, st)
         if w.gemm:
             return self._blocks_gemm(w, specs, kv, pos, B, T, S, st)
         for i, blk in enumerate(self.transformer.h):
@@ -460,8 +530,13 @@ class LLaMA(nn.Module):
     def _head(self, x, M, specs, out, st, w):
         cfg = self.config
         C, V = cfg.n_embd, cfg.padded_vocab_size
-        f, W, sz = specs["head"]
         ln = self.transformer.ln_f
+        if w.generic:  # ln_f + lm_head on the any-shape kernels
+            xn = w.xn if M <= w.xn.shape[0] else torch.empty_like(x)
+            _hip.call("llj_g_rmsnorm", x.data_ptr(), x.stride(0), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), C, M, C, st)
+            self._glinear(specs["head"], xn, M, C, V, out, None, st)
+            return
+        f, W, sz = specs["head"]
         rs = nst = None
         if f == 2:
             xn = torch.empty_like(x)
@@ -529,10 +604,14 @@ class _BlockHost:
         blk, cfg = self.blk, self.cfg
         B, T, C = x.shape
         M = B * T
-        specs = {"layers": [(_wspec(blk.attn.c_attn), _wspec(blk.attn.c_proj), _wspec(blk.mlp.c_fc1),
-                             _wspec(blk.mlp.c_fc2), _wspec(blk.mlp.c_proj))]}
-        need_i8 = any(s[0] == 2 for s in specs["layers"][0])
-        w = _Work(cfg, M, x.device, need_i8)
+        mods = (blk.attn.c_attn, blk.attn.c_proj, blk.mlp.c_fc1, blk.mlp.c_fc2, blk.mlp.c_proj)
+        if cfg.kernel_support() is not None:  # the any-shape kernels
+            specs = {"layers": [tuple(_gspec(m) for m in mods)]}
+            w = _Work(cfg, M, x.device, False, generic=True)
+        else:
+            specs = {"layers": [tuple(_wspec(m) for m in mods)]}
+            need_i8 = any(s[0] == 2 for s in specs["layers"][0])
+            w = _Work(cfg, M, x.device, need_i8)
         w.x.copy_(x.reshape(M, C))
         kv = [(torch.zeros(B, cfg.n_head, T, C // cfg.n_head, dtype=torch.bfloat16, device=x.device),
                torch.zeros(B, cfg.n_head, T, C // cfg.n_head, dtype=torch.bfloat16, device=x.device))]
@@ -559,6 +638,11 @@ class _OneBlock:
 
     def _attention(self, *a):
         LLaMA._attention(self, *a)
+
+    def _blocks_generic(self, *a):
+        LLaMA._blocks_generic(self, *a)
+
+    _glinear = staticmethod(LLaMA._glinear)
 
 
 class CausalSelfAttention(nn.Module):

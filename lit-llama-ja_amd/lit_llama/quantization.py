@@ -77,6 +77,7 @@ class ColBlockQuantizedLinear(torch.nn.Module):
         self.register_buffer("_sz", None, persistent=False)
         self._qkey = None   # (data_ptr, version) of quant_weight right after its in-place repack
         self._szkey = None  # (scales, zeros) identity the _sz pairs were built from
+        self._g = None      # any-shape path: (key, fp32 scales, fp32 zeros)
 
     # ---- reference buffer utilities (quantization.py:374-409) -------------------------
     def pack_weight(self, weight):
@@ -180,12 +181,28 @@ class ColBlockQuantizedLinear(torch.nn.Module):
             self.quant_weight.t().view(-1).copy_(ref.t().reshape(-1))
             self._qkey = None
         self._szkey = None
+        self._g = None
         return super()._apply(fn, *args, **kwargs)
 
     def _wspec(self):
         """(wfmt, weight operand, sz operand) for the fused model kernels."""
         self._prepare()
         return self.wfmt, self.quant_weight, self._sz
+
+    def _gspec(self):
+        """Operands of the any-shape kernel (llj_g_linear, csrc/generic.hip) for shapes the
+        streaming tiling does not take: (0, quant_weight in the reference's column-major layout,
+        fp32 scales (N, G), fp32 zeros (N, G), bits, group). Nothing is repacked."""
+        qw = self._reference_codes()
+        if qw is self.quant_weight and not qw.t().is_contiguous():
+            self.quant_weight = qw = qw.t().contiguous().t()
+        _hip.require_device(qw, "ColBlockQuantizedLinear.quant_weight")
+        sc, zr = self.scales, self.zeros
+        key = (sc.data_ptr(), sc._version, zr.data_ptr(), zr._version, qw.device)
+        if self._g is None or self._g[0] != key:
+            self._g = (key, sc.to(device=qw.device, dtype=torch.float32).contiguous(),
+                       zr.to(device=qw.device, dtype=torch.float32).contiguous())
+        return 0, qw, self._g[1], self._g[2], self.bits, self.tile_cols
 
     @property
     def wfmt(self) -> int:
@@ -199,8 +216,17 @@ class ColBlockQuantizedLinear(torch.nn.Module):
         _hip.require_device(inp, "input")
         if inp.dtype != torch.bfloat16:
             raise TypeError(f"ColBlockQuantizedLinear HIP path computes in bfloat16, got {inp.dtype}")
-        self._prepare()
         K, N = self.in_features, self.out_features
+        if not self._supported():  # the any-shape kernel on the reference buffers
+            if self.bias is not None:
+                raise NotImplementedError("biased ColBlockQuantizedLinear outside the streaming tiling")
+            x2 = inp.reshape(-1, K).contiguous()
+            out = torch.empty((x2.shape[0], N), dtype=inp.dtype, device=inp.device)
+            kind, qw, sc, zr, bits, group = self._gspec()
+            _hip.call("llj_g_linear", kind, x2.data_ptr(), K, x2.shape[0], K, qw.data_ptr(), sc.data_ptr(), zr.data_ptr(),
+                      bits, group, N, out.data_ptr(), N, None, 0, _hip.stream())
+            return out.reshape(*inp.shape[:-1], N)
+        self._prepare()
         x2 = _as_rows(inp, K)
         out = torch.empty((x2.shape[0], N), dtype=inp.dtype, device=inp.device)
         bias = None if self.bias is None else self.bias.to(torch.bfloat16)

@@ -36,8 +36,8 @@ def _header_decls():
                 kinds.append("f")
             elif a.startswith("int"):
                 kinds.append("i")
-            elif a.startswith("unsigned long long"):
-                kinds.append("u64")
+            elif a.startswith("unsigned long long") or a.startswith("size_t"):
+                kinds.append("u64")  # ctypes: c_size_t is c_ulong is c_ulonglong on LP64
             else:
                 raise AssertionError(f"unexpected argument kind {a!r} in {name}")
         decls[name] = (ret, kinds)
@@ -181,8 +181,8 @@ def test_product_path_has_no_cpu_fallback():
 
 
 def test_unsupported_configs_are_named():
-    """Configurations the kernels do not take are reported with the reason (LLaMAConfig.
-    kernel_support), and a GPU-side construction of one raises instead of failing mid-forward."""
+    """Configurations the streaming kernels do not tile are reported with the reason (LLaMAConfig.
+    kernel_support); those models run on the any-shape kernels (tests/test_generic_gpu.py)."""
     from lit_llama import LLaMAConfig
 
     assert "780" in LLaMAConfig.from_name("125M").kernel_support()  # JA fork config, reference model.py:48-51

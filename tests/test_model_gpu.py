@@ -526,17 +526,6 @@ def gen_kw(model, prompt, n, **kw):
     return G.generate(model, torch.from_numpy(prompt).cuda(), n, **kw).cpu().numpy()
 
 
-def test_unsupported_config_raises_at_construction():
-    """The JA fork's 125M config (n_embd 780, head_size 78; reference model.py:48-51) built on the
-    GPU fails at construction with the reason, not with EINVAL mid-forward."""
-    from lit_llama import LLaMA
-    from lit_llama.utils import EmptyInitOnDevice
-
-    with pytest.raises(NotImplementedError, match="780"):
-        with EmptyInitOnDevice(device=torch.device("cuda"), dtype=torch.bfloat16):
-            LLaMA.from_name("125M")
-
-
 def test_generate_main_end_to_end(tmp_path, capsys):
     """generate.py main (reference generate.py:92-155) end to end on a random 19M checkpoint:
     checkpoint -> llama_model_lookup -> HF tokenizer encode -> generate with the CLI defaults

@@ -102,11 +102,6 @@ def main():
             torch.cuda.synchronize()
             t = tr.view(-1, 128).cpu().numpy().astype(np.float64)[:G]
             res["probe_one_alloc_stream_end_us"] = float(np.median((t[:, 120] - t[:, 121]) / 100.0))
-            tr.zero_()
-            eng_.probe_stream(st, plain=True)
-            torch.cuda.synchronize()
-            t = tr.view(-1, 128).cpu().numpy().astype(np.float64)[:G]
-            res["probe_plain_loop_stream_end_us"] = float(np.median((t[:, 120] - t[:, 121]) / 100.0))
             eng_.layers = saved_layers
             eng_.plan.layers = eng_.layers.data_ptr()
             del big
@@ -147,8 +142,7 @@ def main():
         print(f"loader op {r['op']} last DMA issued: median {r['median_us']:.2f} max {r['max_us']:.2f}")
     print("loader-only probe, last DMA of each op (us after the loader's start): " +
           " ".join(f"{v:.2f}" for v in res["probe_loader_op_issued"]) + f"; stream end {res['probe_stream_end_us']:.1f}; "
-          f"weights in one allocation: stream end {res['probe_one_alloc_stream_end_us']:.1f}; "
-          f"plain issue loop: {res['probe_plain_loop_stream_end_us']:.1f}")
+          f"weights in one allocation: stream end {res['probe_one_alloc_stream_end_us']:.1f}")
     print(f"loader end {res['loader_end_median_us']:.1f}; head staged {res['head_staged_median_us']:.1f}, "
           f"head done {res['head_done_median_us']:.1f} (max {res['head_done_max_us']:.1f})")
 

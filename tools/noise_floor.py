@@ -14,6 +14,9 @@ GEMM is exact in every order; its dequantization product SCA * SCB / 127^2 * acc
 association) and its fp16 outlier side product take the alternative orders.
 
 Usage: python tools/noise_floor.py [--out profiles/r03_noise_floor.json]  (CPU, a few minutes)
+       python tools/noise_floor.py --generic [--out profiles/r03_noise_floor_generic.json]
+         the any-shape configs of tests/test_generic_gpu.py (reference test n_embd 32 x 16 layers,
+         3 x 64 rows no-cache; 125M prompt rows + decode steps, bf16 and gptq.int4)
 """
 from __future__ import annotations
 
@@ -119,12 +122,52 @@ def rels(a, b):
             for i in range(a.shape[0]) for s in range(a.shape[1])]
 
 
+def _case(name, outs):
+    case = {"case": name, "rel_base_vs_f64": rels(outs["base"], outs["f64"]),
+            "rel_base_vs_chunk": rels(outs["base"], outs["chunk"]), "rel_f64_vs_chunk": rels(outs["f64"], outs["chunk"])}
+    case["floor_max"] = max(max(case[k]) for k in case if k.startswith("rel_"))
+    case["floor_mean"] = float(np.mean([v for k in case if k.startswith("rel_") for v in case[k]]))
+    print(f"[noise] {name}: floor max {case['floor_max']:.3e} mean {case['floor_mean']:.3e}", flush=True)
+    return case
+
+
+def generic_cases():
+    from tests import test_generic_gpu as TG
+
+    cases = []
+    cfg = TG.REF_TEST
+    pb, _, lin = T.oracle_linears(T.make_params(cfg, 32), None)
+    idx = np.random.default_rng(3).integers(0, cfg.vocab_size, (3, 64))
+    cases.append(_case("ref-test n_embd 32 x16 no-cache 3x64 rows",
+                       {o: orc_variant(cfg, pb, lin, o).forward(idx) for o in ("base", "f64", "chunk")}))
+    cfg = TG.C125
+    p = T.make_params(cfg, 125)
+    ids = np.random.default_rng(12).integers(3, cfg.vocab_size, (2, 12 + 5))
+    for mode in (None, "gptq.int4"):
+        pb, _, lin = T.oracle_linears(p, mode)
+        outs_rows, outs_steps = {}, {}
+        for o in ("base", "f64", "chunk"):
+            st, rows = T._oracle_steps(orc_variant(cfg, pb, lin, o), ids, t_prompt=12, steps=4, s=32, all_rows=True)
+            outs_rows[o], outs_steps[o] = rows, st
+        cases.append(_case(f"125M {mode} prompt rows", outs_rows))
+        cases.append(_case(f"125M {mode} steps", outs_steps))
+    return cases
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=str(REPO / "profiles" / "r03_noise_floor.json"))
+    ap.add_argument("--out", default=None)
     ap.add_argument("--widths", default="4096,5120")
+    ap.add_argument("--generic", action="store_true")
     args = ap.parse_args()
     res = {"what": __doc__.split("\n\n")[0], "cases": []}
+    if args.generic:
+        res["cases"] = generic_cases()
+        out = args.out or str(REPO / "profiles" / "r03_noise_floor_generic.json")
+        Path(out).write_text(json.dumps(res, indent=1))
+        print(f"wrote {out}")
+        return
+    args.out = args.out or str(REPO / "profiles" / "r03_noise_floor.json")
     for width in [int(w) for w in args.widths.split(",")]:
         cfg = T.C7 if width == 4096 else T.C13
         p = T.make_params(cfg, T.SEEDS[width])
