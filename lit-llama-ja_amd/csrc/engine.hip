@@ -117,7 +117,8 @@ __device__ __forceinline__ uint32_t bf_key(uint32_t b) { return (b & 0x8000u) ? 
 // profiling stamps (plan.trace != NULL): [g][128]; consumers: 0 start, per layer l at 2 + 12 l:
 // +0 x staged, +1 QKV done, +2 attention done, +3 y staged, +4 c_proj done, +5 x_mid staged,
 // +6 SwiGLU done, +7 h staged, +8 down done; the loader: 100 + op index of its last DMA of each op
-// (per layer, layers 0..1 only: 100..107), 120 stream end, 121 loader start; 126 head staged, 127 head done
+// (per layer, layers 0..1 only: 100..107), 108..119 inside consume (QKV / SwiGLU of layers 0, 1: A
+// in registers, blocks done, barrier passed), 120 stream end, 121 loader start; 126 head staged, 127 head done
 __device__ __forceinline__ void stamp(const llj_engine_plan& P, int lane, int k) {
   if (P.trace && lane == 0 && k < 128) P.trace[(size_t)blockIdx.x * 128 + k] = __builtin_amdgcn_s_memrealtime();
 }
@@ -161,7 +162,7 @@ __device__ __forceinline__ const char* op_weight(const llj_engine_plan& P, int l
 // carve (bytes, 16-aligned): ctl words | A (max(C, H) bf16) | xres[2] (C bf16) | red[2][NC][TG][2][16]
 // f32 | eop[2] (epilogue operands) | misc[64] f32 ([0, NC) sums of squares, [16, 16 + NC) row sums,
 // [32, 32 + NC) argmax, [48] last-arriver flag) | attention scratch | ring (nb x 1 KiB)
-constexpr int kCtlWords = 32;  // [0] landed, [1 .. NC] freed per consumer, [16] consumer barrier
+constexpr int kCtlWords = 32;  // [0] landed, [1 .. NC] next block per consumer, [16] consumer barrier, [17] max wanted block
 struct Lds {
   unsigned* ctl;
   unsigned char* ring;
@@ -197,7 +198,9 @@ struct Ctx {
   unsigned long long t0;
   bool aborted;
   unsigned bar_gen;   // consumer barriers passed
+  const llj_engine_plan* plan;
   int n_used;         // CU-stream index of the next block of this op (consumers)
+  int stamp_base;     // profiling: stamp index base inside consume (-1 = none)
 };
 
 // bounded spin bookkeeping: true = give up (a timeout here or anywhere in the grid). Global polls
@@ -456,15 +459,27 @@ __device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop,
     }
   }
   const int per_tile = kc * nm;
+  const llj_engine_plan* SP = X.plan;
+  if (X.stamp_base >= 0 && w == 0) stamp(*SP, lane, X.stamp_base + 0);  // A fragments in registers
   int gbase = X.n_used;  // CU-stream index of the current group's first block
   int landed = 0;
   unsigned it = 0;
-  // block b's bytes from the ring, once the loader has published it as landed
-  auto take = [&](int b) -> u32x4 {
+  // wait for block b; a consumer that has to wait records b in ctl[17] (LDS max) so the loader,
+  // stalled on a full ring, knows to publish landings early (the read-ahead means b may be past
+  // this consumer's published next block)
+  auto wait_landed = [&](int b) {
+    if (landed > b) return;
+    landed = (int)lds_ld(L.ctl + 0);
+    if (landed > b) return;
+    if (lane == 0) __hip_atomic_fetch_max(L.ctl + 17, (unsigned)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     while (landed <= b) {
       landed = (int)lds_ld(L.ctl + 0);
       if (landed > b || spin_fail_lds(X, it)) break;
     }
+  };
+  // block b's bytes from the ring, once the loader has published it as landed
+  auto take = [&](int b) -> u32x4 {
+    wait_landed(b);
     const unsigned q = __umulhi((unsigned)b, L.nb_magic);
     return *reinterpret_cast<const u32x4*>(L.ring + (size_t)((unsigned)b - q * (unsigned)L.nb) * 1024 + 16 * lane);
   };
@@ -512,7 +527,9 @@ __device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop,
       }
     }
     gbase += ng * per_tile;
+    if (X.stamp_base >= 0 && w == 0 && j0 == 0) stamp(*SP, lane, X.stamp_base + 1);  // group's blocks done
     cbarrier(X, L);
+    if (X.stamp_base >= 0 && w == 0 && j0 == 0) stamp(*SP, lane, X.stamp_base + 2);  // barrier passed
     for (int jj = w; jj < ng; jj += NC) {
       const int slot = j0 + jj;
       const int tile = s.g + slot * s.G;
@@ -766,6 +783,10 @@ __device__ __forceinline__ void loader(Ctx& X, const Lds& L, const llj_engine_pl
   const bool free_run = (P.flags & 2) != 0;  // profiling: stream the step with no consumers
   const uint32_t lane16 = 16u * (uint32_t)X.lane;
   stamp(P, X.lane, 121);
+  if (P.flags & 4) {  // profiling: consumers alone (every block "landed", nothing streamed; results invalid)
+    if (X.lane == 0) lds_st(L.ctl + 0, 0x7fffffffu);
+    return;
+  }
   int b = 0, slot = 0;
   int pub = 0;    // blocks published as landed
   int limit = nb; // blocks that may be issued before the consumers' counts are read again
@@ -785,19 +806,20 @@ __device__ __forceinline__ void loader(Ctx& X, const Lds& L, const llj_engine_pl
             // slots of blocks < F are free, so blocks < F + nb may be issued
             unsigned it = 0;
             for (;;) {
-              int F = 0x7fffffff, Fmax = 0;
+              int F = 0x7fffffff;
 #pragma unroll
               for (int w = 0; w < NC; ++w) {
                 const int f = (int)lds_ld(L.ctl + 1 + w);
                 F = f < F ? f : F;
-                Fmax = f > Fmax ? f : Fmax;
               }
               limit = F + nb;
               if (limit >= b + n) break;
-              // ring full. A consumer waiting for an unpublished block gets the oldest group in
-              // flight published (a wait for just those DMAs); draining the whole window here
-              // instead would make every ring-bound phase stop-and-go at one DMA latency per group
-              if (Fmax >= pub && pub < b) {
+              // ring full. A consumer waiting for an unpublished block (ctl[17]: the highest block
+              // any consumer has waited for) gets the oldest group in flight published (a wait for
+              // just those DMAs); draining the whole window here instead would make every
+              // ring-bound phase stop-and-go at one DMA latency per group
+              const int want = (int)lds_ld(L.ctl + 17);
+              if (want >= pub && pub < b) {
                 const int keep_n = b - pub > LG ? b - pub - LG : 0;
                 const int kq = ((keep_n >> 3) << 3) < 56 ? ((keep_n >> 3) << 3) : 56;
                 wait_vm_le(kq);
@@ -850,6 +872,8 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
   X.aborted = false;
   X.bar_gen = 0;
   X.n_used = 0;
+  X.stamp_base = -1;
+  X.plan = &P;
   X.t0 = __builtin_amdgcn_s_memrealtime();
   const int C = s.C, H = s.H;
   Lds L;
@@ -945,6 +969,7 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
                              op == OP_DOWN ? H : C);
     if (X.wave == 0 && l < 8 && op != OP_HEAD) stamp(P, X.lane, sb + 2 * op + (op == OP_QKV ? 0 : 1));
     if (op == OP_HEAD && X.wave == 0) stamp(P, X.lane, 126);
+    X.stamp_base = (l < 2 && (op == OP_SW || op == OP_QKV)) ? 108 + 3 * (2 * l + (op == OP_SW)) : -1;
     consume(X, L, eop, op, asum, red_par, E);
     if (X.wave == 0 && l < 8 && op == OP_DOWN) stamp(P, X.lane, sb + 8);
   }

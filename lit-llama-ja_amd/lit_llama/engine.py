@@ -137,6 +137,15 @@ class _Engine:
         finally:
             self.plan.flags &= ~2
 
+    def probe_consumers(self, st) -> None:
+        """Profiling only: one step with every ring block taken as landed and nothing streamed --
+        the consumers' and edges' own time. Results and the session's state are invalid after."""
+        self.plan.flags |= 4
+        try:
+            self.step(st)
+        finally:
+            self.plan.flags &= ~4
+
     def step(self, st) -> None:
         rc = _hip.lib().llj_engine_step(ctypes.byref(self.plan), st)
         if rc != 0:

@@ -109,6 +109,25 @@ def main():
             s.graph = None  # recapture with the trace pointer
             s.decode(2)
             torch.cuda.synchronize()
+            traced = tr.clone()
+            # consumers alone (nothing streamed): the step without the weight stream
+            tr.zero_()
+            s.engine.probe_consumers(st)
+            torch.cuda.synchronize()
+            tc = tr.view(-1, 128).cpu().numpy().astype(np.float64)
+            Gc = int((tc[:, 0] > 0).sum())
+            tc = tc[:Gc]
+            rc = (tc - tc[:, 0:1]) / 100.0
+            res["consumers_only_phases"] = [
+                {"layer": l, "phase": nm, "median_us": float(np.median(rc[:, 2 + 12 * l + k]))}
+                for l in range(min(2, args.layers)) for k, nm in enumerate(NAMES)]
+            res["consumers_only_head_done_us"] = float(np.median(rc[:, 127]))
+            res["consumers_only_inside"] = {
+                f"L{l} {op}": {"A_in_regs": float(np.median(rc[:, 108 + 3 * (2 * l + i)])),
+                               "blocks_done": float(np.median(rc[:, 109 + 3 * (2 * l + i)])),
+                               "barrier_passed": float(np.median(rc[:, 110 + 3 * (2 * l + i)]))}
+                for l in range(2) for i, op in enumerate(("QKV", "SwiGLU"))}
+            tr.copy_(traced)
             t = tr.view(-1, 128).cpu().numpy()
             G = int((t[:, 0] > 0).sum())
             t = t[:G].astype(np.float64)
@@ -143,6 +162,13 @@ def main():
     print("loader-only probe, last DMA of each op (us after the loader's start): " +
           " ".join(f"{v:.2f}" for v in res["probe_loader_op_issued"]) + f"; stream end {res['probe_stream_end_us']:.1f}; "
           f"weights in one allocation: stream end {res['probe_one_alloc_stream_end_us']:.1f}")
+    prev = 0.0
+    for r in res["consumers_only_phases"]:
+        print(f"consumers only L{r['layer']} {r['phase']:>13}: median {r['median_us']:8.2f} (+{r['median_us'] - prev:6.2f})")
+        prev = r["median_us"]
+    print(f"consumers only: head done {res['consumers_only_head_done_us']:.1f} us")
+    for k, v in res["consumers_only_inside"].items():
+        print(f"consumers only inside {k}: " + ", ".join(f"{a} {b:.2f}" for a, b in v.items()))
     print(f"loader end {res['loader_end_median_us']:.1f}; head staged {res['head_staged_median_us']:.1f}, "
           f"head done {res['head_done_median_us']:.1f} (max {res['head_done_max_us']:.1f})")
 
