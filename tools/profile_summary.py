@@ -36,7 +36,12 @@ def op_of(name: str, grid: int) -> str | None:
     if not name.startswith("llj::gemv_kernel<"):
         return None
     a = [int(x) for x in name[len("llj::gemv_kernel<"):-1].split(",")]
-    ep, nw = a[2], a[3]
+    ep, nw, mb = a[2], a[3], a[5]
+    if mb != 1:
+        # a multi-row instantiation in the bs=1 run is a prompt slice (8 rows of the 16-token
+        # prompt): its second slice reads the weights back from the 256 MB MALL, so its HBM bytes
+        # fall below the algorithmic bytes (the round-2 "0.809x" row) -- not a decode op
+        return None
     wgs = grid // (nw * 64)
     if ep == 2:
         return "qkv"
