@@ -126,6 +126,14 @@ int llj_attention_split(const void* q, const void* kcache, const void* vcache, v
  * statistics of the next RMSNorm (model.py:281), handed to the norm-fused op that follows. */
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
                      int N, int K, const void* i8ws, int i8_row0, float* nstat_out, void* stream);
+/* llj_linear_resid (M <= 8, not int8) + the NEXT RMSNorm (model.py:276-283) of the updated x, done
+ * by the last M workgroups to finish, one row each: xn (M, N) = RMSNorm(x) * norm_w and rowsum[m]
+ * = fp32 sum of xn's bf16 row (the int4 offset term of the GEMV that reads xn). sync: two
+ * unsigned counters, zero before the first call; the kernel leaves them zero (graph-replay safe).
+ * Replaces a separate llj_rmsnorm_rows launch per norm at batched decode. N <= 8192. */
+int llj_linear_resid_norm(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
+                          int N, int K, const void* norm_w, float eps, void* xn, float* rowsum, unsigned* sync,
+                          void* stream);
 
 /* h[M, H] = silu(rms_2(x) . W1^T) * (rms_2(x) . W2^T)  (model.py:173, 258). M <= 8. */
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
