@@ -1,5 +1,7 @@
-"""Timing of the int8 (LLM.int8) GEMV entry points on one shape, with and without outlier
-columns (profiling aid): python tools/i8_bench.py"""
+"""Timing of the int8 (LLM.int8) GEMV (llj_linear_resid, wfmt 2) at the 7B shapes and bs 1 / 8,
+by outlier regime of the activation: none; SURVEY section 8(d)'s C3 regime (6 of the K columns
+scaled x20); 40 and 300 columns x25 (the synthetic-weight model's own range). Weights cycle through
+8 copies (> the 256 MB MALL). Prints one JSON line per case: python tools/i8_bench.py"""
 from __future__ import annotations
 
 import json
@@ -29,11 +31,12 @@ def main():
         cbs = [cb] + [cb.clone() for _ in range(NC - 1)]
         del W
         for M in (1, 8):
-            for nout in (0, 40, 300):
+            for nout, mult in ((0, 1), (6, 20), (40, 25), (300, 25)):
                 x = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
+                x.clamp_(-5.5, 5.5)  # no accidental outliers (|x| >= 6.0) outside the injected columns
                 if nout:
                     cols = torch.randperm(K, device=dev, generator=g)[:nout]
-                    x[:, cols] *= 25
+                    x[:, cols] *= mult
                 ws = torch.empty(L.llj_i8_ws_bytes(M, K), dtype=torch.uint8, device=dev)
                 y = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
                 _hip.call("llj_i8_stats", x.data_ptr(), K, M, K, 6.0, ws.data_ptr(), st)
@@ -55,8 +58,10 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / 200
-                print(json.dumps({"N": N, "K": K, "M": M, "outliers": nout, "us": round(us, 2),
-                                  "GBps": round(N * K / us / 1e3, 1)}), flush=True)
+                print(json.dumps({"N": N, "K": K, "M": M, "outlier_cols": nout, "outlier_mult": mult,
+                                  "us": round(us, 2), "GBps": round((N * K + 4 * N + 2 * M * (K + 2 * N)) / us / 1e3, 1),
+                                  "frac_of_8TBs": round((N * K + 4 * N + 2 * M * (K + 2 * N)) / us / 1e3 / 8000, 3)}),
+                      flush=True)
 
 
 if __name__ == "__main__":

@@ -31,13 +31,14 @@ def short(name: str) -> str:
     return name.split("(")[0].replace("void ", "").strip()
 
 
-def op_of(name: str, grid: int) -> str | None:
-    """7B decode op of a gemv instantiation (template args WF, AM, EP, NW, D, MB, TPW) by grid."""
+def op_of(name: str, grid: int, multi: bool = False) -> str | None:
+    """7B decode op of a gemv instantiation (template args WF, AM, EP, NW, D, MB, TPW) by grid;
+    multi: the run's decode rows are batched (bs=8 passes), so MB = 8 forms are decode ops."""
     if not name.startswith("llj::gemv_kernel<"):
         return None
     a = [int(x) for x in name[len("llj::gemv_kernel<"):-1].split(",")]
     ep, nw, mb = a[2], a[3], a[5]
-    if mb != 1:
+    if mb != 1 and not multi:
         # a multi-row instantiation in the bs=1 run is a prompt slice (8 rows of the 16-token
         # prompt): its second slice reads the weights back from the 256 MB MALL, so its HBM bytes
         # fall below the algorithmic bytes (the round-2 "0.809x" row) -- not a decode op
@@ -84,8 +85,8 @@ def main():
         out["passes"][tag] = sorted(names)
     for key, cs in groups.items():
         tag, n, grid = key.split("|")
-        k = out["kernels"].setdefault(f"{n} grid {grid}", {"op": op_of(n, int(grid))})
-        prefix = tag.split("_")[0]  # bs1 / c1 / c3
+        prefix = tag.split("_")[0]  # bs1 / bs8 / c1 / c3
+        k = out["kernels"].setdefault(f"{n} grid {grid}", {"op": op_of(n, int(grid), multi=prefix == "bs8")})
         ent = k.setdefault(prefix, {})
         ent["dispatches"] = max(ent.get("dispatches", 0), max(len(v) for v in cs.values()))
         for c, v in cs.items():
@@ -97,8 +98,8 @@ def main():
                 continue
             if "FETCH_SIZE" in ent and "WRITE_SIZE" in ent:
                 ent["hbm_bytes"] = (2 * ent["FETCH_SIZE"] + ent["WRITE_SIZE"]) * 1024
-                if prefix == "bs1" and k["op"]:
-                    ent["algorithmic_bytes"] = algo_bytes_int4(k["op"])
+                if prefix in ("bs1", "bs8") and k["op"]:
+                    ent["algorithmic_bytes"] = algo_bytes_int4(k["op"], 8 if prefix == "bs8" else 1)
                     ent["traffic_over_algorithmic"] = round(ent["hbm_bytes"] / ent["algorithmic_bytes"], 3)
             if "SQ_VALU_MFMA_BUSY_CYCLES" in ent and ent.get("GRBM_GUI_ACTIVE"):
                 ent["mfma_busy"] = ent["SQ_VALU_MFMA_BUSY_CYCLES"] / (ent["GRBM_GUI_ACTIVE"] / 8 * 1024)
