@@ -1161,13 +1161,27 @@ constexpr int nw_of() { return AM == AM_GLOBAL ? 2 * kNW : kNW; }
 #ifndef LLJ_DR
 #define LLJ_DR 8  // chunks in flight per wave for the residual ops (attn / mlp c_proj; 8 vs 4: bs=1 1.167 -> 1.157 ms, bs=8 1.819 -> 1.803)
 #endif
-template <int EP>
-constexpr int d_of() { return EP == EP_SWIGLU ? kD : EP == EP_RESID ? LLJ_DR : LLJ_D1; }
+// batched rows (MB > 1, multi-tile workgroups): chunks in flight per wave (r1[D][TPW] registers
+// scale with the tiles per workgroup) and waves per workgroup, tunable apart from the M == 1 forms
+#ifndef LLJ_DM
+#define LLJ_DM LLJ_D1  // single-matrix ops (QKV, lm_head)
+#endif
+#ifndef LLJ_DMS
+#define LLJ_DMS LLJ_D  // SwiGLU (two matrices)
+#endif
+#ifndef LLJ_NWM
+#define LLJ_NWM LLJ_NW
+#endif
+template <int EP, int MB = 1>
+constexpr int d_of() {
+  return MB > 1 ? (EP == EP_SWIGLU ? LLJ_DMS : EP == EP_RESID ? LLJ_DR : LLJ_DM)
+                : (EP == EP_SWIGLU ? kD : EP == EP_RESID ? LLJ_DR : LLJ_D1);
+}
 
 template <int WF, int AM, int EP, int MB, int NW, int TPW>
 static int launch_t(const GemvParams& p, hipStream_t s) {
   const size_t sm = gemv_smem(WF, AM, p.M, p.K, NW, TPW);
-  auto kern = gemv_kernel<WF, AM, EP, NW, d_of<EP>(), MB, TPW>;
+  auto kern = gemv_kernel<WF, AM, EP, NW, d_of<EP, MB>(), MB, TPW>;
   static bool attr_set = false;  // per instantiation; set before any graph capture
   if (sm > 64 * 1024 && !attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1203,6 +1217,7 @@ static int launch(const GemvParams& p, hipStream_t s) {
     }
   }
   if (WF != WF_I8 && AM != AM_GLOBAL && p.M == 1) return launch_mb<WF, AM, EP, 1>(p, s);
+  if constexpr (AM != AM_GLOBAL && WF != WF_I8) return launch_mb<WF, AM, EP, 8, LLJ_NWM>(p, s);
   return launch_mb<WF, AM, EP, 8>(p, s);
 }
 

@@ -11,7 +11,9 @@ from pathlib import Path
 
 import torch
 
-LIB_PATH = Path(__file__).resolve().parent / "_lljamd.so"
+# LLJ_LIB: another build of the same library (experiment variants built by _build.build(out=...,
+# defines=...)); the product loads the in-tree _lljamd.so
+LIB_PATH = Path(os.environ["LLJ_LIB"]) if os.environ.get("LLJ_LIB") else Path(__file__).resolve().parent / "_lljamd.so"
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
