@@ -120,6 +120,17 @@ size_t llj_attention_ws_bytes(int rows, int n_head, int head_size, int nsplit);
 int llj_attention_split(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
                         int n_head, int head_size, int S, int nsplit, void* part_ws, void* stream);
 
+/* Decode attention in ONE launch (replaces the one-block-per-head llj_attention at bs = 1 and the
+ * two-launch llj_attention_split; reference model.py:237 via CausalSelfAttention.forward): nsplit
+ * blocks per (row, head), block s over the key chunks s, s + nsplit, ...; each writes its
+ * unnormalized softmax partial and the last to arrive (per-(row, head) ticket) merges the nsplit
+ * partials in a fixed order (result independent of arrival order) and writes y. ws:
+ * llj_attention_decode_ws_bytes(B*T, n_head, head_size, nsplit) bytes, ZERO-FILLED before the
+ * first launch (its tickets); every launch leaves them at zero again. Not concurrent-safe on one ws. */
+size_t llj_attention_decode_ws_bytes(int rows, int n_head, int head_size, int nsplit);
+int llj_attention_decode(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                         int n_head, int head_size, int S, int nsplit, void* ws, void* stream);
+
 /* x[M, N] += A[M, K] . W^T (attn.c_proj / mlp.c_proj + residual add, model.py:172-173).
  * nstat_out (optional, M <= 16, not int8): per 16-column tile t of the new x, the bf16-rounded
  * squares summed over the tile's columns, nstat_out[t * 16 + m] (fp32; N / 16 partials): the
@@ -165,6 +176,20 @@ int llj_gemm_silu_mul(int wfmt, const void* A, int lda, const void* W, const voi
  * with norm_w NULL; model.py:204-228). */
 int llj_gemm_qkv_rope(int wfmt, const void* x, const void* W, const void* sz, void* q_out, void* kcache, void* vcache,
                       const float* rope, const int* pos, int B, int T, int C, int n_head, int S, void* stream);
+/* LLM.int8() prompt rows (Linear8bitLt.forward for any M, reference quantization.py:36-75 over
+ * bitsandbytes MatMul8bitLt): the four GEMMs above for CB (N, K) int8 in the I8P tiling and SCB
+ * (N) fp32, with i8ws = llj_i8_stats / llj_i8_norm_stats of A (all M rows): int8 MFMA over the
+ * quantized rows + the fp16 outlier side product, y = f16(f16(acc * SCA * SCB / 127^2) + side), then
+ * the same epilogues. N % 128 == 0, K % 128 == 0. */
+int llj_gemm_i8_linear(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* C, int ldc,
+                       int M, int N, int K, void* stream);
+int llj_gemm_i8_resid(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* x, int ldx,
+                      int M, int N, int K, void* stream);
+int llj_gemm_i8_silu_mul(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* h, int ldh,
+                         int M, int N, int K, void* stream);
+int llj_gemm_i8_qkv_rope(const void* x, const void* CB, const void* SCB, const void* i8ws, void* q_out, void* kcache,
+                         void* vcache, const float* rope, const int* pos, int B, int T, int C, int n_head, int S,
+                         void* stream);
 
 /* ---------------------------------------------------------------- LLM.int8() */
 /* Bytes of the activation-statistics workspace for an (M, K) activation (host function). */

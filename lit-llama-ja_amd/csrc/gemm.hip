@@ -29,15 +29,24 @@
 // dequantizes each B fragment to bf16((q - z_g) * s_g) with its chunk's group pair -- exactly the
 // weights of the reference's grouped forward, F.linear over get_weight(bf16)
 // (quantization.py:390-421) -- so its epilogue takes the accumulator as is.
+// LLM.int8() (Linear8bitLt, reference quantization.py:36-75 over bitsandbytes' MatMul8bitLt):
+// the activation quantized once by llj_i8_stats (aq rows, outlier columns 0, SCA per row) and CB
+// in the I8P tiling (per 16 columns x 128 k: 2 KiB = the two 64-deep MFMA steps, a lane's 16 B
+// being its B fragment) are staged per 128-deep chunk (16 KiB each) and multiplied with MFMA
+// 16x16x64 i8 into int32; after the K loop the fp16 outlier side product runs on the same tile:
+// the outlier columns 32 at a time, f16(A) (from the bf16 rows) and f16(CB * SCB / 127) gathered
+// into LDS, MFMA 16x16x32 f16 into fp32 (products exact, fp32 sums); the epilogue forms the GEMV's
+// y = f16(f16(acc * SCA * SCB / 127^2) + side) (bnb's mm_dequant in fp16 + the fp16 outlier matmul).
 // Tile order is XCD-aware: the 8 XCDs take contiguous ranges of tiles; inside a range bf16 weights
 // go m fastest (the row tiles of one weight panel run together on one XCD and share it through its
 // L2), int4 weights n fastest (one 128-row A panel shared while the XCD sweeps the columns).
 #include "common.h"
+#include "i8ws.h"
 #include "lit_llama_amd.h"
 
 namespace llj {
 
-enum : int { GWF_W4 = 0, GWF_BF16 = 1, GWF_W8 = 3, GWF_W4G = 4 };
+enum : int { GWF_W4 = 0, GWF_BF16 = 1, GWF_I8 = 2, GWF_W8 = 3, GWF_W4G = 4 };
 enum : int { GEP_STORE = 0, GEP_RESID = 1, GEP_QKV = 2, GEP_SILU_MUL = 3 };
 
 struct GemmParams {
@@ -56,6 +65,7 @@ struct GemmParams {
   const int* pos;
   int n_head, head_size, S, T;
   int gch;  // GWF_W4G: group size in 128-deep chunks; sz = (scale, 128 + zero) per (group, column), (G, N)
+  const char* i8ws;  // GWF_I8: llj_i8_stats workspace of A (aq, SCA, outlier list); sz = (const float*) SCB
 };
 
 constexpr int kGBM = 128, kGBN = 128, kGBK = 64, kGNT = 256;
@@ -72,9 +82,15 @@ constexpr int kAP = kGBK + 8;  // A / bf16-B LDS row pitch (elements): 144 B
 
 template <int WF>
 constexpr size_t gemm_b_bytes() {
-  return (WF == GWF_W4 || WF == GWF_W4G) ? (size_t)kGBN * kGBK / 2 : WF == GWF_W8 ? (size_t)kGBN * kGBK
-                                                                                 : (size_t)kGBN * kAP * 2;
+  return (WF == GWF_W4 || WF == GWF_W4G) ? (size_t)kGBN * kGBK / 2
+         : WF == GWF_W8                  ? (size_t)kGBN * kGBK
+         : WF == GWF_I8                  ? (size_t)kGBN * 128  // 8 I8P tile blocks of 2 KiB
+                                         : (size_t)kGBN * kAP * 2;
 }
+// GWF_I8 side product staging (in the A / B buffers after the K loop): 32 outlier columns per
+// round, f16 rows of 64 B at a pitch of 80 B
+constexpr int kSideK = 32, kSideP = 40;  // pitch in halves
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 template <int WF>
 constexpr size_t gemm_lds_bytes() {
   return 2 * ((size_t)kGBM * kAP * 2 + gemm_b_bytes<WF>()) + kGBM * sizeof(float);
@@ -85,10 +101,11 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool NIB = WF == GWF_W4 || WF == GWF_W8;  // nibble-coded: offset removed with the A row sums
   constexpr bool GRP = WF == GWF_W4G;                  // grouped int4: dequantized to the weight values
+  constexpr bool I8 = WF == GWF_I8;                    // LLM.int8(): int8 MFMA + fp16 outlier side product
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave & 1, wc = wave >> 1;
   const int row = lane & 15, g = lane >> 4;
-  const int M = p.M, K = p.K, KC = K / kGBK, KC128 = K / 128;
+  const int M = p.M, K = p.K, KC = I8 ? K / 128 : K / kGBK, KC128 = K / 128;
   const int mtiles = (M + kGBM - 1) / kGBM, ntiles = p.N / kGBN;
   const int total = mtiles * ntiles;
   int t = blockIdx.x;
@@ -97,7 +114,7 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   // panels x every row panel, so a weight panel is fetched once and shared through L2 by all
   // its row tiles (n fastest re-streamed every weight panel once per 128-row panel)
   // (bf16 weights: 7B T = 2048 window 86.3 -> 71.9 ms; int4 weights, 4x smaller: 40.0 vs 40.6 ms, kept n fastest)
-  constexpr bool MF = WF == GWF_BF16 && LLJ_GEMM_MFAST;
+  constexpr bool MF = (WF == GWF_BF16 || I8) && LLJ_GEMM_MFAST;
   const int nb = MF ? t / mtiles : t % ntiles, mb = MF ? t % mtiles : t / ntiles;
   const int m0 = mb * kGBM, n0 = nb * kGBN;
 
@@ -112,13 +129,29 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   const int ar = tid >> 1, ah = tid & 1;
   const int agm = m0 + ar < M ? m0 + ar : M - 1;  // rows past M: a clamped copy, never stored
   const bf16_t* asrc = p.A + (size_t)agm * p.lda + ah * 32;
+  I8Layout L8{};
+  if constexpr (I8) {
+    const I8WsHeader h8 = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
+    L8 = i8_layout(p.i8ws, h8.mtot, h8.K);
+  }
+  // GWF_I8: the thread's half of its row of the quantized activation (128 B per 128-deep chunk)
+  const int8_t* aqsrc = I8 ? L8.aq + (size_t)agm * K + ah * 64 : nullptr;
   // register ring of GDEPTH chunks in flight (chunk c lives in slot c % GDEPTH)
   constexpr int GDEPTH = (NIB || GRP) ? LLJ_GDEPTH : 1;
-  constexpr int BV = (WF == GWF_W4 || GRP) ? 1 : WF == GWF_W8 ? 2 : 4;
+  constexpr int BV = (WF == GWF_W4 || GRP) ? 1 : WF == GWF_W8 ? 2 : 4;  // GWF_I8: 4 (64 B of its tile block)
   u32x4 areg[GDEPTH][4], breg[GDEPTH][BV];
   float2 szr[GDEPTH][4];  // GWF_W4G: (scale, 128 + zero) of the chunk's group for the lane's column of tile j
   auto load_chunk = [&](int slot, int c) {
     c = c < KC ? c : KC - 1;  // past the end: a valid duplicate, never stored
+    if constexpr (I8) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) areg[slot][v] = *reinterpret_cast<const u32x4*>(aqsrc + (size_t)c * 128 + 16 * v);
+      const u32x4* w = reinterpret_cast<const u32x4*>(p.W);  // I8P: (tile, chunk) block of 128 x 16 B
+      const size_t o = ((size_t)(n0 / 16 + (tid >> 5)) * KC128 + c) * 128 + (tid & 31);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) breg[slot][v] = __builtin_nontemporal_load(w + o + 32 * v);
+      return;
+    }
 #pragma unroll
     for (int v = 0; v < 4; ++v) areg[slot][v] = *reinterpret_cast<const u32x4*>(asrc + (size_t)c * kGBK + 8 * v);
     if constexpr (WF == GWF_W4 || GRP) {
@@ -144,6 +177,15 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   };
   f32x2 rsum2 = {0.f, 0.f};  // this thread's share of sum_k A[ar, k]
   auto store_chunk = [&](int slot, int buf) {
+    if constexpr (I8) {  // A rows of 128 B at the bf16 pitch (144 B); B: the 8 tile blocks as stored
+      unsigned char* a8 = reinterpret_cast<unsigned char*>(As(buf)) + ar * (kAP * 2) + ah * 64;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        *reinterpret_cast<u32x4*>(a8 + 16 * v) = areg[slot][v];
+        reinterpret_cast<u32x4*>(Bs(buf))[(tid >> 5) * 128 + (tid & 31) + 32 * v] = breg[slot][v];
+      }
+      return;
+    }
     bf16_t* a = As(buf) + ar * kAP + ah * 32;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -170,10 +212,14 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   asm volatile("" : "+v"(mag));
   if constexpr (WF == GWF_W8) asm volatile("" : "+v"(mag_hi));
   f32x4 acc[4][4];
+  i32x4 iacc[4][4];  // GWF_I8
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) {
+      acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      iacc[i][j] = i32x4{0, 0, 0, 0};
+    }
 
   auto step = [&](int slot, int c) {  // chunk c: stage it, refill its slot with c + GDEPTH, multiply
     const int buf = c & 1;
@@ -183,6 +229,25 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
     store_chunk(slot, buf);
     __syncthreads();  // chunk c staged; every wave is done with chunk c - 1's buffer
     load_chunk(slot, c + GDEPTH);
+    if constexpr (I8) {  // two 64-deep MFMA steps; lane group g: k = 64 s + 16 g + [0, 16)
+      const unsigned char* a8 = reinterpret_cast<const unsigned char*>(As(buf));
+      const u32x4* b8 = reinterpret_cast<const u32x4*>(Bs(buf));
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        i32x4 af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i] = __builtin_bit_cast(i32x4, *reinterpret_cast<const u32x4*>(a8 + (wr * 64 + 16 * i + row) * (kAP * 2) +
+                                                                            64 * s + 16 * g));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = __builtin_bit_cast(i32x4, b8[(wc * 4 + j) * 128 + 64 * s + lane]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) iacc[i][j] = mfma_i8(af[i], bfr[j], iacc[i][j]);
+      }
+      return;
+    }
     const bf16_t* a = As(buf);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {  // MFMA k-steps of the chunk: k = 32 s + 8 g + [0, 8)
@@ -252,6 +317,80 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   if (!ah) rs_lds[ar] = rsum;
   __syncthreads();
 
+  // ---- GWF_I8: fp16 outlier side product into sacc (the K loop's LDS is free now)
+  f32x4 sacc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (I8) {
+    int* s_pre = reinterpret_cast<int*>(smem);  // [kNSB + 1] prefix of the per-block outlier counts
+    int* s_k = s_pre + 64;                      // [kSideK] this round's columns
+    _Float16* sa16 = reinterpret_cast<_Float16*>(smem + 512);          // [128 rows][kSideP]
+    _Float16* sb16 = sa16 + kGBM * kSideP;                             // [128 columns][kSideP]
+    const I8WsHeader h8 = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
+    if (tid < 64) {
+      const int cn = tid < h8.nsb ? L8.cnt[tid] : 0;
+      int x = cn;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      s_pre[tid + 1] = x;
+      if (tid == 0) s_pre[0] = 0;
+    }
+    __syncthreads();
+    const int total = s_pre[h8.nsb];
+    const int sn = n0 + (tid >> 1);  // staging: W column (B) / A row (A) tid >> 1, outliers 16 ah + [0, 16)
+    const float scb = reinterpret_cast<const float*>(p.sz)[sn] / 127.f;
+    for (int c0 = 0; c0 < total; c0 += kSideK) {
+      if (tid < kSideK) {
+        const int fi = c0 + tid;
+        int k = -1;
+        if (fi < total) {
+          int b = 0;
+          while (b + 1 < h8.nsb && s_pre[b + 1] <= fi) ++b;
+          k = L8.list[b * h8.kb + (fi - s_pre[b])];
+        }
+        s_k[tid] = k;
+      }
+      __syncthreads();
+      {
+        _Float16 av[16], wv[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int k = s_k[16 * ah + e];
+          const int kk = k < 0 ? 0 : k;
+          const float a = bf2f(p.A[(size_t)agm * p.lda + kk]);
+          const int q = reinterpret_cast<const int8_t*>(p.W)[  // byte (sn, kk) of the I8P tiling
+              (((size_t)(sn >> 4) * KC128 + (kk >> 7)) * 2 + ((kk & 127) >> 6)) * 1024 +
+              (16 * ((kk >> 4) & 3) + (sn & 15)) * 16 + (kk & 15)];
+          av[e] = k < 0 ? (_Float16)0.f : (_Float16)a;
+          wv[e] = k < 0 ? (_Float16)0.f : (_Float16)((float)q * scb);
+        }
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          *reinterpret_cast<f16x8*>(sa16 + ar * kSideP + 16 * ah + 8 * v) =
+              f16x8{av[8 * v], av[8 * v + 1], av[8 * v + 2], av[8 * v + 3], av[8 * v + 4], av[8 * v + 5], av[8 * v + 6], av[8 * v + 7]};
+          *reinterpret_cast<f16x8*>(sb16 + ar * kSideP + 16 * ah + 8 * v) =
+              f16x8{wv[8 * v], wv[8 * v + 1], wv[8 * v + 2], wv[8 * v + 3], wv[8 * v + 4], wv[8 * v + 5], wv[8 * v + 6], wv[8 * v + 7]};
+        }
+      }
+      __syncthreads();
+      f16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const f16x8*>(sa16 + (wr * 64 + 16 * i + row) * kSideP + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const f16x8*>(sb16 + (wc * 64 + 16 * j + row) * kSideP + 8 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bfr[j], sacc[i][j], 0, 0, 0);
+      __syncthreads();
+    }
+  }
+
   // ---- epilogue: lane holds rows m0 + wr*64 + 16i + 4g + r, column n0 + wc*64 + 16j + row
   const int Cd = p.n_head * p.head_size;
 #pragma unroll
@@ -259,6 +398,7 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
     const int n = n0 + wc * 64 + 16 * j + row;
     float2 szn = make_float2(1.f, 0.f);
     if constexpr (NIB) szn = p.sz[n];
+    if constexpr (I8) szn.x = reinterpret_cast<const float*>(p.sz)[n];  // SCB
     const int nblk = n0 + wc * 64 + 16 * j;  // first column of this 16-column block
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -269,6 +409,11 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
         float y = acc[i][j][r];
         if constexpr (NIB) y = szn.x * (y - szn.y * rs_lds[ml]);
         const bool live = m < M;
+        if constexpr (I8) {  // mm_dequant in fp16, + the fp16 outlier product, in fp16 (the GEMV's epilogue)
+          const float sa = L8.sca[live ? m : M - 1];
+          y = (float)iacc[i][j][r] * (sa * szn.x * (1.f / (127.f * 127.f)));
+          y = (float)(_Float16)((float)(_Float16)y + sacc[i][j][r]);
+        }
         if constexpr (EP == GEP_QKV) {
           const float v = round_bf(y);  // c_attn output in bf16 (model.py:204), RoPE in fp32
           const float partner = lane_xor1(v);
@@ -346,6 +491,7 @@ static int gemm_run(int wfmt, GemmParams& p, void* stream) {
     return (p.sz && p.gch >= 1 && p.K % 128 == 0) ? gemm_launch<GWF_W4G, EP>(p, s) : LLJ_EINVAL;
   }
   if (wfmt == GWF_BF16) return gemm_launch<GWF_BF16, EP>(p, s);
+  if (wfmt == GWF_I8) return (p.sz && p.i8ws && p.K % 128 == 0) ? gemm_launch<GWF_I8, EP>(p, s) : LLJ_EINVAL;
   return LLJ_EINVAL;
 }
 
@@ -377,6 +523,43 @@ int llj_gemm_silu_mul(int wfmt, const void* A, int lda, const void* W, const voi
   p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = W; p.sz = (const float2*)sz;
   p.C = (bf16_t*)h; p.ldc = ldh;
   return gemm_run<GEP_SILU_MUL>(wfmt, p, stream);
+}
+
+// LLM.int8() forms (wfmt 2): W = CB in the I8P tiling, sz = SCB (fp32), i8ws = llj_i8_stats of A
+int llj_gemm_i8_linear(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* C, int ldc,
+                       int M, int N, int K, void* stream) {
+  GemmParams p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = CB; p.sz = (const float2*)SCB;
+  p.C = (bf16_t*)C; p.ldc = ldc; p.i8ws = (const char*)i8ws;
+  return gemm_run<GEP_STORE>(GWF_I8, p, stream);
+}
+
+int llj_gemm_i8_resid(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* x, int ldx,
+                      int M, int N, int K, void* stream) {
+  GemmParams p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = CB; p.sz = (const float2*)SCB;
+  p.C = (bf16_t*)x; p.ldc = ldx; p.i8ws = (const char*)i8ws;
+  return gemm_run<GEP_RESID>(GWF_I8, p, stream);
+}
+
+int llj_gemm_i8_silu_mul(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* h, int ldh,
+                         int M, int N, int K, void* stream) {
+  GemmParams p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = CB; p.sz = (const float2*)SCB;
+  p.C = (bf16_t*)h; p.ldc = ldh; p.i8ws = (const char*)i8ws;
+  return gemm_run<GEP_SILU_MUL>(GWF_I8, p, stream);
+}
+
+int llj_gemm_i8_qkv_rope(const void* x, const void* CB, const void* SCB, const void* i8ws, void* q_out, void* kcache,
+                         void* vcache, const float* rope, const int* pos, int B, int T, int C, int n_head, int S,
+                         void* stream) {
+  if (B < 1 || T < 1 || n_head < 1 || C % n_head || S < 1 || !pos || !rope) return LLJ_EINVAL;
+  GemmParams p{};
+  p.A = (const bf16_t*)x; p.lda = C; p.M = B * T; p.N = 3 * C; p.K = C; p.W = CB; p.sz = (const float2*)SCB;
+  p.q_out = (bf16_t*)q_out; p.kcache = (bf16_t*)kcache; p.vcache = (bf16_t*)vcache; p.rope = rope; p.pos = pos;
+  p.n_head = n_head; p.head_size = C / n_head; p.S = S; p.T = T; p.i8ws = (const char*)i8ws;
+  if (p.head_size & 1 || C % 16) return LLJ_EINVAL;
+  return gemm_run<GEP_QKV>(GWF_I8, p, stream);
 }
 
 int llj_gemm_qkv_rope(int wfmt, const void* x, const void* W, const void* sz, void* q_out, void* kcache, void* vcache,

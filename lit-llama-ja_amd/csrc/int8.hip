@@ -51,6 +51,57 @@ __global__ __launch_bounds__(256) void i8_stats_kernel(const bf16_t* __restrict_
   }
 }
 
+// Pass 1 for many rows (prompt windows, M >= kRowsStatsMin): block (k-block b, 32-row group);
+// wave w takes rows r0 + w, r0 + w + 4, ... (8 rows, loaded together), its lanes the k-block's
+// vectors of 8 columns (kb <= 512). Per-(k-block, row) maxima of the elements below the threshold
+// into part; outlier columns OR-ed into the flag bytes (zeroed before the launch) by 32-bit atomics.
+// The list / counts follow from the complete flags in pass 2 (i8_quant_act_kernel, `list`). Same
+// workspace bytes as i8_stats_kernel (max and OR do not depend on the order).
+constexpr int kRowsStatsMin = 32;
+__global__ __launch_bounds__(256) void i8_stats_rows_kernel(const bf16_t* __restrict__ A, int lda, int M, int K,
+                                                            float thr, char* __restrict__ ws, int kb) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const I8Layout L = i8_layout(ws, M, K);
+  if (b == 0 && blockIdx.y == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb};
+  const int k0 = b * kb, k1 = min(K, k0 + kb);
+  const int nv = k1 > k0 ? (k1 - k0) >> 3 : 0;
+  const bool act = lane < nv;
+  const int kk = k0 + 8 * (act ? lane : 0);
+  const int r0 = blockIdx.y * 32 + wave;
+  uint4 xa[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = r0 + 4 * i < M ? r0 + 4 * i : M - 1;
+    xa[i] = *reinterpret_cast<const uint4*>(A + (size_t)m * lda + (kk < K ? kk : 0));
+  }
+  unsigned fl = 0;  // bit e: column kk + e is an outlier in one of this wave's rows
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = r0 + 4 * i;  // uniform per wave
+    if (m >= M) break;
+    float mx = 0.f;
+    if (act) {
+      const uint32_t aw[4] = {xa[i].x, xa[i].y, xa[i].z, xa[i].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float av = fabsf(to_f16f((e & 1) ? bfhi(aw[e >> 1]) : bflo(aw[e >> 1])));
+        if (av >= thr) fl |= 1u << e;
+        else mx = fmaxf(mx, av);
+      }
+    }
+    mx = wave_max(mx);
+    if (lane == 0) L.part[(size_t)b * M + m] = mx;
+  }
+  if (act && fl) {
+    auto bytes = [](unsigned f4) {
+      return (f4 & 1u) | ((f4 & 2u) << 7) | ((f4 & 4u) << 14) | ((f4 & 8u) << 21);
+    };
+    unsigned* fw = reinterpret_cast<unsigned*>(L.flag + kk);
+    if (fl & 0xFu) atomicOr(fw, bytes(fl & 0xFu));
+    if (fl >> 4) atomicOr(fw + 1, bytes(fl >> 4));
+  }
+}
+
 // Pass 1 fused with the RMSNorm before it (decode rows, M <= MR): every block reduces the
 // sums of squares of all M rows itself -- the rmsnorm_kernel's summation order exactly (thread t:
 // vectors t, t + 256, ... in order; wave sums; the 4 wave partials in order), so r is bit-identical
@@ -301,11 +352,27 @@ __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restr
 // vectors of 8 per thread, K <= 8 * 256 * QV) are loaded BEFORE the k-block maxima are reduced, so
 // both reads share one memory latency.
 constexpr int QV = 8;
+// list: also compact the flags of k-blocks m, m + M, ... into the list / counts (after
+// i8_stats_rows_kernel, whose flags are complete only at this launch).
 __global__ __launch_bounds__(256) void i8_quant_act_kernel(const bf16_t* __restrict__ A, int lda, int M, int K,
-                                                           char* __restrict__ ws) {
+                                                           char* __restrict__ ws, bool list = false) {
   __shared__ float s_sca;
   const int m = blockIdx.x, tid = threadIdx.x;
   const I8Layout L = i8_layout(ws, M, K);
+  if (list && tid < 64) {
+    const int kb = i8_kb(K), lane = tid;
+    for (int b = m; b < kNSB; b += M) {
+      const int k0 = b * kb, k1 = min(K, k0 + kb);
+      int c = 0;
+      for (int i0 = 0; i0 < k1 - k0; i0 += 64) {
+        const bool f = i0 + lane < k1 - k0 && L.flag[k0 + i0 + lane];
+        const unsigned long long bal = __ballot(f);
+        if (f) L.list[b * kb + c + __popcll(bal & ((1ull << lane) - 1ull))] = k0 + i0 + lane;
+        c += __popcll(bal);
+      }
+      if (lane == 0) L.cnt[b] = c;
+    }
+  }
   const bf16_t* ar = A + (size_t)m * lda;
   int8_t* qr = L.aq + (size_t)m * K;
   const int nv = K / 8;
@@ -404,6 +471,17 @@ int llj_i8_stats(const void* A, int lda, int M, int K, float threshold, void* ws
   LLJ_REQUIRE(M > 0 && K > 0 && K % 16 == 0 && lda % 8 == 0 && i8_kb(K) <= 1024);
   if (int e = i8_prep_one(false, (const bf16_t*)A, lda, nullptr, 0.f, nullptr, M, K, threshold, ws, stream); e <= 0)
     return -e;  // one launch (decode batches), or past its envelope (> 0): the two passes
+  hipStream_t s = (hipStream_t)stream;
+  if (M >= kRowsStatsMin && i8_kb(K) <= 512 && lda % 8 == 0) {  // many rows: a 2-D pass 1
+    const I8Offsets o = i8_offsets(M, K);
+    if (hipError_t e = hipMemsetAsync((char*)ws + o.flag, 0, (size_t)K, s)) return (int)e;
+    hipLaunchKernelGGL(i8_stats_rows_kernel, dim3(kNSB, (M + 31) / 32), dim3(256), 0, s, (const bf16_t*)A, lda, M, K,
+                       threshold, (char*)ws, i8_kb(K));
+    LLJ_CHECK_LAUNCH();
+    hipLaunchKernelGGL(i8_quant_act_kernel, dim3(M), dim3(256), 0, s, (const bf16_t*)A, lda, M, K, (char*)ws, true);
+    LLJ_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(i8_stats_kernel, dim3(kNSB), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)A, lda, M, K,
                      threshold, (char*)ws, i8_kb(K));
   LLJ_CHECK_LAUNCH();

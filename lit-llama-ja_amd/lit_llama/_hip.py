@@ -34,6 +34,11 @@ SIGNATURES = {
     "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I,
                           _P],
     "llj_attention_split": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
+    "llj_attention_decode": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
+    "llj_gemm_i8_linear": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "llj_gemm_i8_resid": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "llj_gemm_i8_silu_mul": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "llj_gemm_i8_qkv_rope": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_gptq_block": [_P, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P],
     "llj_colblock_pack": [_P, _I, _I, _P, _P, _I, _P, _P],
     "llj_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
@@ -88,6 +93,8 @@ def lib() -> ctypes.CDLL:
         L.llj_i8_ws_bytes.restype = ctypes.c_size_t
         L.llj_attention_ws_bytes.argtypes = [_I, _I, _I, _I]
         L.llj_attention_ws_bytes.restype = ctypes.c_size_t
+        L.llj_attention_decode_ws_bytes.argtypes = [_I, _I, _I, _I]
+        L.llj_attention_decode_ws_bytes.restype = ctypes.c_size_t
         L.llj_engine_arena_bytes.argtypes = [_I, _I]
         L.llj_engine_arena_bytes.restype = ctypes.c_size_t
         _lib = L

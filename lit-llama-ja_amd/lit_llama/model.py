@@ -103,6 +103,16 @@ ATTN_SPLIT_KEYS = 256  # 7B bs=1 at p = 2000 (S = 2048): 33.1 us one block, 14.4
 FLASH_MIN_T = 32
 
 
+# decode attention in ONE launch (llj_attention_decode): ATTN_DEC_SPLIT blocks per (row, head) over
+# interleaved key chunks and an in-kernel last-arriver merge, for short caches when rows * n_head
+# <= ATTN_DEC_MAX_RH (bs = 1: 32 blocks of one head each would leave most CUs idle), and for long
+# caches in place of the part + combine launches (ATTN_DEC_LONG)
+ATTN_DEC = os.environ.get("LLJ_ATTN_DEC", "1") != "0"  # (A/B switch)
+ATTN_DEC_SPLIT = 8
+ATTN_DEC_MAX_RH = 64
+ATTN_DEC_LONG = True
+
+
 def attn_splits(S: int) -> int:
     """key ranges per (row, head) for a cache of S slots (1 = the one-block attention)."""
     if S < ATTN_SPLIT_MIN_S:
@@ -130,10 +140,10 @@ POST_NORM = os.environ.get("LLJ_POST_NORM", "0") != "0"  # (A/B switch)
 
 # prefill / no-cache calls with at least this many rows (B * T) run the MFMA-tiled GEMMs
 # (llj_gemm_*) instead of the weight-streaming GEMVs in 8 / 16-row slices, when every Linear of
-# the model is int4 W4P (per-row or grouped scales), gptq.int8 W8P or bf16 and the shapes tile by
-# 128 (LLM.int8 keeps the GEMV slices)
+# the model is int4 W4P (per-row or grouped scales), gptq.int8 W8P, LLM.int8 I8P (int8 MFMA + fp16
+# outlier side product, llj_gemm_i8_*) or bf16 and the shapes tile by 128
 GEMM_MIN_ROWS = 32
-_GEMM_FMTS = (0, 1, 3, 4)  # weight formats (low byte of wfmt; 4 = grouped int4) the prefill GEMMs take
+_GEMM_FMTS = (0, 1, 2, 3, 4)  # weight formats (low byte of wfmt; 4 = grouped int4) the prefill GEMMs take
 
 
 def _gemm_fmt(wfmt: int) -> bool:
@@ -198,6 +208,7 @@ class _Work:
             self.h = torch.empty(M, H, dtype=bf, device=device)
             self.gemm = self.flash = self.pre = self.hand = self.post = False
             self.i8ws = self.att_ws = self.nst = self.rs = self.sync = None
+            self.att_dec = 0
             return
         self.gemm = gemm  # many rows: the prefill GEMMs (LLaMA._blocks_gemm)
         self.flash = False  # T-row prompt attention on the MFMA flash kernel (set by LLaMA._run)
@@ -227,7 +238,16 @@ class _Work:
         # split-K attention partials for long caches (llj_attention_split)
         self.nsplit = attn_splits(S)
         self.att_ws = None
-        if self.nsplit > 1:
+        self.att_dec = 0  # > 0: llj_attention_decode with this many blocks per (row, head)
+        if ATTN_DEC:
+            if self.nsplit > 1 and ATTN_DEC_LONG:
+                self.att_dec = self.nsplit
+            elif self.nsplit == 1 and M * cfg.n_head <= ATTN_DEC_MAX_RH:
+                self.att_dec = ATTN_DEC_SPLIT
+        if self.att_dec:  # zero-filled: the per-(row, head) tickets start (and every launch ends) at 0
+            nb = _hip.lib().llj_attention_decode_ws_bytes(M, cfg.n_head, C // cfg.n_head, self.att_dec)
+            self.att_ws = torch.zeros(nb, dtype=torch.uint8, device=device)
+        elif self.nsplit > 1:
             nb = _hip.lib().llj_attention_ws_bytes(M, cfg.n_head, C // cfg.n_head, self.nsplit)
             self.att_ws = torch.empty(nb, dtype=torch.uint8, device=device)
 
@@ -395,6 +415,9 @@ class LLaMA(nn.Module):
         if w.flash:
             _hip.call("llj_attention_prefill", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
                       pos.data_ptr(), B, T, nh, C // nh, S, st)
+        elif w.att_dec:
+            _hip.call("llj_attention_decode", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
+                      pos.data_ptr(), B, T, nh, C // nh, S, w.att_dec, w.att_ws.data_ptr(), st)
         elif w.att_ws is not None:
             _hip.call("llj_attention_split", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
                       pos.data_ptr(), B, T, nh, C // nh, S, w.nsplit, w.att_ws.data_ptr(), st)
@@ -417,20 +440,47 @@ class LLaMA(nn.Module):
         C, H, nh = cfg.n_embd, MLP.hidden(cfg), cfg.n_head
         M = B * T
         P = _hip.ptr
+        I8ws = P(w.i8ws)
         for i, blk in enumerate(self.transformer.h):
             (fa, wa, sa), (fp, wp, sp), (f1, w1, s1), (f2, w2, s2), (fd, wd, sd) = specs["layers"][i]
             kc, vc = kv[i]
-            _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps, w.xn.data_ptr(),
-                      None, M, C, st)
-            _hip.call("llj_gemm_qkv_rope", fa, w.xn.data_ptr(), wa.data_ptr(), P(sa), w.q.data_ptr(), kc.data_ptr(),
-                      vc.data_ptr(), self.rope_cache.data_ptr(), pos.data_ptr(), B, T, C, nh, S, st)
+            if fa == 2:  # LLM.int8: the norm + the activation statistics of all M rows, then the int8 GEMM
+                self._i8_norm_prep(w.x, blk.rms_1, w.xn, M, C, w, st)
+                _hip.call("llj_gemm_i8_qkv_rope", w.xn.data_ptr(), wa.data_ptr(), P(sa), I8ws, w.q.data_ptr(),
+                          kc.data_ptr(), vc.data_ptr(), self.rope_cache.data_ptr(), pos.data_ptr(), B, T, C, nh, S, st)
+            else:
+                _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
+                          w.xn.data_ptr(), None, M, C, st)
+                _hip.call("llj_gemm_qkv_rope", fa, w.xn.data_ptr(), wa.data_ptr(), P(sa), w.q.data_ptr(),
+                          kc.data_ptr(), vc.data_ptr(), self.rope_cache.data_ptr(), pos.data_ptr(), B, T, C, nh, S, st)
             self._attention(w, kc, vc, pos, B, T, S, st)
-            _hip.call("llj_gemm_resid", fp, w.y.data_ptr(), C, wp.data_ptr(), P(sp), w.x.data_ptr(), C, M, C, C, st)
-            _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(),
-                      None, M, C, st)
-            _hip.call("llj_gemm_linear", f1, w.xn.data_ptr(), C, w1.data_ptr(), P(s1), w.h.data_ptr(), H, M, H, C, st)
-            _hip.call("llj_gemm_silu_mul", f2, w.xn.data_ptr(), C, w2.data_ptr(), P(s2), w.h.data_ptr(), H, M, H, C, st)
-            _hip.call("llj_gemm_resid", fd, w.h.data_ptr(), H, wd.data_ptr(), P(sd), w.x.data_ptr(), C, M, C, H, st)
+            self._gemm_resid(fp, w.y, wp, sp, w.x, M, C, C, w, st)
+            if f1 != f2:
+                raise TypeError("c_fc1 and c_fc2 must share a weight format")
+            if f1 == 2:
+                self._i8_norm_prep(w.x, blk.rms_2, w.xn, M, C, w, st)
+                _hip.call("llj_gemm_i8_linear", w.xn.data_ptr(), C, w1.data_ptr(), P(s1), I8ws, w.h.data_ptr(), H, M,
+                          H, C, st)
+                _hip.call("llj_gemm_i8_silu_mul", w.xn.data_ptr(), C, w2.data_ptr(), P(s2), I8ws, w.h.data_ptr(), H,
+                          M, H, C, st)
+            else:
+                _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
+                          w.xn.data_ptr(), None, M, C, st)
+                _hip.call("llj_gemm_linear", f1, w.xn.data_ptr(), C, w1.data_ptr(), P(s1), w.h.data_ptr(), H, M, H, C,
+                          st)
+                _hip.call("llj_gemm_silu_mul", f2, w.xn.data_ptr(), C, w2.data_ptr(), P(s2), w.h.data_ptr(), H, M, H,
+                          C, st)
+            self._gemm_resid(fd, w.h, wd, sd, w.x, M, C, H, w, st)
+
+    def _gemm_resid(self, f, A, W, sz, x, M, N, K, w, st):
+        """x += A . W^T for many rows (LLM.int8: the statistics of A first)."""
+        if f == 2:
+            self._i8_prep(A, M, K, w, st)
+            _hip.call("llj_gemm_i8_resid", A.data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz), _hip.ptr(w.i8ws),
+                      x.data_ptr(), x.stride(0), M, N, K, st)
+        else:
+            _hip.call("llj_gemm_resid", f, A.data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz), x.data_ptr(),
+                      x.stride(0), M, N, K, st)
 
     @staticmethod
     def _glinear(spec, A, M, K, N, out, resid, st):
@@ -569,6 +619,10 @@ class LLaMA(nn.Module):
         if f == 2:
             xn = torch.empty_like(x)
             self._i8_norm_prep(x, ln, xn, M, C, w, st)
+            if M >= GEMM_MIN_ROWS and C % 128 == 0 and V % 128 == 0:  # many rows: the int8 GEMM
+                _hip.call("llj_gemm_i8_linear", xn.data_ptr(), C, W.data_ptr(), _hip.ptr(sz), _hip.ptr(w.i8ws),
+                          out.data_ptr(), out.stride(0), M, V, C, st)
+                return
             src, nw = xn, None
         elif M >= GEMM_MIN_ROWS and _gemm_fmt(f) and C % 128 == 0 and V % 128 == 0:  # many rows: GEMM
             xn = torch.empty_like(x)

@@ -701,6 +701,38 @@ def test_attention_split_keys(hip, hs, nh, B, T_, S, p0, nsplit):
     assert_bf16_close(y.float().cpu().numpy(), _attn_oracle(q, kc, vc, pos, S, T_, nh, hs), "split attention")
 
 
+@pytest.mark.parametrize("hs,nh,B,T_,S,p0,nsplit", [(128, 32, 1, 1, 144, 80, 8), (128, 4, 1, 1, 144, 143, 8),
+                                                   (128, 3, 8, 1, 144, 200, 8), (64, 4, 2, 5, 16, 0, 8),
+                                                   (128, 2, 1, 1, 10, 37, 3), (128, 4, 1, 1, 2048, 2000, 8),
+                                                   (128, 3, 2, 1, 2048, 40, 16), (64, 4, 2, 5, 600, 300, 5),
+                                                   (128, 2, 8, 1, 1024, 1023, 8), (128, 2, 1, 1, 511, 17, 40)])
+def test_attention_decode_one_launch(hip, hs, nh, B, T_, S, p0, nsplit):
+    """One-launch split attention (llj_attention_decode: nsplit blocks per (row, head), in-kernel
+    last-arriver merge in a fixed order) against the oracle: short caches (16-key chunks, empty
+    splits), long caches (128-key chunks), prefill rows (T > 1), the rolled ring (p0 >= S) and more
+    than 16 splits per head. Three launches on one workspace give bitwise-equal outputs and leave the
+    tickets at zero (the merge order does not depend on which block arrives last)."""
+    rng = np.random.default_rng(hs + S + p0 + nsplit + 11)
+    C = nh * hs
+    kc = bf16(rng.standard_normal((B, nh, S, hs)))
+    vc = bf16(rng.standard_normal((B, nh, S, hs)))
+    q = bf16(rng.standard_normal((B * T_, C)) * 2)
+    pos = np.arange(p0, p0 + T_, dtype=np.int32)
+    ws = torch.zeros(hip.llj_attention_decode_ws_bytes(B * T_, nh, hs, nsplit), dtype=torch.uint8, device=dev)
+    qd, kd, vd, pd = T(q, torch.bfloat16), T(kc, torch.bfloat16), T(vc, torch.bfloat16), T(pos)
+    outs = []
+    for _ in range(3):
+        y = torch.empty(B * T_, C, dtype=torch.bfloat16, device=dev)
+        call(hip, "llj_attention_decode", qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), y.data_ptr(), pd.data_ptr(),
+             B, T_, nh, hs, S, nsplit, ws.data_ptr(), st())
+        outs.append(y)
+    torch.cuda.synchronize()
+    tickets = ws[:B * T_ * nh * 4].view(torch.int32)
+    assert int(tickets.abs().sum()) == 0, "tickets not returned to zero"
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert_bf16_close(outs[0].float().cpu().numpy(), _attn_oracle(q, kc, vc, pos, S, T_, nh, hs), "decode attention")
+
+
 @pytest.mark.parametrize("M", [1, 8])
 def test_int8_fused_ops_7b_shapes(hip, M):
     """llm.int8 (wfmt 2) through every fused entry point the model uses, at the 7B shapes (C 4096,
@@ -867,6 +899,117 @@ def test_gemm_linear_and_resid(hip, wfmt, M, N, K):
     assert_bf16_close(o[:M], y, f"gemm wfmt={wfmt} M={M} N={N} K={K}")
     assert (o[M] == 7.0).all(), "wrote past row M"
     assert_bf16_close(xr.float().cpu().numpy(), x0 + bf16(y), f"gemm resid wfmt={wfmt}")
+
+
+def _i8_operands(hip, W):
+    """CB / SCB of an LLM.int8 weight (llj_i8_quant_weight, checked against the oracle's rule) and
+    CB re-tiled into I8P (what Linear8bitLt holds on the device)."""
+    N, K = W.shape
+    cb = torch.empty(N, K, dtype=torch.int8, device=dev)
+    scb = torch.empty(N, dtype=torch.float32, device=dev)
+    call(hip, "llj_i8_quant_weight", T(W, torch.bfloat16).data_ptr(), 1, cb.data_ptr(), scb.data_ptr(), N, K, st())
+    cbt = torch.empty_like(cb)
+    call(hip, "llj_i8_repack", cb.data_ptr(), cbt.data_ptr(), N, K, st())
+    torch.cuda.synchronize()
+    cb_ref, scb_ref = O.int8_quantize_weight(W)
+    np.testing.assert_array_equal(cb.cpu().numpy(), cb_ref)
+    return cbt, scb, cb_ref, scb_ref
+
+
+def _i8_act(rng, M, K, outliers):
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    if outliers:
+        x[:, rng.choice(K, outliers, replace=False)] *= 25.0
+    return bf16(x)
+
+
+@pytest.mark.parametrize("M,K", [(32, 4096), (300, 4096), (64, 11008), (2048, 4096)])
+def test_i8_stats_many_rows(hip, M, K):
+    """llj_i8_stats for prompt rows (M >= 32: the 2-D pass 1 with atomic column flags, then the row
+    quantization with the list compaction): every byte of the workspace against the numpy
+    restatement of the LLM.int8() rules."""
+    rng = np.random.default_rng(M + K)
+    x = _i8_act(rng, M, K, 7)
+    x[M // 2, 5] = 40.0  # an outlier column set by one row only
+    ws = torch.full((hip.llj_i8_ws_bytes(M, K),), 0xAB, dtype=torch.uint8, device=dev)
+    call(hip, "llj_i8_stats", T(x, torch.bfloat16).data_ptr(), K, M, K, 6.0, ws.data_ptr(), st())
+    torch.cuda.synchronize()
+    _check_i8_ws(ws.cpu().numpy(), x, M, K)
+
+
+@pytest.mark.parametrize("outliers", [0, 6, 300])
+@pytest.mark.parametrize("M,N,K", [(40, 256, 4096), (300, 4096, 4096), (129, 384, 11008)])
+def test_gemm_i8_linear_resid_silu(hip, M, N, K, outliers):
+    """LLM.int8() prefill GEMM (int8 MFMA over the quantized rows + the fp16 outlier side product;
+    llj_gemm_i8_linear / _resid / _silu_mul) against the oracle's restatement (bitsandbytes absent:
+    parity unpinned) and against the int8 GEMV on the same workspace."""
+    rng = np.random.default_rng(M + N + K + outliers)
+    W = bf16(rng.standard_normal((N, K)) * 0.02)
+    W2 = bf16(rng.standard_normal((N, K)) * 0.02)
+    cbt, scb, cb_ref, scb_ref = _i8_operands(hip, W)
+    cbt2, scb2, cb_ref2, scb_ref2 = _i8_operands(hip, W2)
+    x = _i8_act(rng, M, K, outliers)
+    xd = T(x, torch.bfloat16)
+    ws = torch.empty(hip.llj_i8_ws_bytes(M, K), dtype=torch.uint8, device=dev)
+    call(hip, "llj_i8_stats", xd.data_ptr(), K, M, K, 6.0, ws.data_ptr(), st())
+    out = torch.full((M + 1, N), 7.0, dtype=torch.bfloat16, device=dev)  # row M: canary
+    call(hip, "llj_gemm_i8_linear", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), out.data_ptr(), N,
+         M, N, K, st())
+    x0 = bf16(rng.standard_normal((M, N)).astype(np.float32))
+    xr = T(x0, torch.bfloat16)
+    call(hip, "llj_gemm_i8_resid", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), xr.data_ptr(), N,
+         M, N, K, st())
+    gv = torch.empty(M, N, dtype=torch.bfloat16, device=dev)  # the int8 GEMV in 8-row slices
+    for r0 in range(0, M, 8):
+        r = min(8, M - r0)
+        call(hip, "llj_linear", 2, xd[r0].data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), None, gv[r0].data_ptr(), N, r,
+             N, K, ws.data_ptr(), r0, None, st())
+    h = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    call(hip, "llj_gemm_i8_linear", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), h.data_ptr(), N,
+         M, N, K, st())
+    call(hip, "llj_gemm_i8_silu_mul", xd.data_ptr(), K, cbt2.data_ptr(), scb2.data_ptr(), ws.data_ptr(), h.data_ptr(),
+         N, M, N, K, st())
+    torch.cuda.synchronize()
+    ref = O.int8_linear(x, cb_ref, scb_ref)
+    o = out.float().cpu().numpy()
+    assert (o[M] == 7.0).all(), "wrote past row M"
+    assert_bf16_close(o[:M], ref, f"gemm int8 M={M} N={N} K={K} outliers={outliers}", rel=2e-2)
+    assert_bf16_close(o[:M], gv.float().cpu().numpy(), "gemm int8 vs GEMV", rel=2e-2)
+    assert_bf16_close(xr.float().cpu().numpy(), x0 + bf16(ref), "gemm int8 resid", rel=2e-2)
+    hexp = bf16(bf16(O.silu(bf16(ref))) * bf16(O.int8_linear(x, cb_ref2, scb_ref2)))
+    assert_bf16_close(h.float().cpu().numpy(), hexp, "gemm int8 swiglu", rel=3e-2)
+
+
+@pytest.mark.parametrize("B,T_,nh,hs,outliers", [(1, 200, 32, 128, 6), (3, 40, 4, 64, 0)])
+def test_gemm_i8_qkv_rope_kv(hip, B, T_, nh, hs, outliers):
+    """llj_gemm_i8_qkv_rope: LLM.int8 c_attn + RoPE + KV-cache write for a whole prompt."""
+    rng = np.random.default_rng(B * T_ + 77)
+    C, S = nh * hs, 256
+    M = B * T_
+    x = _i8_act(rng, M, C, outliers)
+    rope = O.build_rope_cache(512, hs)
+    pos = np.arange(5, 5 + T_, dtype=np.int32)
+    W = bf16(rng.standard_normal((3 * C, C)) * 0.02)
+    cbt, scb, cb_ref, scb_ref = _i8_operands(hip, W)
+    xd, rd, pd = T(x, torch.bfloat16), T(rope), T(pos)
+    ws = torch.empty(hip.llj_i8_ws_bytes(M, C), dtype=torch.uint8, device=dev)
+    call(hip, "llj_i8_stats", xd.data_ptr(), C, M, C, 6.0, ws.data_ptr(), st())
+    q = torch.zeros(M, C, dtype=torch.bfloat16, device=dev)
+    kc = torch.zeros(B, nh, S, hs, dtype=torch.bfloat16, device=dev)
+    vc = torch.zeros_like(kc)
+    call(hip, "llj_gemm_i8_qkv_rope", xd.data_ptr(), cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), q.data_ptr(),
+         kc.data_ptr(), vc.data_ptr(), rd.data_ptr(), pd.data_ptr(), B, T_, C, nh, S, st())
+    torch.cuda.synchronize()
+    qkv = bf16(O.int8_linear(x, cb_ref, scb_ref))
+    qe = O.apply_rope(qkv[:, :C].reshape(B, T_, nh, hs), rope[pos]).reshape(M, C)
+    ke = O.apply_rope(qkv[:, C:2 * C].reshape(B, T_, nh, hs), rope[pos])
+    ve = qkv[:, 2 * C:].reshape(B, T_, nh, hs)
+    assert_bf16_close(q.float().cpu().numpy(), qe, "int8 gemm q", rel=2e-2)
+    slots = pos % S
+    kg = kc.float().cpu().numpy()[:, :, slots].transpose(0, 2, 1, 3)
+    vg = vc.float().cpu().numpy()[:, :, slots].transpose(0, 2, 1, 3)
+    assert_bf16_close(kg, ke, "int8 gemm k", rel=2e-2)
+    assert_bf16_close(vg, ve, "int8 gemm v", rel=2e-2)
 
 
 @pytest.mark.parametrize("wfmt", [0, 1, 3, W4G_128, 4 | (2 << 8)])

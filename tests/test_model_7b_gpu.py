@@ -163,12 +163,13 @@ def test_13b_width_decode_vs_oracle(B):
     _check(_gpu_steps(model, ids), _oracle_steps(orc, ids), REL["gptq.int4"], f"13b gptq.int4 B={B}")
 
 
-@pytest.mark.parametrize("mode", ["gptq.int4", None])
+@pytest.mark.parametrize("mode", ["gptq.int4", None, "llm.int8"])
 def test_7b_width_prefill_gemm_flash_vs_oracle(mode):
     """A 64-token prompt at 7B width through LLaMA.forward takes the prefill path (>= GEMM_MIN_ROWS
     rows: rmsnorm_rows -> MFMA GEMM QKV + RoPE + KV write -> flash attention -> GEMM residual ->
     GEMM SwiGLU (two passes) -> GEMM residual, lm_head GEMM): every prompt row's logits against the
-    oracle, then decode steps from the caches it wrote."""
+    oracle, then decode steps from the caches it wrote. llm.int8: the int8 MFMA GEMMs with the fp16
+    outlier side product (llj_gemm_i8_*) after the many-row statistics pass."""
     from lit_llama import model as MD
 
     t = 64
