@@ -78,6 +78,9 @@ constexpr int kGBM = 128, kGBN = 128, kGBK = 64, kGNT = 256;
 #ifndef LLJ_GDEPTH
 #define LLJ_GDEPTH 2  // W4: chunks in flight per thread (register ring); bf16 keeps 1 (registers)
 #endif
+#ifndef LLJ_GDEPTH_DENSE
+#define LLJ_GDEPTH_DENSE 1  // bf16 / int8 (32 VGPRs of A + B per chunk in flight)
+#endif
 constexpr int kAP = kGBK + 8;  // A / bf16-B LDS row pitch (elements): 144 B
 
 template <int WF>
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   // GWF_I8: the thread's half of its row of the quantized activation (128 B per 128-deep chunk)
   const int8_t* aqsrc = I8 ? L8.aq + (size_t)agm * K + ah * 64 : nullptr;
   // register ring of GDEPTH chunks in flight (chunk c lives in slot c % GDEPTH)
-  constexpr int GDEPTH = (NIB || GRP) ? LLJ_GDEPTH : 1;
+  constexpr int GDEPTH = (NIB || GRP) ? LLJ_GDEPTH : LLJ_GDEPTH_DENSE;
   constexpr int BV = (WF == GWF_W4 || GRP) ? 1 : WF == GWF_W8 ? 2 : 4;  // GWF_I8: 4 (64 B of its tile block)
   u32x4 areg[GDEPTH][4], breg[GDEPTH][BV];
   float2 szr[GDEPTH][4];  // GWF_W4G: (scale, 128 + zero) of the chunk's group for the lane's column of tile j

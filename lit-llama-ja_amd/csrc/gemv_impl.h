@@ -216,10 +216,15 @@ __device__ __forceinline__ int kofs(int t, int grp) {
 // (`stage`, free A-image space) once per workgroup, then thread t (column t % 16, every
 // (NW*4)-th outlier of the chunk) accumulates; the four lanes of a wave sharing a column are
 // combined by shuffles and the per-wave partials land in part[NW][8][16]. Ends with a barrier.
+// Fast path (every k-block has <= SPC = NT / kNSB outlier columns and <= kSideChunk in total): the
+// list entries were loaded speculatively in the prologue (`spk`: entry tid % SPC of k-block
+// tid / SPC), so after the stream the chain is prefix (LDS) -> the f16(A) values and the tile's 16
+// CB bytes of each column in ONE memory latency -> accumulate from LDS, instead of list -> A ->
+// CB (three). Same per-thread accumulation order: bit-identical to the general path.
 constexpr int kSideChunk = 256;
 template <int NW>
 __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float* SCB, int n0, float* part,
-                             unsigned char* stage, int cnt_lane) {
+                             unsigned char* stage, int cnt_lane, int spk) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nl = tid & 15, g = tid >> 4;
   constexpr int NG = NW * 4, NT = NW * 64;
@@ -240,11 +245,41 @@ __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float*
     }
     s_pre[tid + 1] = x;
     if (tid == 0) s_pre[0] = 0;
+    const unsigned long long ov = __ballot(tid < h.nsb && c > NT / kNSB);
+    if (tid == 0) s_pre[63] = ov != 0ull;  // a k-block past the speculative entries
   }
   __syncthreads();
   const int total = s_pre[h.nsb];
+  const bool general = s_pre[63] || total > kSideChunk;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int c0 = 0; c0 < total; c0 += kSideChunk) {
+  if (!general) {
+    constexpr int SPC = NT / kNSB;
+    _Float16* s_a16 = reinterpret_cast<_Float16*>(s_k);                      // [8][kSideChunk]
+    uint32_t* s_cb = reinterpret_cast<uint32_t*>(s_a16 + 8 * kSideChunk);  // [kSideChunk][16 bytes]
+    const int b = tid / SPC, j = tid % SPC;
+    if (b < h.nsb && j < s_pre[b + 1] - s_pre[b]) {
+      const int i = s_pre[b] + j, k = spk, kk = k & 127;
+      float av[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) av[m] = bf2f(p.A[(size_t)(m < M ? m : 0) * p.lda + k]);
+      const int8_t* cbp = CB + (((size_t)(n0 >> 4) * (p.K >> 7) + (k >> 7)) * 2 + (kk >> 6)) * 1024 +
+                          (16 * ((kk >> 4) & 3)) * 16 + (kk & 15);
+      uint32_t cw[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int c = 0; c < 16; ++c) cw[c >> 2] |= (uint32_t)(uint8_t)cbp[c * 16] << (8 * (c & 3));
+#pragma unroll
+      for (int m = 0; m < 8; ++m) s_a16[m * kSideChunk + i] = m < M ? (_Float16)av[m] : (_Float16)0.f;
+      *reinterpret_cast<uint4*>(s_cb + 4 * i) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+    }
+    __syncthreads();
+    const int8_t* cb8 = reinterpret_cast<const int8_t*>(s_cb);
+    for (int i = g; i < total; i += NG) {
+      const float w = (float)(_Float16)((float)cb8[i * 16 + nl] * scb);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) acc[m] += (float)s_a16[m * kSideChunk + i] * w;
+    }
+  }
+  for (int c0 = 0; c0 < (general ? total : 0); c0 += kSideChunk) {
     const int len = min(kSideChunk, total - c0);
     for (int i = tid; i < len; i += NT) {
       const int fi = c0 + i;
@@ -748,10 +783,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   for (int d = 0; d < D; ++d) load(d, d);  // the weight stream starts before any A wait
   // int8: the per-k-block outlier counts the side product starts from, loaded now (one memory
   // latency less in the tail; needed once the stream is done)
-  int i8cnt = 0;
-  if constexpr (I8) {
+  int i8cnt = 0, i8spk = 0;
+  if constexpr (I8) {  // + the speculative outlier-list entries of the side product's fast path
     const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
-    i8cnt = i8_layout(p.i8ws, h.mtot, h.K).cnt[lane < kNSB ? lane : 0];
+    const I8Layout L8 = i8_layout(p.i8ws, h.mtot, h.K);
+    i8cnt = L8.cnt[lane < kNSB ? lane : 0];
+    constexpr int SPC = NT / kNSB;
+    const int sb = tid / SPC < kNSB ? tid / SPC : 0;
+    i8spk = L8.list[sb * h.kb + tid % SPC];
   }
   LLJ_STAMP(1);
   float2 e_cs[TPW][4];
@@ -823,10 +862,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     if (ALDS) __syncthreads();  // every wave is done reading the A image it aliases
     if constexpr (I8) {
       i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W), reinterpret_cast<const float*>(p.sz), ntj[0] * 16,
-                       side, smem, i8cnt);
+                       side, smem, i8cnt, i8spk);
       if (DUAL)
         i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W2), reinterpret_cast<const float*>(p.sz2),
-                         ntj[0] * 16, side + NW * 8 * 16, smem, i8cnt);
+                         ntj[0] * 16, side + NW * 8 * 16, smem, i8cnt, i8spk);
     }
     if constexpr (I8) {
       int* mine = reinterpret_cast<int*>(red) + (size_t)(wave * 64 + lane) * NV;

@@ -107,7 +107,7 @@ FLASH_MIN_T = 32
 # interleaved key chunks and an in-kernel last-arriver merge, for short caches when rows * n_head
 # <= ATTN_DEC_MAX_RH (bs = 1: 32 blocks of one head each would leave most CUs idle), and for long
 # caches in place of the part + combine launches (ATTN_DEC_LONG)
-ATTN_DEC = os.environ.get("LLJ_ATTN_DEC", "1") != "0"  # (A/B switch)
+ATTN_DEC = os.environ.get("LLJ_ATTN_DEC", "0") != "0"  # (A/B switch; measured slower at bs=1)
 ATTN_DEC_SPLIT = 8
 ATTN_DEC_MAX_RH = 64
 ATTN_DEC_LONG = True
