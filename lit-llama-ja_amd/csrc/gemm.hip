@@ -78,8 +78,22 @@ constexpr int kGBM = 128, kGBN = 128, kGBK = 64, kGNT = 256;
 #ifndef LLJ_GDEPTH
 #define LLJ_GDEPTH 2  // W4: chunks in flight per thread (register ring); bf16 keeps 1 (registers)
 #endif
+// 256 x 128 tiles with 8 waves (4 row groups x 2 column groups of 64 x 64) for M >= 256: a weight
+// panel's 128-deep chunk feeds twice the rows (A + B bytes per MFMA 0.75x), one workgroup per CU
+#ifndef LLJ_GEMM_BM256
+#define LLJ_GEMM_BM256 1  // bf16 (7B 2048-token window 70.5 -> 42.6 ms with 2 chunks in flight)
+#endif
+#ifndef LLJ_GEMM_BM256_I8
+#define LLJ_GEMM_BM256_I8 1  // LLM.int8
+#endif
+#ifndef LLJ_GEMM_BM256_W4
+#define LLJ_GEMM_BM256_W4 0  // int4 W4P
+#endif
 #ifndef LLJ_GDEPTH_DENSE
-#define LLJ_GDEPTH_DENSE 1  // bf16 / int8 (32 VGPRs of A + B per chunk in flight)
+#define LLJ_GDEPTH_DENSE 1  // bf16 / int8 in 128-row tiles (32 VGPRs of A + B per chunk in flight)
+#endif
+#ifndef LLJ_GDEPTH_DENSE256
+#define LLJ_GDEPTH_DENSE256 2  // bf16 / int8 in 256-row tiles (7B bf16 window 59.6 ms at 1, 42.6 at 2)
 #endif
 constexpr int kAP = kGBK + 8;  // A / bf16-B LDS row pitch (elements): 144 B
 
@@ -94,22 +108,25 @@ constexpr size_t gemm_b_bytes() {
 // round, f16 rows of 64 B at a pitch of 80 B
 constexpr int kSideK = 32, kSideP = 40;  // pitch in halves
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-template <int WF>
+template <int WF, int BM = kGBM>
 constexpr size_t gemm_lds_bytes() {
-  return 2 * ((size_t)kGBM * kAP * 2 + gemm_b_bytes<WF>()) + kGBM * sizeof(float);
+  return 2 * ((size_t)BM * kAP * 2 + gemm_b_bytes<WF>()) + BM * sizeof(float);
 }
 
-template <int WF, int EP>
-__global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
+// BM: rows per tile (128, or 256 for bf16 with 8 waves: 4 row groups x 2 column groups of 64 x 64)
+template <int WF, int EP, int BM = kGBM>
+__global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
+  static_assert(BM == kGBM || WF == GWF_BF16 || WF == GWF_I8 || WF == GWF_W4, "256-row tiles: bf16, int8, int4");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool NIB = WF == GWF_W4 || WF == GWF_W8;  // nibble-coded: offset removed with the A row sums
   constexpr bool GRP = WF == GWF_W4G;                  // grouped int4: dequantized to the weight values
   constexpr bool I8 = WF == GWF_I8;                    // LLM.int8(): int8 MFMA + fp16 outlier side product
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave & 1, wc = wave >> 1;
+  constexpr int WRN = BM / 64;  // row groups of waves
+  const int wr = wave % WRN, wc = wave / WRN;
   const int row = lane & 15, g = lane >> 4;
   const int M = p.M, K = p.K, KC = I8 ? K / 128 : K / kGBK, KC128 = K / 128;
-  const int mtiles = (M + kGBM - 1) / kGBM, ntiles = p.N / kGBN;
+  const int mtiles = (M + BM - 1) / BM, ntiles = p.N / kGBN;
   const int total = mtiles * ntiles;
   int t = blockIdx.x;
   if (total % 8 == 0) t = (t % 8) * (total / 8) + t / 8;  // contiguous tile range per XCD
@@ -119,10 +136,10 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   // (bf16 weights: 7B T = 2048 window 86.3 -> 71.9 ms; int4 weights, 4x smaller: 40.0 vs 40.6 ms, kept n fastest)
   constexpr bool MF = (WF == GWF_BF16 || I8) && LLJ_GEMM_MFAST;
   const int nb = MF ? t / mtiles : t % ntiles, mb = MF ? t % mtiles : t / ntiles;
-  const int m0 = mb * kGBM, n0 = nb * kGBN;
+  const int m0 = mb * BM, n0 = nb * kGBN;
 
   // LDS: [A buf 0][A buf 1][B buf 0][B buf 1][row sums]
-  constexpr size_t kAB = (size_t)kGBM * kAP * 2, kBB = gemm_b_bytes<WF>();
+  constexpr size_t kAB = (size_t)BM * kAP * 2, kBB = gemm_b_bytes<WF>();
   auto As = [&](int b) { return reinterpret_cast<bf16_t*>(smem + b * kAB); };
   auto Bs = [&](int b) { return smem + 2 * kAB + b * kBB; };
   float* rs_lds = reinterpret_cast<float*>(smem + 2 * (kAB + kBB));
@@ -140,8 +157,13 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   // GWF_I8: the thread's half of its row of the quantized activation (128 B per 128-deep chunk)
   const int8_t* aqsrc = I8 ? L8.aq + (size_t)agm * K + ah * 64 : nullptr;
   // register ring of GDEPTH chunks in flight (chunk c lives in slot c % GDEPTH)
-  constexpr int GDEPTH = (NIB || GRP) ? LLJ_GDEPTH : LLJ_GDEPTH_DENSE;
-  constexpr int BV = (WF == GWF_W4 || GRP) ? 1 : WF == GWF_W8 ? 2 : 4;  // GWF_I8: 4 (64 B of its tile block)
+  constexpr int GDEPTH = (NIB || GRP) ? LLJ_GDEPTH : BM == 256 ? LLJ_GDEPTH_DENSE256 : LLJ_GDEPTH_DENSE;
+  constexpr int BV = (WF == GWF_W4 || GRP) ? 1 : WF == GWF_W8 ? 2 : BM == 256 ? 2 : 4;  // GWF_I8: 4 (64 B of its tile block)
+  // bf16 B with 256-row tiles: 512 threads over the 128 weight rows, a quarter row (32 B) each
+  const int br = BM == 256 ? tid >> 2 : ar, bq = BM == 256 ? tid & 3 : ah;
+  // int8 B: the 8 tile blocks of 128 x 16 B over TPB threads each; int4 B: the first 256 threads
+  constexpr int TPB = BM / 4;
+  const int bt = tid & 255;
   u32x4 areg[GDEPTH][4], breg[GDEPTH][BV];
   float2 szr[GDEPTH][4];  // GWF_W4G: (scale, 128 + zero) of the chunk's group for the lane's column of tile j
   auto load_chunk = [&](int slot, int c) {
@@ -150,17 +172,17 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
 #pragma unroll
       for (int v = 0; v < 4; ++v) areg[slot][v] = *reinterpret_cast<const u32x4*>(aqsrc + (size_t)c * 128 + 16 * v);
       const u32x4* w = reinterpret_cast<const u32x4*>(p.W);  // I8P: (tile, chunk) block of 128 x 16 B
-      const size_t o = ((size_t)(n0 / 16 + (tid >> 5)) * KC128 + c) * 128 + (tid & 31);
+      const size_t o = ((size_t)(n0 / 16 + tid / TPB) * KC128 + c) * 128 + tid % TPB;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) breg[slot][v] = __builtin_nontemporal_load(w + o + 32 * v);
+      for (int v = 0; v < BV; ++v) breg[slot][v] = __builtin_nontemporal_load(w + o + TPB * v);
       return;
     }
 #pragma unroll
     for (int v = 0; v < 4; ++v) areg[slot][v] = *reinterpret_cast<const u32x4*>(asrc + (size_t)c * kGBK + 8 * v);
     if constexpr (WF == GWF_W4 || GRP) {
       const u32x4* w = reinterpret_cast<const u32x4*>(p.W);
-      const size_t nt = (size_t)(n0 / 16 + (tid >> 5));
-      breg[slot][0] = __builtin_nontemporal_load(w + (nt * KC128 + (c >> 1)) * 64 + 32 * (c & 1) + (tid & 31));
+      const size_t nt = (size_t)(n0 / 16 + (bt >> 5));  // (256-row tiles: threads 256.. load a copy, never stored)
+      breg[slot][0] = __builtin_nontemporal_load(w + (nt * KC128 + (c >> 1)) * 64 + 32 * (c & 1) + (bt & 31));
       if constexpr (GRP) {
         const size_t go = (size_t)((c >> 1) / p.gch) * p.N + n0 + wc * 64 + row;
 #pragma unroll
@@ -173,9 +195,9 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
       breg[slot][0] = __builtin_nontemporal_load(w + o);
       breg[slot][1] = __builtin_nontemporal_load(w + o + 64);
     } else {
-      const bf16_t* w = reinterpret_cast<const bf16_t*>(p.W) + (size_t)(n0 + ar) * K + (size_t)c * kGBK + ah * 32;
+      const bf16_t* w = reinterpret_cast<const bf16_t*>(p.W) + (size_t)(n0 + br) * K + (size_t)c * kGBK + bq * 8 * BV;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) breg[slot][v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w + 8 * v));
+      for (int v = 0; v < BV; ++v) breg[slot][v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w + 8 * v));
     }
   };
   f32x2 rsum2 = {0.f, 0.f};  // this thread's share of sum_k A[ar, k]
@@ -183,10 +205,9 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
     if constexpr (I8) {  // A rows of 128 B at the bf16 pitch (144 B); B: the 8 tile blocks as stored
       unsigned char* a8 = reinterpret_cast<unsigned char*>(As(buf)) + ar * (kAP * 2) + ah * 64;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        *reinterpret_cast<u32x4*>(a8 + 16 * v) = areg[slot][v];
-        reinterpret_cast<u32x4*>(Bs(buf))[(tid >> 5) * 128 + (tid & 31) + 32 * v] = breg[slot][v];
-      }
+      for (int v = 0; v < 4; ++v) *reinterpret_cast<u32x4*>(a8 + 16 * v) = areg[slot][v];
+#pragma unroll
+      for (int v = 0; v < BV; ++v) reinterpret_cast<u32x4*>(Bs(buf))[(tid / TPB) * 128 + tid % TPB + TPB * v] = breg[slot][v];
       return;
     }
     bf16_t* a = As(buf) + ar * kAP + ah * 32;
@@ -199,14 +220,14 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
       }
     }
     if constexpr (WF == GWF_W4 || GRP) {
-      reinterpret_cast<u32x4*>(Bs(buf))[tid] = breg[slot][0];
+      if (BM == 128 || tid < 256) reinterpret_cast<u32x4*>(Bs(buf))[tid] = breg[slot][0];
     } else if constexpr (WF == GWF_W8) {  // [low plane halves 4 KiB][high plane halves 4 KiB]
       reinterpret_cast<u32x4*>(Bs(buf))[tid] = breg[slot][0];
       reinterpret_cast<u32x4*>(Bs(buf))[kGNT + tid] = breg[slot][1];
     } else {
-      bf16_t* b = reinterpret_cast<bf16_t*>(Bs(buf)) + ar * kAP + ah * 32;
+      bf16_t* b = reinterpret_cast<bf16_t*>(Bs(buf)) + br * kAP + bq * 8 * BV;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) *reinterpret_cast<u32x4*>(b + 8 * v) = breg[slot][v];
+      for (int v = 0; v < BV; ++v) *reinterpret_cast<u32x4*>(b + 8 * v) = breg[slot][v];
     }
   };
 
@@ -330,7 +351,7 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
     int* s_pre = reinterpret_cast<int*>(smem);  // [kNSB + 1] prefix of the per-block outlier counts
     int* s_k = s_pre + 64;                      // [kSideK] this round's columns
     _Float16* sa16 = reinterpret_cast<_Float16*>(smem + 512);          // [128 rows][kSideP]
-    _Float16* sb16 = sa16 + kGBM * kSideP;                             // [128 columns][kSideP]
+    _Float16* sb16 = sa16 + BM * kSideP;                               // [128 columns][kSideP]
     const I8WsHeader h8 = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
     if (tid < 64) {
       const int cn = tid < h8.nsb ? L8.cnt[tid] : 0;
@@ -345,7 +366,7 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
     }
     __syncthreads();
     const int total = s_pre[h8.nsb];
-    const int sn = n0 + (tid >> 1);  // staging: W column (B) / A row (A) tid >> 1, outliers 16 ah + [0, 16)
+    const int sn = n0 + (bt >> 1);  // staging: W column (B) bt >> 1 / A row (A) ar, outliers 16 ah + [0, 16)
     const float scb = reinterpret_cast<const float*>(p.sz)[sn] / 127.f;
     for (int c0 = 0; c0 < total; c0 += kSideK) {
       if (tid < kSideK) {
@@ -376,7 +397,8 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
         for (int v = 0; v < 2; ++v) {
           *reinterpret_cast<f16x8*>(sa16 + ar * kSideP + 16 * ah + 8 * v) =
               f16x8{av[8 * v], av[8 * v + 1], av[8 * v + 2], av[8 * v + 3], av[8 * v + 4], av[8 * v + 5], av[8 * v + 6], av[8 * v + 7]};
-          *reinterpret_cast<f16x8*>(sb16 + ar * kSideP + 16 * ah + 8 * v) =
+          if (BM == 128 || tid < 256)
+            *reinterpret_cast<f16x8*>(sb16 + (bt >> 1) * kSideP + 16 * ah + 8 * v) =
               f16x8{wv[8 * v], wv[8 * v + 1], wv[8 * v + 2], wv[8 * v + 3], wv[8 * v + 4], wv[8 * v + 5], wv[8 * v + 6], wv[8 * v + 7]};
         }
       }
@@ -466,18 +488,18 @@ __global__ __launch_bounds__(kGNT) void gemm_kernel(GemmParams p) {
   }
 }
 
-template <int WF, int EP>
+template <int WF, int EP, int BM = kGBM>
 static int gemm_launch(const GemmParams& p, hipStream_t s) {
-  auto kern = gemm_kernel<WF, EP>;
+  auto kern = gemm_kernel<WF, EP, BM>;
   static bool attr_set = false;  // per instantiation, before any graph capture
-  const size_t lds = gemm_lds_bytes<WF>();
+  const size_t lds = gemm_lds_bytes<WF, BM>();
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  const int tiles = ((p.M + kGBM - 1) / kGBM) * (p.N / kGBN);
-  hipLaunchKernelGGL(kern, dim3(tiles), dim3(kGNT), lds, s, p);
+  const int tiles = ((p.M + BM - 1) / BM) * (p.N / kGBN);
+  hipLaunchKernelGGL(kern, dim3(tiles), dim3(2 * BM), lds, s, p);
   LLJ_CHECK_LAUNCH();
   return 0;
 }
@@ -487,14 +509,25 @@ static int gemm_run(int wfmt, GemmParams& p, void* stream) {
   if (p.M < 1 || p.N % kGBN || p.K % kGBK || p.K < kGBK || (p.lda & 7)) return LLJ_EINVAL;
   if (EP != GEP_QKV && (!p.C || (p.ldc & 1))) return LLJ_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  if (wfmt == GWF_W4) return p.sz ? gemm_launch<GWF_W4, EP>(p, s) : LLJ_EINVAL;
+  if (wfmt == GWF_W4) {
+    if (!p.sz) return LLJ_EINVAL;
+    if (LLJ_GEMM_BM256_W4 && p.M >= 256) return gemm_launch<GWF_W4, EP, 256>(p, s);
+    return gemm_launch<GWF_W4, EP>(p, s);
+  }
   if (wfmt == GWF_W8) return p.sz ? gemm_launch<GWF_W8, EP>(p, s) : LLJ_EINVAL;
   if ((wfmt & 0xff) == GWF_W4G) {  // grouped int4: group size (128-deep chunks) in the bits above
     p.gch = wfmt >> 8;
     return (p.sz && p.gch >= 1 && p.K % 128 == 0) ? gemm_launch<GWF_W4G, EP>(p, s) : LLJ_EINVAL;
   }
-  if (wfmt == GWF_BF16) return gemm_launch<GWF_BF16, EP>(p, s);
-  if (wfmt == GWF_I8) return (p.sz && p.i8ws && p.K % 128 == 0) ? gemm_launch<GWF_I8, EP>(p, s) : LLJ_EINVAL;
+  if (wfmt == GWF_BF16) {
+    if (LLJ_GEMM_BM256 && p.M >= 256) return gemm_launch<GWF_BF16, EP, 256>(p, s);
+    return gemm_launch<GWF_BF16, EP>(p, s);
+  }
+  if (wfmt == GWF_I8) {
+    if (!p.sz || !p.i8ws || p.K % 128) return LLJ_EINVAL;
+    if (LLJ_GEMM_BM256_I8 && p.M >= 256) return gemm_launch<GWF_I8, EP, 256>(p, s);
+    return gemm_launch<GWF_I8, EP>(p, s);
+  }
   return LLJ_EINVAL;
 }
 

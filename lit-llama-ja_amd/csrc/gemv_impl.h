@@ -216,7 +216,7 @@ __device__ __forceinline__ int kofs(int t, int grp) {
 // (`stage`, free A-image space) once per workgroup, then thread t (column t % 16, every
 // (NW*4)-th outlier of the chunk) accumulates; the four lanes of a wave sharing a column are
 // combined by shuffles and the per-wave partials land in part[NW][8][16]. Ends with a barrier.
-// Fast path (every k-block has <= SPC = NT / kNSB outlier columns and <= kSideChunk in total): the
+// Fast path (every k-block has <= SPC = NT / kNSB outlier columns): the
 // list entries were loaded speculatively in the prologue (`spk`: entry tid % SPC of k-block
 // tid / SPC), so after the stream the chain is prefix (LDS) -> the f16(A) values and the tile's 16
 // CB bytes of each column in ONE memory latency -> accumulate from LDS, instead of list -> A ->
@@ -250,33 +250,41 @@ __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float*
   }
   __syncthreads();
   const int total = s_pre[h.nsb];
-  const bool general = s_pre[63] || total > kSideChunk;
+  const bool general = s_pre[63];
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (!general) {
+  if (!general) {  // every entry is one thread's speculative list load: one memory latency in all
     constexpr int SPC = NT / kNSB;
     _Float16* s_a16 = reinterpret_cast<_Float16*>(s_k);                      // [8][kSideChunk]
     uint32_t* s_cb = reinterpret_cast<uint32_t*>(s_a16 + 8 * kSideChunk);  // [kSideChunk][16 bytes]
     const int b = tid / SPC, j = tid % SPC;
-    if (b < h.nsb && j < s_pre[b + 1] - s_pre[b]) {
-      const int i = s_pre[b] + j, k = spk, kk = k & 127;
-      float av[8];
+    const bool mine = b < h.nsb && j < s_pre[b + 1] - s_pre[b];
+    const int i = mine ? s_pre[b] + j : -1;
+    float av[8];
+    uint32_t cw[4] = {0, 0, 0, 0};
+    if (mine) {
+      const int k = spk, kk = k & 127;
 #pragma unroll
       for (int m = 0; m < 8; ++m) av[m] = bf2f(p.A[(size_t)(m < M ? m : 0) * p.lda + k]);
       const int8_t* cbp = CB + (((size_t)(n0 >> 4) * (p.K >> 7) + (k >> 7)) * 2 + (kk >> 6)) * 1024 +
                           (16 * ((kk >> 4) & 3)) * 16 + (kk & 15);
-      uint32_t cw[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int c = 0; c < 16; ++c) cw[c >> 2] |= (uint32_t)(uint8_t)cbp[c * 16] << (8 * (c & 3));
-#pragma unroll
-      for (int m = 0; m < 8; ++m) s_a16[m * kSideChunk + i] = m < M ? (_Float16)av[m] : (_Float16)0.f;
-      *reinterpret_cast<uint4*>(s_cb + 4 * i) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
     }
-    __syncthreads();
-    const int8_t* cb8 = reinterpret_cast<const int8_t*>(s_cb);
-    for (int i = g; i < total; i += NG) {
-      const float w = (float)(_Float16)((float)cb8[i * 16 + nl] * scb);
+    for (int c0 = 0; c0 < total; c0 += kSideChunk) {  // rounds of kSideChunk entries (LDS)
+      if (i >= c0 && i < c0 + kSideChunk) {
 #pragma unroll
-      for (int m = 0; m < 8; ++m) acc[m] += (float)s_a16[m * kSideChunk + i] * w;
+        for (int m = 0; m < 8; ++m) s_a16[m * kSideChunk + i - c0] = m < M ? (_Float16)av[m] : (_Float16)0.f;
+        *reinterpret_cast<uint4*>(s_cb + 4 * (i - c0)) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+      }
+      __syncthreads();
+      const int8_t* cb8 = reinterpret_cast<const int8_t*>(s_cb);
+      const int len = min(kSideChunk, total - c0);
+      for (int ii = g; ii < len; ii += NG) {  // NG divides kSideChunk: the general path's order
+        const float w = (float)(_Float16)((float)cb8[ii * 16 + nl] * scb);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) acc[m] += (float)s_a16[m * kSideChunk + ii] * w;
+      }
+      __syncthreads();
     }
   }
   for (int c0 = 0; c0 < (general ? total : 0); c0 += kSideChunk) {

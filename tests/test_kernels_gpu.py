@@ -980,7 +980,7 @@ def test_gemm_i8_linear_resid_silu(hip, M, N, K, outliers):
     assert_bf16_close(h.float().cpu().numpy(), hexp, "gemm int8 swiglu", rel=3e-2)
 
 
-@pytest.mark.parametrize("B,T_,nh,hs,outliers", [(1, 200, 32, 128, 6), (3, 40, 4, 64, 0)])
+@pytest.mark.parametrize("B,T_,nh,hs,outliers", [(1, 200, 32, 128, 6), (3, 40, 4, 64, 0), (1, 300, 8, 128, 6)])
 def test_gemm_i8_qkv_rope_kv(hip, B, T_, nh, hs, outliers):
     """llj_gemm_i8_qkv_rope: LLM.int8 c_attn + RoPE + KV-cache write for a whole prompt."""
     rng = np.random.default_rng(B * T_ + 77)
@@ -1012,12 +1012,14 @@ def test_gemm_i8_qkv_rope_kv(hip, B, T_, nh, hs, outliers):
     assert_bf16_close(vg, ve, "int8 gemm v", rel=2e-2)
 
 
+@pytest.mark.parametrize("M", [150, 300])
 @pytest.mark.parametrize("wfmt", [0, 1, 3, W4G_128, 4 | (2 << 8)])
-def test_gemm_swiglu_two_pass(hip, wfmt):
+def test_gemm_swiglu_two_pass(hip, wfmt, M):
     """c_fc1 into h (llj_gemm_linear), then c_fc2 with the silu * mul epilogue in place
-    (llj_gemm_silu_mul): model.py:258 with the reference's bf16 rounding points."""
-    rng = np.random.default_rng(70 + wfmt)
-    M, C, H = 150, 1024, 2816
+    (llj_gemm_silu_mul): model.py:258 with the reference's bf16 rounding points. M = 300 takes
+    the 256-row tiles (bf16 / int8, int4 where enabled)."""
+    rng = np.random.default_rng(70 + wfmt + M)
+    C, H = 1024, 2816
     W1, W1d, s1 = quant_operands(hip, rng, wfmt, H, C)
     W2, W2d, s2 = quant_operands(hip, rng, wfmt, H, C)
     x = bf16(rng.standard_normal((M, C)).astype(np.float32))
@@ -1032,7 +1034,7 @@ def test_gemm_swiglu_two_pass(hip, wfmt):
 
 
 @pytest.mark.parametrize("wfmt", [0, 1, 3, W4G_128, 4 | (2 << 8)])
-@pytest.mark.parametrize("B,T_,nh,hs", [(1, 200, 32, 128), (3, 40, 4, 64)])
+@pytest.mark.parametrize("B,T_,nh,hs", [(1, 200, 32, 128), (3, 40, 4, 64), (2, 150, 8, 128)])
 def test_gemm_qkv_rope_kv(hip, wfmt, B, T_, nh, hs):
     """llj_gemm_qkv_rope: c_attn + RoPE + KV-cache write for a whole prompt (ring slots p % S)."""
     rng = np.random.default_rng(B * T_ + wfmt)

@@ -4,16 +4,17 @@
 # mode, summarized per kernel on the box into gpurun_out/$1.json.
 #   mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)
 OUT=$1
+MODES=${2:-gptq.int4 none}
 R=$GRAFT_REPO_ROOT
 D=/tmp/$OUT
 mkdir -p $D $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 150 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $D -o pf \
-  -- python3 $R/tools/prefill_bench.py --T 2048 --modes gptq.int4 none --iters 1 > $D/pf.log 2>&1
+  -- python3 $R/tools/prefill_bench.py --T 2048 --modes $MODES --iters 1 > $D/pf.log 2>&1
 echo "rc=$?"
-python3 - "$D" "$R/gpurun_out/$OUT.json" <<'PY'
+python3 - "$D" "$R/gpurun_out/$OUT.json" "$MODES" <<'PY'
 import csv, glob, json, sys, collections
-d, out = sys.argv[1], sys.argv[2]
+d, out, modes = sys.argv[1], sys.argv[2], sys.argv[3]
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 cnt = collections.Counter()
 for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
@@ -32,7 +33,7 @@ for k, v in agg.items():
     if v.get("GRBM_GUI_ACTIVE"):
         e["mfma_busy"] = v["SQ_VALU_MFMA_BUSY_CYCLES"] / (v["GRBM_GUI_ACTIVE"] / 8 * 1024)
     res[k] = e
-json.dump({"what": "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE over tools/prefill_bench.py --T 2048 --modes gptq.int4 none --iters 1 (7B)",
+json.dump({"what": f"rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE over tools/prefill_bench.py --T 2048 --modes {modes} --iters 1 (7B)",
            "formula": "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)", "kernels": res},
           open(out, "w"), indent=1)
 print(json.dumps({k: round(e.get("mfma_busy", -1), 3) for k, e in res.items()}))
