@@ -216,15 +216,19 @@ __device__ __forceinline__ int kofs(int t, int grp) {
 // (`stage`, free A-image space) once per workgroup, then thread t (column t % 16, every
 // (NW*4)-th outlier of the chunk) accumulates; the four lanes of a wave sharing a column are
 // combined by shuffles and the per-wave partials land in part[NW][8][16]. Ends with a barrier.
-// Fast path (every k-block has <= SPC = NT / kNSB outlier columns): the
-// list entries were loaded speculatively in the prologue (`spk`: entry tid % SPC of k-block
-// tid / SPC), so after the stream the chain is prefix (LDS) -> the f16(A) values and the tile's 16
+// Fast path (every k-block has <= SPC = kSpE * NT / kNSB outlier columns): the list entries were
+// loaded speculatively in the prologue (`spk[e]`: entry q % SPC of k-block q / SPC, q = tid + NT e),
+// so after the stream the chain is prefix (LDS) -> the f16(A) values and the tile's 16
 // CB bytes of each column in ONE memory latency -> accumulate from LDS, instead of list -> A ->
 // CB (three). Same per-thread accumulation order: bit-identical to the general path.
 constexpr int kSideChunk = 256;
+// speculative list entries per thread: 24 (4 waves) / 32 (8 waves) per k-block, so ~300 random
+// outlier columns (9.4 per k-block on average) stay on the fast path
+template <int NW>
+constexpr int kSpE = NW == 4 ? 3 : 2;
 template <int NW>
 __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float* SCB, int n0, float* part,
-                             unsigned char* stage, int cnt_lane, int spk) {
+                             unsigned char* stage, int cnt_lane, const int (&spk)[kSpE<NW>]) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nl = tid & 15, g = tid >> 4;
   constexpr int NG = NW * 4, NT = NW * 64;
@@ -245,7 +249,7 @@ __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float*
     }
     s_pre[tid + 1] = x;
     if (tid == 0) s_pre[0] = 0;
-    const unsigned long long ov = __ballot(tid < h.nsb && c > NT / kNSB);
+    const unsigned long long ov = __ballot(tid < h.nsb && c > kSpE<NW> * NT / kNSB);
     if (tid == 0) s_pre[63] = ov != 0ull;  // a k-block past the speculative entries
   }
   __syncthreads();
@@ -253,28 +257,36 @@ __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float*
   const bool general = s_pre[63];
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (!general) {  // every entry is one thread's speculative list load: one memory latency in all
-    constexpr int SPC = NT / kNSB;
+    constexpr int E = kSpE<NW>, SPC = E * NT / kNSB;
     _Float16* s_a16 = reinterpret_cast<_Float16*>(s_k);                      // [8][kSideChunk]
     uint32_t* s_cb = reinterpret_cast<uint32_t*>(s_a16 + 8 * kSideChunk);  // [kSideChunk][16 bytes]
-    const int b = tid / SPC, j = tid % SPC;
-    const bool mine = b < h.nsb && j < s_pre[b + 1] - s_pre[b];
-    const int i = mine ? s_pre[b] + j : -1;
-    float av[8];
-    uint32_t cw[4] = {0, 0, 0, 0};
-    if (mine) {
-      const int k = spk, kk = k & 127;
+    int ie[E];
+    float av[E][8];
+    uint32_t cw[E][4];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) av[m] = bf2f(p.A[(size_t)(m < M ? m : 0) * p.lda + k]);
+    for (int e = 0; e < E; ++e) {
+      const int q = tid + NT * e, b = q / SPC, j = q % SPC;
+      const bool mine = b < h.nsb && j < s_pre[b + 1] - s_pre[b];
+      ie[e] = mine ? s_pre[b] + j : -1;
+      const int k = mine ? spk[e] : 0, kk = k & 127;  // (k = 0: a valid address, never stored)
+#pragma unroll
+      for (int m = 0; m < 8; ++m) av[e][m] = bf2f(p.A[(size_t)(m < M ? m : 0) * p.lda + k]);
       const int8_t* cbp = CB + (((size_t)(n0 >> 4) * (p.K >> 7) + (k >> 7)) * 2 + (kk >> 6)) * 1024 +
                           (16 * ((kk >> 4) & 3)) * 16 + (kk & 15);
 #pragma unroll
-      for (int c = 0; c < 16; ++c) cw[c >> 2] |= (uint32_t)(uint8_t)cbp[c * 16] << (8 * (c & 3));
+      for (int w = 0; w < 4; ++w) cw[e][w] = 0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) cw[e][c >> 2] |= (uint32_t)(uint8_t)cbp[c * 16] << (8 * (c & 3));
     }
     for (int c0 = 0; c0 < total; c0 += kSideChunk) {  // rounds of kSideChunk entries (LDS)
-      if (i >= c0 && i < c0 + kSideChunk) {
 #pragma unroll
-        for (int m = 0; m < 8; ++m) s_a16[m * kSideChunk + i - c0] = m < M ? (_Float16)av[m] : (_Float16)0.f;
-        *reinterpret_cast<uint4*>(s_cb + 4 * (i - c0)) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+      for (int e = 0; e < E; ++e) {
+        const int i = ie[e];
+        if (i >= c0 && i < c0 + kSideChunk) {
+#pragma unroll
+          for (int m = 0; m < 8; ++m) s_a16[m * kSideChunk + i - c0] = m < M ? (_Float16)av[e][m] : (_Float16)0.f;
+          *reinterpret_cast<uint4*>(s_cb + 4 * (i - c0)) = make_uint4(cw[e][0], cw[e][1], cw[e][2], cw[e][3]);
+        }
       }
       __syncthreads();
       const int8_t* cb8 = reinterpret_cast<const int8_t*>(s_cb);
@@ -791,14 +803,17 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   for (int d = 0; d < D; ++d) load(d, d);  // the weight stream starts before any A wait
   // int8: the per-k-block outlier counts the side product starts from, loaded now (one memory
   // latency less in the tail; needed once the stream is done)
-  int i8cnt = 0, i8spk = 0;
+  int i8cnt = 0, i8spk[kSpE<NW>] = {};
   if constexpr (I8) {  // + the speculative outlier-list entries of the side product's fast path
     const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
     const I8Layout L8 = i8_layout(p.i8ws, h.mtot, h.K);
     i8cnt = L8.cnt[lane < kNSB ? lane : 0];
-    constexpr int SPC = NT / kNSB;
-    const int sb = tid / SPC < kNSB ? tid / SPC : 0;
-    i8spk = L8.list[sb * h.kb + tid % SPC];
+    constexpr int SPC = kSpE<NW> * NT / kNSB;
+#pragma unroll
+    for (int e = 0; e < kSpE<NW>; ++e) {
+      const int q = tid + NT * e, sb = q / SPC < kNSB ? q / SPC : 0;
+      i8spk[e] = L8.list[sb * h.kb + q % SPC];
+    }
   }
   LLJ_STAMP(1);
   float2 e_cs[TPW][4];

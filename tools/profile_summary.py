@@ -66,6 +66,17 @@ def algo_bytes_int4(op: str, M: int = 1) -> float:
             "lm_head": lin(V, C) + M * C * 2 + M * V * 2}[op]
 
 
+def algo_bytes_int8(op: str, M: int = 1) -> float:
+    """LLM.int8 GEMV (wfmt 2): int8 CB codes + fp32 SCB + the quantized rows (int8) + bf16 out / residual."""
+    def lin(N, K):
+        return N * K + 4 * N
+    return {"qkv": lin(3 * C, C) + M * C + M * 3 * C * 2,
+            "attn.c_proj": lin(C, C) + M * C + 2 * M * C * 2,
+            "swiglu": 2 * lin(H, C) + M * C + M * H * 2,
+            "mlp.c_proj": lin(C, H) + M * H + 2 * M * C * 2,
+            "lm_head": lin(V, C) + M * C + M * V * 2}[op]
+
+
 def main():
     d = Path(sys.argv[1])
     out = {"source": str(d), "passes": {}, "kernels": {}}
@@ -100,6 +111,9 @@ def main():
                 ent["hbm_bytes"] = (2 * ent["FETCH_SIZE"] + ent["WRITE_SIZE"]) * 1024
                 if prefix in ("bs1", "bs8") and k["op"]:
                     ent["algorithmic_bytes"] = algo_bytes_int4(k["op"], 8 if prefix == "bs8" else 1)
+                    ent["traffic_over_algorithmic"] = round(ent["hbm_bytes"] / ent["algorithmic_bytes"], 3)
+                elif prefix == "c3" and k["op"] and name.startswith("llj::gemv_kernel<2,"):
+                    ent["algorithmic_bytes"] = algo_bytes_int8(k["op"], 1)
                     ent["traffic_over_algorithmic"] = round(ent["hbm_bytes"] / ent["algorithmic_bytes"], 3)
             if "SQ_VALU_MFMA_BUSY_CYCLES" in ent and ent.get("GRBM_GUI_ACTIVE"):
                 ent["mfma_busy"] = ent["SQ_VALU_MFMA_BUSY_CYCLES"] / (ent["GRBM_GUI_ACTIVE"] / 8 * 1024)
