@@ -719,8 +719,11 @@ class _OneBlock:
     def _i8_norm_prep(self, *a):
         LLaMA._i8_norm_prep(self, *a)
 
-    def _resid(self, *a):
-        LLaMA._resid(self, *a)
+    def _resid(self, *a, **kw):
+        LLaMA._resid(self, *a, **kw)
+
+    def _gemm_resid(self, *a):
+        LLaMA._gemm_resid(self, *a)
 
     def _attention(self, *a):
         LLaMA._attention(self, *a)
