@@ -180,15 +180,23 @@ int llj_gemm_qkv_rope(int wfmt, const void* x, const void* W, const void* sz, vo
  * bitsandbytes MatMul8bitLt): the four GEMMs above for CB (N, K) int8 in the I8P tiling and SCB
  * (N) fp32, with i8ws = llj_i8_stats / llj_i8_norm_stats of A (all M rows): int8 MFMA over the
  * quantized rows + the fp16 outlier side product, y = f16(f16(acc * SCA * SCB / 127^2) + side), then
- * the same epilogues. N % 128 == 0, K % 128 == 0. */
-int llj_gemm_i8_linear(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* C, int ldc,
-                       int M, int N, int K, void* stream);
-int llj_gemm_i8_resid(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* x, int ldx,
-                      int M, int N, int K, void* stream);
-int llj_gemm_i8_silu_mul(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* h, int ldh,
-                         int M, int N, int K, void* stream);
-int llj_gemm_i8_qkv_rope(const void* x, const void* CB, const void* SCB, const void* i8ws, void* q_out, void* kcache,
-                         void* vcache, const float* rope, const int* pos, int B, int T, int C, int n_head, int S,
+ * the same epilogues. N % 128 == 0, K % 128 == 0. ao16 / w16 / kpad: llj_i8_gather_* (optional). */
+int llj_gemm_i8_linear(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, const void* ao16,
+                       const void* w16, int kpad, void* C, int ldc, int M, int N, int K, void* stream);
+int llj_gemm_i8_resid(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, const void* ao16,
+                      const void* w16, int kpad, void* x, int ldx, int M, int N, int K, void* stream);
+int llj_gemm_i8_silu_mul(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, const void* ao16,
+                         const void* w16, int kpad, void* h, int ldh, int M, int N, int K, void* stream);
+int llj_gemm_i8_qkv_rope(const void* x, const void* CB, const void* SCB, const void* i8ws, const void* ao16,
+                         const void* w16, int kpad, void* q_out, void* kcache, void* vcache, const float* rope,
+                         const int* pos, int B, int T, int C, int n_head, int S, void* stream);
+/* The outlier columns of an activation (its llj_i8_stats workspace) gathered as f16 rows
+ * ao16[M][kpad] and of a weight (CB in I8P, SCB) as f16(CB * SCB / 127) rows w16[N][kpad], zero past
+ * the outlier count up to a multiple of 64 (kpad >= K rounded up to 64, kpad % 8 == 0): with both
+ * passed to llj_gemm_i8_* (else NULL, NULL, 0) the fp16 outlier side product runs as a dense f16
+ * GEMM over them (bitsandbytes' fp16 matmul of the outlier sub-matrices). */
+int llj_i8_gather_act(const void* A, int lda, int M, int K, const void* i8ws, void* ao16, int kpad, void* stream);
+int llj_i8_gather_weight(const void* CB, const void* SCB, int N, int K, const void* i8ws, void* w16, int kpad,
                          void* stream);
 
 /* ---------------------------------------------------------------- LLM.int8() */

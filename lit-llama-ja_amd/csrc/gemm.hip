@@ -66,6 +66,12 @@ struct GemmParams {
   int n_head, head_size, S, T;
   int gch;  // GWF_W4G: group size in 128-deep chunks; sz = (scale, 128 + zero) per (group, column), (G, N)
   const char* i8ws;  // GWF_I8: llj_i8_stats workspace of A (aq, SCA, outlier list); sz = (const float*) SCB
+  // GWF_I8 (optional): the outlier columns pre-gathered by llj_i8_gather_act / _weight, f16 rows of
+  // stride kpad, zero past the outlier count up to a multiple of 64: the side product then runs as
+  // a dense f16 GEMM over them (coalesced 64-deep chunks) instead of per-tile gathers
+  const _Float16* ao16;
+  const _Float16* w16;
+  int kpad;
 };
 
 constexpr int kGBM = 128, kGBN = 128, kGBK = 64, kGNT = 256;
@@ -110,7 +116,10 @@ constexpr int kSideK = 32, kSideP = 40;  // pitch in halves
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 template <int WF, int BM = kGBM>
 constexpr size_t gemm_lds_bytes() {
-  return 2 * ((size_t)BM * kAP * 2 + gemm_b_bytes<WF>()) + BM * sizeof(float);
+  // GWF_I8: also the dense side loop's two (A, B) f16 chunk buffers at the bf16 pitch
+  const size_t main = 2 * ((size_t)BM * kAP * 2 + gemm_b_bytes<WF>()) + BM * sizeof(float);
+  const size_t side = 2 * ((size_t)BM * kAP * 2 + (size_t)kGBN * kAP * 2);
+  return WF == GWF_I8 && side > main ? side : main;
 }
 
 // BM: rows per tile (128, or 256 for bf16 with 8 waves: 4 row groups x 2 column groups of 64 x 64)
@@ -368,7 +377,50 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
     const int total = s_pre[h8.nsb];
     const int sn = n0 + (bt >> 1);  // staging: W column (B) bt >> 1 / A row (A) ar, outliers 16 ah + [0, 16)
     const float scb = reinterpret_cast<const float*>(p.sz)[sn] / 127.f;
-    for (int c0 = 0; c0 < total; c0 += kSideK) {
+    if (p.ao16) {  // dense f16 GEMM over the pre-gathered outlier columns, 64-deep chunks
+      __syncthreads();  // every thread has read `total` before the chunk buffers overwrite s_pre
+      const int SKC = (total + 63) >> 6;
+      constexpr int BVD = BM == 256 ? 2 : 4;
+      _Float16* SA = reinterpret_cast<_Float16*>(smem);  // [2][BM][kAP]
+      _Float16* SB = SA + 2 * BM * kAP;                  // [2][128][kAP]
+      u32x4 ra[4], rb[BVD];
+      auto sload = [&](int c) {
+        const _Float16* a = p.ao16 + (size_t)agm * p.kpad + c * 64 + ah * 32;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) ra[v] = *reinterpret_cast<const u32x4*>(a + 8 * v);
+        const _Float16* b = p.w16 + (size_t)(n0 + br) * p.kpad + c * 64 + bq * 8 * BVD;
+#pragma unroll
+        for (int v = 0; v < BVD; ++v) rb[v] = *reinterpret_cast<const u32x4*>(b + 8 * v);
+      };
+      if (SKC > 0) sload(0);
+      for (int c = 0; c < SKC; ++c) {
+        const int buf = c & 1;
+        _Float16* sa = SA + (size_t)buf * BM * kAP;
+        _Float16* sb = SB + (size_t)buf * kGBN * kAP;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) *reinterpret_cast<u32x4*>(sa + ar * kAP + ah * 32 + 8 * v) = ra[v];
+#pragma unroll
+        for (int v = 0; v < BVD; ++v) *reinterpret_cast<u32x4*>(sb + br * kAP + bq * 8 * BVD + 8 * v) = rb[v];
+        __syncthreads();  // chunk c staged; every wave is done with chunk c - 1's buffer
+        if (c + 1 < SKC) sload(c + 1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          f16x8 af[4], bfr[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            af[i] = *reinterpret_cast<const f16x8*>(sa + (wr * 64 + 16 * i + row) * kAP + 32 * s2 + 8 * g);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            bfr[j] = *reinterpret_cast<const f16x8*>(sb + (wc * 64 + 16 * j + row) * kAP + 32 * s2 + 8 * g);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              sacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bfr[j], sacc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    for (int c0 = 0; c0 < (p.ao16 ? 0 : total); c0 += kSideK) {
       if (tid < kSideK) {
         const int fi = c0 + tid;
         int k = -1;
@@ -525,6 +577,7 @@ static int gemm_run(int wfmt, GemmParams& p, void* stream) {
   }
   if (wfmt == GWF_I8) {
     if (!p.sz || !p.i8ws || p.K % 128) return LLJ_EINVAL;
+    if (!p.ao16 != !p.w16 || (p.ao16 && (p.kpad < ((p.K + 63) & ~63) || p.kpad % 8))) return LLJ_EINVAL;
     if (LLJ_GEMM_BM256_I8 && p.M >= 256) return gemm_launch<GWF_I8, EP, 256>(p, s);
     return gemm_launch<GWF_I8, EP>(p, s);
   }
@@ -562,35 +615,39 @@ int llj_gemm_silu_mul(int wfmt, const void* A, int lda, const void* W, const voi
 }
 
 // LLM.int8() forms (wfmt 2): W = CB in the I8P tiling, sz = SCB (fp32), i8ws = llj_i8_stats of A
-int llj_gemm_i8_linear(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* C, int ldc,
-                       int M, int N, int K, void* stream) {
+int llj_gemm_i8_linear(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, const void* ao16,
+                       const void* w16, int kpad, void* C, int ldc, int M, int N, int K, void* stream) {
   GemmParams p{};
+  p.ao16 = (const _Float16*)ao16; p.w16 = (const _Float16*)w16; p.kpad = kpad;
   p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = CB; p.sz = (const float2*)SCB;
   p.C = (bf16_t*)C; p.ldc = ldc; p.i8ws = (const char*)i8ws;
   return gemm_run<GEP_STORE>(GWF_I8, p, stream);
 }
 
-int llj_gemm_i8_resid(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* x, int ldx,
-                      int M, int N, int K, void* stream) {
+int llj_gemm_i8_resid(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, const void* ao16,
+                      const void* w16, int kpad, void* x, int ldx, int M, int N, int K, void* stream) {
   GemmParams p{};
+  p.ao16 = (const _Float16*)ao16; p.w16 = (const _Float16*)w16; p.kpad = kpad;
   p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = CB; p.sz = (const float2*)SCB;
   p.C = (bf16_t*)x; p.ldc = ldx; p.i8ws = (const char*)i8ws;
   return gemm_run<GEP_RESID>(GWF_I8, p, stream);
 }
 
-int llj_gemm_i8_silu_mul(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, void* h, int ldh,
-                         int M, int N, int K, void* stream) {
+int llj_gemm_i8_silu_mul(const void* A, int lda, const void* CB, const void* SCB, const void* i8ws, const void* ao16,
+                         const void* w16, int kpad, void* h, int ldh, int M, int N, int K, void* stream) {
   GemmParams p{};
+  p.ao16 = (const _Float16*)ao16; p.w16 = (const _Float16*)w16; p.kpad = kpad;
   p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = CB; p.sz = (const float2*)SCB;
   p.C = (bf16_t*)h; p.ldc = ldh; p.i8ws = (const char*)i8ws;
   return gemm_run<GEP_SILU_MUL>(GWF_I8, p, stream);
 }
 
-int llj_gemm_i8_qkv_rope(const void* x, const void* CB, const void* SCB, const void* i8ws, void* q_out, void* kcache,
-                         void* vcache, const float* rope, const int* pos, int B, int T, int C, int n_head, int S,
-                         void* stream) {
+int llj_gemm_i8_qkv_rope(const void* x, const void* CB, const void* SCB, const void* i8ws, const void* ao16,
+                         const void* w16, int kpad, void* q_out, void* kcache, void* vcache, const float* rope,
+                         const int* pos, int B, int T, int C, int n_head, int S, void* stream) {
   if (B < 1 || T < 1 || n_head < 1 || C % n_head || S < 1 || !pos || !rope) return LLJ_EINVAL;
   GemmParams p{};
+  p.ao16 = (const _Float16*)ao16; p.w16 = (const _Float16*)w16; p.kpad = kpad;
   p.A = (const bf16_t*)x; p.lda = C; p.M = B * T; p.N = 3 * C; p.K = C; p.W = CB; p.sz = (const float2*)SCB;
   p.q_out = (bf16_t*)q_out; p.kcache = (bf16_t*)kcache; p.vcache = (bf16_t*)vcache; p.rope = rope; p.pos = pos;
   p.n_head = n_head; p.head_size = C / n_head; p.S = S; p.T = T; p.i8ws = (const char*)i8ws;

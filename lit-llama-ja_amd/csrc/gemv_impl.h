@@ -224,8 +224,11 @@ __device__ __forceinline__ int kofs(int t, int grp) {
 constexpr int kSideChunk = 256;
 // speculative list entries per thread: 24 (4 waves) / 32 (8 waves) per k-block, so ~300 random
 // outlier columns (9.4 per k-block on average) stay on the fast path
+#ifndef LLJ_I8_SPE
+#define LLJ_I8_SPE 0  // 0: 3 (4 waves) / 2 (8 waves); else that many entries per thread (A/B)
+#endif
 template <int NW>
-constexpr int kSpE = NW == 4 ? 3 : 2;
+constexpr int kSpE = LLJ_I8_SPE ? LLJ_I8_SPE : (NW == 4 ? 3 : 2);
 template <int NW>
 __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float* SCB, int n0, float* part,
                              unsigned char* stage, int cnt_lane, const int (&spk)[kSpE<NW>]) {

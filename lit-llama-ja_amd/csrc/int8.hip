@@ -439,6 +439,67 @@ __global__ __launch_bounds__(256) void i8_quant_weight_kernel(const void* __rest
 }
 
 
+// ---- outlier gathers for the LLM.int8 prefill GEMM's side product (llj_gemm_i8_*): the outlier
+// columns (ascending, from the per-k-block lists) of the activation as f16 rows ao16[M][kpad] and of
+// the weight as f16(CB * SCB / 127) rows w16[N][kpad]; entries past the outlier count up to the next
+// multiple of 64 are zero, so the GEMM reads whole 64-deep chunks with 16-byte loads.
+// The flat list is rebuilt in LDS by every block (counts prefix + the per-block lists).
+__device__ __forceinline__ int i8_flat_list(const I8Layout& L, const I8WsHeader& h, int* s_pre, int* s_list) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (tid < 64) {
+    const int c = tid < h.nsb ? L.cnt[tid] : 0;
+    int x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    s_pre[tid + 1] = x;
+    if (tid == 0) s_pre[0] = 0;
+  }
+  __syncthreads();
+  for (int b = 0; b < h.nsb; ++b)
+    for (int j = tid; j < s_pre[b + 1] - s_pre[b]; j += blockDim.x) s_list[s_pre[b] + j] = L.list[b * h.kb + j];
+  __syncthreads();
+  return s_pre[h.nsb];
+}
+
+__global__ __launch_bounds__(256) void i8_gather_act_kernel(const bf16_t* __restrict__ A, int lda, const char* __restrict__ ws,
+                                                            _Float16* __restrict__ ao16, int kpad) {
+  extern __shared__ int g_lds[];
+  const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(ws);
+  const I8Layout L = i8_layout(ws, h.mtot, h.K);
+  const int total = i8_flat_list(L, h, g_lds, g_lds + 80);
+  const int* s_list = g_lds + 80;
+  const int m = blockIdx.x, nop = (total + 63) & ~63;
+  for (int j = threadIdx.x; j < nop; j += 256)
+    ao16[(size_t)m * kpad + j] = j < total ? (_Float16)bf2f(A[(size_t)m * lda + s_list[j]]) : (_Float16)0.f;
+}
+
+// block: 16 weight rows (one I8P tile) x the outlier columns; thread: row tid >> 4, columns
+// (tid & 15) + 16 i (16 consecutive halves per row and step: coalesced stores)
+__global__ __launch_bounds__(256) void i8_gather_weight_kernel(const int8_t* __restrict__ CB, const float* __restrict__ SCB,
+                                                               int K, const char* __restrict__ ws,
+                                                               _Float16* __restrict__ w16, int kpad) {
+  extern __shared__ int g_lds[];
+  const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(ws);
+  const I8Layout L = i8_layout(ws, h.mtot, h.K);
+  const int total = i8_flat_list(L, h, g_lds, g_lds + 80);
+  const int* s_list = g_lds + 80;
+  const int nt = blockIdx.x, r = threadIdx.x >> 4, n = nt * 16 + r, nop = (total + 63) & ~63;
+  const float scb = SCB[n] / 127.f;
+  for (int j = threadIdx.x & 15; j < nop; j += 16) {
+    _Float16 w = (_Float16)0.f;
+    if (j < total) {
+      const int k = s_list[j], kk = k & 127;
+      const int q = CB[(((size_t)nt * (K >> 7) + (k >> 7)) * 2 + (kk >> 6)) * 1024 + (16 * ((kk >> 4) & 3) + r) * 16 +
+                       (kk & 15)];
+      w = (_Float16)((float)q * scb);
+    }
+    w16[(size_t)n * kpad + j] = w;
+  }
+}
+
 // i8_prep_one_kernel for M <= 8, K <= 6 * 2048 (with the norm 4 * 2048), M * (k-block width / 8) <= 1024: returns 0 after the
 // launch (or -hipError), 1 when the shape is outside that envelope (nothing launched)
 static int i8_prep_one(bool norm, const bf16_t* x, int lda, const bf16_t* w, float eps, bf16_t* xn, int M, int K,
@@ -513,6 +574,27 @@ int llj_i8_norm_stats(const void* x, const void* norm_w, float eps, void* xn, in
 #undef LLJ_NS
   LLJ_CHECK_LAUNCH();
   hipLaunchKernelGGL(i8_quant_act_kernel, dim3(M), dim3(256), 0, s, (const bf16_t*)xn, K, M, K, (char*)ws);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_i8_gather_act(const void* A, int lda, int M, int K, const void* ws, void* ao16, int kpad, void* stream) {
+  LLJ_REQUIRE(M > 0 && K > 0 && kpad >= ((K + 63) & ~63) && kpad % 8 == 0 && ws && ao16);
+  const size_t lds = (80 + (size_t)K) * sizeof(int);
+  LLJ_REQUIRE(lds <= 65536);
+  hipLaunchKernelGGL(i8_gather_act_kernel, dim3(M), dim3(256), lds, (hipStream_t)stream, (const bf16_t*)A, lda,
+                     (const char*)ws, (_Float16*)ao16, kpad);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_i8_gather_weight(const void* CB, const void* SCB, int N, int K, const void* ws, void* w16, int kpad,
+                         void* stream) {
+  LLJ_REQUIRE(N > 0 && N % 16 == 0 && K % 128 == 0 && kpad >= ((K + 63) & ~63) && kpad % 8 == 0 && ws && w16);
+  const size_t lds = (80 + (size_t)K) * sizeof(int);
+  LLJ_REQUIRE(lds <= 65536);
+  hipLaunchKernelGGL(i8_gather_weight_kernel, dim3(N / 16), dim3(256), lds, (hipStream_t)stream, (const int8_t*)CB,
+                     (const float*)SCB, K, (const char*)ws, (_Float16*)w16, kpad);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

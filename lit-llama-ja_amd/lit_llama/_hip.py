@@ -35,10 +35,12 @@ SIGNATURES = {
                           _P],
     "llj_attention_split": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
     "llj_attention_decode": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
-    "llj_gemm_i8_linear": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P],
-    "llj_gemm_i8_resid": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P],
-    "llj_gemm_i8_silu_mul": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P],
-    "llj_gemm_i8_qkv_rope": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "llj_gemm_i8_linear": [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P],
+    "llj_gemm_i8_resid": [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P],
+    "llj_gemm_i8_silu_mul": [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P],
+    "llj_gemm_i8_qkv_rope": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "llj_i8_gather_act": [_P, _I, _I, _I, _P, _P, _I, _P],
+    "llj_i8_gather_weight": [_P, _P, _I, _I, _P, _P, _I, _P],
     "llj_gptq_block": [_P, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P],
     "llj_colblock_pack": [_P, _I, _I, _P, _P, _I, _P, _P],
     "llj_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],

@@ -149,6 +149,10 @@ _GEMM_FMTS = (0, 1, 2, 3, 4)  # weight formats (low byte of wfmt; 4 = grouped in
 def _gemm_fmt(wfmt: int) -> bool:
     return (wfmt & 0xFF) in _GEMM_FMTS
 
+# LLM.int8 prompt rows: the outlier columns of each GEMM's activation and weight pre-gathered as f16
+# rows (llj_i8_gather_act / _weight), so the fp16 side product runs as a dense f16 GEMM over them
+I8_GATHER = True
+
 # int8 decode: RMSNorm + LLM.int8() statistics in one launch pair up to this many rows
 I8_NORM_STATS_MAX_M = 16
 
@@ -399,6 +403,23 @@ class LLaMA(nn.Module):
         _hip.call("llj_rmsnorm", x.data_ptr(), norm.scale.data_ptr(), norm.eps, xn.data_ptr(), M, K, st)
         self._i8_prep(xn, M, K, w, st)
 
+    def _i8_gathered(self, A, M, K, lins, w, st):
+        """(ao16, [w16 per (W, sz, N) in lins], kpad): the outlier columns of A (statistics already in
+        w.i8ws) and of each weight as f16 rows for the LLM.int8 GEMMs (I8_GATHER), else (None, Nones, 0).
+        Stream-ordered: freed after the call, reused only by later work on the same stream."""
+        if not I8_GATHER:
+            return None, [None] * len(lins), 0
+        kpad = (K + 63) // 64 * 64
+        ao = torch.empty(M, kpad, dtype=torch.float16, device=A.device)
+        _hip.call("llj_i8_gather_act", A.data_ptr(), A.stride(0), M, K, w.i8ws.data_ptr(), ao.data_ptr(), kpad, st)
+        out = []
+        for W, sz, N in lins:
+            t = torch.empty(N, kpad, dtype=torch.float16, device=A.device)
+            _hip.call("llj_i8_gather_weight", W.data_ptr(), _hip.ptr(sz), N, K, w.i8ws.data_ptr(), t.data_ptr(), kpad,
+                      st)
+            out.append(t)
+        return ao, out, kpad
+
     def _flash_ok(self, pos, T, S):
         """prompt rows attend through the flash kernel: T >= FLASH_MIN_T, head_size 64 / 128,
         positions contiguous and inside the cache without wrapping (one host read of pos; prompts
@@ -446,8 +467,10 @@ class LLaMA(nn.Module):
             kc, vc = kv[i]
             if fa == 2:  # LLM.int8: the norm + the activation statistics of all M rows, then the int8 GEMM
                 self._i8_norm_prep(w.x, blk.rms_1, w.xn, M, C, w, st)
-                _hip.call("llj_gemm_i8_qkv_rope", w.xn.data_ptr(), wa.data_ptr(), P(sa), I8ws, w.q.data_ptr(),
-                          kc.data_ptr(), vc.data_ptr(), self.rope_cache.data_ptr(), pos.data_ptr(), B, T, C, nh, S, st)
+                ao, (wg,), kp = self._i8_gathered(w.xn, M, C, [(wa, sa, 3 * C)], w, st)
+                _hip.call("llj_gemm_i8_qkv_rope", w.xn.data_ptr(), wa.data_ptr(), P(sa), I8ws, P(ao), P(wg), kp,
+                          w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), self.rope_cache.data_ptr(), pos.data_ptr(),
+                          B, T, C, nh, S, st)
             else:
                 _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
                           w.xn.data_ptr(), None, M, C, st)
@@ -459,10 +482,11 @@ class LLaMA(nn.Module):
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")
             if f1 == 2:
                 self._i8_norm_prep(w.x, blk.rms_2, w.xn, M, C, w, st)
-                _hip.call("llj_gemm_i8_linear", w.xn.data_ptr(), C, w1.data_ptr(), P(s1), I8ws, w.h.data_ptr(), H, M,
-                          H, C, st)
-                _hip.call("llj_gemm_i8_silu_mul", w.xn.data_ptr(), C, w2.data_ptr(), P(s2), I8ws, w.h.data_ptr(), H,
-                          M, H, C, st)
+                ao, (g1, g2), kp = self._i8_gathered(w.xn, M, C, [(w1, s1, H), (w2, s2, H)], w, st)
+                _hip.call("llj_gemm_i8_linear", w.xn.data_ptr(), C, w1.data_ptr(), P(s1), I8ws, P(ao), P(g1), kp,
+                          w.h.data_ptr(), H, M, H, C, st)
+                _hip.call("llj_gemm_i8_silu_mul", w.xn.data_ptr(), C, w2.data_ptr(), P(s2), I8ws, P(ao), P(g2), kp,
+                          w.h.data_ptr(), H, M, H, C, st)
             else:
                 _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
                           w.xn.data_ptr(), None, M, C, st)
@@ -476,8 +500,9 @@ class LLaMA(nn.Module):
         """x += A . W^T for many rows (LLM.int8: the statistics of A first)."""
         if f == 2:
             self._i8_prep(A, M, K, w, st)
+            ao, (wg,), kp = self._i8_gathered(A, M, K, [(W, sz, N)], w, st)
             _hip.call("llj_gemm_i8_resid", A.data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz), _hip.ptr(w.i8ws),
-                      x.data_ptr(), x.stride(0), M, N, K, st)
+                      _hip.ptr(ao), _hip.ptr(wg), kp, x.data_ptr(), x.stride(0), M, N, K, st)
         else:
             _hip.call("llj_gemm_resid", f, A.data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz), x.data_ptr(),
                       x.stride(0), M, N, K, st)
@@ -620,8 +645,9 @@ class LLaMA(nn.Module):
             xn = torch.empty_like(x)
             self._i8_norm_prep(x, ln, xn, M, C, w, st)
             if M >= GEMM_MIN_ROWS and C % 128 == 0 and V % 128 == 0:  # many rows: the int8 GEMM
+                ao, (wg,), kp = self._i8_gathered(xn, M, C, [(W, sz, V)], w, st)
                 _hip.call("llj_gemm_i8_linear", xn.data_ptr(), C, W.data_ptr(), _hip.ptr(sz), _hip.ptr(w.i8ws),
-                          out.data_ptr(), out.stride(0), M, V, C, st)
+                          _hip.ptr(ao), _hip.ptr(wg), kp, out.data_ptr(), out.stride(0), M, V, C, st)
                 return
             src, nw = xn, None
         elif M >= GEMM_MIN_ROWS and _gemm_fmt(f) and C % 128 == 0 and V % 128 == 0:  # many rows: GEMM

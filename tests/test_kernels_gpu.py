@@ -937,12 +937,30 @@ def test_i8_stats_many_rows(hip, M, K):
     _check_i8_ws(ws.cpu().numpy(), x, M, K)
 
 
+def _i8_gather(hip, xd, M, K, ws, weights, on):
+    """(ao16, [w16], kpad) pointers for llj_gemm_i8_* (the pre-gathered outlier matrices), or Nones."""
+    if not on:
+        return None, [None] * len(weights), 0, []
+    kpad = (K + 63) // 64 * 64
+    ao = torch.full((M, kpad), float("nan"), dtype=torch.float16, device=dev)  # past the pad: never read
+    call(hip, "llj_i8_gather_act", xd.data_ptr(), K, M, K, ws.data_ptr(), ao.data_ptr(), kpad, st())
+    keep, ptrs = [ao], []
+    for cbt, scb, N in weights:
+        t = torch.full((N, kpad), float("nan"), dtype=torch.float16, device=dev)
+        call(hip, "llj_i8_gather_weight", cbt.data_ptr(), scb.data_ptr(), N, K, ws.data_ptr(), t.data_ptr(), kpad, st())
+        keep.append(t)
+        ptrs.append(t.data_ptr())
+    return ao.data_ptr(), ptrs, kpad, keep
+
+
+@pytest.mark.parametrize("gather", [False, True])
 @pytest.mark.parametrize("outliers", [0, 6, 300])
 @pytest.mark.parametrize("M,N,K", [(40, 256, 4096), (300, 4096, 4096), (129, 384, 11008)])
-def test_gemm_i8_linear_resid_silu(hip, M, N, K, outliers):
+def test_gemm_i8_linear_resid_silu(hip, M, N, K, outliers, gather):
     """LLM.int8() prefill GEMM (int8 MFMA over the quantized rows + the fp16 outlier side product;
     llj_gemm_i8_linear / _resid / _silu_mul) against the oracle's restatement (bitsandbytes absent:
-    parity unpinned) and against the int8 GEMV on the same workspace."""
+    parity unpinned) and against the int8 GEMV on the same workspace; the side product either
+    gathered per tile or as a dense f16 GEMM over the pre-gathered outlier matrices (gather)."""
     rng = np.random.default_rng(M + N + K + outliers)
     W = bf16(rng.standard_normal((N, K)) * 0.02)
     W2 = bf16(rng.standard_normal((N, K)) * 0.02)
@@ -952,23 +970,24 @@ def test_gemm_i8_linear_resid_silu(hip, M, N, K, outliers):
     xd = T(x, torch.bfloat16)
     ws = torch.empty(hip.llj_i8_ws_bytes(M, K), dtype=torch.uint8, device=dev)
     call(hip, "llj_i8_stats", xd.data_ptr(), K, M, K, 6.0, ws.data_ptr(), st())
+    ao, (g1, g2), kp, keep = _i8_gather(hip, xd, M, K, ws, [(cbt, scb, N), (cbt2, scb2, N)], gather)
     out = torch.full((M + 1, N), 7.0, dtype=torch.bfloat16, device=dev)  # row M: canary
-    call(hip, "llj_gemm_i8_linear", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), out.data_ptr(), N,
-         M, N, K, st())
+    call(hip, "llj_gemm_i8_linear", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), ao, g1, kp,
+         out.data_ptr(), N, M, N, K, st())
     x0 = bf16(rng.standard_normal((M, N)).astype(np.float32))
     xr = T(x0, torch.bfloat16)
-    call(hip, "llj_gemm_i8_resid", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), xr.data_ptr(), N,
-         M, N, K, st())
+    call(hip, "llj_gemm_i8_resid", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), ao, g1, kp,
+         xr.data_ptr(), N, M, N, K, st())
     gv = torch.empty(M, N, dtype=torch.bfloat16, device=dev)  # the int8 GEMV in 8-row slices
     for r0 in range(0, M, 8):
         r = min(8, M - r0)
         call(hip, "llj_linear", 2, xd[r0].data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), None, gv[r0].data_ptr(), N, r,
              N, K, ws.data_ptr(), r0, None, st())
     h = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-    call(hip, "llj_gemm_i8_linear", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), h.data_ptr(), N,
-         M, N, K, st())
-    call(hip, "llj_gemm_i8_silu_mul", xd.data_ptr(), K, cbt2.data_ptr(), scb2.data_ptr(), ws.data_ptr(), h.data_ptr(),
-         N, M, N, K, st())
+    call(hip, "llj_gemm_i8_linear", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), ao, g1, kp,
+         h.data_ptr(), N, M, N, K, st())
+    call(hip, "llj_gemm_i8_silu_mul", xd.data_ptr(), K, cbt2.data_ptr(), scb2.data_ptr(), ws.data_ptr(), ao, g2, kp,
+         h.data_ptr(), N, M, N, K, st())
     torch.cuda.synchronize()
     ref = O.int8_linear(x, cb_ref, scb_ref)
     o = out.float().cpu().numpy()
@@ -980,8 +999,9 @@ def test_gemm_i8_linear_resid_silu(hip, M, N, K, outliers):
     assert_bf16_close(h.float().cpu().numpy(), hexp, "gemm int8 swiglu", rel=3e-2)
 
 
+@pytest.mark.parametrize("gather", [False, True])
 @pytest.mark.parametrize("B,T_,nh,hs,outliers", [(1, 200, 32, 128, 6), (3, 40, 4, 64, 0), (1, 300, 8, 128, 6)])
-def test_gemm_i8_qkv_rope_kv(hip, B, T_, nh, hs, outliers):
+def test_gemm_i8_qkv_rope_kv(hip, B, T_, nh, hs, outliers, gather):
     """llj_gemm_i8_qkv_rope: LLM.int8 c_attn + RoPE + KV-cache write for a whole prompt."""
     rng = np.random.default_rng(B * T_ + 77)
     C, S = nh * hs, max(256, T_ + 8)  # no ring wrap: every slot written once
@@ -997,8 +1017,9 @@ def test_gemm_i8_qkv_rope_kv(hip, B, T_, nh, hs, outliers):
     q = torch.zeros(M, C, dtype=torch.bfloat16, device=dev)
     kc = torch.zeros(B, nh, S, hs, dtype=torch.bfloat16, device=dev)
     vc = torch.zeros_like(kc)
-    call(hip, "llj_gemm_i8_qkv_rope", xd.data_ptr(), cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), q.data_ptr(),
-         kc.data_ptr(), vc.data_ptr(), rd.data_ptr(), pd.data_ptr(), B, T_, C, nh, S, st())
+    ao, (g1,), kp, keep = _i8_gather(hip, xd, M, C, ws, [(cbt, scb, 3 * C)], gather)
+    call(hip, "llj_gemm_i8_qkv_rope", xd.data_ptr(), cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), ao, g1, kp,
+         q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rd.data_ptr(), pd.data_ptr(), B, T_, C, nh, S, st())
     torch.cuda.synchronize()
     qkv = bf16(O.int8_linear(x, cb_ref, scb_ref))
     qe = O.apply_rope(qkv[:, :C].reshape(B, T_, nh, hs), rope[pos]).reshape(M, C)
