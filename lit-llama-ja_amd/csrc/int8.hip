@@ -472,8 +472,17 @@ __global__ __launch_bounds__(256) void i8_gather_act_kernel(const bf16_t* __rest
   const int total = i8_flat_list(L, h, g_lds, g_lds + 80);
   const int* s_list = g_lds + 80;
   const int m = blockIdx.x, nop = (total + 63) & ~63;
-  for (int j = threadIdx.x; j < nop; j += 256)
-    ao16[(size_t)m * kpad + j] = j < total ? (_Float16)bf2f(A[(size_t)m * lda + s_list[j]]) : (_Float16)0.f;
+  for (int j0 = threadIdx.x; j0 < nop; j0 += 256 * 8) {  // 8 loads in flight per thread
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + 256 * u;
+      v[u] = j < total ? bf2f(A[(size_t)m * lda + s_list[j]]) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (j0 + 256 * u < nop) ao16[(size_t)m * kpad + j0 + 256 * u] = (_Float16)v[u];
+  }
 }
 
 // block: 16 weight rows (one I8P tile) x the outlier columns; thread: row tid >> 4, columns
@@ -488,15 +497,19 @@ __global__ __launch_bounds__(256) void i8_gather_weight_kernel(const int8_t* __r
   const int* s_list = g_lds + 80;
   const int nt = blockIdx.x, r = threadIdx.x >> 4, n = nt * 16 + r, nop = (total + 63) & ~63;
   const float scb = SCB[n] / 127.f;
-  for (int j = threadIdx.x & 15; j < nop; j += 16) {
-    _Float16 w = (_Float16)0.f;
-    if (j < total) {
-      const int k = s_list[j], kk = k & 127;
-      const int q = CB[(((size_t)nt * (K >> 7) + (k >> 7)) * 2 + (kk >> 6)) * 1024 + (16 * ((kk >> 4) & 3) + r) * 16 +
-                       (kk & 15)];
-      w = (_Float16)((float)q * scb);
+  for (int j0 = threadIdx.x & 15; j0 < nop; j0 += 16 * 8) {  // 8 byte loads in flight per thread
+    int q[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + 16 * u;
+      const int k = j < total ? s_list[j] : 0, kk = k & 127;
+      q[u] = CB[(((size_t)nt * (K >> 7) + (k >> 7)) * 2 + (kk >> 6)) * 1024 + (16 * ((kk >> 4) & 3) + r) * 16 + (kk & 15)];
     }
-    w16[(size_t)n * kpad + j] = w;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + 16 * u;
+      if (j < nop) w16[(size_t)n * kpad + j] = j < total ? (_Float16)((float)q[u] * scb) : (_Float16)0.f;
+    }
   }
 }
 
