@@ -222,13 +222,15 @@ __device__ __forceinline__ int kofs(int t, int grp) {
 // CB bytes of each column in ONE memory latency -> accumulate from LDS, instead of list -> A ->
 // CB (three). Same per-thread accumulation order: bit-identical to the general path.
 constexpr int kSideChunk = 256;
-// speculative list entries per thread: 24 (4 waves) / 32 (8 waves) per k-block, so ~300 random
-// outlier columns (9.4 per k-block on average) stay on the fast path
+// speculative list entries per thread: 8 (4 waves) / 32 (8 waves) per k-block, so ~300 random
+// outlier columns of the down projection's input (9.4 per k-block on average) stay on the fast path
 #ifndef LLJ_I8_SPE
-#define LLJ_I8_SPE 0  // 0: 3 (4 waves) / 2 (8 waves); else that many entries per thread (A/B)
+#define LLJ_I8_SPE 0  // 0: 1 (4 waves, K = 4096) / 2 (8 waves, K = 11008); else that many per thread (A/B)
 #endif
+// (A/B on one box, profiles/r03_c3_side_fastpath.json: each extra entry costs ~0.6 us per call at few
+// outliers; at ~300 columns two entries save 6.5 us on the 8-wave down projection)
 template <int NW>
-constexpr int kSpE = LLJ_I8_SPE ? LLJ_I8_SPE : (NW == 4 ? 3 : 2);
+constexpr int kSpE = LLJ_I8_SPE ? LLJ_I8_SPE : (NW == 4 ? 1 : 2);
 template <int NW>
 __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float* SCB, int n0, float* part,
                              unsigned char* stage, int cnt_lane, const int (&spk)[kSpE<NW>]) {
