@@ -95,6 +95,9 @@ constexpr int kGBM = 128, kGBN = 128, kGBK = 64, kGNT = 256;
 #ifndef LLJ_GEMM_BM256_W4
 #define LLJ_GEMM_BM256_W4 1  // int4 W4P (39.6 -> 38.4 ms; 256 VGPRs + 64-72 B of scratch per lane)
 #endif
+#ifndef LLJ_GEMM_MFAST_W4
+#define LLJ_GEMM_MFAST_W4 0  // int4: m-fastest tile order too (A/B)
+#endif
 #ifndef LLJ_GDEPTH_DENSE
 #define LLJ_GDEPTH_DENSE 1  // bf16 / int8 in 128-row tiles (32 VGPRs of A + B per chunk in flight)
 #endif
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
   // panels x every row panel, so a weight panel is fetched once and shared through L2 by all
   // its row tiles (n fastest re-streamed every weight panel once per 128-row panel)
   // (bf16 weights: 7B T = 2048 window 86.3 -> 71.9 ms; int4 weights, 4x smaller: 40.0 vs 40.6 ms, kept n fastest)
-  constexpr bool MF = (WF == GWF_BF16 || I8) && LLJ_GEMM_MFAST;
+  constexpr bool MF = (WF == GWF_BF16 || I8 || (WF == GWF_W4 && LLJ_GEMM_MFAST_W4)) && LLJ_GEMM_MFAST;
   const int nb = MF ? t / mtiles : t % ntiles, mb = MF ? t % mtiles : t / ntiles;
   const int m0 = mb * BM, n0 = nb * kGBN;
 

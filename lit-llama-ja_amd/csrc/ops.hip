@@ -3,6 +3,9 @@
 // greedy (top_k = 1) next-token selection.
 #include "common.h"
 #include "attention.h"
+#ifndef LLJ_NORM_SC1
+#define LLJ_NORM_SC1 0
+#endif
 #include "lit_llama_amd.h"
 
 namespace llj {
@@ -77,7 +80,13 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__
     const uint32_t o0 = norm_pair(a.x, g.x, r), o1 = norm_pair(a.y, g.y, r), o2 = norm_pair(a.z, g.z, r),
                    o3 = norm_pair(a.w, g.w, r);
     rsum += bflo(o0) + bfhi(o0) + bflo(o1) + bfhi(o1) + bflo(o2) + bfhi(o2) + bflo(o3) + bfhi(o3);
+#if LLJ_NORM_SC1  // write-through (sc1) 8-byte stores, as the GEMV epilogues (A/B)
+    unsigned long long* d8 = reinterpret_cast<unsigned long long*>(yr + v);
+    __hip_atomic_store(d8, (unsigned long long)o0 | ((unsigned long long)o1 << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d8 + 1, (unsigned long long)o2 | ((unsigned long long)o3 << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
     yr[v] = make_uint4(o0, o1, o2, o3);
+#endif
   };
   if (regs) {
 #pragma unroll
