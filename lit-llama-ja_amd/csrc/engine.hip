@@ -8,26 +8,34 @@
 // Why: a launch boundary costs 1.2-1.9 us and every launch re-ramps its weight stream behind the
 // activation it waits for. Here the weight stream never stops at an op edge
 // (MI355X_MICROARCH.md price list: ldsdma-fill, prefetch-credit, allgather, engine-vs-launches):
-//  * grid = one 256-thread workgroup per CU, resident for the whole step (LDS > half a CU).
-//  * wave 3 of every workgroup is a LOADER: it streams this CU's weight blocks (1 KiB W4P tiles =
-//    16 columns x 128 k) into an LDS ring by LDS-DMA (global_load_lds_dwordx4 ... nt) in the order
-//    the CU consumes them, across op and layer boundaries -- weights do not depend on
+//  * grid = one 512-thread workgroup per CU, resident for the whole step (LDS > half a CU).
+//  * the last wave of every workgroup is a LOADER: it streams this CU's weight blocks (1 KiB W4P
+//    tiles = 16 columns x 128 k) into an LDS ring by LDS-DMA (global_load_lds_dwordx4 ... nt) in
+//    the order the CU consumes them, across op and layer boundaries -- weights do not depend on
 //    activations, so the next op's blocks land while the consumers wait for that op's input. It
-//    publishes `landed` (blocks in LDS) and waits on the consumers' `freed` counts before reusing a
+//    publishes `landed` (blocks in LDS) and waits on the consumers' progress words before reusing a
 //    slot. Its DMAs never sit in a consumer's vmcnt queue.
-//  * waves 0-2 CONSUME: block b of the CU stream goes to wave b % 3 (bf16 MFMA 16x16x32 on the
-//    dequantized codes, as the GEMVs), partial sums meet in LDS, one wave runs each tile's epilogue.
-//    They synchronise through an LDS counter barrier (the loader never joins a barrier).
+//  * the other NC waves CONSUME: chunk c of a tile goes to wave c % NC (bf16 MFMA 16x16x32 on the
+//    dequantized codes, as the GEMVs) in a software pipeline -- the ring read of a wave's next block
+//    is in flight while it dequantizes and multiplies the current one, landing checks are scalar and
+//    re-read the loader's word only when the cached count is behind; partial sums meet in LDS, one
+//    wave runs each tile's epilogue. They synchronise through an LDS counter barrier.
 //  * op outputs travel between CUs as 8-byte {tag, payload} granules written by one agent-scope
 //    (sc1) store each and read by sc1 polling loads: the data is its own flag, no fence, no grid
 //    barrier. tag = epoch * 128 + layer + 1 (epoch advanced on the device once per step), never 0.
-//  * each op's tiles are dealt round-robin over the CUs (tile t on CU t % G).
-// Per layer: gather x -> rms_1 -> QKV tiles (RoPE, KV-cache write, publish q/k/v) -> attention of
-// head h on CU h * (G / n_head) (gathers its q/k/v, reads the cache rows of earlier positions) ->
-// gather y -> c_proj tile + residual (publish x_mid) -> gather x_mid -> rms_2 -> SwiGLU tiles
-// (publish h) -> gather h -> down tile + residual (publish x). After the last layer: ln_f +
-// lm_head tiles (logits to HBM, per-CU argmax publish); the last CU to arrive picks the token,
-// writes it and advances the device position and the epoch.
+//  * QKV is dealt per (head h, 16-dim slice j) unit: the CU of unit (h, j) computes the q, k and v
+//    columns h * hs + 16 j + [0, 16), so attention needs no q/k/v hand-off: it computes the partial
+//    scores of its 16 dims for every key, the J = hs / 16 CUs of a head exchange them as granules
+//    (one hop), each sums the J partials in the same order (bitwise-equal scores on every CU of the
+//    head), runs the softmax and P.V over its own 16 value dims, and publishes its slice of y. With
+//    U = n_head * J = CUs (7B: 256) the J CUs of a head share an XCD (block b on XCD b % 8: speed
+//    only, never correctness). Every other op's tile t runs on CU t % G.
+// Per layer: gather x -> rms_1 -> QKV tiles (RoPE, KV-cache write, q/k/v slices into LDS) ->
+// partial scores -> score exchange -> softmax, P.V -> publish y slice -> gather y -> c_proj tile +
+// residual (publish x_mid) -> gather x_mid -> rms_2 -> SwiGLU tiles (publish h) -> gather h -> down
+// tile + residual (publish x). After the last layer: ln_f + lm_head tiles (logits to HBM, per-CU
+// argmax publish); the last CU to arrive picks the token, writes it and advances the device position
+// and the epoch.
 // Numerics follow the GEMV path (gemv_impl.h): bf16 rounding points of the reference, int4 offset
 // removed with the row sum of the normalized input, RoPE / softmax in fp32.
 // Every spin is bounded (kSpinTicks from the step's start); a timeout sets ctl[2] and turns every
@@ -45,7 +53,7 @@ constexpr int NWV = LLJ_ENG_NC + 1;  // waves per workgroup (two per SIMD at 8)
 constexpr int NC = LLJ_ENG_NC;  // consumer waves (0 .. NC-1); wave NC is the loader
 static_assert(NC >= 3 && NC <= 15, "consumer waves");
 constexpr int NTH = 64 * NWV;
-constexpr int TG = 4;      // tiles per partial-sum group (accumulators per wave: TG x 2 matrices)
+constexpr int TG = 4;      // tiles per partial-sum group (the red scratch holds TG tiles x 2 matrices)
 #ifndef LLJ_ENG_D
 #define LLJ_ENG_D 48       // DMAs the loader keeps in flight (vmcnt immediate)
 #endif
@@ -55,29 +63,32 @@ constexpr int GK = 8;      // granules per lane per gather batch (x, y, x_mid: o
 constexpr int GN = 6;      // RMSNorm gain pairs per lane (C / 2 <= GN * 64 * NC: C <= 5376)
 constexpr unsigned long long kSpinTicks = 5000000ull;  // 50 ms of s_memrealtime (100 MHz)
 constexpr int kMaxCUs = LLJ_ENGINE_MAX_CUS;
+constexpr int kMaxS = 512;  // cache slots (the score exchange arena holds kMaxS keys per unit)
+constexpr int kKPT = (kMaxS + 64 * NC - 1) / (64 * NC);  // keys per consumer thread at most
 
 enum : int { OP_QKV = 0, OP_O = 1, OP_SW = 2, OP_DOWN = 3, OP_HEAD = 4, OP_END = 5 };
 enum : unsigned { ERR_TIMEOUT = 1u };
 
 // granule arena (u64 units) and the control words behind it
 struct Arena {
-  unsigned long long *gx, *gqkv, *gy, *gxm, *gh, *garg;
+  unsigned long long *gx, *gy, *gxm, *gh, *garg, *gsc;
   unsigned* ctl;  // [0] epoch, [1] end-of-step arrivals, [2] error bits
 };
 __host__ __device__ inline size_t arena_granules(int C, int H) {
-  return (size_t)3 * (C / 2) + (size_t)3 * C / 2 + (size_t)H / 2 + (size_t)kMaxCUs;  // x, y, x_mid | qkv | h | argmax
+  // x, y, x_mid | h | argmax | partial scores: (C / 16 units) x kMaxS keys
+  return (size_t)3 * (C / 2) + (size_t)H / 2 + (size_t)kMaxCUs + (size_t)(C / 16) * kMaxS;
 }
 __device__ inline Arena arena_of(const llj_engine_plan& P) {
   Arena a;
   unsigned long long* b = reinterpret_cast<unsigned long long*>(P.arena);
   const int C = P.C, H = P.H;
   a.gx = b;
-  a.gqkv = a.gx + C / 2;
-  a.gy = a.gqkv + 3 * C / 2;
+  a.gy = a.gx + C / 2;
   a.gxm = a.gy + C / 2;
   a.gh = a.gxm + C / 2;
   a.garg = a.gh + H / 2;
-  a.ctl = reinterpret_cast<unsigned*>(a.garg + kMaxCUs);
+  a.gsc = a.garg + kMaxCUs;
+  a.ctl = reinterpret_cast<unsigned*>(a.gsc + (size_t)(C / 16) * kMaxS);
   return a;
 }
 
@@ -87,23 +98,13 @@ __device__ __forceinline__ unsigned long long ld_gran(const unsigned long long* 
 __device__ __forceinline__ void st_gran(unsigned long long* p, unsigned tag, uint32_t v) {
   __hip_atomic_store(p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// LDS-DMA of one 16-byte piece per lane into LDS byte address lds (wave-uniform) + 16 * lane,
-// non-temporal (weights are read once per step). Invisible to the compiler's wait counting: the
-// loader counts its own DMAs (wait_vm). Its LDS reads are done first (lgkmcnt(0)).
-__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
-  unsigned keep;
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-               "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds)
-               : "memory");
-}
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 __device__ __forceinline__ unsigned lds_ld(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ __forceinline__ void lds_st(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }  // compiler-only ordering point
 
 __device__ __forceinline__ bf16x8 dequant(uint32_t w, uint32_t msk, uint32_t mag) {
   uint4 b = make_uint4(and_or(w, msk, mag), and_or(w >> 4, msk, mag), and_or(w >> 8, msk, mag), and_or(w >> 12, msk, mag));
@@ -116,35 +117,45 @@ __device__ __forceinline__ uint32_t bf_key(uint32_t b) { return (b & 0x8000u) ? 
 
 // profiling stamps (plan.trace != NULL): [g][128]; consumers: 0 start, per layer l at 2 + 12 l:
 // +0 x staged, +1 QKV done, +2 attention done, +3 y staged, +4 c_proj done, +5 x_mid staged,
-// +6 SwiGLU done, +7 h staged, +8 down done; the loader: 100 + op index of its last DMA of each op
-// (per layer, layers 0..1 only: 100..107), 108..119 inside consume (QKV / SwiGLU of layers 0, 1: A
-// in registers, blocks done, barrier passed), 120 stream end, 121 loader start; 126 head staged, 127 head done
+// +6 SwiGLU done, +7 h staged, +8 down done, +9 scores published; the loader: 100 + op index of its
+// last DMA of each op (per layer, layers 0..1 only: 100..107), 108..119 inside consume (QKV /
+// SwiGLU of layers 0, 1: A in registers, blocks done, barrier passed), 120 stream end, 121 loader
+// start; 126 head staged, 127 head done
 __device__ __forceinline__ void stamp(const llj_engine_plan& P, int lane, int k) {
   if (P.trace && lane == 0 && k < 128) P.trace[(size_t)blockIdx.x * 128 + k] = __builtin_amdgcn_s_memrealtime();
-}
-
-// a pointer loaded by a vector load, moved to SGPRs: the compiler waits for the load HERE (once),
-// not at its first use inside a DMA loop, where that wait would also drain every DMA in flight
-__device__ __forceinline__ const char* sgpr_ptr(const char* p) {
-  const uint64_t v = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return reinterpret_cast<const char*>(((uint64_t)hi << 32) | lo);
 }
 
 // ------------------------------------------------------------------------------------ schedule
 struct Shape {
   int C, H, V, nh, hs, S, L, G, g;
+  int J;     // 16-dim slices per head (hs / 16)
+  int unit;  // this CU's QKV unit u = h * J + j, or -1 (more CUs than units)
 };
+// QKV unit of CU g: with U = n_head * J == G (7B) and G % 8 == 0, J == 8, the J units of head h go to
+// CUs g = h % 8 + 8 (J (h / 8) + j), which share g % 8 (one XCD under round-robin placement);
+// otherwise unit g
+__device__ __forceinline__ int unit_of_cu(int g, int G, int nh, int J) {
+  const int U = nh * J;
+  if (U == G && (G & 7) == 0 && J == 8 && (nh & 7) == 0) {
+    const int x = g & 7, m = g >> 3;
+    return (x + 8 * (m / J)) * J + (m % J);
+  }
+  return g < U ? g : -1;
+}
 __device__ __forceinline__ int op_ntiles(const Shape& s, int op) {
   return op == OP_QKV ? 3 * s.C / 16 : op == OP_SW ? s.H / 16 : op == OP_HEAD ? s.V / 16 : s.C / 16;
 }
 __device__ __forceinline__ int op_kc(const Shape& s, int op) { return (op == OP_DOWN ? s.H : s.C) >> 7; }
 __device__ __forceinline__ int op_nmat(int op) { return op == OP_SW ? 2 : 1; }
 __device__ __forceinline__ int tiles_of_cu(const Shape& s, int op) {
+  if (op == OP_QKV) return s.unit >= 0 ? 3 : 0;
   const int n = op_ntiles(s, op);
   return s.g < n ? (n - s.g + s.G - 1) / s.G : 0;
 }
-__device__ __forceinline__ int op_blocks(const Shape& s, int op) { return tiles_of_cu(s, op) * op_kc(s, op) * op_nmat(op); }
+// tile of slot j of this CU's share of op: QKV slots 0 / 1 / 2 = the q / k / v columns of its unit
+__device__ __forceinline__ int tile_of(const Shape& s, int op, int j) {
+  return op == OP_QKV ? j * (s.C / 16) + s.unit : s.g + j * s.G;
+}
 // Weight pointer of (layer, op, matrix) for the loader wave, read by a scalar load (the layer table
 // is written by the host before the launch and only read here). A compiler-visible vector load
 // would be followed by s_waitcnt vmcnt(0) at its use -- a wait that also drains every LDS-DMA the
@@ -163,6 +174,8 @@ __device__ __forceinline__ const char* op_weight(const llj_engine_plan& P, int l
 // f32 | eop[2] (epilogue operands) | misc[64] f32 ([0, NC) sums of squares, [16, 16 + NC) row sums,
 // [32, 32 + NC) argmax, [48] last-arriver flag) | attention scratch | ring (nb x 1 KiB)
 constexpr int kCtlWords = 32;  // [0] landed, [1 .. NC] next block per consumer, [16] consumer barrier, [17] max wanted block
+// attention scratch (f32): q / k / v slices [3][16], per-wave max / sum [2][NC], per-wave P.V [NC][16]
+constexpr int kAttFloats = 48 + 2 * NC + 16 * NC;
 struct Lds {
   unsigned* ctl;
   unsigned char* ring;
@@ -179,14 +192,14 @@ __host__ __device__ inline size_t al16(size_t b) { return (b + 15) & ~(size_t)15
 // epilogue operands staged per op: (scale, 128 + zero) of both matrices for every tile of the CU
 // (at most kEopTiles), or the RoPE (cos, sin) pairs of the QKV tiles
 constexpr int kEopTiles = 16;
-__host__ __device__ inline size_t lds_fixed(int C, int H, int hs) {
+__host__ __device__ inline size_t lds_fixed(int C, int H) {
   const int K = C > H ? C : H;
   return (size_t)kCtlWords * 4 + al16((size_t)K * 2) + 2 * al16((size_t)C * 2) + (size_t)2 * NC * TG * 2 * 16 * 4 +
-         (size_t)2 * kEopTiles * 2 * 16 * 8 + 64 * 4 + al16((size_t)(3 * hs + 2 * NC + NC * hs) * 4);
+         (size_t)2 * kEopTiles * 2 * 16 * 8 + 64 * 4 + al16((size_t)kAttFloats * 4);
 }
 // ring blocks that fit next to the fixed part in `budget` bytes
-__host__ __device__ inline int ring_blocks(int C, int H, int hs, size_t budget) {
-  const size_t f = lds_fixed(C, H, hs);
+__host__ __device__ inline int ring_blocks(int C, int H, size_t budget) {
+  const size_t f = lds_fixed(C, H);
   return f >= budget ? 0 : (int)((budget - f) / 1024) & ~7;  // whole runs of 8 slots (the loader's DMA runs)
 }
 
@@ -200,6 +213,7 @@ struct Ctx {
   unsigned bar_gen;   // consumer barriers passed
   const llj_engine_plan* plan;
   int n_used;         // CU-stream index of the next block of this op (consumers)
+  int landed;         // blocks published as landed, as last read (consumers; monotone)
   int stamp_base;     // profiling: stamp index base inside consume (-1 = none)
 };
 
@@ -295,7 +309,7 @@ __device__ __forceinline__ void stage_sz(Ctx& X, float2* eop, const llj_engine_p
                        : op == OP_O   ? reinterpret_cast<const float2*>(Ly->sz_o)
                        : op == OP_SW  ? reinterpret_cast<const float2*>(m ? Ly->sz_fc2 : Ly->sz_fc1)
                                       : reinterpret_cast<const float2*>(Ly->sz_down);
-    eop[(j * 2 + m) * 16 + c] = sz[16 * (s.g + j * s.G) + c];
+    eop[(j * 2 + m) * 16 + c] = sz[16 * tile_of(s, op, j) + c];
   }
 }
 
@@ -384,26 +398,24 @@ __device__ __forceinline__ void epilogue(Ctx& X, const Lds& L, int op, Epi& E, i
   const Shape& s = X.s;
   const int lane = X.lane;
   switch (op) {
-    case OP_QKV: {
+    case OP_QKV: {  // slot sl = 0 q, 1 k, 2 v of this CU's (head, 16-dim slice) unit
       const int C = s.C, hs = s.hs;
-      const int region = (16 * tile) / C;  // 0 q, 1 k, 2 v (uniform per tile)
-      const int nc = n - region * C;
+      const int nc = n - sl * C;
       const int hh = nc / hs, dd = nc % hs;
       const float v = round_bf(y1);  // c_attn output in bf16 (model.py:204)
       const float partner = lane_xor1(v);
       float out = v;
-      if (region < 2) {  // RoPE in fp32 (model.py:318-329)
-        const float2 cs = E.rcs[(sl < TG ? sl : 0) * 8 + ((lane & 15) >> 1)];
+      if (sl < 2) {  // RoPE in fp32 (model.py:318-329)
+        const float2 cs = E.rcs[sl * 8 + ((lane & 15) >> 1)];
         out = (dd & 1) ? (v * cs.x + partner * cs.y) : (v * cs.x - partner * cs.y);
       }
-      const uint32_t ob = (uint32_t)f2bf(out);
+      const uint32_t ob = (uint32_t)f2bf(out);  // the bf16 q / k / v (type_as, model.py:329)
       const uint32_t pr = lane_xor1(ob);
-      if (lane < 16 && !(lane & 1)) {
-        st_gran(E.ar.gqkv + n / 2, E.tag, ob | (pr << 16));
-        if (region > 0) {  // the cache row of this position, for later steps
-          bf16_t* dst = (region == 1 ? E.kcache : E.vcache) + ((size_t)hh * s.S + E.slot) * hs + dd;
-          *reinterpret_cast<uint32_t*>(dst) = ob | (pr << 16);
-        }
+      // the slice stays in this CU's LDS for the attention (q pre-scaled by log2(e) / sqrt(hs))
+      if (lane < 16) L.att[sl * 16 + lane] = bf2f((bf16_t)ob) * (sl == 0 ? 1.4426950408889634f / sqrtf((float)hs) : 1.f);
+      if (sl > 0 && lane < 16 && !(lane & 1)) {  // the cache row of this position, for later steps
+        bf16_t* dst = (sl == 1 ? E.kcache : E.vcache) + ((size_t)hh * s.S + E.slot) * hs + dd;
+        *reinterpret_cast<uint32_t*>(dst) = ob | (pr << 16);
       }
       break;
     }
@@ -431,25 +443,28 @@ __device__ __forceinline__ void epilogue(Ctx& X, const Lds& L, int op, Epi& E, i
 
 // Consume this CU's blocks of `op`. Stream order (the loader's): tile groups of TG tiles, tile-major
 // inside a group -- for tile slot jj: for chunk c: for matrix m (contiguous 1 KiB blocks of a tile
-// for the DMA) -- and consumer w owns the chunks c = w (mod NC) of every tile. For K <= AREG_C * NC *
-// 128 the consumer holds the A fragments of all its chunks in registers for the whole op (one LDS
-// read per block: the weights); longer K (the down projection) reads them per chunk. After each
-// chunk a consumer publishes in ctl[1 + w] the stream index of its next block (every block of its
-// below that index is taken). Partial sums of output row 0 go to red per tile; after each group the
-// epilogue of tile slot jj runs on consumer jj % NC, lanes 0..15 (column 16 tile + lane).
-// Code size matters more than unrolling here: the whole step runs from a 64 KiB instruction cache
-// shared by two CUs, so this is the only instance of the block loop in the kernel.
+// for the DMA) -- and consumer w owns the chunks c = w (mod NC) of every tile. Per tile (per batch
+// of 4 chunks for long K) a wave waits, by a scalar compare with its cached landed count, for its
+// last block; issues every ring read of the tile (and, for long K, the A fragments) at once, branch
+// free, so the compiler counts each chunk's wait (lgkmcnt(N)) instead of draining; publishes in
+// ctl[1 + w] the stream index of its next block (its reads are ahead of that LDS write: one wave's
+// LDS operations execute in order); then dequantizes and multiplies chunk by chunk. For K <=
+// AREG_C * NC * 128 the A fragments of all a wave's chunks stay in registers for the whole op.
+// Partial sums of output row 0 go to red per tile; after each group the epilogue of tile slot jj
+// runs on consumer jj % NC, lanes 0..15 (column 16 tile + lane).
 constexpr int AREG_C = 5;  // chunks per consumer whose A fragments stay in registers (K <= 4480 at NC 7)
-__device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop, int op, float asum, int& red_par, Epi& E) {
+constexpr int KB = 3;      // chunks per read batch of the long-K form (3 x 5 reads: lgkmcnt counts to 15)
+template <int NM, bool AREG>
+__device__ __forceinline__ void consume_t(Ctx& X, const Lds& L, const float2* eop, int op, float asum, int& red_par, Epi& E) {
   const Shape& s = X.s;
-  const int nt = tiles_of_cu(s, op), kc = op_kc(s, op), nm = op_nmat(op);
+  const int nt = tiles_of_cu(s, op), kc = op_kc(s, op);
   const int lane = X.lane, grp = lane >> 4, w = X.wave;
   uint32_t msk = 0x000F000Fu, mag = 0x43004300u;  // bf16 128 + q via one v_and_or_b32 per pair
   asm volatile("" : "+s"(msk));
   asm volatile("" : "+v"(mag));
-  const bool areg = kc <= AREG_C * NC;
-  bf16x8 ar[AREG_C][4];
-  if (areg) {
+  const int nch = kc > w ? (kc - w + NC - 1) / NC : 0;  // chunks of every tile this wave takes
+  bf16x8 ar[AREG ? AREG_C : 1][4];
+  if constexpr (AREG) {
 #pragma unroll
     for (int ci = 0; ci < AREG_C; ++ci) {
       const int c = w + ci * NC < kc ? w + ci * NC : 0;
@@ -458,81 +473,104 @@ __device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop,
       for (int t = 0; t < 4; ++t) ar[ci][t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(arow + 8 * t));
     }
   }
-  const int per_tile = kc * nm;
+  const int per_tile = kc * NM;
   const llj_engine_plan* SP = X.plan;
   if (X.stamp_base >= 0 && w == 0) stamp(*SP, lane, X.stamp_base + 0);  // A fragments in registers
   int gbase = X.n_used;  // CU-stream index of the current group's first block
-  int landed = 0;
-  unsigned it = 0;
-  // wait for block b; a consumer that has to wait records b in ctl[17] (LDS max) so the loader,
-  // stalled on a full ring, knows to publish landings early (the read-ahead means b may be past
-  // this consumer's published next block)
+  // block b landed (b wave-uniform): a scalar compare with the cached count; the loader's word is
+  // re-read only when behind, and a consumer that has to wait records b in ctl[17] (LDS max) so the
+  // loader, stalled on a full ring, knows to publish landings early
   auto wait_landed = [&](int b) {
-    if (landed > b) return;
-    landed = (int)lds_ld(L.ctl + 0);
-    if (landed > b) return;
+    if (X.landed > b) return;
+    X.landed = uniform((int)lds_ld(L.ctl + 0));
+    if (X.landed > b) return;
     if (lane == 0) __hip_atomic_fetch_max(L.ctl + 17, (unsigned)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (landed <= b) {
-      landed = (int)lds_ld(L.ctl + 0);
-      if (landed > b || spin_fail_lds(X, it)) break;
+    unsigned it = 0;
+    for (;;) {
+      X.landed = uniform((int)lds_ld(L.ctl + 0));
+      if (X.landed > b || spin_fail_lds(X, it)) break;
     }
   };
-  // block b's bytes from the ring, once the loader has published it as landed
-  auto take = [&](int b) -> u32x4 {
-    wait_landed(b);
+  auto ring = [&](int b) -> u32x4 {
     const unsigned q = __umulhi((unsigned)b, L.nb_magic);
     return *reinterpret_cast<const u32x4*>(L.ring + (size_t)((unsigned)b - q * (unsigned)L.nb) * 1024 + 16 * lane);
   };
-  auto chunk = [&](const bf16x8* av, int b, f32x4& a0, f32x4& a1) {
-    const u32x4 w0 = take(b);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) a0 = mfma_bf16(av[t], dequant(w0[t], msk, mag), a0);
-    if (nm == 2) {
-      const u32x4 w1 = take(b + 1);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) a1 = mfma_bf16(av[t], dequant(w1[t], msk, mag), a1);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slots' bytes are in registers
+  auto progress = [&](int next) {
+    cbar();
+    if (lane == 0) lds_st(L.ctl + 1 + w, (unsigned)next);
   };
   for (int j0 = 0; j0 < nt; j0 += TG) {
     const int ng = nt - j0 < TG ? nt - j0 : TG;
+    const int gend = gbase + ng * per_tile;
     float* red = L.red + (size_t)red_par * NC * TG * 2 * 16;
     for (int jj = 0; jj < ng; ++jj) {
-      const int tb = gbase + jj * per_tile;  // the tile's first block
-      const int tnext = jj + 1 < ng ? tb + per_tile + w * nm : gbase + ng * per_tile;
+      const int tb = gbase + jj * per_tile;                            // the tile's first block
+      const int tnext = jj + 1 < ng ? tb + per_tile + w * NM : gend;  // this wave's first block after the tile
       f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-      if (areg) {
+      if (nch == 0) {
+        progress(tnext);
+      } else if constexpr (AREG) {
+        wait_landed(tb + (w + (nch - 1) * NC) * NM + NM - 1);
+        u32x4 wt[AREG_C][NM];
+#pragma unroll
+        for (int ci = 0; ci < AREG_C; ++ci) {  // chunks past nch re-read chunk w (landed; unused)
+          const int b = tb + (w + (ci < nch ? ci : 0) * NC) * NM;
+#pragma unroll
+          for (int m = 0; m < NM; ++m) wt[ci][m] = ring(b + m);
+        }
+        progress(tnext);
 #pragma unroll
         for (int ci = 0; ci < AREG_C; ++ci) {
-          const int c = w + ci * NC;
-          if (c >= kc) break;
-          chunk(ar[ci], tb + c * nm, a0, a1);
-          if (lane == 0) lds_st(L.ctl + 1 + w, (unsigned)(c + NC < kc ? tb + (c + NC) * nm : tnext));
-        }
-      } else {
-        for (int c = w; c < kc; c += NC) {
-          const bf16_t* arow = L.A + 128 * c + 32 * grp;
-          bf16x8 av[4];
+          if (ci < nch) {
 #pragma unroll
-          for (int t = 0; t < 4; ++t) av[t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(arow + 8 * t));
-          chunk(av, tb + c * nm, a0, a1);
-          if (lane == 0) lds_st(L.ctl + 1 + w, (unsigned)(c + NC < kc ? tb + (c + NC) * nm : tnext));
+            for (int t = 0; t < 4; ++t) a0 = mfma_bf16(ar[ci][t], dequant(wt[ci][0][t], msk, mag), a0);
+            if constexpr (NM == 2) {
+#pragma unroll
+              for (int t = 0; t < 4; ++t) a1 = mfma_bf16(ar[ci][t], dequant(wt[ci][1][t], msk, mag), a1);
+            }
+          }
+        }
+      } else {  // long K (the down projection): batches of KB chunks, A fragments read with the weights
+        for (int c0 = w; c0 < kc; c0 += KB * NC) {
+          const int nbat = (kc - c0 + NC - 1) / NC < KB ? (kc - c0 + NC - 1) / NC : KB;
+          wait_landed(tb + (c0 + (nbat - 1) * NC) * NM + NM - 1);
+          u32x4 wt[KB][NM];
+          bf16x8 af[KB][4];
+#pragma unroll
+          for (int u = 0; u < KB; ++u) {
+            const int c = u < nbat ? c0 + u * NC : c0;
+#pragma unroll
+            for (int m = 0; m < NM; ++m) wt[u][m] = ring(tb + c * NM + m);
+            const bf16_t* arow = L.A + 128 * c + 32 * grp;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) af[u][t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(arow + 8 * t));
+          }
+          progress(c0 + KB * NC < kc ? tb + (c0 + KB * NC) * NM : tnext);
+#pragma unroll
+          for (int u = 0; u < KB; ++u) {
+            if (u < nbat) {
+#pragma unroll
+              for (int t = 0; t < 4; ++t) a0 = mfma_bf16(af[u][t], dequant(wt[u][0][t], msk, mag), a0);
+              if constexpr (NM == 2) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) a1 = mfma_bf16(af[u][t], dequant(wt[u][1][t], msk, mag), a1);
+              }
+            }
+          }
         }
       }
-      if (w >= kc && lane == 0) lds_st(L.ctl + 1 + w, (unsigned)tnext);  // no chunk of this tile
-      // partial sums of output row 0 (lanes 0..15, register 0) -> red[parity][wave][jj][m][col]
-      if (lane < 16) {
+      if (lane < 16) {  // partial sums of output row 0 (lanes 0..15, register 0)
         red[((w * TG + jj) * 2 + 0) * 16 + lane] = a0[0];
         red[((w * TG + jj) * 2 + 1) * 16 + lane] = a1[0];
       }
     }
-    gbase += ng * per_tile;
+    gbase = gend;
     if (X.stamp_base >= 0 && w == 0 && j0 == 0) stamp(*SP, lane, X.stamp_base + 1);  // group's blocks done
     cbarrier(X, L);
     if (X.stamp_base >= 0 && w == 0 && j0 == 0) stamp(*SP, lane, X.stamp_base + 2);  // barrier passed
     for (int jj = w; jj < ng; jj += NC) {
       const int slot = j0 + jj;
-      const int tile = s.g + slot * s.G;
+      const int tile = tile_of(s, op, slot);
       const int col = lane & 15;
       const int n = 16 * tile + col;
       float y1 = 0.f, y2 = 0.f;
@@ -551,154 +589,148 @@ __device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop,
   }
   X.n_used = gbase;
 }
+// (C <= AREG_C * NC * 128 is required by llj_engine_step: only the down projection takes the long-K form)
+__device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop, int op, float asum, int& red_par, Epi& E) {
+  if (op == OP_SW) consume_t<2, true>(X, L, eop, op, asum, red_par, E);
+  else if (op == OP_DOWN) consume_t<1, false>(X, L, eop, op, asum, red_par, E);
+  else consume_t<1, true>(X, L, eop, op, asum, red_par, E);
+}
 
-// Attention of head h on this CU (model.py:237 for the token at position p) by the NC consumer
-// waves: q / k / v of the head from the QKV granules, keys of earlier positions from the cache
-// (slots written by earlier steps; slot p % S is being written by this step and is skipped), the
-// current key from the granules. 16 lanes per key, online softmax per 16-lane group, groups merged
-// by lane swaps, waves through LDS. y_h published as granules.
+// Attention of this CU's unit (head h, dims 16 j + [0, 16)) for the token at position p
+// (model.py:237, SDPA with scale 1 / sqrt(hs) over the valid keys): the q / k / v slices are in LDS
+// from the QKV epilogue. 1) every consumer thread takes keys kk = t + 64 NC r: the partial score
+// q . k over the 16 dims (cache rows of earlier positions; slot p % S is this step's and is
+// skipped, the current key comes from LDS) -> one granule per (key, slice) in this head's score
+// region; 2) the J partials of each key are read back from the head's J CUs and summed in slice
+// order, so every CU of the head holds the bitwise-same scores; 3) softmax in fp32 (exp2 of
+// log2(e)-scaled scores) and P.V over this CU's 16 value dims (kept in registers since step 1);
+// 4) y slice -> bf16 -> 8 granules of y.
 template <int HS>
-__device__ __forceinline__ void attention_head(Ctx& X, const Lds& L, const llj_engine_plan& P, const Arena& ar, int l, int h, int p,
-                               unsigned tag) {
+__device__ __forceinline__ void attention_dims(Ctx& X, const Lds& L, const llj_engine_plan& P, const Arena& ar, int l, int p,
+                                            unsigned tag) {
   const Shape& s = X.s;
-  constexpr int DPL = HS / 16;
-  constexpr int NG = NC * 4;  // 16-lane key groups
-  constexpr int U = 8;
-  const int C = s.C, Sc = s.S;
-  float* sq = L.att;            // [HS] q (fp32, pre-scaled by log2(e) / sqrt(hs))
-  float* sk = sq + HS;          // [HS] current k
-  float* sv = sk + HS;          // [HS] current v
-  float* s_m = sv + HS;         // [NC]
-  float* s_l = s_m + NC;        // [NC]
-  float* s_o = s_l + NC;        // [NC][HS]
-  const float scale_log2 = 1.4426950408889634f / sqrtf((float)HS);
-  if (X.wave < 3) {  // wave 0: q, 1: k, 2: v of head h (HS / 2 granules each)
-    const unsigned long long* src = ar.gqkv + (X.wave * C + h * HS) / 2;
-    float* dst = X.wave == 0 ? sq : X.wave == 1 ? sk : sv;
-    const float mul = X.wave == 0 ? scale_log2 : 1.f;
-    for (int b0 = 0; b0 < HS / 2; b0 += 64) {
-      const int idx = b0 + X.lane;
-      unsigned long long v;
-      unsigned it = 0;
-      for (;;) {
-        v = ld_gran(src + (idx < HS / 2 ? idx : 0));
-        if (__all(idx >= HS / 2 || (unsigned)(v >> 32) == tag)) break;
-        if (spin_fail(X, it)) break;
-      }
-      if (idx < HS / 2) {
-        dst[2 * idx] = bflo((uint32_t)v) * mul;
-        dst[2 * idx + 1] = bfhi((uint32_t)v) * mul;
-      }
-    }
-  }
-  cbarrier(X, L);
-  const int sub = X.lane & 15, kg = (X.wave * 64 + X.lane) >> 4;
+  constexpr int J = HS / 16;
+  const int u = s.unit, h = u / J, j = u % J;
+  const int Sc = s.S;
   const int nprev = p < Sc ? p : Sc - 1;  // earlier positions still in the window
+  const int NK = nprev + 1;
   const int cur_slot = p % Sc;
-  const bf16_t* kc = reinterpret_cast<const bf16_t*>(P.layers[l].kcache) + (size_t)h * Sc * HS + sub * DPL;
-  const bf16_t* vc = reinterpret_cast<const bf16_t*>(P.layers[l].vcache) + (size_t)h * Sc * HS + sub * DPL;
-  float qf[DPL];
+  const float* aq = L.att;
+  const float* ak = aq + 16;
+  const float* av = ak + 16;
+  float* s_m = L.att + 48;
+  float* s_l = s_m + NC;
+  float* s_o = s_l + NC;  // [NC][16]
+  const int t = X.wave * 64 + X.lane;
+  const bf16_t* kc = reinterpret_cast<const bf16_t*>(P.layers[l].kcache) + (size_t)h * Sc * HS + 16 * j;
+  const bf16_t* vc = reinterpret_cast<const bf16_t*>(P.layers[l].vcache) + (size_t)h * Sc * HS + 16 * j;
+  unsigned long long* gs = ar.gsc + (size_t)h * J * kMaxS;  // [key][J]
+  u32x4 kr[kKPT][2], vr[kKPT][2];
 #pragma unroll
-  for (int i = 0; i < DPL; ++i) qf[i] = sq[sub * DPL + i];
-  float mx = -INFINITY, lsum = 0.f, o[DPL];
-#pragma unroll
-  for (int i = 0; i < DPL; ++i) o[i] = 0.f;
-  auto step = [&](float sc, const float* vv) {
-    const float mn = fmaxf(mx, sc);
-    const float corr = exp2f(mx - mn);
-    const float pj = exp2f(sc - mn);
-    lsum = lsum * corr + pj;
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) o[i] = o[i] * corr + pj * vv[i];
-    mx = mn;
-  };
-  for (int j0 = kg; j0 < nprev; j0 += NG * U) {
-    uint32_t kw[U][DPL / 2], vw[U][DPL / 2];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = j0 + NG * u < nprev ? j0 + NG * u : 0;
-      const int slot = p < Sc ? j : (j < cur_slot ? j : j + 1);
-      const size_t eo = (size_t)slot * HS;
-#pragma unroll
-      for (int i = 0; i < DPL / 2; ++i) {
-        kw[u][i] = reinterpret_cast<const uint32_t*>(kc + eo)[i];
-        vw[u][i] = reinterpret_cast<const uint32_t*>(vc + eo)[i];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      float sc = 0.f;
-#pragma unroll
-      for (int i = 0; i < DPL / 2; ++i) sc += qf[2 * i] * bflo(kw[u][i]) + qf[2 * i + 1] * bfhi(kw[u][i]);
-      sc = row16_sum(sc);
-      if (j0 + NG * u >= nprev) continue;
-      float vv[DPL];
-#pragma unroll
-      for (int i = 0; i < DPL / 2; ++i) {
-        vv[2 * i] = bflo(vw[u][i]);
-        vv[2 * i + 1] = bfhi(vw[u][i]);
-      }
-      step(sc, vv);
-    }
+  for (int r = 0; r < kKPT; ++r) {  // cache rows (32 B of K and of V per key), branch-free
+    const int kk = t + 64 * NC * r;
+    const int ki = kk < nprev ? kk : 0;
+    const int slot = p < Sc ? ki : (ki < cur_slot ? ki : ki + 1);
+    const u32x4* kp = reinterpret_cast<const u32x4*>(kc + (size_t)slot * HS);
+    const u32x4* vp = reinterpret_cast<const u32x4*>(vc + (size_t)slot * HS);
+    kr[r][0] = kp[0];
+    kr[r][1] = kp[1];
+    vr[r][0] = vp[0];
+    vr[r][1] = vp[1];
   }
-  if (kg == NG - 1) {  // the current key (this step's k / v: not yet readable from the cache)
+  float q[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) q[d] = aq[d];
+#pragma unroll
+  for (int r = 0; r < kKPT; ++r) {
+    const int kk = t + 64 * NC * r;
     float sc = 0.f;
+    if (kk == nprev) {  // the current key (this step's k: not read back from the cache)
 #pragma unroll
-    for (int i = 0; i < DPL; ++i) sc += qf[i] * sk[sub * DPL + i];
-    sc = row16_sum(sc);
-    float vv[DPL];
+      for (int d = 0; d < 16; ++d) sc += q[d] * ak[d];
+    } else {
 #pragma unroll
-    for (int i = 0; i < DPL; ++i) vv[i] = sv[sub * DPL + i];
-    step(sc, vv);
-  }
-  {  // merge the 4 groups of a wave (rows 0+1 and 2+3, then the halves)
-    float mlo, mhi, llo, lhi, olo[DPL], ohi[DPL];
-    auto merge = [&]() {
-      const float M = fmaxf(mlo, mhi);
-      const float flo = mlo == -INFINITY ? 0.f : exp2f(mlo - M);
-      const float fhi = mhi == -INFINITY ? 0.f : exp2f(mhi - M);
-      mx = M;
-      lsum = llo * flo + lhi * fhi;
-#pragma unroll
-      for (int i = 0; i < DPL; ++i) o[i] = olo[i] * flo + ohi[i] * fhi;
-    };
-    lane_halves<false>(mx, mlo, mhi);
-    lane_halves<false>(lsum, llo, lhi);
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) lane_halves<false>(o[i], olo[i], ohi[i]);
-    merge();
-    lane_halves<true>(mx, mlo, mhi);
-    lane_halves<true>(lsum, llo, lhi);
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) lane_halves<true>(o[i], olo[i], ohi[i]);
-    merge();
-  }
-  if (X.lane < 16) {
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) s_o[X.wave * HS + sub * DPL + i] = o[i];
-    if (sub == 0) {
-      s_m[X.wave] = mx;
-      s_l[X.wave] = lsum;
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t wv = kr[r][i >> 2][i & 3];
+        sc += q[2 * i] * bflo(wv) + q[2 * i + 1] * bfhi(wv);
+      }
     }
+    if (kk < NK) st_gran(gs + (size_t)kk * J + j, tag, __float_as_uint(sc));
+  }
+  if (X.wave == 0 && l < 8) stamp(P, X.lane, 2 + 12 * l + 9);
+  // the head's J partials of every key, summed in slice order
+  float sfull[kKPT];
+#pragma unroll
+  for (int r = 0; r < kKPT; ++r) {
+    const int kk = t + 64 * NC * r;
+    const int ki = kk < NK ? kk : 0;
+    unsigned long long v[J];
+    unsigned it = 0;
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int jj = 0; jj < J; ++jj) v[jj] = ld_gran(gs + (size_t)ki * J + jj);
+#pragma unroll
+      for (int jj = 0; jj < J; ++jj) ok &= kk >= NK || (unsigned)(v[jj] >> 32) == tag;
+      if (__all(ok)) break;
+      if (spin_fail(X, it)) break;
+    }
+    float a = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj) a += __uint_as_float((uint32_t)v[jj]);
+    sfull[r] = kk < NK ? a : -INFINITY;
+  }
+  // softmax over the NK keys (every consumer wave), then P.V over this CU's 16 dims
+  float mx = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < kKPT; ++r) mx = fmaxf(mx, sfull[r]);
+  mx = wave_max(mx);
+  if (X.lane == 0) s_m[X.wave] = mx;
+  cbarrier(X, L);
+  float M = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < NC; ++w) M = fmaxf(M, s_m[w]);
+  float lsum = 0.f, o[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) o[d] = 0.f;
+#pragma unroll
+  for (int r = 0; r < kKPT; ++r) {
+    const int kk = t + 64 * NC * r;
+    const float e = kk < NK ? exp2f(sfull[r] - M) : 0.f;
+    lsum += e;
+    if (kk == nprev) {
+#pragma unroll
+      for (int d = 0; d < 16; ++d) o[d] += e * av[d];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t wv = vr[r][i >> 2][i & 3];
+        o[2 * i] += e * bflo(wv);
+        o[2 * i + 1] += e * bfhi(wv);
+      }
+    }
+  }
+  lsum = wave_sum(lsum);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) o[d] = wave_sum(o[d]);
+  if (X.lane == 0) {
+    s_l[X.wave] = lsum;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) s_o[X.wave * 16 + d] = o[d];
   }
   cbarrier(X, L);
-  const int d = X.wave * 64 + X.lane;
-  if (d < HS) {
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NC; ++w) M = fmaxf(M, s_m[w]);
+  if (X.wave == 0) {
+    const int d = X.lane & 15;
     float Ls = 0.f, O = 0.f;
 #pragma unroll
     for (int w = 0; w < NC; ++w) {
-      const float f = s_m[w] == -INFINITY ? 0.f : exp2f(s_m[w] - M);
-      Ls += s_l[w] * f;
-      O += s_o[w * HS + d] * f;
+      Ls += s_l[w];
+      O += s_o[w * 16 + d];
     }
     const uint32_t ob = (uint32_t)f2bf(O / Ls);
     const uint32_t pr = lane_xor1(ob);
-    if (!(d & 1)) st_gran(ar.gy + (h * HS + d) / 2, tag, ob | (pr << 16));
+    if (X.lane < 16 && !(X.lane & 1)) st_gran(ar.gy + (h * HS + 16 * j + d) / 2, tag, ob | (pr << 16));
   }
-  cbarrier(X, L);  // the scratch is free again
 }
 
 // ------------------------------------------------------------------------------------ loader
@@ -798,7 +830,7 @@ __device__ __forceinline__ void loader(Ctx& X, const Lds& L, const llj_engine_pl
       const char* w1 = op_weight(P, l, op, nm - 1);
       const int per_tile = kc * nm;
       for (int j = 0; j < nt; ++j) {
-        const uint32_t toff = (uint32_t)(s.g + j * s.G) * (uint32_t)kc * 1024u;  // the tile's first chunk
+        const uint32_t toff = (uint32_t)tile_of(s, op, j) * (uint32_t)kc * 1024u;  // the tile's first chunk
         for (int r0 = 0; r0 < per_tile; r0 += LG) {
           const int n = per_tile - r0 < LG ? per_tile - r0 : LG;
           if (!free_run && b + n > limit) {
@@ -867,11 +899,14 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
   Shape& s = X.s;
   s.C = P.C; s.H = P.H; s.V = P.V; s.nh = P.n_head; s.hs = P.C / P.n_head; s.S = P.S; s.L = P.n_layer;
   s.G = gridDim.x; s.g = blockIdx.x;
+  s.J = s.hs / 16;
+  s.unit = unit_of_cu(s.g, s.G, s.nh, s.J);
   X.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   X.lane = threadIdx.x & 63;
   X.aborted = false;
   X.bar_gen = 0;
   X.n_used = 0;
+  X.landed = 0;
   X.stamp_base = -1;
   X.plan = &P;
   X.t0 = __builtin_amdgcn_s_memrealtime();
@@ -894,7 +929,7 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
     L.misc = reinterpret_cast<float*>(smem + o);
     o += 64 * 4;
     L.att = reinterpret_cast<float*>(smem + o);
-    o += al16((size_t)(3 * s.hs + 2 * NC + NC * s.hs) * 4);
+    o += al16((size_t)kAttFloats * 4);
     L.ring = smem + o;
     L.nb = P.ring_blocks;
     L.nb_magic = (unsigned)((0x100000000ull + (unsigned)L.nb - 1) / (unsigned)L.nb);
@@ -915,9 +950,6 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
   const int tok = P.cur[0];
   int red_par = 0;
   const int hs = s.hs;
-  const int att_stride = s.G / s.nh;
-  const bool att_cu = (s.g % att_stride) == 0 && s.g / att_stride < s.nh;
-  const int att_h = s.g / att_stride;
   Epi E;
   E.ar = ar;
   E.slot = p % s.S;
@@ -939,9 +971,10 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
     float2* eop = L.eop + (op & 1) * kEopTiles * 2 * 16;
     if (op == OP_O) {
       if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 1);
-      if (att_cu) {  // attention of one head on the attention CUs
-        if (hs == 128) attention_head<128>(X, L, P, ar, l, att_h, p, tag);
-        else attention_head<64>(X, L, P, ar, l, att_h, p, tag);
+      if (s.unit >= 0) {  // attention of this CU's (head, 16-dim slice) unit
+        cbarrier(X, L);   // the QKV epilogue's q / k / v slices are in LDS
+        if (hs == 128) attention_dims<128>(X, L, P, ar, l, p, tag);
+        else attention_dims<64>(X, L, P, ar, l, p, tag);
       }
       if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 2);
     } else if (X.wave == 0 && l < 8 && op != OP_QKV) {
@@ -954,7 +987,7 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
       const int nt = tiles_of_cu(s, OP_QKV);
       for (int k = X.lane + 64 * X.wave; k < nt * 8 && k < 8 * TG; k += 64 * NC) {
         const int j = k >> 3, pr = k & 7;
-        const int n = 16 * (s.g + j * s.G) + 2 * pr;
+        const int n = 16 * tile_of(s, OP_QKV, j) + 2 * pr;
         const int dd = (n % C) % hs;
         rcs[k] = *reinterpret_cast<const float2*>(P.rope + ((size_t)p * (hs >> 1) + (dd >> 1)) * 2);
       }
@@ -1031,7 +1064,7 @@ size_t llj_engine_arena_bytes(int C, int H) { return eng::arena_granules(C, H) *
 
 int llj_engine_ring_blocks(int C, int H, int n_head) {
   if (n_head < 1 || C % n_head) return 0;
-  return eng::ring_blocks(C, H, C / n_head, 160 * 1024);
+  return eng::ring_blocks(C, H, 160 * 1024);
 }
 
 int llj_engine_step(const llj_engine_plan* plan, void* stream) {
@@ -1039,19 +1072,20 @@ int llj_engine_step(const llj_engine_plan* plan, void* stream) {
   const llj_engine_plan& P = *plan;
   const int hs = P.n_head > 0 ? P.C / P.n_head : 0;
   LLJ_REQUIRE(P.layers && P.n_layer >= 1 && P.n_layer <= 126 && P.C % 128 == 0 && P.H % 128 == 0 && P.V % 16 == 0);
-  LLJ_REQUIRE(P.V <= 65536 && (hs == 64 || hs == 128) && P.S >= 1 && P.arena && P.pos && P.cur && P.logits);
+  LLJ_REQUIRE(P.V <= 65536 && (hs == 64 || hs == 128) && P.S >= 1 && P.S <= eng::kMaxS && P.arena && P.pos && P.cur &&
+              P.logits);
   LLJ_REQUIRE(P.C / 2 <= eng::GN * 64 * eng::NC);  // stage's gain registers
+  LLJ_REQUIRE(P.C <= eng::AREG_C * eng::NC * 128);  // A fragments of the K = C ops in registers
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return LLJ_EINVAL;
   const int G = P.grid > 0 ? P.grid : cus;
-  LLJ_REQUIRE(G >= 1 && G <= cus && G <= eng::kMaxCUs && P.n_head <= G);
-  // at most TG QKV tiles per CU (RoPE operands) and kEopTiles tiles per op
-  LLJ_REQUIRE((3 * P.C / 16 + G - 1) / G <= eng::TG && (P.V / 16 + G - 1) / G <= eng::kEopTiles &&
-              (P.H / 16 + G - 1) / G <= eng::kEopTiles);
-  const int nb = eng::ring_blocks(P.C, P.H, hs, 160 * 1024);
+  LLJ_REQUIRE(G >= 1 && G <= cus && G <= eng::kMaxCUs);
+  // one QKV unit (head, 16-dim slice) per CU at most; kEopTiles tiles per op
+  LLJ_REQUIRE(P.C / 16 <= G && (P.V / 16 + G - 1) / G <= eng::kEopTiles && (P.H / 16 + G - 1) / G <= eng::kEopTiles);
+  const int nb = eng::ring_blocks(P.C, P.H, 160 * 1024);
   LLJ_REQUIRE(P.ring_blocks >= 2 * eng::D && P.ring_blocks <= nb && P.ring_blocks % eng::LG == 0);
-  const size_t lds = eng::lds_fixed(P.C, P.H, hs) + (size_t)P.ring_blocks * 1024;
+  const size_t lds = eng::lds_fixed(P.C, P.H) + (size_t)P.ring_blocks * 1024;
   LLJ_REQUIRE(lds <= 160 * 1024 && lds > 80 * 1024);  // one workgroup per CU, every one resident
   static bool attr = false;
   if (!attr) {

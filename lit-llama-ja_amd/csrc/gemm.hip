@@ -67,8 +67,9 @@ struct GemmParams {
   int gch;  // GWF_W4G: group size in 128-deep chunks; sz = (scale, 128 + zero) per (group, column), (G, N)
   const char* i8ws;  // GWF_I8: llj_i8_stats workspace of A (aq, SCA, outlier list); sz = (const float*) SCB
   // GWF_I8 (optional): the outlier columns pre-gathered by llj_i8_gather_act / _weight, f16 rows of
-  // stride kpad, zero past the outlier count up to a multiple of 64: the side product then runs as
-  // a dense f16 GEMM over them (coalesced 64-deep chunks) instead of per-tile gathers
+  // stride kpad (a fixed capacity, multiple of 64), zero past the outlier count up to a multiple of
+  // 64: the side product then runs as a dense f16 GEMM over them (coalesced 64-deep chunks) instead
+  // of per-tile gathers; a count above kpad (nothing gathered) takes the per-tile side product
   const _Float16* ao16;
   const _Float16* w16;
   int kpad;
@@ -380,7 +381,8 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
     const int total = s_pre[h8.nsb];
     const int sn = n0 + (bt >> 1);  // staging: W column (B) bt >> 1 / A row (A) ar, outliers 16 ah + [0, 16)
     const float scb = reinterpret_cast<const float*>(p.sz)[sn] / 127.f;
-    if (p.ao16) {  // dense f16 GEMM over the pre-gathered outlier columns, 64-deep chunks
+    const bool gathered = p.ao16 && total <= p.kpad;  // else: more outliers than the gathers' capacity
+    if (gathered) {  // dense f16 GEMM over the pre-gathered outlier columns, 64-deep chunks
       __syncthreads();  // every thread has read `total` before the chunk buffers overwrite s_pre
       const int SKC = (total + 63) >> 6;
       constexpr int BVD = BM == 256 ? 2 : 4;
@@ -423,7 +425,7 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
         }
       }
     }
-    for (int c0 = 0; c0 < (p.ao16 ? 0 : total); c0 += kSideK) {
+    for (int c0 = 0; c0 < (gathered ? 0 : total); c0 += kSideK) {
       if (tid < kSideK) {
         const int fi = c0 + tid;
         int k = -1;
@@ -580,7 +582,7 @@ static int gemm_run(int wfmt, GemmParams& p, void* stream) {
   }
   if (wfmt == GWF_I8) {
     if (!p.sz || !p.i8ws || p.K % 128) return LLJ_EINVAL;
-    if (!p.ao16 != !p.w16 || (p.ao16 && (p.kpad < ((p.K + 63) & ~63) || p.kpad % 8))) return LLJ_EINVAL;
+    if (!p.ao16 != !p.w16 || (p.ao16 && (p.kpad < 64 || p.kpad % 64))) return LLJ_EINVAL;
     if (LLJ_GEMM_BM256_I8 && p.M >= 256) return gemm_launch<GWF_I8, EP, 256>(p, s);
     return gemm_launch<GWF_I8, EP>(p, s);
   }

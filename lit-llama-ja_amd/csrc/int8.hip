@@ -443,8 +443,10 @@ __global__ __launch_bounds__(256) void i8_quant_weight_kernel(const void* __rest
 // columns (ascending, from the per-k-block lists) of the activation as f16 rows ao16[M][kpad] and of
 // the weight as f16(CB * SCB / 127) rows w16[N][kpad]; entries past the outlier count up to the next
 // multiple of 64 are zero, so the GEMM reads whole 64-deep chunks with 16-byte loads.
-// The flat list is rebuilt in LDS by every block (counts prefix + the per-block lists).
-__device__ __forceinline__ int i8_flat_list(const I8Layout& L, const I8WsHeader& h, int* s_pre, int* s_list) {
+// The flat list is rebuilt in LDS by every block (counts prefix + the per-block lists), its first
+// `cap` entries only: kpad is a fixed capacity (the host cannot know the count without a sync);
+// when the count exceeds it nothing is gathered and the GEMM runs its per-tile side product.
+__device__ __forceinline__ int i8_flat_list(const I8Layout& L, const I8WsHeader& h, int* s_pre, int* s_list, int cap) {
   const int tid = threadIdx.x, lane = tid & 63;
   if (tid < 64) {
     const int c = tid < h.nsb ? L.cnt[tid] : 0;
@@ -458,6 +460,7 @@ __device__ __forceinline__ int i8_flat_list(const I8Layout& L, const I8WsHeader&
     if (tid == 0) s_pre[0] = 0;
   }
   __syncthreads();
+  if (s_pre[h.nsb] > cap) return s_pre[h.nsb];  // over capacity: the caller gathers nothing
   for (int b = 0; b < h.nsb; ++b)
     for (int j = tid; j < s_pre[b + 1] - s_pre[b]; j += blockDim.x) s_list[s_pre[b] + j] = L.list[b * h.kb + j];
   __syncthreads();
@@ -469,7 +472,8 @@ __global__ __launch_bounds__(256) void i8_gather_act_kernel(const bf16_t* __rest
   extern __shared__ int g_lds[];
   const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(ws);
   const I8Layout L = i8_layout(ws, h.mtot, h.K);
-  const int total = i8_flat_list(L, h, g_lds, g_lds + 80);
+  const int total = i8_flat_list(L, h, g_lds, g_lds + 80, kpad);
+  if (total > kpad) return;  // the GEMM sees the same count and takes its per-tile side product
   const int* s_list = g_lds + 80;
   const int m = blockIdx.x, nop = (total + 63) & ~63;
   for (int j0 = threadIdx.x; j0 < nop; j0 += 256 * 8) {  // 8 loads in flight per thread
@@ -493,7 +497,8 @@ __global__ __launch_bounds__(256) void i8_gather_weight_kernel(const int8_t* __r
   extern __shared__ int g_lds[];
   const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(ws);
   const I8Layout L = i8_layout(ws, h.mtot, h.K);
-  const int total = i8_flat_list(L, h, g_lds, g_lds + 80);
+  const int total = i8_flat_list(L, h, g_lds, g_lds + 80, kpad);
+  if (total > kpad) return;
   const int* s_list = g_lds + 80;
   const int nt = blockIdx.x, r = threadIdx.x >> 4, n = nt * 16 + r, nop = (total + 63) & ~63;
   const float scb = SCB[n] / 127.f;
@@ -592,8 +597,8 @@ int llj_i8_norm_stats(const void* x, const void* norm_w, float eps, void* xn, in
 }
 
 int llj_i8_gather_act(const void* A, int lda, int M, int K, const void* ws, void* ao16, int kpad, void* stream) {
-  LLJ_REQUIRE(M > 0 && K > 0 && kpad >= ((K + 63) & ~63) && kpad % 8 == 0 && ws && ao16);
-  const size_t lds = (80 + (size_t)K) * sizeof(int);
+  LLJ_REQUIRE(M > 0 && K > 0 && kpad >= 64 && kpad % 64 == 0 && ws && ao16);
+  const size_t lds = (80 + (size_t)kpad) * sizeof(int);
   LLJ_REQUIRE(lds <= 65536);
   hipLaunchKernelGGL(i8_gather_act_kernel, dim3(M), dim3(256), lds, (hipStream_t)stream, (const bf16_t*)A, lda,
                      (const char*)ws, (_Float16*)ao16, kpad);
@@ -603,8 +608,8 @@ int llj_i8_gather_act(const void* A, int lda, int M, int K, const void* ws, void
 
 int llj_i8_gather_weight(const void* CB, const void* SCB, int N, int K, const void* ws, void* w16, int kpad,
                          void* stream) {
-  LLJ_REQUIRE(N > 0 && N % 16 == 0 && K % 128 == 0 && kpad >= ((K + 63) & ~63) && kpad % 8 == 0 && ws && w16);
-  const size_t lds = (80 + (size_t)K) * sizeof(int);
+  LLJ_REQUIRE(N > 0 && N % 16 == 0 && K % 128 == 0 && kpad >= 64 && kpad % 64 == 0 && ws && w16);
+  const size_t lds = (80 + (size_t)kpad) * sizeof(int);
   LLJ_REQUIRE(lds <= 65536);
   hipLaunchKernelGGL(i8_gather_weight_kernel, dim3(N / 16), dim3(256), lds, (hipStream_t)stream, (const int8_t*)CB,
                      (const float*)SCB, K, (const char*)ws, (_Float16*)w16, kpad);

@@ -64,6 +64,11 @@ def engine_supported(model: LLaMA, specs, batch: int, S: int) -> str | None:
         return "shape"
     if cfg.padded_vocab_size > 65536:
         return "vocabulary > 65536"
+    cus = torch.cuda.get_device_properties(model.transformer.wte.weight.device).multi_processor_count
+    if cfg.n_embd // 16 > cus:  # one QKV unit (head, 16-dim slice) per CU (13B: 320 units > 256 CUs)
+        return f"{cfg.n_embd // 16} QKV units > {cus} CUs"
+    if cfg.n_embd > 4480:  # the K = C ops keep their A fragments in registers (csrc/engine.hip AREG_C)
+        return "n_embd > 4480"
     fmts = {sp[0] for layer in specs["layers"] for sp in layer} | {specs["head"][0]}
     if fmts != {0}:
         return "not every Linear is per-row int4 (W4P)"

@@ -152,6 +152,12 @@ def _gemm_fmt(wfmt: int) -> bool:
 # LLM.int8 prompt rows: the outlier columns of each GEMM's activation and weight pre-gathered as f16
 # rows (llj_i8_gather_act / _weight), so the fp16 side product runs as a dense f16 GEMM over them
 I8_GATHER = True
+# their capacity in outlier columns: all of K while the f16 weight rows of one call stay within
+# I8_GATHER_BUDGET bytes (7B: every Linear; the 65B c_fc1 + c_fc2 pair caps at 2,880 columns), and
+# at most I8_GATHER_MAX, the gathers' LDS list ((80 + kpad) * 4 <= 64 KiB); real checkpoints have
+# 6-20 outlier columns, synthetic random weights up to all of K
+I8_GATHER_BUDGET = 256 << 20
+I8_GATHER_MAX = 16256
 
 # int8 decode: RMSNorm + LLM.int8() statistics in one launch pair up to this many rows
 I8_NORM_STATS_MAX_M = 16
@@ -406,10 +412,14 @@ class LLaMA(nn.Module):
     def _i8_gathered(self, A, M, K, lins, w, st):
         """(ao16, [w16 per (W, sz, N) in lins], kpad): the outlier columns of A (statistics already in
         w.i8ws) and of each weight as f16 rows for the LLM.int8 GEMMs (I8_GATHER), else (None, Nones, 0).
+        kpad is a fixed capacity (the count stays on the device): every outlier column while the f16
+        weight rows fit I8_GATHER_BUDGET bytes, and at most I8_GATHER_MAX (the gathers' LDS list); a
+        count above it gathers nothing and the GEMM runs its per-tile side product.
         Stream-ordered: freed after the call, reused only by later work on the same stream."""
         if not I8_GATHER:
             return None, [None] * len(lins), 0
-        kpad = (K + 63) // 64 * 64
+        rows = sum(N for _, _, N in lins)
+        kpad = min((K + 63) // 64 * 64, I8_GATHER_MAX, max(64, I8_GATHER_BUDGET // (2 * rows) // 64 * 64))
         ao = torch.empty(M, kpad, dtype=torch.float16, device=A.device)
         _hip.call("llj_i8_gather_act", A.data_ptr(), A.stride(0), M, K, w.i8ws.data_ptr(), ao.data_ptr(), kpad, st)
         out = []
@@ -610,7 +620,6 @@ class LLaMA(nn.Module):
                    else getattr(self.transformer, "ln_f", None))  # (Block.forward: no ln_f, no norm after)
             self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st, w.nst if w.hand else None,
                         post=nxt if w.post else None)
-            w.xn_ready = w.post and nxt is not None
 
     def _resid(self, f, A, W, sz, x, M, N, K, w, st, nst=None, post=None):
         """x += A . W^T; with `nst` (the norm hand-off, N / 16 tiles x 16 rows) also the next

@@ -938,10 +938,14 @@ def test_i8_stats_many_rows(hip, M, K):
 
 
 def _i8_gather(hip, xd, M, K, ws, weights, on):
-    """(ao16, [w16], kpad) pointers for llj_gemm_i8_* (the pre-gathered outlier matrices), or Nones."""
+    """(ao16, [w16], kpad) pointers for llj_gemm_i8_* (the pre-gathered outlier matrices), or Nones.
+    on: True = capacity for every column as the model sizes it (model.py _i8_gathered), "cap64" = a
+    64-column capacity (more outliers than that: nothing gathered, the GEMM's per-tile side product)."""
     if not on:
         return None, [None] * len(weights), 0, []
-    kpad = (K + 63) // 64 * 64
+    from lit_llama.model import I8_GATHER_MAX
+
+    kpad = 64 if on == "cap64" else min((K + 63) // 64 * 64, I8_GATHER_MAX)
     ao = torch.full((M, kpad), float("nan"), dtype=torch.float16, device=dev)  # past the pad: never read
     call(hip, "llj_i8_gather_act", xd.data_ptr(), K, M, K, ws.data_ptr(), ao.data_ptr(), kpad, st())
     keep, ptrs = [ao], []
@@ -953,14 +957,16 @@ def _i8_gather(hip, xd, M, K, ws, weights, on):
     return ao.data_ptr(), ptrs, kpad, keep
 
 
-@pytest.mark.parametrize("gather", [False, True])
+@pytest.mark.parametrize("gather", [False, True, "cap64"])
 @pytest.mark.parametrize("outliers", [0, 6, 300])
-@pytest.mark.parametrize("M,N,K", [(40, 256, 4096), (300, 4096, 4096), (129, 384, 11008)])
+@pytest.mark.parametrize("M,N,K", [(40, 256, 4096), (300, 4096, 4096), (129, 384, 11008), (48, 256, 17920)])
 def test_gemm_i8_linear_resid_silu(hip, M, N, K, outliers, gather):
     """LLM.int8() prefill GEMM (int8 MFMA over the quantized rows + the fp16 outlier side product;
     llj_gemm_i8_linear / _resid / _silu_mul) against the oracle's restatement (bitsandbytes absent:
     parity unpinned) and against the int8 GEMV on the same workspace; the side product either
-    gathered per tile or as a dense f16 GEMM over the pre-gathered outlier matrices (gather)."""
+    gathered per tile or as a dense f16 GEMM over the pre-gathered outlier matrices (gather), also
+    past the gathers' capacity (cap64 with 300 columns) and at K = 17,920 (30B mlp.c_proj: the
+    gathers' list capped at I8_GATHER_MAX entries of LDS)."""
     rng = np.random.default_rng(M + N + K + outliers)
     W = bf16(rng.standard_normal((N, K)) * 0.02)
     W2 = bf16(rng.standard_normal((N, K)) * 0.02)
@@ -978,9 +984,10 @@ def test_gemm_i8_linear_resid_silu(hip, M, N, K, outliers, gather):
     xr = T(x0, torch.bfloat16)
     call(hip, "llj_gemm_i8_resid", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), ao, g1, kp,
          xr.data_ptr(), N, M, N, K, st())
-    gv = torch.empty(M, N, dtype=torch.bfloat16, device=dev)  # the int8 GEMV in 8-row slices
-    for r0 in range(0, M, 8):
-        r = min(8, M - r0)
+    gv = torch.empty(M, N, dtype=torch.bfloat16, device=dev)  # the int8 GEMV in 8-row slices (4 at K > 12k: LDS)
+    sl = 8 if 8 * (K + 16) <= 96 * 1024 else 4
+    for r0 in range(0, M, sl):
+        r = min(sl, M - r0)
         call(hip, "llj_linear", 2, xd[r0].data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), None, gv[r0].data_ptr(), N, r,
              N, K, ws.data_ptr(), r0, None, st())
     h = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
@@ -999,7 +1006,7 @@ def test_gemm_i8_linear_resid_silu(hip, M, N, K, outliers, gather):
     assert_bf16_close(h.float().cpu().numpy(), hexp, "gemm int8 swiglu", rel=3e-2)
 
 
-@pytest.mark.parametrize("gather", [False, True])
+@pytest.mark.parametrize("gather", [False, True, "cap64"])
 @pytest.mark.parametrize("B,T_,nh,hs,outliers", [(1, 200, 32, 128, 6), (3, 40, 4, 64, 0), (1, 300, 8, 128, 6)])
 def test_gemm_i8_qkv_rope_kv(hip, B, T_, nh, hs, outliers, gather):
     """llj_gemm_i8_qkv_rope: LLM.int8 c_attn + RoPE + KV-cache write for a whole prompt."""
