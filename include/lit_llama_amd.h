@@ -262,26 +262,35 @@ int llj_sample(const void* logits, int ldl, int M, int V, float temperature, int
 /* ---------------------------------------------------------------- any-shape path (csrc/generic.hip)
  * LLaMA configurations the streaming kernels do not tile (n_embd % 128 != 0, head size not 64 /
  * 128: the JA fork's 125M, n_embd 780 / head 78, reference lit_llama/model.py:48-51; the reference
- * test's n_embd 32 / head 2, tests/test_model.py:108-112). Plain kernels, the reference's bf16
- * rounding points; LLaMA.forward and the decode session route such models here. */
+ * test's n_embd 32 / head 2, tests/test_model.py:108-112), and every fp32 model. Plain kernels;
+ * dt selects the activation type of every operand (and of dense weights, KV cache, logits):
+ * 0 = bf16 with the reference's bf16 rounding points, 1 = fp32 with none (the reference's float32
+ * model: evaluate/full.py:55, 84 default dtype, generate.py:121 on a host without a GPU).
+ * LLaMA.forward and the decode session route such models here. */
+/* out[m] = wte[idx[m]] (model.py:110), any C; bumps *pos_inc when not NULL (decode step). */
+int llj_g_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, int dt, void* stream);
 /* RMSNorm (model.py:276-283) of M rows of any width C (row strides ldx / ldy). */
-int llj_g_rmsnorm(const void* x, int ldx, const void* w, float eps, void* y, int ldy, int M, int C, void* stream);
-/* y[m, n] = bf16(x[m] . W[n]) for M rows, or bf16(resid[m, n] + that) when resid != NULL (may be y).
- * wkind 1: dense bf16 W (N, K) row-major (nn.Linear). wkind 0: ColBlockQuantizedLinear's buffers as
- * the reference stores them -- quant_weight column-major (byte (n, j) at j*N + n, 8/bits codes per
- * byte, low bits first), scales / zeros fp32 (N, G), G = ceil(K / group), group = tile_cols (K for
- * tile_cols = -1); weight element (q - zero) * scale in fp32 (quantization.py:250-267, 390-409). */
+int llj_g_rmsnorm(const void* x, int ldx, const void* w, float eps, void* y, int ldy, int M, int C, int dt, void* stream);
+/* y[m, n] = x[m] . W[n] for M rows, or resid[m, n] + that when resid != NULL (may be y); rounded to
+ * bf16 at the reference's points when dt = 0. wkind 1: dense W (N, K) row-major of the activation
+ * type (nn.Linear). wkind 0: ColBlockQuantizedLinear's buffers as the reference stores them --
+ * quant_weight column-major (byte (n, j) at j*N + n, 8/bits codes per byte, low bits first), scales
+ * / zeros fp32 (N, G), G = ceil(K / group), group = tile_cols (K for tile_cols = -1); weight element
+ * (q - zero) * scale in fp32 (quantization.py:250-267, 390-409). */
 int llj_g_linear(int wkind, const void* x, int ldx, int M, int K, const void* W, const float* scales, const float* zeros,
-                 int bits, int group, int N, void* y, int ldy, const void* resid, int ldr, void* stream);
+                 int bits, int group, int N, void* y, int ldy, const void* resid, int ldr, int dt, void* stream);
 /* c_attn output qkv (B*T, 3C) -> q_out (B*T, C) with RoPE, k (RoPE) / v into cache slot pos[t] % S
  * (model.py:204-228, 312-329); rope (block_size, hs/2, 2) fp32; head size even. */
 int llj_g_rope_kv(const void* qkv, void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
-                  int C, int n_head, int S, void* stream);
+                  int C, int n_head, int S, int dt, void* stream);
 /* Causal attention as llj_attention, any head size ((S + hs) * 4 bytes of LDS <= 64 KiB). */
 int llj_g_attention(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T, int C,
-                    int n_head, int S, void* stream);
-/* h[i] = bf16(bf16(silu(a1[i])) * a2[i]), i < n (model.py:258-259). */
-int llj_g_silu_mul(const void* a1, const void* a2, void* h, size_t n, void* stream);
+                    int n_head, int S, int dt, void* stream);
+/* h[i] = silu(a1[i]) * a2[i], i < n (model.py:258-259; dt 0: bf16(bf16(silu(a1)) * a2)). */
+int llj_g_silu_mul(const void* a1, const void* a2, void* h, size_t n, int dt, void* stream);
+/* Greedy next token over fp32 logits (generate.py:66-74, top_k = 1), as llj_argmax. */
+int llj_g_argmax(const float* logits, int ldl, int M, int V, int* out_idx, int* tokens_out, int tok_stride, const int* pos,
+                 void* stream);
 
 /* Measurement aid (no reference counterpart): reads `bytes` (a multiple of 16) at p once with
  * non-temporal 16-byte loads over `grid` workgroups of 256 and writes one float per workgroup to

@@ -4,29 +4,60 @@
 // run here. Plain kernels: one output per wave (linear) or per thread, fp32 accumulation, the
 // reference's bf16 rounding points (the same ones the fast kernels keep). Slower by design: these
 // shapes are small models, and none of them is the headline workload.
+// Every kernel also runs in fp32 (dt = 1: activations, dense weights, KV cache and logits fp32, no
+// bf16 rounding -- the reference's float32 model, e.g. evaluate/full.py's default dtype and the
+// CPU config of generate.py:121): LLaMA.forward routes an fp32 model here whatever its shape.
 #include "common.h"
 #include "lit_llama_amd.h"
 
 namespace llj {
 
-// ---- RMSNorm (model.py:276-283 on bf16 tensors): one block per row, any C
-__global__ __launch_bounds__(256) void g_rmsnorm_kernel(const bf16_t* __restrict__ x, int ldx, const bf16_t* __restrict__ w,
-                                                        float eps, bf16_t* __restrict__ y, int ldy, int C) {
+// element access of the activation type: bf16 (the reference's rounding points) or fp32 (none)
+template <typename T>
+__device__ __forceinline__ float ldv(const T* p, size_t i) {
+  if constexpr (sizeof(T) == 2) return bf2f(p[i]);
+  else return p[i];
+}
+template <typename T>
+__device__ __forceinline__ void stv(T* p, size_t i, float v) {
+  if constexpr (sizeof(T) == 2) p[i] = f2bf(v);
+  else p[i] = v;
+}
+template <typename T>
+__device__ __forceinline__ float rnd(float v) {
+  if constexpr (sizeof(T) == 2) return round_bf(v);
+  else return v;
+}
+
+// ---- embedding (model.py:110), any C, optionally bumping the device-side decode position
+template <typename T>
+__global__ __launch_bounds__(256) void g_embedding_kernel(const int* __restrict__ idx, const T* __restrict__ wte,
+                                                          T* __restrict__ out, int C, int* pos_inc) {
+  const int m = blockIdx.x;
+  const size_t r = (size_t)idx[m];
+  for (int v = threadIdx.x; v < C; v += blockDim.x) out[(size_t)m * C + v] = wte[r * C + v];
+  if (pos_inc && m == 0 && threadIdx.x == 0) *pos_inc += 1;
+}
+
+// ---- RMSNorm (model.py:276-283; on bf16 tensors every op rounds): one block per row, any C
+template <typename T>
+__global__ __launch_bounds__(256) void g_rmsnorm_kernel(const T* __restrict__ x, int ldx, const T* __restrict__ w,
+                                                        float eps, T* __restrict__ y, int ldy, int C) {
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x;
-  const bf16_t* xr = x + (size_t)m * ldx;
+  const T* xr = x + (size_t)m * ldx;
   float ss = 0.f;
   for (int k = tid; k < C; k += 256) {
-    const float v = bf2f(xr[k]);
-    ss += round_bf(v * v);  // x * x in bf16 (model.py:281)
+    const float v = ldv(xr, k);
+    ss += rnd<T>(v * v);  // x * x (model.py:281)
   }
   ss = wave_sum(ss);
   if ((tid & 63) == 0) red[tid >> 6] = ss;
   __syncthreads();
   const float tot = red[0] + red[1] + red[2] + red[3];
-  const float r = round_bf(rsqrtf(round_bf(round_bf(tot / (float)C) + eps)));
-  bf16_t* yr = y + (size_t)m * ldy;
-  for (int k = tid; k < C; k += 256) yr[k] = f2bf(round_bf(bf2f(w[k]) * round_bf(bf2f(xr[k]) * r)));
+  const float r = rnd<T>(rsqrtf(rnd<T>(rnd<T>(tot / (float)C) + eps)));
+  T* yr = y + (size_t)m * ldy;
+  for (int k = tid; k < C; k += 256) stv(yr, k, ldv(w, k) * rnd<T>(ldv(xr, k) * r));
 }
 
 // ---- y[m, n] = bf16(sum_k x[m, k] W[n, k]) or, with resid, bf16(resid[m, n] + that) (the residual
@@ -35,13 +66,13 @@ __global__ __launch_bounds__(256) void g_rmsnorm_kernel(const bf16_t* __restrict
 // (n, j) at j N + n, 8 / bits codes per byte, code of k = j epb + r at bits r * bits), per-group
 // fp32 scales / zeros (N, G), group = tile_cols (K for -1); the weight element is the Triton path's
 // (q - zero) * scale in fp32 (quantization.py:250-267, 390-409). One wave per output column, lanes
-// over k, up to 8 rows per wave.
+// over k, up to 8 rows per wave. T: activation (and dense weight) type.
 constexpr int GL_ROWS = 8;
-template <int WK>
-__global__ __launch_bounds__(256) void g_linear_kernel(const bf16_t* __restrict__ x, int ldx, int M, int K,
+template <int WK, typename T>
+__global__ __launch_bounds__(256) void g_linear_kernel(const T* __restrict__ x, int ldx, int M, int K,
                                                        const void* __restrict__ W, const float* __restrict__ sc,
                                                        const float* __restrict__ zr, int bits, int group, int N,
-                                                       bf16_t* __restrict__ y, int ldy, const bf16_t* resid, int ldr) {
+                                                       T* __restrict__ y, int ldy, const T* resid, int ldr) {
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= N) return;
@@ -56,7 +87,7 @@ __global__ __launch_bounds__(256) void g_linear_kernel(const bf16_t* __restrict_
   for (int k = lane; k < K; k += 64) {
     float wv;
     if (WK == 1) {
-      wv = bf2f(reinterpret_cast<const bf16_t*>(W)[(size_t)n * K + k]);
+      wv = ldv(reinterpret_cast<const T*>(W), (size_t)n * K + k);
     } else {
       const int j = k / epb, sh = (k - j * epb) * bits;
       const uint32_t q = ((uint32_t)reinterpret_cast<const unsigned char*>(W)[(size_t)j * N + n] >> sh) & mask;
@@ -65,39 +96,40 @@ __global__ __launch_bounds__(256) void g_linear_kernel(const bf16_t* __restrict_
     }
 #pragma unroll
     for (int r = 0; r < GL_ROWS; ++r)
-      if (r < mr) acc[r] += bf2f(x[(size_t)(m0 + r) * ldx + k]) * wv;
+      if (r < mr) acc[r] += ldv(x, (size_t)(m0 + r) * ldx + k) * wv;
   }
 #pragma unroll
   for (int r = 0; r < GL_ROWS; ++r) {
     const float s = wave_sum(acc[r]);
     if (lane == r && r < mr) {
       const size_t m = (size_t)(m0 + r);
-      float v = round_bf(s);
-      if (resid) v = round_bf(bf2f(resid[m * ldr + n]) + v);
-      y[m * ldy + n] = f2bf(v);
+      float v = rnd<T>(s);
+      if (resid) v = ldv(resid, m * ldr + n) + v;
+      stv(y, m * ldy + n, v);
     }
   }
 }
 
 // ---- q / k / v split of c_attn's output (model.py:204), apply_rope on q and k in fp32
 // (model.py:312-329), k / v of the token at position p into cache slot p % S. Block (row, head).
-__global__ __launch_bounds__(64) void g_rope_kv_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ q_out,
-                                                       bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+template <typename TT>
+__global__ __launch_bounds__(64) void g_rope_kv_kernel(const TT* __restrict__ qkv, TT* __restrict__ q_out,
+                                                       TT* __restrict__ kc, TT* __restrict__ vc,
                                                        const float* __restrict__ rope, const int* __restrict__ pos,
                                                        int T, int C, int nh, int S) {
   const int m = blockIdx.x, h = blockIdx.y;
   const int hs = C / nh, b = m / T, t = m - b * T;
   const int p = pos[t], slot = p % S;
-  const bf16_t* row = qkv + (size_t)m * 3 * C + h * hs;
+  const TT* row = qkv + (size_t)m * 3 * C + h * hs;
   const size_t cbase = (((size_t)b * nh + h) * S + slot) * hs;
   for (int i = threadIdx.x; i < hs / 2; i += 64) {
     const float c = rope[((size_t)p * (hs / 2) + i) * 2], s = rope[((size_t)p * (hs / 2) + i) * 2 + 1];
-    const float q0 = bf2f(row[2 * i]), q1 = bf2f(row[2 * i + 1]);
-    const float k0 = bf2f(row[C + 2 * i]), k1 = bf2f(row[C + 2 * i + 1]);
-    q_out[(size_t)m * C + h * hs + 2 * i] = f2bf(q0 * c - q1 * s);
-    q_out[(size_t)m * C + h * hs + 2 * i + 1] = f2bf(q1 * c + q0 * s);
-    kc[cbase + 2 * i] = f2bf(k0 * c - k1 * s);
-    kc[cbase + 2 * i + 1] = f2bf(k1 * c + k0 * s);
+    const float q0 = ldv(row, 2 * i), q1 = ldv(row, 2 * i + 1);
+    const float k0 = ldv(row, C + 2 * i), k1 = ldv(row, C + 2 * i + 1);
+    stv(q_out, (size_t)m * C + h * hs + 2 * i, q0 * c - q1 * s);
+    stv(q_out, (size_t)m * C + h * hs + 2 * i + 1, q1 * c + q0 * s);
+    stv(kc, cbase + 2 * i, k0 * c - k1 * s);
+    stv(kc, cbase + 2 * i + 1, k1 * c + k0 * s);
     vc[cbase + 2 * i] = row[2 * C + 2 * i];
     vc[cbase + 2 * i + 1] = row[2 * C + 2 * i + 1];
   }
@@ -105,9 +137,10 @@ __global__ __launch_bounds__(64) void g_rope_kv_kernel(const bf16_t* __restrict_
 
 // ---- causal attention (model.py:237, the tril mask rows): row m at position p attends cache
 // slots [0, p] (all S slots once p >= S: the ring holds the last S positions). Scores in LDS,
-// fp32 softmax, y = bf16(P V / sum). Block (row, head); LDS: S + hs floats.
-__global__ __launch_bounds__(256) void g_attention_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
-                                                          const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
+// fp32 softmax, y = P V / sum (rounded to bf16 on the bf16 path). Block (row, head); LDS: S + hs floats.
+template <typename TT>
+__global__ __launch_bounds__(256) void g_attention_kernel(const TT* __restrict__ q, const TT* __restrict__ kc,
+                                                          const TT* __restrict__ vc, TT* __restrict__ y,
                                                           const int* __restrict__ pos, int T, int C, int nh, int S) {
   extern __shared__ float g_att_lds[];
   __shared__ float red[4];
@@ -118,14 +151,14 @@ __global__ __launch_bounds__(256) void g_attention_kernel(const bf16_t* __restri
   float* sc = g_att_lds;       // [S]
   float* sq = g_att_lds + S;   // [hs]
   const float scale = 1.f / sqrtf((float)hs);
-  for (int d = tid; d < hs; d += 256) sq[d] = bf2f(q[(size_t)m * C + h * hs + d]) * scale;
+  for (int d = tid; d < hs; d += 256) sq[d] = ldv(q, (size_t)m * C + h * hs + d) * scale;
   __syncthreads();
   const size_t kb = ((size_t)b * nh + h) * S * hs;
   float mx = -INFINITY;
   for (int j = tid; j < nvis; j += 256) {
-    const bf16_t* kr = kc + kb + (size_t)j * hs;
+    const TT* kr = kc + kb + (size_t)j * hs;
     float s = 0.f;
-    for (int d = 0; d < hs; ++d) s += sq[d] * bf2f(kr[d]);
+    for (int d = 0; d < hs; ++d) s += sq[d] * ldv(kr, d);
     sc[j] = s;
     mx = fmaxf(mx, s);
   }
@@ -148,17 +181,49 @@ __global__ __launch_bounds__(256) void g_attention_kernel(const bf16_t* __restri
   const float inv = 1.f / l;
   for (int d = tid; d < hs; d += 256) {
     float o = 0.f;
-    for (int j = 0; j < nvis; ++j) o += sc[j] * bf2f(vc[kb + (size_t)j * hs + d]);
-    y[(size_t)m * C + h * hs + d] = f2bf(o * inv);
+    for (int j = 0; j < nvis; ++j) o += sc[j] * ldv(vc, kb + (size_t)j * hs + d);
+    stv(y, (size_t)m * C + h * hs + d, o * inv);
   }
 }
 
-// ---- h = bf16(bf16(silu(a1)) * a2) (model.py:258-259 on bf16 tensors)
-__global__ __launch_bounds__(256) void g_silu_mul_kernel(const bf16_t* __restrict__ a1, const bf16_t* __restrict__ a2,
-                                                         bf16_t* __restrict__ h, size_t n) {
+// ---- h = silu(a1) * a2 (model.py:258-259; bf16: bf16(bf16(silu(a1)) * a2))
+template <typename T>
+__global__ __launch_bounds__(256) void g_silu_mul_kernel(const T* __restrict__ a1, const T* __restrict__ a2,
+                                                         T* __restrict__ h, size_t n) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-    const float a = bf2f(a1[i]);
-    h[i] = f2bf(round_bf(a / (1.f + __expf(-a))) * bf2f(a2[i]));
+    const float a = ldv(a1, i);
+    stv(h, i, rnd<T>(a / (1.f + expf(-a))) * ldv(a2, i));
+  }
+}
+
+// ---- greedy next token over fp32 logits (lowest index on ties), as llj_argmax for bf16 ones
+__global__ __launch_bounds__(1024) void g_argmax_kernel(const float* __restrict__ logits, int ldl, int V,
+                                                        int* __restrict__ out_idx, int* __restrict__ tokens_out,
+                                                        int tok_stride, const int* __restrict__ pos) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const float* lr = logits + (size_t)m * ldl;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int v = tid; v < V; v += 1024) {
+    const float x = lr[v];
+    if (x > best || (x == best && v < bi)) { best = x; bi = v; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  if ((tid & 63) == 0) { sv[tid >> 6] = best; si[tid >> 6] = bi; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 16; ++w)
+      if (sv[w] > best || (sv[w] == best && si[w] < bi)) { best = sv[w]; bi = si[w]; }
+    if (bi == 0x7fffffff) bi = 0;  // all-NaN row
+    out_idx[m] = bi;
+    if (tokens_out) tokens_out[(size_t)m * tok_stride + pos[0] + 1] = bi;
   }
 }
 
@@ -166,59 +231,94 @@ __global__ __launch_bounds__(256) void g_silu_mul_kernel(const bf16_t* __restric
 
 using namespace llj;
 
+#define LLJ_DT(dt, CALL_BF16, CALL_F32) \
+  do {                                 \
+    if ((dt) == 0) CALL_BF16;          \
+    else CALL_F32;                     \
+  } while (0)
+
 extern "C" {
 LLJ_TRACE_EXPORT(generic)
 
-int llj_g_rmsnorm(const void* x, int ldx, const void* w, float eps, void* y, int ldy, int M, int C, void* stream) {
-  LLJ_REQUIRE(x && w && y && M > 0 && C > 0 && ldx >= C && ldy >= C);
-  hipLaunchKernelGGL(g_rmsnorm_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, (const bf16_t*)w,
-                     eps, (bf16_t*)y, ldy, C);
+int llj_g_embedding(const int* idx, const void* wte, void* out, int M, int C, int* pos_inc, int dt, void* stream) {
+  LLJ_REQUIRE(idx && wte && out && M > 0 && C > 0 && (dt == 0 || dt == 1));
+  hipStream_t s = (hipStream_t)stream;
+  LLJ_DT(dt, hipLaunchKernelGGL(g_embedding_kernel<bf16_t>, dim3(M), dim3(256), 0, s, idx, (const bf16_t*)wte, (bf16_t*)out, C, pos_inc),
+         hipLaunchKernelGGL(g_embedding_kernel<float>, dim3(M), dim3(256), 0, s, idx, (const float*)wte, (float*)out, C, pos_inc));
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_g_rmsnorm(const void* x, int ldx, const void* w, float eps, void* y, int ldy, int M, int C, int dt, void* stream) {
+  LLJ_REQUIRE(x && w && y && M > 0 && C > 0 && ldx >= C && ldy >= C && (dt == 0 || dt == 1));
+  hipStream_t s = (hipStream_t)stream;
+  LLJ_DT(dt, hipLaunchKernelGGL(g_rmsnorm_kernel<bf16_t>, dim3(M), dim3(256), 0, s, (const bf16_t*)x, ldx, (const bf16_t*)w, eps, (bf16_t*)y, ldy, C),
+         hipLaunchKernelGGL(g_rmsnorm_kernel<float>, dim3(M), dim3(256), 0, s, (const float*)x, ldx, (const float*)w, eps, (float*)y, ldy, C));
   LLJ_CHECK_LAUNCH();
   return 0;
 }
 
 int llj_g_linear(int wkind, const void* x, int ldx, int M, int K, const void* W, const float* scales, const float* zeros,
-                 int bits, int group, int N, void* y, int ldy, const void* resid, int ldr, void* stream) {
-  LLJ_REQUIRE(x && W && y && M > 0 && K > 0 && N > 0 && ldx >= K && ldy >= N && (!resid || ldr >= N));
+                 int bits, int group, int N, void* y, int ldy, const void* resid, int ldr, int dt, void* stream) {
+  LLJ_REQUIRE(x && W && y && M > 0 && K > 0 && N > 0 && ldx >= K && ldy >= N && (!resid || ldr >= N) && (dt == 0 || dt == 1));
   LLJ_REQUIRE(wkind == 1 || (wkind == 0 && scales && zeros && (bits == 2 || bits == 4 || bits == 8) && group > 0 &&
                              K % (8 / bits) == 0));
   const dim3 grid((N + 3) / 4, (M + GL_ROWS - 1) / GL_ROWS);
-  if (wkind == 1)
-    hipLaunchKernelGGL(g_linear_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, M, K, W, scales,
-                       zeros, 16, K, N, (bf16_t*)y, ldy, (const bf16_t*)resid, ldr);
-  else
-    hipLaunchKernelGGL(g_linear_kernel<0>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, M, K, W, scales,
-                       zeros, bits, group, N, (bf16_t*)y, ldy, (const bf16_t*)resid, ldr);
+  hipStream_t s = (hipStream_t)stream;
+#define LLJ_GL(WK, T) \
+  hipLaunchKernelGGL((g_linear_kernel<WK, T>), grid, dim3(256), 0, s, (const T*)x, ldx, M, K, W, scales, zeros, \
+                     WK == 1 ? 16 : bits, WK == 1 ? K : group, N, (T*)y, ldy, (const T*)resid, ldr)
+  if (wkind == 1) LLJ_DT(dt, LLJ_GL(1, bf16_t), LLJ_GL(1, float));
+  else LLJ_DT(dt, LLJ_GL(0, bf16_t), LLJ_GL(0, float));
+#undef LLJ_GL
   LLJ_CHECK_LAUNCH();
   return 0;
 }
 
 int llj_g_rope_kv(const void* qkv, void* q_out, void* kcache, void* vcache, const float* rope, const int* pos, int B, int T,
-                  int C, int n_head, int S, void* stream) {
+                  int C, int n_head, int S, int dt, void* stream) {
   LLJ_REQUIRE(qkv && q_out && kcache && vcache && rope && pos && B > 0 && T > 0 && n_head > 0 && C % n_head == 0 &&
-              (C / n_head) % 2 == 0 && S > 0);
-  hipLaunchKernelGGL(g_rope_kv_kernel, dim3(B * T, n_head), dim3(64), 0, (hipStream_t)stream, (const bf16_t*)qkv,
-                     (bf16_t*)q_out, (bf16_t*)kcache, (bf16_t*)vcache, rope, pos, T, C, n_head, S);
+              (C / n_head) % 2 == 0 && S > 0 && (dt == 0 || dt == 1));
+  hipStream_t s = (hipStream_t)stream;
+  LLJ_DT(dt, hipLaunchKernelGGL(g_rope_kv_kernel<bf16_t>, dim3(B * T, n_head), dim3(64), 0, s, (const bf16_t*)qkv, (bf16_t*)q_out,
+                                (bf16_t*)kcache, (bf16_t*)vcache, rope, pos, T, C, n_head, S),
+         hipLaunchKernelGGL(g_rope_kv_kernel<float>, dim3(B * T, n_head), dim3(64), 0, s, (const float*)qkv, (float*)q_out,
+                            (float*)kcache, (float*)vcache, rope, pos, T, C, n_head, S));
   LLJ_CHECK_LAUNCH();
   return 0;
 }
 
 int llj_g_attention(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T, int C,
-                    int n_head, int S, void* stream) {
-  LLJ_REQUIRE(q && kcache && vcache && y && pos && B > 0 && T > 0 && n_head > 0 && C % n_head == 0 && S > 0);
+                    int n_head, int S, int dt, void* stream) {
+  LLJ_REQUIRE(q && kcache && vcache && y && pos && B > 0 && T > 0 && n_head > 0 && C % n_head == 0 && S > 0 &&
+              (dt == 0 || dt == 1));
   const size_t lds = (size_t)(S + C / n_head) * 4;
   LLJ_REQUIRE(lds <= 64 * 1024);
-  hipLaunchKernelGGL(g_attention_kernel, dim3(B * T, n_head), dim3(256), lds, (hipStream_t)stream, (const bf16_t*)q,
-                     (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, C, n_head, S);
+  hipStream_t s = (hipStream_t)stream;
+  LLJ_DT(dt, hipLaunchKernelGGL(g_attention_kernel<bf16_t>, dim3(B * T, n_head), dim3(256), lds, s, (const bf16_t*)q,
+                                (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, C, n_head, S),
+         hipLaunchKernelGGL(g_attention_kernel<float>, dim3(B * T, n_head), dim3(256), lds, s, (const float*)q,
+                            (const float*)kcache, (const float*)vcache, (float*)y, pos, T, C, n_head, S));
   LLJ_CHECK_LAUNCH();
   return 0;
 }
 
-int llj_g_silu_mul(const void* a1, const void* a2, void* h, size_t n, void* stream) {
-  LLJ_REQUIRE(a1 && a2 && h && n > 0);
+int llj_g_silu_mul(const void* a1, const void* a2, void* h, size_t n, int dt, void* stream) {
+  LLJ_REQUIRE(a1 && a2 && h && n > 0 && (dt == 0 || dt == 1));
   const size_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(g_silu_mul_kernel, dim3(blocks < 4096 ? (unsigned)blocks : 4096u), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)a1, (const bf16_t*)a2, (bf16_t*)h, n);
+  const unsigned g = blocks < 4096 ? (unsigned)blocks : 4096u;
+  hipStream_t s = (hipStream_t)stream;
+  LLJ_DT(dt, hipLaunchKernelGGL(g_silu_mul_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)a1, (const bf16_t*)a2, (bf16_t*)h, n),
+         hipLaunchKernelGGL(g_silu_mul_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)a1, (const float*)a2, (float*)h, n));
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_g_argmax(const float* logits, int ldl, int M, int V, int* out_idx, int* tokens_out, int tok_stride, const int* pos,
+                 void* stream) {
+  LLJ_REQUIRE(logits && out_idx && M > 0 && V > 0 && ldl >= V && (!tokens_out || pos));
+  hipLaunchKernelGGL(g_argmax_kernel, dim3(M), dim3(1024), 0, (hipStream_t)stream, logits, ldl, V, out_idx, tokens_out,
+                     tok_stride, pos);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

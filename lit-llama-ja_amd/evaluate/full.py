@@ -46,14 +46,18 @@ def perplexity(model: LLaMA, encoded_text: torch.Tensor, window: int = WINDOW):
 
 def main(text_path: str, *, checkpoint_path: Optional[Path] = None,
          tokenizer_path: Path = Path("checkpoints/lit-llama/tokenizer.model"), model_size: str = "7B",
-         quantize: Optional[str] = None) -> dict:
-    """reference evaluate/full.py:46-140 (same flags; dtype is the kernels' bfloat16)."""
+         dtype: str = "float32", quantize: Optional[str] = None) -> dict:
+    """reference evaluate/full.py:46-140 (same flags, dtype default float32 as there: an fp32 model
+    runs every op on the any-shape kernels in fp32; bfloat16 takes the fused MFMA prefill path)."""
     from quantize.gptq import tokenizer_for
 
+    dt = getattr(torch, dtype, None)
+    if not isinstance(dt, torch.dtype):  # reference evaluate/full.py:78-81
+        raise ValueError(f"{dtype} is not a valid dtype.")
     if not checkpoint_path:
         checkpoint_path = Path(f"checkpoints/lit-llama/{model_size}/lit-llama.pth")
     assert checkpoint_path.is_file() and tokenizer_path.is_file()
-    with EmptyInitOnDevice(device=torch.device("cuda"), dtype=torch.bfloat16, quantization_mode=quantize):
+    with EmptyInitOnDevice(device=torch.device("cuda"), dtype=dt, quantization_mode=quantize):
         print("Loading model ...", file=sys.stderr)
         t0 = time.time()
         model = LLaMA.from_name(model_size)
@@ -82,7 +86,8 @@ if __name__ == "__main__":
     ap.add_argument("--checkpoint_path", type=Path, default=None)
     ap.add_argument("--tokenizer_path", type=Path, default=Path("checkpoints/lit-llama/tokenizer.model"))
     ap.add_argument("--model_size", default="7B")
+    ap.add_argument("--dtype", default="float32")
     ap.add_argument("--quantize", default=None, choices=[None, "llm.int8", "gptq.int4", "gptq.int8"])
     a = ap.parse_args()
     main(a.text_path, checkpoint_path=a.checkpoint_path, tokenizer_path=a.tokenizer_path, model_size=a.model_size,
-         quantize=a.quantize)
+         dtype=a.dtype, quantize=a.quantize)

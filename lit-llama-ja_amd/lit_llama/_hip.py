@@ -65,11 +65,13 @@ SIGNATURES = {
     "llj_engine_step": [_P, _P],
     "llj_engine_ring_blocks": [_I, _I, _I],
     "llj_stream_read": [_P, ctypes.c_size_t, _P, _I, _P],
-    "llj_g_rmsnorm": [_P, _I, _P, _F, _P, _I, _I, _I, _P],
-    "llj_g_linear": [_I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _I, _P],
-    "llj_g_rope_kv": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
-    "llj_g_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
-    "llj_g_silu_mul": [_P, _P, _P, ctypes.c_size_t, _P],
+    "llj_g_embedding": [_P, _P, _P, _I, _I, _P, _I, _P],
+    "llj_g_rmsnorm": [_P, _I, _P, _F, _P, _I, _I, _I, _I, _P],
+    "llj_g_linear": [_I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _I, _I, _P],
+    "llj_g_rope_kv": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "llj_g_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "llj_g_silu_mul": [_P, _P, _P, ctypes.c_size_t, _I, _P],
+    "llj_g_argmax": [_P, _I, _I, _I, _P, _P, _I, _P, _P],
 }
 
 _lib = None

@@ -56,6 +56,8 @@ def engine_supported(model: LLaMA, specs, batch: int, S: int) -> str | None:
         return "disabled (LLJ_ENGINE=0)"
     cfg = model.config
     hs = cfg.n_embd // cfg.n_head
+    if model._generic():
+        return "any-shape / fp32 path"
     if batch != 1:
         return "batch > 1"
     if S > ENGINE_MAX_S:
@@ -180,7 +182,7 @@ class DecodeSession:
         self.cur = torch.zeros(batch, dtype=torch.int32, device=dev)
         self.pos = torch.zeros(1, dtype=torch.int32, device=dev)
         self.tokens = torch.zeros(batch, total_len, dtype=torch.int32, device=dev)
-        self.logits = torch.empty(batch, cfg.padded_vocab_size, dtype=torch.bfloat16, device=dev)
+        self.logits = torch.empty(batch, cfg.padded_vocab_size, dtype=model.act_dtype(), device=dev)
         self.use_graph = use_graph
         self.graph = None
         self.t_prompt = 0
@@ -199,7 +201,12 @@ class DecodeSession:
     def _choose(self, st):
         """next token of every row from self.logits -> cur and tokens[:, pos + 1]"""
         cfg = self.model.config
-        if self.top_k == 1:
+        if self.logits.dtype == torch.float32:  # the fp32 model (any-shape path): greedy only
+            if self.top_k != 1:
+                raise NotImplementedError("sampling (top_k != 1) over float32 logits: use a bfloat16 model")
+            _hip.call("llj_g_argmax", self.logits.data_ptr(), self.logits.stride(0), self.B, cfg.padded_vocab_size,
+                      self.cur.data_ptr(), self.tokens.data_ptr(), self.total, self.pos.data_ptr(), st)
+        elif self.top_k == 1:
             _hip.call("llj_argmax", self.logits.data_ptr(), self.logits.stride(0), self.B, cfg.padded_vocab_size,
                       self.cur.data_ptr(), self.tokens.data_ptr(), self.total, self.pos.data_ptr(), st)
         else:
@@ -228,7 +235,7 @@ class DecodeSession:
         # decode-step operands (fixed for the session)
         self.specs = m._layer_specs()
         if m._generic():  # the any-shape kernels (csrc/generic.hip)
-            self.work = _Work(m.config, B, self.dev, False, self.S, generic=True)
+            self.work = _Work(m.config, B, self.dev, False, self.S, generic=True, dtype=m.act_dtype())
         else:
             need_i8 = any(s[0] == 2 for layer in self.specs["layers"] for s in layer) or self.specs["head"][0] == 2
             self.work = _Work(m.config, B, self.dev, need_i8, self.S)
@@ -248,8 +255,12 @@ class DecodeSession:
                           self.temperature, self.top_k, _hip.ptr(self.uniforms), self.seed, self.cur.data_ptr(),
                           self.tokens.data_ptr(), self.total, self.pos.data_ptr(), st)
             return
-        _hip.call("llj_embedding", self.cur.data_ptr(), m.transformer.wte.weight.data_ptr(), w.x.data_ptr(), B,
-                  cfg.n_embd, self.pos.data_ptr(), st)
+        if w.generic:
+            _hip.call("llj_g_embedding", self.cur.data_ptr(), m.transformer.wte.weight.data_ptr(), w.x.data_ptr(), B,
+                      cfg.n_embd, self.pos.data_ptr(), w.dt, st)
+        else:
+            _hip.call("llj_embedding", self.cur.data_ptr(), m.transformer.wte.weight.data_ptr(), w.x.data_ptr(), B,
+                      cfg.n_embd, self.pos.data_ptr(), st)
         m._blocks(w, self.specs, m.kv_caches, self.pos, B, 1, self.S, st)
         m._head(w.x, B, self.specs, self.logits, st, w)
         self._choose(st)

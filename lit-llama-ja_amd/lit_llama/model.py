@@ -17,8 +17,9 @@ position p is stored in slot p % S, which holds the same key set as the referenc
 roll-by-one sliding window (model.py:221-227); `kv_caches` therefore equals the reference's
 caches up to a rotation of the slot axis once more than S tokens were seen.
 
-The model must live on a ROCm GPU in bfloat16 (the reference's GPU precision, generate.py:121);
-there is no CPU path.
+The model must live on a ROCm GPU, in bfloat16 (the reference's GPU precision, generate.py:121) or
+in float32 (the reference's CPU / evaluate/full.py default precision: every op then runs on the
+any-shape kernels in fp32); there is no CPU path.
 """
 from __future__ import annotations
 
@@ -166,6 +167,15 @@ I8_NORM_STATS_MAX_M = 16
 _ROWSUM_FMTS = (0, 3)
 
 
+def _dt_code(dtype) -> int:
+    """dt argument of the any-shape kernels: 0 bf16, 1 fp32."""
+    if dtype == torch.bfloat16:
+        return 0
+    if dtype == torch.float32:
+        return 1
+    raise TypeError(f"activations must be bfloat16 or float32, got {dtype}")
+
+
 def _wspec(lin: nn.Module):
     """(wfmt, weight operand, scale operand) of a Linear for the HIP kernels."""
     if hasattr(lin, "_wspec"):
@@ -184,14 +194,15 @@ def _wspec(lin: nn.Module):
 
 def _gspec(lin: nn.Module):
     """Operands of a Linear for the any-shape kernel llj_g_linear: (wkind, W, scales, zeros, bits,
-    group) -- wkind 1 dense bf16, 0 ColBlockQuantizedLinear on its reference buffers."""
+    group) -- wkind 1 dense (bf16 or fp32, the activation type), 0 ColBlockQuantizedLinear on its
+    reference buffers."""
     if hasattr(lin, "_gspec"):
         return lin._gspec()
     if isinstance(lin, nn.Linear):
         w = lin.weight
         _hip.require_device(w, "Linear.weight")
-        if w.dtype != torch.bfloat16 or not w.is_contiguous():
-            raise TypeError("dense Linear weights must be contiguous bfloat16 on the GPU")
+        if w.dtype not in (torch.bfloat16, torch.float32) or not w.is_contiguous():
+            raise TypeError("dense Linear weights must be contiguous bfloat16 or float32 on the GPU")
         if lin.bias is not None:
             raise NotImplementedError("biased dense Linear is not on the LLaMA path")
         return 1, w, None, None, 16, w.shape[1]
@@ -203,11 +214,13 @@ class _Work:
     """Per-call scratch for M rows (allocated from torch's caching allocator)."""
 
     def __init__(self, cfg: LLaMAConfig, M: int, device, need_i8: bool, S: int = 0, gemm: bool = False,
-                 generic: bool = False):
+                 generic: bool = False, dtype=torch.bfloat16):
         C, H = cfg.n_embd, MLP.hidden(cfg)
         bf = torch.bfloat16
         self.generic = generic  # the any-shape kernels (LLaMA._blocks_generic)
+        self.dt = _dt_code(dtype)
         if generic:
+            bf = dtype  # fp32 models run here with fp32 activations
             self.x = torch.empty(M, C, dtype=bf, device=device)
             self.xn = torch.empty(M, C, dtype=bf, device=device)
             self.qkv = torch.empty(M, 3 * C, dtype=bf, device=device)
@@ -337,16 +350,24 @@ class LLaMA(nn.Module):
     def _alloc_kv(self, B, S, device, n=None):
         hs = self.config.n_embd // self.config.n_head
         shape = (B, self.config.n_head, S, hs)
-        return [(torch.zeros(shape, device=device, dtype=torch.bfloat16),
-                 torch.zeros(shape, device=device, dtype=torch.bfloat16))
+        dt = self.act_dtype()  # the reference's cache dtype is the activation dtype (model.py:117-120)
+        return [(torch.zeros(shape, device=device, dtype=dt), torch.zeros(shape, device=device, dtype=dt))
                 for _ in range(self.config.n_layer if n is None else n)]
+
+    def act_dtype(self) -> torch.dtype:
+        """The activation dtype: the embedding's (bf16 or fp32)."""
+        return self.transformer.wte.weight.dtype
 
     def _check_dtype(self):
         wte = self.transformer.wte.weight
         _hip.require_device(wte, "LLaMA parameters")
-        if wte.dtype != torch.bfloat16:
-            raise TypeError("the MI355X path computes in bfloat16: build the model under "
+        if wte.dtype not in (torch.bfloat16, torch.float32):
+            raise TypeError("the MI355X path computes in bfloat16 or float32: build the model under "
                             "EmptyInitOnDevice(device='cuda', dtype=torch.bfloat16) or call model.to(torch.bfloat16)")
+        if wte.dtype == torch.float32:  # the fp32 model: every norm / dense weight fp32 as well
+            for n, prm in self.named_parameters():
+                if prm.dtype != torch.float32:
+                    raise TypeError(f"float32 model with a {prm.dtype} parameter {n}")
 
     def _run(self, idx, pos, S, kv, all_rows=True, last_only_out=None):
         """Embedding -> n_layer blocks -> ln_f -> lm_head for B*T rows; returns (B, T, V)
@@ -357,15 +378,19 @@ class LLaMA(nn.Module):
         dev = idx.device
         specs = self._layer_specs()
         if self._generic():
-            w = _Work(cfg, M, dev, False, S, generic=True)
+            w = _Work(cfg, M, dev, False, S, generic=True, dtype=self.act_dtype())
         else:
             need_i8 = any(s[0] == 2 for layer in specs["layers"] for s in layer) or specs["head"][0] == 2
             w = _Work(cfg, M, dev, need_i8, S, gemm=self._gemm_ok(specs, M))
             w.flash = self._flash_ok(pos, T, S)
         st = _hip.stream()
         ids = idx.reshape(-1).to(torch.int32)
-        _hip.call("llj_embedding", ids.data_ptr(), self.transformer.wte.weight.data_ptr(), w.x.data_ptr(), M,
-                  cfg.n_embd, None, st)
+        if w.generic:
+            _hip.call("llj_g_embedding", ids.data_ptr(), self.transformer.wte.weight.data_ptr(), w.x.data_ptr(), M,
+                      cfg.n_embd, None, w.dt, st)
+        else:
+            _hip.call("llj_embedding", ids.data_ptr(), self.transformer.wte.weight.data_ptr(), w.x.data_ptr(), M,
+                      cfg.n_embd, None, st)
         self._blocks(w, specs, kv, pos, B, T, S, st)
         V = cfg.padded_vocab_size
         if last_only_out is not None:
@@ -375,13 +400,14 @@ class LLaMA(nn.Module):
                 rows = w.x.view(B, T, -1)[:, -1].contiguous()
                 self._head(rows, B, specs, last_only_out, st, w)
             return last_only_out
-        logits = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
+        logits = torch.empty(M, V, dtype=self.act_dtype(), device=dev)
         self._head(w.x, M, specs, logits, st, w)
         return logits.view(B, T, V)
 
     def _generic(self) -> bool:
-        """True when this configuration runs on the any-shape kernels (kernel_support)."""
-        return self.config.kernel_support() is not None
+        """True when this model runs on the any-shape kernels: a configuration outside the
+        streaming tiling (kernel_support), or fp32 activations."""
+        return self.config.kernel_support() is not None or self.act_dtype() == torch.float32
 
     # -- weight operands, gathered once per call
     def _layer_specs(self):
@@ -520,9 +546,11 @@ class LLaMA(nn.Module):
     @staticmethod
     def _glinear(spec, A, M, K, N, out, resid, st):
         kind, W, sc, zr, bits, group = spec
+        if kind == 1 and W.dtype != A.dtype:
+            raise TypeError(f"dense Linear weight {W.dtype} with {A.dtype} activations")
         _hip.call("llj_g_linear", kind, A.data_ptr(), A.stride(0), M, K, W.data_ptr(), _hip.ptr(sc), _hip.ptr(zr), bits,
                   group, N, out.data_ptr(), out.stride(0), None if resid is None else resid.data_ptr(),
-                  0 if resid is None else resid.stride(0), st)
+                  0 if resid is None else resid.stride(0), _dt_code(A.dtype), st)
 
     def _blocks_generic(self, w, specs, kv, pos, B, T, S, st):
         """The blocks on the any-shape kernels (csrc/generic.hip), per layer (model.py:162-175):
@@ -535,18 +563,18 @@ class LLaMA(nn.Module):
             sa, sp, s1, s2, sd = specs["layers"][i]
             kc, vc = kv[i]
             _hip.call("llj_g_rmsnorm", w.x.data_ptr(), C, blk.rms_1.scale.data_ptr(), blk.rms_1.eps, w.xn.data_ptr(), C,
-                      M, C, st)
+                      M, C, w.dt, st)
             self._glinear(sa, w.xn, M, C, 3 * C, w.qkv, None, st)
             _hip.call("llj_g_rope_kv", w.qkv.data_ptr(), w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(),
-                      self.rope_cache.data_ptr(), pos.data_ptr(), B, T, C, nh, S, st)
+                      self.rope_cache.data_ptr(), pos.data_ptr(), B, T, C, nh, S, w.dt, st)
             _hip.call("llj_g_attention", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(), pos.data_ptr(),
-                      B, T, C, nh, S, st)
+                      B, T, C, nh, S, w.dt, st)
             self._glinear(sp, w.y, M, C, C, w.x, w.x, st)
             _hip.call("llj_g_rmsnorm", w.x.data_ptr(), C, blk.rms_2.scale.data_ptr(), blk.rms_2.eps, w.xn.data_ptr(), C,
-                      M, C, st)
+                      M, C, w.dt, st)
             self._glinear(s1, w.xn, M, C, H, w.a1, None, st)
             self._glinear(s2, w.xn, M, C, H, w.a2, None, st)
-            _hip.call("llj_g_silu_mul", w.a1.data_ptr(), w.a2.data_ptr(), w.h.data_ptr(), M * H, st)
+            _hip.call("llj_g_silu_mul", w.a1.data_ptr(), w.a2.data_ptr(), w.h.data_ptr(), M * H, w.dt, st)
             self._glinear(sd, w.h, M, H, C, w.x, w.x, st)
 
     def _blocks(self, w, specs, kv, pos, B, T, S, st):
@@ -645,7 +673,8 @@ class LLaMA(nn.Module):
         ln = self.transformer.ln_f
         if w.generic:  # ln_f + lm_head on the any-shape kernels
             xn = w.xn if M <= w.xn.shape[0] else torch.empty_like(x)
-            _hip.call("llj_g_rmsnorm", x.data_ptr(), x.stride(0), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), C, M, C, st)
+            _hip.call("llj_g_rmsnorm", x.data_ptr(), x.stride(0), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), C, M, C,
+                      w.dt, st)
             self._glinear(specs["head"], xn, M, C, V, out, None, st)
             return
         f, W, sz = specs["head"]
@@ -726,16 +755,16 @@ class _BlockHost:
         B, T, C = x.shape
         M = B * T
         mods = (blk.attn.c_attn, blk.attn.c_proj, blk.mlp.c_fc1, blk.mlp.c_fc2, blk.mlp.c_proj)
-        if cfg.kernel_support() is not None:  # the any-shape kernels
+        if cfg.kernel_support() is not None or x.dtype == torch.float32:  # the any-shape kernels
             specs = {"layers": [tuple(_gspec(m) for m in mods)]}
-            w = _Work(cfg, M, x.device, False, generic=True)
+            w = _Work(cfg, M, x.device, False, generic=True, dtype=x.dtype)
         else:
             specs = {"layers": [tuple(_wspec(m) for m in mods)]}
             need_i8 = any(s[0] == 2 for s in specs["layers"][0])
             w = _Work(cfg, M, x.device, need_i8)
         w.x.copy_(x.reshape(M, C))
-        kv = [(torch.zeros(B, cfg.n_head, T, C // cfg.n_head, dtype=torch.bfloat16, device=x.device),
-               torch.zeros(B, cfg.n_head, T, C // cfg.n_head, dtype=torch.bfloat16, device=x.device))]
+        kv = [(torch.zeros(B, cfg.n_head, T, C // cfg.n_head, dtype=w.x.dtype, device=x.device),
+               torch.zeros(B, cfg.n_head, T, C // cfg.n_head, dtype=w.x.dtype, device=x.device))]
         pos = torch.arange(T, device=x.device, dtype=torch.int32)
         shim = _OneBlock(blk, rope.float().contiguous(), cfg)
         LLaMA._blocks(shim, w, specs, kv, pos, B, T, T, _hip.stream())
@@ -802,6 +831,16 @@ class MLP(nn.Module):
         x2 = x.reshape(-1, K).contiguous()
         M = x2.shape[0]
         H = self.c_fc1.out_features
+        if x.dtype == torch.float32 or K % 128:  # fp32 / any-shape: the generic kernels
+            st = _hip.stream()
+            a1 = torch.empty(M, H, dtype=x.dtype, device=x.device)
+            a2 = torch.empty_like(a1)
+            out = torch.empty(M, self.c_proj.out_features, dtype=x.dtype, device=x.device)
+            LLaMA._glinear(_gspec(self.c_fc1), x2, M, K, H, a1, None, st)
+            LLaMA._glinear(_gspec(self.c_fc2), x2, M, K, H, a2, None, st)
+            _hip.call("llj_g_silu_mul", a1.data_ptr(), a2.data_ptr(), a1.data_ptr(), M * H, _dt_code(x.dtype), st)
+            LLaMA._glinear(_gspec(self.c_proj), a1, M, H, self.c_proj.out_features, out, None, st)
+            return out.view(*x.shape[:-1], out.shape[1])
         (f1, w1, s1), (f2, w2, s2), (fd, wd, sd) = _wspec(self.c_fc1), _wspec(self.c_fc2), _wspec(self.c_proj)
         if f1 != f2:
             raise TypeError("c_fc1 and c_fc2 must share a weight format")
@@ -841,11 +880,15 @@ class RMSNorm(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         _hip.require_device(x, "x")
-        if x.dtype != torch.bfloat16 or self.scale.dtype != torch.bfloat16 or self.dim not in (-1, x.dim() - 1):
-            raise TypeError("RMSNorm HIP path: bfloat16 input/scale over the last dim")
+        if x.dtype not in (torch.bfloat16, torch.float32) or self.scale.dtype != x.dtype or self.dim not in (-1, x.dim() - 1):
+            raise TypeError("RMSNorm HIP path: bfloat16 (or float32) input and scale over the last dim")
         C = x.shape[-1]
         x2 = x.reshape(-1, C).contiguous()
         y = torch.empty_like(x2)
+        if x.dtype == torch.float32:
+            _hip.call("llj_g_rmsnorm", x2.data_ptr(), C, self.scale.data_ptr(), self.eps, y.data_ptr(), C, x2.shape[0], C,
+                      1, _hip.stream())
+            return y.view_as(x)
         _hip.call("llj_rmsnorm", x2.data_ptr(), self.scale.data_ptr(), self.eps, y.data_ptr(), x2.shape[0], C,
                   _hip.stream())
         return y.view_as(x)

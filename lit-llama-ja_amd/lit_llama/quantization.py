@@ -214,17 +214,17 @@ class ColBlockQuantizedLinear(torch.nn.Module):
 
     def forward(self, inp):
         _hip.require_device(inp, "input")
-        if inp.dtype != torch.bfloat16:
-            raise TypeError(f"ColBlockQuantizedLinear HIP path computes in bfloat16, got {inp.dtype}")
+        if inp.dtype not in (torch.bfloat16, torch.float32):
+            raise TypeError(f"ColBlockQuantizedLinear HIP path computes in bfloat16 or float32, got {inp.dtype}")
         K, N = self.in_features, self.out_features
-        if not self._supported():  # the any-shape kernel on the reference buffers
+        if not self._supported() or inp.dtype == torch.float32:  # the any-shape kernel on the reference buffers
             if self.bias is not None:
-                raise NotImplementedError("biased ColBlockQuantizedLinear outside the streaming tiling")
+                raise NotImplementedError("biased ColBlockQuantizedLinear on the any-shape / fp32 path")
             x2 = inp.reshape(-1, K).contiguous()
             out = torch.empty((x2.shape[0], N), dtype=inp.dtype, device=inp.device)
             kind, qw, sc, zr, bits, group = self._gspec()
             _hip.call("llj_g_linear", kind, x2.data_ptr(), K, x2.shape[0], K, qw.data_ptr(), sc.data_ptr(), zr.data_ptr(),
-                      bits, group, N, out.data_ptr(), N, None, 0, _hip.stream())
+                      bits, group, N, out.data_ptr(), N, None, 0, 0 if inp.dtype == torch.bfloat16 else 1, _hip.stream())
             return out.reshape(*inp.shape[:-1], N)
         self._prepare()
         x2 = _as_rows(inp, K)

@@ -151,9 +151,12 @@ def int8_linear(x: np.ndarray, cb: np.ndarray, scb: np.ndarray, threshold: float
     reference quantization.py:45), restated:
       A16 = A.half(); outlier columns = {k : any row |A16[m,k]| >= threshold}
       SCA[m] = absmax over the row's non-outlier elements; CA = round(A16*127/SCA), with
-      outlier columns zeroed; out = (CA @ CB^T)_int32 * SCA*SCB/127^2
-      + A16[:, outl] @ (CB[:, outl]*SCB/127)^T   (fp16 side product, fp32-accumulated here).
-    Returns fp32 (the caller casts back to the activation dtype)."""
+      outlier columns zeroed; out = f16(f16((CA @ CB^T)_int32 * SCA*SCB/127^2)
+      + A16[:, outl] @ f16(CB[:, outl]*SCB/127)^T)   (mm_dequant writes fp16; the fp16 side product
+      is fp32-accumulated and added to it in one fp16 rounding -- the rounding points of the decode /
+      prefill kernels, csrc/gemv_impl.h mm_dequant epilogue; bitsandbytes is unpinned, so which fp16
+      points its own MatMul8bitLt used cannot be checked here).
+    Returns fp32 holding fp16 values (the caller casts back to the activation dtype)."""
     A = x.astype(F32).reshape(-1, x.shape[-1])
     a16 = A.astype(np.float16).astype(F32)
     big = np.abs(a16) >= threshold
@@ -165,10 +168,11 @@ def int8_linear(x: np.ndarray, cb: np.ndarray, scb: np.ndarray, threshold: float
     ca[:, outl] = 0
     # int32-range accumulation, exact in float64 (|sum| <= 127^2 * K < 2^53) and BLAS-fast
     acc = ca.astype(np.float64) @ cb.astype(np.float64).T
-    out = acc.astype(F32) * (sca[:, None] * scb[None, :] / F32(127.0 * 127.0))
+    out = (acc.astype(F32) * (sca[:, None] * scb[None, :] / F32(127.0 * 127.0))).astype(np.float16).astype(F32)
     if outl.size:
         wsub = (cb[:, outl].astype(F32) * (scb[:, None] / F32(127.0))).astype(np.float16).astype(F32)
-        out = out + a16[:, outl] @ wsub.T
+        out = (out + a16[:, outl] @ wsub.T).astype(F32)
+    out = out.astype(np.float16).astype(F32)
     return out.reshape(*x.shape[:-1], cb.shape[0]).astype(F32)
 
 

@@ -22,5 +22,7 @@ for v in "48 0" "96 96" "96 160"; do
   echo "pmc $v rc=$?" >> $O/status.log
 done
 cd $R
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "gemm_i8" -x -q --timeout 120 --timeout-method thread > $O/t_i8.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "i8 or int8" -q --timeout 120 --timeout-method thread > $O/t_i8.log 2>&1
 echo "i8 tests rc=$?" >> $O/status.log
+timeout -k 10 300 python -u -m pytest tests/test_model_7b_gpu.py -k "int8" -s -q --timeout 200 --timeout-method thread > $O/t_7b_i8.log 2>&1
+echo "7b i8 tests rc=$?" >> $O/status.log

@@ -12,8 +12,14 @@ Orders compared, per Linear y = x W^T (W dequantized for gptq.int4):
 and the fp32 mean of every bf16 RMSNorm (model.py:281) taken in the same order. LLM.int8's int32
 GEMM is exact in every order; its dequantization product SCA * SCB / 127^2 * acc (float64 / another
 association) and its fp16 outlier side product take the alternative orders.
+  gpu    (round 4) the base Linears with the decode kernels' own formulas for everything else: RoPE
+         as fma(x0, cos, -(x1 sin)) (one rounding), attention scores on q pre-scaled by
+         log2(e) / sqrt(hs) with exp2 and the 1 / sum applied after P.V, SiLU as
+         x / (1 + exp2(-x log2(e))) -- another valid fp32 evaluation of model.py:237, 258, 312-329.
+         Its bf16 flips are what reach LLM.int8's per-row int8 codes (a Linear-order change barely
+         moves an int8 model: its GEMM is exact), so it is the variant that prices that mode.
 
-Usage: python tools/noise_floor.py [--out profiles/r03_noise_floor.json]  (CPU, a few minutes)
+Usage: python tools/noise_floor.py [--out profiles/r04_noise_floor.json] [--batches 1,8]  (CPU, ~10 minutes)
        python tools/noise_floor.py --generic [--out profiles/r03_noise_floor_generic.json]
          the any-shape configs of tests/test_generic_gpu.py (reference test n_embd 32 x 16 layers,
          3 x 64 rows no-cache; 125M prompt rows + decode steps, bf16 and gptq.int4)
@@ -79,9 +85,11 @@ class AltLinear:
             out = (acc * (sca[:, None].astype(np.float64) * s.scb[None, :] / (127.0 * 127.0))).astype(F32)
         else:  # the same product associated as (acc * SCA) * (SCB / 127^2)
             out = ((acc.astype(F32) * sca[:, None]) * (s.scb[None, :] / F32(127.0 * 127.0))).astype(F32)
+        out = out.astype(np.float16).astype(F32)  # mm_dequant's fp16 output (oracle.int8_linear)
         if outl.size:
             wsub = (s.cb[:, outl].astype(F32) * (s.scb[:, None] / F32(127.0))).astype(np.float16).astype(F32)
             out = out + (a16[:, outl].astype(np.float64) @ wsub.T.astype(np.float64)).astype(F32)
+        out = out.astype(np.float16).astype(F32)
         return out.reshape(*x.shape[:-1], s.cb.shape[0]).astype(F32)
 
 
@@ -111,10 +119,75 @@ class AltOracle(O.OracleLLaMA):
         return r16(r16(scale.astype(F32)) * r16(x * r))
 
 
+class GpuFormulaOracle(O.OracleLLaMA):
+    """The oracle with the decode kernels' formulas for RoPE, softmax and SiLU (Linears as base)."""
+
+    LOG2E = F32(1.4426950408889634)
+
+    @staticmethod
+    def _rope(x, rope):
+        B, T, nh, hs = x.shape
+        xs = x.astype(np.float64).reshape(B, T, nh, hs // 2, 2)
+        r = rope[:T].reshape(1, T, 1, hs // 2, 2).astype(np.float64)
+        # fma(x0, c, -(x1 s)): the product x1 s rounded to fp32, the rest in one rounding
+        t0 = (xs[..., 1] * r[..., 1]).astype(F32).astype(np.float64)
+        t1 = (xs[..., 0] * r[..., 1]).astype(F32).astype(np.float64)
+        o0 = (xs[..., 0] * r[..., 0] - t0).astype(F32)
+        o1 = (xs[..., 1] * r[..., 0] + t1).astype(F32)
+        return np.stack([o0, o1], -1).reshape(B, T, nh, hs).astype(F32)
+
+    def _block(self, i, x, rope, mask, S, input_pos):
+        cfg, p, pre = self.cfg, self.p, f"transformer.h.{i}."
+        B, T, C = x.shape
+        nh, hs = cfg.n_head, cfg.head_size
+        h = self._norm(x, p[pre + "rms_1.scale"])
+        qkv = self._r(self.lin[pre + "attn.c_attn"](h))
+        q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+        q = self._r(self._rope(q.reshape(B, T, nh, hs), rope)).transpose(0, 2, 1, 3)
+        k = self._r(self._rope(k.reshape(B, T, nh, hs), rope)).transpose(0, 2, 1, 3)
+        v = v.reshape(B, T, nh, hs).transpose(0, 2, 1, 3)
+        if input_pos is not None:
+            ck, cv = self.kv[i]
+            pos = input_pos
+            if pos[-1] >= S:
+                pos = np.array([S - 1])
+                ck = np.roll(ck, -1, axis=2)
+                cv = np.roll(cv, -1, axis=2)
+            ck = ck.copy(); cv = cv.copy()
+            ck[:, :, pos] = k
+            cv[:, :, pos] = v
+            self.kv[i] = [ck, cv]
+            k, v = ck, cv
+        qs = (q * (self.LOG2E / F32(np.sqrt(F32(hs))))).astype(F32)
+        att = (qs @ k.transpose(0, 1, 3, 2)).astype(F32)
+        att = np.where(mask[None, None], att, -np.inf)
+        e = np.exp2((att - att.max(-1, keepdims=True)).astype(F32)).astype(F32)
+        y = ((e @ v).astype(F32) / e.sum(-1, keepdims=True, dtype=F32)).astype(F32)
+        y = self._r(y.transpose(0, 2, 1, 3).reshape(B, T, C))
+        x = self._r(x + self._r(self.lin[pre + "attn.c_proj"](y)))
+        h = self._norm(x, p[pre + "rms_2.scale"])
+        a1 = self._r(self.lin[pre + "mlp.c_fc1"](h))
+        a2 = self._r(self.lin[pre + "mlp.c_fc2"](h))
+        sl = (a1 / (F32(1.0) + np.exp2((-a1 * self.LOG2E).astype(F32)))).astype(F32)
+        m = self._r(self._r(sl) * a2)
+        return self._r(x + self._r(self.lin[pre + "mlp.c_proj"](m)))
+
+
 def orc_variant(cfg, pb, lin, order):
     if order == "base":
         return O.OracleLLaMA(cfg, pb, linears=lin, act_bf16=True)
+    if order == "gpu":
+        return GpuFormulaOracle(cfg, pb, linears=lin, act_bf16=True)
     return AltOracle(cfg, pb, lin, order)
+
+
+ORDERS = ("base", "f64", "chunk", "gpu")
+
+
+def pair_rels(outs):
+    """rel L2 of every pair of variants, per (row, step)"""
+    keys = list(outs)
+    return {f"rel_{a}_vs_{b}": rels(outs[a], outs[b]) for i, a in enumerate(keys) for b in keys[i + 1:]}
 
 
 def rels(a, b):
@@ -158,6 +231,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--widths", default="4096,5120")
+    ap.add_argument("--batches", default="1,8")
+    ap.add_argument("--modes", default=None, help="comma list of gptq.int4, bf16, llm.int8 (default: all)")
     ap.add_argument("--generic", action="store_true")
     args = ap.parse_args()
     res = {"what": __doc__.split("\n\n")[0], "cases": []}
@@ -167,29 +242,33 @@ def main():
         Path(out).write_text(json.dumps(res, indent=1))
         print(f"wrote {out}")
         return
-    args.out = args.out or str(REPO / "profiles" / "r03_noise_floor.json")
+    args.out = args.out or str(REPO / "profiles" / "r04_noise_floor.json")
+    batches = [int(b) for b in args.batches.split(",")]
     for width in [int(w) for w in args.widths.split(",")]:
         cfg = T.C7 if width == 4096 else T.C13
         p = T.make_params(cfg, T.SEEDS[width])
         modes = ["gptq.int4", None, "llm.int8"] if width == 4096 else ["gptq.int4"]
+        if args.modes:
+            modes = [None if m == "bf16" else m for m in args.modes.split(",") if (m == "bf16" and None in modes) or m in modes]
         for mode in modes:
             pb, _, lin = T.oracle_linears(p, mode)
-            rng_seed = (1 + 17) if width == 4096 else (1 + 31)  # the tests' B = 1 ids
-            ids = np.random.default_rng(rng_seed).integers(3, cfg.vocab_size, (1, T.T_PROMPT + T.STEPS + 1))
-            outs = {}
-            for order in ("base", "f64", "chunk"):
-                t0 = time.time()
-                outs[order] = T._oracle_steps(orc_variant(cfg, pb, lin, order), ids)
-                print(f"[noise] width {width} {mode} {order}: {time.time() - t0:.1f} s", flush=True)
-            case = {"width": width, "mode": str(mode), "batch": 1, "steps": T.STEPS + 1,
-                    "rel_base_vs_f64": rels(outs["base"], outs["f64"]),
-                    "rel_base_vs_chunk": rels(outs["base"], outs["chunk"]),
-                    "rel_f64_vs_chunk": rels(outs["f64"], outs["chunk"])}
-            case["floor_max"] = max(max(case[k]) for k in case if k.startswith("rel_"))
-            case["floor_mean"] = float(np.mean([v for k in case if k.startswith("rel_") for v in case[k]]))
-            print(f"[noise] width {width} {mode}: floor max {case['floor_max']:.3e} mean {case['floor_mean']:.3e}",
-                  flush=True)
-            res["cases"].append(case)
+            for B in batches:
+                rng_seed = (B + 17) if width == 4096 else (B + 31)  # the tests' ids for this batch
+                ids = np.random.default_rng(rng_seed).integers(3, cfg.vocab_size, (B, T.T_PROMPT + T.STEPS + 1))
+                outs = {}
+                for order in ORDERS:
+                    t0 = time.time()
+                    outs[order] = T._oracle_steps(orc_variant(cfg, pb, lin, order), ids)
+                    print(f"[noise] width {width} {mode} B={B} {order}: {time.time() - t0:.1f} s", flush=True)
+                case = {"width": width, "mode": str(mode), "batch": B, "steps": T.STEPS + 1, **pair_rels(outs)}
+                allr = [v for k in case if k.startswith("rel_") for v in case[k]]
+                case["floor_max"] = max(allr)
+                case["floor_mean"] = float(np.mean(allr))
+                gpu = [v for k in case if k.startswith("rel_") and "gpu" in k for v in case[k]]
+                case["floor_max_gpu_formulas"] = max(gpu)
+                print(f"[noise] width {width} {mode} B={B}: floor max {case['floor_max']:.3e} mean "
+                      f"{case['floor_mean']:.3e} (gpu-formula pairs max {case['floor_max_gpu_formulas']:.3e})", flush=True)
+                res["cases"].append(case)
     Path(args.out).write_text(json.dumps(res, indent=1))
     print(f"wrote {args.out}")
 
