@@ -288,6 +288,13 @@ int llj_g_attention(const void* q, const void* kcache, const void* vcache, void*
                     int n_head, int S, int dt, void* stream);
 /* h[i] = silu(a1[i]) * a2[i], i < n (model.py:258-259; dt 0: bf16(bf16(silu(a1)) * a2)). */
 int llj_g_silu_mul(const void* a1, const void* a2, void* h, size_t n, int dt, void* stream);
+/* LLM.int8() (Linear8bitLt, quantization.py:36-75, threshold 6.0; bitsandbytes' algorithm restated)
+ * for any K with bf16 rows: outlier columns, row scales and the int8 / fp16 products in three plain
+ * launches; CB (N, K) int8 row-major, SCB (N) fp32; y (or resid + y, resid may be y) bf16.
+ * ws: llj_g_i8_ws_bytes(M, K) bytes. */
+size_t llj_g_i8_ws_bytes(int M, int K);
+int llj_g_i8_linear(const void* x, int ldx, int M, int K, const void* CB, const float* SCB, float threshold, void* ws, int N,
+                    void* y, int ldy, const void* resid, int ldr, void* stream);
 /* Greedy next token over fp32 logits (generate.py:66-74, top_k = 1), as llj_argmax. */
 int llj_g_argmax(const float* logits, int ldl, int M, int V, int* out_idx, int* tokens_out, int tok_stride, const int* pos,
                  void* stream);

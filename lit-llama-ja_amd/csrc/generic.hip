@@ -231,6 +231,86 @@ __global__ __launch_bounds__(1024) void g_argmax_kernel(const float* __restrict_
 
 using namespace llj;
 
+// ---- LLM.int8() for any K (Linear8bitLt outside the streaming tiling, e.g. the 125M's K = 780):
+// the restated bnb MatMul8bitLt (oracle/llama_np.py int8_linear, reference quantization.py:36-75):
+// A16 = f16(A); outlier columns = {k : any row |A16[m, k]| >= thr}; SCA[m] = max over the row's other
+// columns of |A16|; CA = rint(A16 * (127 / SCA)); y = f16(f16(sum_k CA CB (int32) * SCA SCB / 127^2)
+// + sum_{outliers} A16 f16(CB SCB / 127)), cast to bf16. ws: K flag bytes, then M fp32 SCA.
+__global__ __launch_bounds__(256) void g_i8_flags_kernel(const bf16_t* __restrict__ x, int ldx, int M, int K, float thr,
+                                                         unsigned char* __restrict__ flags) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  bool o = false;
+  for (int m = 0; m < M; ++m) o |= fabsf((float)(_Float16)bf2f(x[(size_t)m * ldx + k])) >= thr;
+  flags[k] = o ? 1 : 0;
+}
+__global__ __launch_bounds__(256) void g_i8_sca_kernel(const bf16_t* __restrict__ x, int ldx, int K,
+                                                       const unsigned char* __restrict__ flags, float* __restrict__ sca) {
+  __shared__ float red[4];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  float mx = 0.f;
+  for (int k = tid; k < K; k += 256)
+    if (!flags[k]) mx = fmaxf(mx, fabsf((float)(_Float16)bf2f(x[(size_t)m * ldx + k])));
+  mx = wave_max(mx);
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  if (tid == 0) sca[m] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+__global__ __launch_bounds__(256) void g_i8_linear_kernel(const bf16_t* __restrict__ x, int ldx, int M, int K,
+                                                          const int8_t* __restrict__ CB, const float* __restrict__ SCB,
+                                                          const unsigned char* __restrict__ flags,
+                                                          const float* __restrict__ sca, int N, bf16_t* __restrict__ y,
+                                                          int ldy, const bf16_t* resid, int ldr) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const int m0 = blockIdx.y * GL_ROWS;
+  const int mr = M - m0 < GL_ROWS ? M - m0 : GL_ROWS;
+  const float scb = SCB[n];
+  float qs[GL_ROWS];
+#pragma unroll
+  for (int r = 0; r < GL_ROWS; ++r) {
+    const float sa = r < mr ? sca[m0 + r] : 1.f;
+    qs[r] = 127.f / (sa == 0.f ? 1.f : sa);
+  }
+  int acc[GL_ROWS];
+  float side[GL_ROWS];
+#pragma unroll
+  for (int r = 0; r < GL_ROWS; ++r) {
+    acc[r] = 0;
+    side[r] = 0.f;
+  }
+  for (int k = lane; k < K; k += 64) {
+    const int cb = CB[(size_t)n * K + k];
+    const bool o = flags[k] != 0;
+    const float w16 = (float)(_Float16)((float)cb * (scb / 127.f));
+#pragma unroll
+    for (int r = 0; r < GL_ROWS; ++r) {
+      if (r < mr) {
+        const float a16 = (float)(_Float16)bf2f(x[(size_t)(m0 + r) * ldx + k]);
+        if (o) side[r] += a16 * w16;
+        else acc[r] += (int)rintf(fminf(fmaxf(a16 * qs[r], -127.f), 127.f)) * cb;
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < GL_ROWS; ++r) {
+    int a = acc[r];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    const float sd = wave_sum(side[r]);
+    if (lane == r && r < mr) {
+      const size_t m = (size_t)(m0 + r);
+      const float sa = sca[m];
+      float v = (float)a * (sa * scb * (1.f / (127.f * 127.f)));
+      v = (float)(_Float16)((float)(_Float16)v + sd);
+      v = round_bf(v);
+      if (resid) v = bf2f(resid[m * ldr + n]) + v;
+      y[m * ldy + n] = f2bf(v);
+    }
+  }
+}
+
 #define LLJ_DT(dt, CALL_BF16, CALL_F32) \
   do {                                 \
     if ((dt) == 0) CALL_BF16;          \
@@ -310,6 +390,24 @@ int llj_g_silu_mul(const void* a1, const void* a2, void* h, size_t n, int dt, vo
   hipStream_t s = (hipStream_t)stream;
   LLJ_DT(dt, hipLaunchKernelGGL(g_silu_mul_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)a1, (const bf16_t*)a2, (bf16_t*)h, n),
          hipLaunchKernelGGL(g_silu_mul_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)a1, (const float*)a2, (float*)h, n));
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t llj_g_i8_ws_bytes(int M, int K) { return (((size_t)K + 15) & ~(size_t)15) + (size_t)M * 4; }
+
+int llj_g_i8_linear(const void* x, int ldx, int M, int K, const void* CB, const float* SCB, float threshold, void* ws, int N,
+                    void* y, int ldy, const void* resid, int ldr, void* stream) {
+  LLJ_REQUIRE(x && CB && SCB && ws && y && M > 0 && K > 0 && N > 0 && ldx >= K && ldy >= N && (!resid || ldr >= N));
+  hipStream_t s = (hipStream_t)stream;
+  unsigned char* flags = (unsigned char*)ws;
+  float* sca = (float*)((char*)ws + (((size_t)K + 15) & ~(size_t)15));
+  hipLaunchKernelGGL(g_i8_flags_kernel, dim3((K + 255) / 256), dim3(256), 0, s, (const bf16_t*)x, ldx, M, K, threshold, flags);
+  LLJ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(g_i8_sca_kernel, dim3(M), dim3(256), 0, s, (const bf16_t*)x, ldx, K, flags, sca);
+  LLJ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(g_i8_linear_kernel, dim3((N + 3) / 4, (M + GL_ROWS - 1) / GL_ROWS), dim3(256), 0, s, (const bf16_t*)x,
+                     ldx, M, K, (const int8_t*)CB, SCB, flags, sca, N, (bf16_t*)y, ldy, (const bf16_t*)resid, ldr);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

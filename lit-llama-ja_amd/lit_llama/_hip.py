@@ -72,6 +72,7 @@ SIGNATURES = {
     "llj_g_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "llj_g_silu_mul": [_P, _P, _P, ctypes.c_size_t, _I, _P],
     "llj_g_argmax": [_P, _I, _I, _I, _P, _P, _I, _P, _P],
+    "llj_g_i8_linear": [_P, _I, _I, _I, _P, _P, _F, _P, _I, _P, _I, _P, _I, _P],
 }
 
 _lib = None
@@ -101,6 +102,8 @@ def lib() -> ctypes.CDLL:
         L.llj_attention_decode_ws_bytes.restype = ctypes.c_size_t
         L.llj_engine_arena_bytes.argtypes = [_I, _I]
         L.llj_engine_arena_bytes.restype = ctypes.c_size_t
+        L.llj_g_i8_ws_bytes.argtypes = [_I, _I]
+        L.llj_g_i8_ws_bytes.restype = ctypes.c_size_t
         _lib = L
     return _lib
 

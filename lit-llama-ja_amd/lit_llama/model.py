@@ -206,8 +206,7 @@ def _gspec(lin: nn.Module):
         if lin.bias is not None:
             raise NotImplementedError("biased dense Linear is not on the LLaMA path")
         return 1, w, None, None, 16, w.shape[1]
-    raise NotImplementedError(f"{type(lin).__name__} has no any-shape kernel (LLM.int8 needs n_embd % 128 == 0 "
-                              "and head size 64 / 128)")
+    raise NotImplementedError(f"{type(lin).__name__} has no any-shape kernel")
 
 
 class _Work:
@@ -546,6 +545,14 @@ class LLaMA(nn.Module):
     @staticmethod
     def _glinear(spec, A, M, K, N, out, resid, st):
         kind, W, sc, zr, bits, group = spec
+        if kind == 2:  # LLM.int8 (Linear8bitLt._gspec): statistics + int8 / fp16 products, bf16 rows
+            if A.dtype != torch.bfloat16:
+                raise TypeError(f"Linear8bitLt computes on bfloat16 activations, got {A.dtype}")
+            ws = torch.empty(_hip.lib().llj_g_i8_ws_bytes(M, K), dtype=torch.uint8, device=A.device)
+            _hip.call("llj_g_i8_linear", A.data_ptr(), A.stride(0), M, K, W.data_ptr(), sc.data_ptr(),
+                      Linear8bitLtThreshold, ws.data_ptr(), N, out.data_ptr(), out.stride(0),
+                      None if resid is None else resid.data_ptr(), 0 if resid is None else resid.stride(0), st)
+            return
         if kind == 1 and W.dtype != A.dtype:
             raise TypeError(f"dense Linear weight {W.dtype} with {A.dtype} activations")
         _hip.call("llj_g_linear", kind, A.data_ptr(), A.stride(0), M, K, W.data_ptr(), _hip.ptr(sc), _hip.ptr(zr), bits,

@@ -370,10 +370,27 @@ class Linear8bitLt(torch.nn.Module):
         self._prepare()
         return 2, self.weight, self.SCB
 
+    def _gspec(self):
+        """Operands of the any-shape LLM.int8 kernel (llj_g_i8_linear) for K % 128 != 0: (2, CB
+        row-major, SCB, None, 8, K)."""
+        if self.SCB is None or self.weight.dtype != torch.int8:
+            self._quantize_weight(self.weight)
+        if self.bias is not None:
+            raise NotImplementedError("biased Linear8bitLt outside the streaming tiling")
+        return 2, self.cb_reference(), self.SCB, None, 8, self.in_features
+
     def forward(self, x):
         _hip.require_device(x, "input")
         if x.dtype != torch.bfloat16:
             raise TypeError(f"Linear8bitLt HIP path computes in bfloat16, got {x.dtype}")
+        if self.in_features % 128 or self.out_features % 16:  # the any-shape LLM.int8 kernels
+            from .model import LLaMA
+
+            K, N = self.in_features, self.out_features
+            x2 = x.reshape(-1, K).contiguous()
+            out = torch.empty((x2.shape[0], N), dtype=x.dtype, device=x.device)
+            LLaMA._glinear(self._gspec(), x2, x2.shape[0], K, N, out, None, _hip.stream())
+            return out.reshape(*x.shape[:-1], N)
         self._prepare()
         bias = None if self.bias is None else self.bias.to(torch.bfloat16)
         return int8_linear(x, self.weight, self.SCB, bias, self.threshold)

@@ -65,9 +65,10 @@ def test_reference_test_config_no_cache_vs_oracle():
     np.testing.assert_allclose(out2, out, rtol=0, atol=1e-6)
 
 
-@pytest.mark.parametrize("mode", [None, "gptq.int4"])
+@pytest.mark.parametrize("mode", [None, "gptq.int4", "llm.int8"])
 def test_125m_prefill_and_decode_vs_oracle(mode):
-    """125M: a 12-token prompt (every row) then 4 teacher-forced decode steps, batch 2."""
+    """125M: a 12-token prompt (every row) then 4 teacher-forced decode steps, batch 2. llm.int8:
+    Linear8bitLt at K = 780 / 2304 on the any-shape LLM.int8 kernels (llj_g_i8_linear)."""
     m, orc = _setup(C125, mode, 125)
     ids = np.random.default_rng(12).integers(3, C125.vocab_size, (2, 12 + 5))
     got, got_rows = _gpu_steps(m, ids, t_prompt=12, steps=4, s=32, all_rows=True)
@@ -115,8 +116,40 @@ def test_generic_linear_grouped_int8_codes_vs_numpy():
     y = torch.from_numpy(res).to(dev).to(torch.bfloat16)
     sct, zrt = torch.from_numpy(sc).to(dev), torch.from_numpy(zr).to(dev)
     _hip.call("llj_g_linear", 0, xt.data_ptr(), K, M, K, qw.data_ptr(), sct.data_ptr(), zrt.data_ptr(), 8, g, N,
-              y.data_ptr(), N, y.data_ptr(), N, _hip.stream())
+              y.data_ptr(), N, y.data_ptr(), N, 0, _hip.stream())
     got = y.float().cpu().numpy()
     err = np.abs(got - ref).max() / np.abs(ref).max()
     print(f"[generic] grouped int8 linear + residual: max err {err:.2e} of max|y|")
     assert err < 1e-2
+
+
+@pytest.mark.parametrize("outliers", [0, 5, 200])
+@pytest.mark.parametrize("M,K,N", [(1, 780, 2340), (7, 2304, 780), (40, 780, 36)])
+def test_generic_int8_linear_vs_oracle(M, K, N, outliers):
+    """llj_g_i8_linear (LLM.int8 for K % 128 != 0: the 125M's 780 / 2304) against the oracle's
+    restatement of bitsandbytes' MatMul8bitLt (parity unpinned: bitsandbytes is absent), with and
+    without outlier columns, plain and with the residual add."""
+    from lit_llama import _hip
+    from tests.helpers import assert_bf16_close
+
+    rng = np.random.default_rng(M + K + outliers)
+    W = O.bf16_round((rng.standard_normal((N, K)) * 0.02).astype(np.float32))
+    cb, scb = O.int8_quantize_weight(W)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    if outliers:
+        x[:, rng.choice(K, outliers, replace=False)] *= 25.0
+    x = O.bf16_round(x)
+    res = O.bf16_round(rng.standard_normal((M, N)).astype(np.float32))
+    dev = torch.device("cuda")
+    xt = torch.from_numpy(x).to(dev).to(torch.bfloat16)
+    cbt, scbt = torch.from_numpy(cb).to(dev), torch.from_numpy(scb).to(dev)
+    ws = torch.empty(_hip.lib().llj_g_i8_ws_bytes(M, K), dtype=torch.uint8, device=dev)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    yr = torch.from_numpy(res).to(dev).to(torch.bfloat16)
+    _hip.call("llj_g_i8_linear", xt.data_ptr(), K, M, K, cbt.data_ptr(), scbt.data_ptr(), 6.0, ws.data_ptr(), N,
+              y.data_ptr(), N, None, 0, _hip.stream())
+    _hip.call("llj_g_i8_linear", xt.data_ptr(), K, M, K, cbt.data_ptr(), scbt.data_ptr(), 6.0, ws.data_ptr(), N,
+              yr.data_ptr(), N, yr.data_ptr(), N, _hip.stream())
+    ref = O.int8_linear(x, cb, scb)
+    assert_bf16_close(y.float().cpu().numpy(), ref, f"generic int8 M={M} K={K} outliers={outliers}", rel=1e-2)
+    assert_bf16_close(yr.float().cpu().numpy(), O.bf16_round(res + O.bf16_round(ref)), "generic int8 resid", rel=1e-2)

@@ -26,3 +26,5 @@ timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "i8 or int8" 
 echo "i8 tests rc=$?" >> $O/status.log
 timeout -k 10 300 python -u -m pytest tests/test_model_7b_gpu.py -k "int8" -s -q --timeout 200 --timeout-method thread > $O/t_7b_i8.log 2>&1
 echo "7b i8 tests rc=$?" >> $O/status.log
+timeout -k 10 300 python -u -m pytest tests/test_fp32_gpu.py tests/test_generic_gpu.py -s -q --timeout 200 --timeout-method thread > $O/t_fp32_generic.log 2>&1
+echo "fp32/generic tests rc=$?" >> $O/status.log

@@ -196,15 +196,14 @@ def rels(a, b):
 
 
 def _case(name, outs):
-    case = {"case": name, "rel_base_vs_f64": rels(outs["base"], outs["f64"]),
-            "rel_base_vs_chunk": rels(outs["base"], outs["chunk"]), "rel_f64_vs_chunk": rels(outs["f64"], outs["chunk"])}
+    case = {"case": name, **pair_rels(outs)}
     case["floor_max"] = max(max(case[k]) for k in case if k.startswith("rel_"))
     case["floor_mean"] = float(np.mean([v for k in case if k.startswith("rel_") for v in case[k]]))
     print(f"[noise] {name}: floor max {case['floor_max']:.3e} mean {case['floor_mean']:.3e}", flush=True)
     return case
 
 
-def generic_cases():
+def generic_cases(generic_modes=(None, "gptq.int4", "llm.int8")):
     from tests import test_generic_gpu as TG
 
     cases = []
@@ -216,10 +215,10 @@ def generic_cases():
     cfg = TG.C125
     p = T.make_params(cfg, 125)
     ids = np.random.default_rng(12).integers(3, cfg.vocab_size, (2, 12 + 5))
-    for mode in (None, "gptq.int4"):
+    for mode in generic_modes:
         pb, _, lin = T.oracle_linears(p, mode)
         outs_rows, outs_steps = {}, {}
-        for o in ("base", "f64", "chunk"):
+        for o in ("base", "f64", "chunk", "gpu"):
             st, rows = T._oracle_steps(orc_variant(cfg, pb, lin, o), ids, t_prompt=12, steps=4, s=32, all_rows=True)
             outs_rows[o], outs_steps[o] = rows, st
         cases.append(_case(f"125M {mode} prompt rows", outs_rows))
@@ -237,8 +236,10 @@ def main():
     args = ap.parse_args()
     res = {"what": __doc__.split("\n\n")[0], "cases": []}
     if args.generic:
-        res["cases"] = generic_cases()
-        out = args.out or str(REPO / "profiles" / "r03_noise_floor_generic.json")
+        gm = (None, "gptq.int4", "llm.int8") if not args.modes else tuple(
+            None if m == "bf16" else m for m in args.modes.split(","))
+        res["cases"] = generic_cases(gm)
+        out = args.out or str(REPO / "profiles" / "r04_noise_floor_generic.json")
         Path(out).write_text(json.dumps(res, indent=1))
         print(f"wrote {out}")
         return
