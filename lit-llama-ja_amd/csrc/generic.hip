@@ -233,8 +233,7 @@ using namespace llj;
 
 // ---- LLM.int8() for any K (Linear8bitLt outside the streaming tiling, e.g. the 125M's K = 780):
 // the restated bnb MatMul8bitLt (oracle/llama_np.py int8_linear, reference quantization.py:36-75):
-// A16 = f16(A); outlier columns = {k : any row |A16[m, k]| >= thr}; SCA[m] = max over the row's other
-// columns of |A16|; CA = rint(A16 * (127 / SCA)); y = f16(f16(sum_k CA CB (int32) * SCA SCB / 127^2)
+// A16 = f16(A); outlier columns = {k : any row |A16[m, k]| >= thr}; SCA[m] = max |A16[m, k]| < thr; CA = rint(A16 * (127 / SCA)); y = f16(f16(sum_k CA CB (int32) * SCA SCB / 127^2)
 // + sum_{outliers} A16 f16(CB SCB / 127)), cast to bf16. ws: K flag bytes, then M fp32 SCA.
 __global__ __launch_bounds__(256) void g_i8_flags_kernel(const bf16_t* __restrict__ x, int ldx, int M, int K, float thr,
                                                          unsigned char* __restrict__ flags) {
@@ -244,13 +243,17 @@ __global__ __launch_bounds__(256) void g_i8_flags_kernel(const bf16_t* __restric
   for (int m = 0; m < M; ++m) o |= fabsf((float)(_Float16)bf2f(x[(size_t)m * ldx + k])) >= thr;
   flags[k] = o ? 1 : 0;
 }
-__global__ __launch_bounds__(256) void g_i8_sca_kernel(const bf16_t* __restrict__ x, int ldx, int K,
-                                                       const unsigned char* __restrict__ flags, float* __restrict__ sca) {
+// SCA[m]: max |A16| over the row's elements below the threshold (element-wise, as double_quant's row
+// statistics; an element under it in an outlier column still counts, its code is then dropped)
+__global__ __launch_bounds__(256) void g_i8_sca_kernel(const bf16_t* __restrict__ x, int ldx, int K, float thr,
+                                                       float* __restrict__ sca) {
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x;
   float mx = 0.f;
-  for (int k = tid; k < K; k += 256)
-    if (!flags[k]) mx = fmaxf(mx, fabsf((float)(_Float16)bf2f(x[(size_t)m * ldx + k])));
+  for (int k = tid; k < K; k += 256) {
+    const float a = fabsf((float)(_Float16)bf2f(x[(size_t)m * ldx + k]));
+    if (a < thr) mx = fmaxf(mx, a);
+  }
   mx = wave_max(mx);
   if ((tid & 63) == 0) red[tid >> 6] = mx;
   __syncthreads();
@@ -404,7 +407,7 @@ int llj_g_i8_linear(const void* x, int ldx, int M, int K, const void* CB, const 
   float* sca = (float*)((char*)ws + (((size_t)K + 15) & ~(size_t)15));
   hipLaunchKernelGGL(g_i8_flags_kernel, dim3((K + 255) / 256), dim3(256), 0, s, (const bf16_t*)x, ldx, M, K, threshold, flags);
   LLJ_CHECK_LAUNCH();
-  hipLaunchKernelGGL(g_i8_sca_kernel, dim3(M), dim3(256), 0, s, (const bf16_t*)x, ldx, K, flags, sca);
+  hipLaunchKernelGGL(g_i8_sca_kernel, dim3(M), dim3(256), 0, s, (const bf16_t*)x, ldx, K, threshold, sca);
   LLJ_CHECK_LAUNCH();
   hipLaunchKernelGGL(g_i8_linear_kernel, dim3((N + 3) / 4, (M + GL_ROWS - 1) / GL_ROWS), dim3(256), 0, s, (const bf16_t*)x,
                      ldx, M, K, (const int8_t*)CB, SCB, flags, sca, N, (bf16_t*)y, ldy, (const bf16_t*)resid, ldr);

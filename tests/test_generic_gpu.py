@@ -28,6 +28,9 @@ C125 = Cfg(block_size=128, n_layer=12, n_head=10, n_embd=780, vocab_size=35000)
 # (max per row, mean over rows): 2x profiles/r03_noise_floor_generic.json
 TOL_REF_TEST = (5.8e-2, 5.8e-3)
 TOL_125M = (3.8e-2, 3.2e-2)
+# llm.int8 re-quantizes every Linear input per row, so the same flips move whole int8 steps: floor max
+# 3.12e-2 / mean 2.16e-2 (profiles/r04_noise_floor_generic.json, with the GPU-formula variant)
+TOL_125M_I8 = (6.3e-2, 4.4e-2)
 
 
 def _check_mean(got, ref, tol, what):
@@ -73,8 +76,9 @@ def test_125m_prefill_and_decode_vs_oracle(mode):
     ids = np.random.default_rng(12).integers(3, C125.vocab_size, (2, 12 + 5))
     got, got_rows = _gpu_steps(m, ids, t_prompt=12, steps=4, s=32, all_rows=True)
     ref, ref_rows = _oracle_steps(orc, ids, t_prompt=12, steps=4, s=32, all_rows=True)
-    _check_mean(got_rows, ref_rows, TOL_125M, f"125M {mode} prompt rows")
-    _check_mean(got, ref, TOL_125M, f"125M {mode} steps")
+    tol = TOL_125M_I8 if mode == "llm.int8" else TOL_125M
+    _check_mean(got_rows, ref_rows, tol, f"125M {mode} prompt rows")
+    _check_mean(got, ref, tol, f"125M {mode} steps")
 
 
 def test_125m_generate_graph_matches_eager_and_wraps():

@@ -233,6 +233,7 @@ def main():
     ap.add_argument("--batches", default="1,8")
     ap.add_argument("--modes", default=None, help="comma list of gptq.int4, bf16, llm.int8 (default: all)")
     ap.add_argument("--generic", action="store_true")
+    ap.add_argument("--prefill", action="store_true")
     args = ap.parse_args()
     res = {"what": __doc__.split("\n\n")[0], "cases": []}
     if args.generic:
@@ -240,6 +241,29 @@ def main():
             None if m == "bf16" else m for m in args.modes.split(","))
         res["cases"] = generic_cases(gm)
         out = args.out or str(REPO / "profiles" / "r04_noise_floor_generic.json")
+        Path(out).write_text(json.dumps(res, indent=1))
+        print(f"wrote {out}")
+        return
+    if args.prefill:  # the 64-token prompt tests (test_7b_width_prefill_gemm_flash_vs_oracle, 13B likewise)
+        for width in [int(w) for w in args.widths.split(",")]:
+            cfg = T.C7 if width == 4096 else T.C13
+            p = T.make_params(cfg, T.SEEDS[width])
+            modes = ["gptq.int4", None, "llm.int8"] if width == 4096 else ["gptq.int4"]
+            if args.modes:
+                modes = [None if m == "bf16" else m for m in args.modes.split(",")
+                         if (m == "bf16" and None in modes) or m in modes]
+            for mode in modes:
+                pb, _, lin = T.oracle_linears(p, mode)
+                ids = np.random.default_rng(64 if width == 4096 else 65).integers(3, cfg.vocab_size, (1, 64 + 3))
+                rows, steps = {}, {}
+                for order in ORDERS:
+                    t0 = time.time()
+                    steps[order], rows[order] = T._oracle_steps(orc_variant(cfg, pb, lin, order), ids, t_prompt=64,
+                                                                steps=2, s=96, all_rows=True)
+                    print(f"[noise] prefill width {width} {mode} {order}: {time.time() - t0:.1f} s", flush=True)
+                res["cases"].append(_case(f"prefill 64 rows width {width} {mode}", rows))
+                res["cases"].append(_case(f"prefill steps width {width} {mode}", steps))
+        out = args.out or str(REPO / "profiles" / "r04_noise_floor_prefill.json")
         Path(out).write_text(json.dumps(res, indent=1))
         print(f"wrote {out}")
         return
