@@ -134,8 +134,15 @@ def aggregate(local_seconds: float, local_tokens: int, ws: int):
 
 
 # ----------------------------------------------------------------------------- model
-def build_model(name: str, mode: str, seed: int = 1234):
-    """LLaMA `name` under quantization `mode` with synthetic weights."""
+def build_model(name: str, mode: str, seed: int = 1234, outliers: str | None = None):
+    """LLaMA `name` under quantization `mode` with synthetic weights.
+
+    llm.int8 only, `outliers` sets the LLM.int8() outlier regime of every Linear input (the
+    activation columns with some |A16| >= 6.0 that take the fp16 side product): None = the random
+    weights' own (~0 in the norm outputs, a few in y, ~300 in the down-projection input h);
+    "none" = no outlier column anywhere (c_attn's v rows and c_fc1 / c_fc2 scaled by 0.5 / 0.4);
+    "6x20" = SURVEY §8d's regime: those scalings plus 6 columns of every Linear input made 20x larger
+    (RMSNorm gains of rms_1 / rms_2 / ln_f, c_attn's v rows, c_fc1 / c_fc2 rows by sqrt(20) each)."""
     from lit_llama import LLaMA
     from lit_llama.utils import EmptyInitOnDevice
 
@@ -161,11 +168,35 @@ def build_model(name: str, mode: str, seed: int = 1234):
             blk.rms_2.scale.fill_(1.0)
         model.transformer.ln_f.scale.fill_(1.0)
     if mode == "llm.int8":  # quantize the random bf16 weights (Linear8bitLt._quantize_weight)
-        for mod in model.modules():
-            if hasattr(mod, "_quantize_weight"):
-                w = torch.empty((mod.out_features, mod.in_features), dtype=torch.bfloat16, device=dev)
+        cfg = model.config
+        C = cfg.n_embd
+        cols = torch.arange(6, device=dev) * (C // 6) + 7  # the 6 outlier columns of every input (< C)
+        for blk in model.transformer.h:
+            for name_, mod in (("qkv", blk.attn.c_attn), ("o", blk.attn.c_proj), ("fc1", blk.mlp.c_fc1),
+                               ("fc2", blk.mlp.c_fc2), ("down", blk.mlp.c_proj)):
+                w = torch.empty((mod.out_features, mod.in_features), dtype=torch.float32, device=dev)
                 w.normal_(0.0, 0.02, generator=g)
-                mod._quantize_weight(w)
+                if outliers in ("none", "6x20"):
+                    if name_ == "qkv":
+                        w[2 * C:] *= 0.5  # v: attention outputs y below 6
+                    elif name_ in ("fc1", "fc2"):
+                        w *= 0.4  # h = silu(a1) a2 below 6
+                    if outliers == "6x20":
+                        if name_ == "qkv":
+                            w[2 * C + cols] *= 20.0  # y columns 20x
+                        elif name_ in ("fc1", "fc2"):
+                            w[cols] *= 20.0 ** 0.5  # h columns 20x
+                mod._quantize_weight(w.to(torch.bfloat16))
+        w = torch.empty((model.lm_head.out_features, C), dtype=torch.bfloat16, device=dev)
+        w.normal_(0.0, 0.02, generator=g)
+        model.lm_head._quantize_weight(w)
+        if outliers == "6x20":
+            with torch.no_grad():
+                for norm in [b.rms_1 for b in model.transformer.h] + [b.rms_2 for b in model.transformer.h] + \
+                        [model.transformer.ln_f]:
+                    norm.scale[cols] = 20.0
+    elif outliers is not None:
+        raise ValueError("outlier regimes are an llm.int8 setting")
     return model.eval()
 
 

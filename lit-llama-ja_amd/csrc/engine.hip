@@ -605,9 +605,27 @@ __device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop,
 // order, so every CU of the head holds the bitwise-same scores; 3) softmax in fp32 (exp2 of
 // log2(e)-scaled scores) and P.V over this CU's 16 value dims (kept in registers since step 1);
 // 4) y slice -> bf16 -> 8 granules of y.
+// The cache rows of this thread's first key (kk = t < 64 NC), loaded at the start of the layer's QKV
+// op so their memory latency hides under the QKV tiles: [K lo, K hi, V lo, V hi]
+__device__ __forceinline__ void kv_prefetch(const Ctx& X, const llj_engine_plan& P, int l, int p, u32x4 (&pre)[4]) {
+  const Shape& s = X.s;
+  const int J = s.J, h = s.unit / J, j = s.unit % J, hs = s.hs, Sc = s.S;
+  const int nprev = p < Sc ? p : Sc - 1, cur_slot = p % Sc;
+  const int t = X.wave * 64 + X.lane;
+  const int ki = t < nprev ? t : 0;
+  const int slot = p < Sc ? ki : (ki < cur_slot ? ki : ki + 1);
+  const size_t off = ((size_t)h * Sc + slot) * hs + 16 * j;
+  const u32x4* kp = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(P.layers[l].kcache) + off);
+  const u32x4* vp = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(P.layers[l].vcache) + off);
+  pre[0] = kp[0];
+  pre[1] = kp[1];
+  pre[2] = vp[0];
+  pre[3] = vp[1];
+}
+
 template <int HS>
 __device__ __forceinline__ void attention_dims(Ctx& X, const Lds& L, const llj_engine_plan& P, const Arena& ar, int l, int p,
-                                            unsigned tag) {
+                                            unsigned tag, const u32x4 (&pre)[4]) {
   const Shape& s = X.s;
   constexpr int J = HS / 16;
   const int u = s.unit, h = u / J, j = u % J;
@@ -626,8 +644,12 @@ __device__ __forceinline__ void attention_dims(Ctx& X, const Lds& L, const llj_e
   const bf16_t* vc = reinterpret_cast<const bf16_t*>(P.layers[l].vcache) + (size_t)h * Sc * HS + 16 * j;
   unsigned long long* gs = ar.gsc + (size_t)h * J * kMaxS;  // [key][J]
   u32x4 kr[kKPT][2], vr[kKPT][2];
+  kr[0][0] = pre[0];
+  kr[0][1] = pre[1];
+  vr[0][0] = pre[2];
+  vr[0][1] = pre[3];
 #pragma unroll
-  for (int r = 0; r < kKPT; ++r) {  // cache rows (32 B of K and of V per key), branch-free
+  for (int r = 1; r < kKPT; ++r) {  // cache rows (32 B of K and of V per key) past the prefetched one, branch-free
     const int kk = t + 64 * NC * r;
     const int ki = kk < nprev ? kk : 0;
     const int slot = p < Sc ? ki : (ki < cur_slot ? ki : ki + 1);
@@ -958,6 +980,7 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
   // epilogue-operand buffers alternate per op (QKV 0, c_proj 1, SwiGLU 0, down 1, lm_head 0)
   float2* rcs = L.eop + kEopTiles * 2 * 16 - 8 * TG;  // RoPE (cos, sin) per QKV tile slot (<= TG per CU)
   E.rcs = rcs;
+  u32x4 kvpre[4] = {};  // this thread's first key's cache rows (kv_prefetch at the QKV op)
   // One loop over (layer, op) -- every stage, consume and epilogue is in the code once (the
   // instruction cache holds the whole step's working set).
   for (int i = 0; i <= 4 * s.L; ++i) {
@@ -973,8 +996,8 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
       if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 1);
       if (s.unit >= 0) {  // attention of this CU's (head, 16-dim slice) unit
         cbarrier(X, L);   // the QKV epilogue's q / k / v slices are in LDS
-        if (hs == 128) attention_dims<128>(X, L, P, ar, l, p, tag);
-        else attention_dims<64>(X, L, P, ar, l, p, tag);
+        if (hs == 128) attention_dims<128>(X, L, P, ar, l, p, tag, kvpre);
+        else attention_dims<64>(X, L, P, ar, l, p, tag, kvpre);
       }
       if (X.wave == 0 && l < 8) stamp(P, X.lane, sb + 2);
     } else if (X.wave == 0 && l < 8 && op != OP_QKV) {
@@ -1003,6 +1026,7 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
     if (X.wave == 0 && l < 8 && op != OP_HEAD) stamp(P, X.lane, sb + 2 * op + (op == OP_QKV ? 0 : 1));
     if (op == OP_HEAD && X.wave == 0) stamp(P, X.lane, 126);
     X.stamp_base = (l < 2 && (op == OP_SW || op == OP_QKV)) ? 108 + 3 * (2 * l + (op == OP_SW)) : -1;
+    if (op == OP_QKV && s.unit >= 0) kv_prefetch(X, P, l, p, kvpre);  // lands while the QKV tiles run
     consume(X, L, eop, op, asum, red_par, E);
     if (X.wave == 0 && l < 8 && op == OP_DOWN) stamp(P, X.lane, sb + 8);
   }

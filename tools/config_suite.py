@@ -2,7 +2,8 @@
 
   C1  LLaMA-7B bf16 (unquantized), bs=1
   C2  LLaMA-7B gptq.int4, bs=1 and bs=8
-  C3  LLaMA-7B llm.int8, bs=8
+  C3  LLaMA-7B llm.int8, bs=8, in three outlier regimes of the Linear inputs (bench.build_model):
+      the random weights' own (C3), none (C3-o0) and SURVEY §8d's 6 columns x20 (C3-o6x20)
   C4  LLaMA-13B gptq.int4, bs=1 (one replica; the driver runs the 8-replica scan)
   X-gptq.int8  LLaMA-7B gptq.int8 (ColBlock bits=8), bs=1 (not a BASELINE config; informational)
   C2-long      LLaMA-7B gptq.int4, bs=1 with a 1900-token prompt in a 2048-slot cache (SURVEY §8d's
@@ -31,9 +32,11 @@ import bench  # noqa: E402
 
 CONFIGS = [("C1", "7B", "none", 1), ("C2", "7B", "gptq.int4", 1), ("C2-bs8", "7B", "gptq.int4", 8),
            ("C2-long", "7B", "gptq.int4", 1),
-           ("C3", "7B", "llm.int8", 8), ("C4", "13B", "gptq.int4", 1),
+           ("C3", "7B", "llm.int8", 8), ("C3-o0", "7B", "llm.int8", 8), ("C3-o6x20", "7B", "llm.int8", 8),
+           ("C4", "13B", "gptq.int4", 1),
            ("X-gptq.int8", "7B", "gptq.int8", 1)]  # extra: the reference's third --quantize mode
 LONG = {"C2-long": (1900, 2048)}  # (prompt length, max_seq_length)
+OUTLIERS = {"C3-o0": "none", "C3-o6x20": "6x20"}  # bench.build_model's llm.int8 outlier regimes
 
 
 def main():
@@ -49,18 +52,19 @@ def main():
     for tag, name, mode, B in CONFIGS:
         if a.only and tag not in a.only.split(","):
             continue
-        key = (name, mode)
+        key = (name, mode, OUTLIERS.get(tag))
         if key not in models:
             models.clear()
             gc.collect()
             torch.cuda.empty_cache()
-            models[key] = bench.build_model(name, None if mode == "none" else mode)
+            models[key] = bench.build_model(name, None if mode == "none" else mode, outliers=OUTLIERS.get(tag))
         model = models[key]
         plen, S = LONG.get(tag, (16, 144))
         r = bench.time_decode(model, B, plen, S, a.warmup, min(a.steps, 2048 - plen - 1 - a.warmup), 1)
         sb = bench.step_bytes(model, B, r["pos_mean"])
         t_step = r["seconds"] / (r["tokens"] // B)
-        line = {"config": tag, "model": f"LLaMA-{name}", "quantize": mode, "batch": B, "prompt_len": plen,
+        line = {"config": tag, "model": f"LLaMA-{name}", "quantize": mode, "outliers": OUTLIERS.get(tag, "random weights"),
+                "batch": B, "prompt_len": plen,
                 "max_seq_length": S,
                 "value": round(r["tokens"] / r["seconds"], 2), "unit": "tokens/s",
                 "ms_per_step": round(t_step * 1e3, 4), "bytes_per_step": sb,

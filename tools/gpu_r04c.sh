@@ -19,3 +19,12 @@ timeout -k 5 30 tools/micro/consume_probe 0 7 1 64 >> $O/consume_probe.log 2>&1
 timeout -k 5 30 tools/micro/consume_probe 0 4 2 64 >> $O/consume_probe.log 2>&1
 timeout -k 5 30 tools/micro/consume_probe 0 8 2 64 >> $O/consume_probe.log 2>&1
 echo "consume probe rc=$?" >> $O/status.log
+cd $R
+for reg in random none 6x20; do timeout -k 10 200 python -u tools/i8_outlier_count.py --outliers $reg --batches 8 >> $O/outliers.log 2>&1; done
+echo "outlier count rc=$?" >> $O/status.log
+cd $R
+timeout -k 10 200 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread > $O/t_engine.log 2>&1
+echo "engine tests rc=$?" >> $O/status.log
+grep -q " passed" $O/t_engine.log && ! grep -q "failed\|error" $O/t_engine.log && \
+  timeout -k 10 240 python -u tools/engine_trace.py --out $O/engine_trace.json > $O/engine_trace.log 2>&1
+echo "trace rc=$?" >> $O/status.log
