@@ -170,7 +170,7 @@ __device__ __forceinline__ const char* op_weight(const llj_engine_plan& P, int l
 }
 
 // ------------------------------------------------------------------------------------ LDS
-// carve (bytes, 16-aligned): ctl words | A (max(C, H) bf16) | xres[2] (C bf16) | red[2][NC][TG][2][16]
+// carve (bytes, 16-aligned): ctl words | A (max(C, H) bf16) | xown[2] (16 bf16) | red[2][NC][TG][2][16]
 // f32 | eop[2] (epilogue operands) | misc[64] f32 ([0, NC) sums of squares, [16, 16 + NC) row sums,
 // [32, 32 + NC) argmax, [48] last-arriver flag) | attention scratch | ring (nb x 1 KiB)
 constexpr int kCtlWords = 32;  // [0] landed, [1 .. NC] next block per consumer, [16] consumer barrier, [17] max wanted block
@@ -180,7 +180,7 @@ struct Lds {
   unsigned* ctl;
   unsigned char* ring;
   bf16_t* A;
-  bf16_t* xres[2];
+  bf16_t* xown[2];  // the raw x / x_mid of this CU's c_proj / down tile columns (the residual inputs)
   float* red;
   float2* eop;  // [2][kEopTiles][2][16]
   float* misc;
@@ -191,10 +191,10 @@ struct Lds {
 __host__ __device__ inline size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
 // epilogue operands staged per op: (scale, 128 + zero) of both matrices for every tile of the CU
 // (at most kEopTiles), or the RoPE (cos, sin) pairs of the QKV tiles
-constexpr int kEopTiles = 16;
+constexpr int kEopTiles = 8;
 __host__ __device__ inline size_t lds_fixed(int C, int H) {
   const int K = C > H ? C : H;
-  return (size_t)kCtlWords * 4 + al16((size_t)K * 2) + 2 * al16((size_t)C * 2) + (size_t)2 * NC * TG * 2 * 16 * 4 +
+  return (size_t)kCtlWords * 4 + al16((size_t)K * 2) + 2 * 32 + (size_t)2 * NC * TG * 2 * 16 * 4 +
          (size_t)2 * kEopTiles * 2 * 16 * 8 + 64 * 4 + al16((size_t)kAttFloats * 4);
 }
 // ring blocks that fit next to the fixed part in `budget` bytes
@@ -314,12 +314,14 @@ __device__ __forceinline__ void stage_sz(Ctx& X, float2* eop, const llj_engine_p
 }
 
 // Stage the input of an op into A (one call site for every op, so its code is in the kernel once):
-// norm ops (QKV, SwiGLU, lm_head): x (gathered, or the embedding row at layer 0) -> xres[buf] raw
-// and A = RMSNorm(x) * gain (model.py:276-283, bf16 rounding points); plain ops (c_proj, down):
-// the gathered vector -> A. Returns sum_k A[k].
+// norm ops (QKV, SwiGLU, lm_head): x (gathered, or the embedding row at layer 0) -> A raw, then
+// A = RMSNorm(x) * gain in place (model.py:276-283, bf16 rounding points) by the same threads that
+// gathered each pair, and the raw pairs of this CU's residual tile columns -> xown[buf]; plain ops
+// (c_proj, down): the gathered vector -> A. Returns sum_k A[k].
 __device__ __forceinline__ float stage(Ctx& X, const Lds& L, bool norm, int buf, const unsigned long long* g, unsigned tag,
                                        const bf16_t* direct, const bf16_t* gain, float eps, int K) {
-  uint32_t* xr2 = reinterpret_cast<uint32_t*>(L.xres[buf]);
+  uint32_t* xo2 = reinterpret_cast<uint32_t*>(L.xown[buf]);
+  const int own0 = 8 * X.s.g;  // first pair of the CU's c_proj / down tile (tile g: n_embd / 16 <= CUs)
   uint32_t* a2 = reinterpret_cast<uint32_t*>(L.A);
   const uint32_t* g2 = reinterpret_cast<const uint32_t*>(gain);
   // this wave's gain pairs, loaded before the wait (K / 2 / (64 NC) <= GN per lane)
@@ -334,9 +336,8 @@ __device__ __forceinline__ float stage(Ctx& X, const Lds& L, bool norm, int buf,
   // one accumulator: the sum of squares (norm) or of the values (plain) -- a select, not two
   // variables (which the compiler turns into a scratch array indexed by `norm`)
   float part = 0.f;
-  uint32_t* dst = norm ? xr2 : a2;
   auto sink = [&](int idx, uint32_t v) {
-    dst[idx] = v;
+    a2[idx] = v;
     const f32x2 f = unpk(v);
     part += norm ? round_bf(f.x * f.x) + round_bf(f.y * f.y) : f.x + f.y;  // model.py:281: x * x in bf16
   };
@@ -358,10 +359,12 @@ __device__ __forceinline__ float stage(Ctx& X, const Lds& L, bool norm, int buf,
 #pragma unroll
     for (int k = 0; k < GN; ++k) {
       const int idx = X.lane + 64 * X.wave + 64 * NC * k;
-      if (idx < K / 2) {
-        const uint32_t o = norm_pair(xr2[idx], gv[k], r);
+      if (idx < K / 2) {  // the pair this thread gathered (gather's index map is this loop's for K / 2 <= 64 NC GK)
+        const uint32_t raw = a2[idx];
+        const uint32_t o = norm_pair(raw, gv[k], r);
         a2[idx] = o;
         asum += bflo(o) + bfhi(o);
+        if (idx >= own0 && idx < own0 + 8) xo2[idx - own0] = raw;
       }
     }
   }
@@ -420,7 +423,7 @@ __device__ __forceinline__ void epilogue(Ctx& X, const Lds& L, int op, Epi& E, i
       break;
     }
     case OP_O:  // x + attn(x) in bf16 (model.py:172)
-      publish_pair(E.ar.gxm, n, E.tag, round_bf(bf2f(L.xres[0][n]) + round_bf(y1)), lane);
+      publish_pair(E.ar.gxm, n, E.tag, round_bf(bf2f(L.xown[0][n & 15]) + round_bf(y1)), lane);
       break;
     case OP_SW: {
       const float a1 = round_bf(y1), a2 = round_bf(y2);
@@ -429,7 +432,7 @@ __device__ __forceinline__ void epilogue(Ctx& X, const Lds& L, int op, Epi& E, i
       break;
     }
     case OP_DOWN:  // model.py:173
-      publish_pair(E.ar.gx, n, E.tag, round_bf(bf2f(L.xres[1][n]) + round_bf(y1)), lane);
+      publish_pair(E.ar.gx, n, E.tag, round_bf(bf2f(L.xown[1][n & 15]) + round_bf(y1)), lane);
       break;
     default: {  // lm_head: bf16 logits + this wave's argmax key
       const uint32_t b = (uint32_t)f2bf(y1);
@@ -940,10 +943,10 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
     o += kCtlWords * 4;
     L.A = reinterpret_cast<bf16_t*>(smem + o);
     o += al16((size_t)(C > H ? C : H) * 2);
-    L.xres[0] = reinterpret_cast<bf16_t*>(smem + o);
-    o += al16((size_t)C * 2);
-    L.xres[1] = reinterpret_cast<bf16_t*>(smem + o);
-    o += al16((size_t)C * 2);
+    L.xown[0] = reinterpret_cast<bf16_t*>(smem + o);
+    o += 32;
+    L.xown[1] = reinterpret_cast<bf16_t*>(smem + o);
+    o += 32;
     L.red = reinterpret_cast<float*>(smem + o);
     o += (size_t)2 * NC * TG * 2 * 16 * 4;
     L.eop = reinterpret_cast<float2*>(smem + o);
@@ -1098,7 +1101,7 @@ int llj_engine_step(const llj_engine_plan* plan, void* stream) {
   LLJ_REQUIRE(P.layers && P.n_layer >= 1 && P.n_layer <= 126 && P.C % 128 == 0 && P.H % 128 == 0 && P.V % 16 == 0);
   LLJ_REQUIRE(P.V <= 65536 && (hs == 64 || hs == 128) && P.S >= 1 && P.S <= eng::kMaxS && P.arena && P.pos && P.cur &&
               P.logits);
-  LLJ_REQUIRE(P.C / 2 <= eng::GN * 64 * eng::NC);  // stage's gain registers
+  LLJ_REQUIRE(P.C / 2 <= eng::GN * 64 * eng::NC && P.C / 2 <= 64 * eng::NC * eng::GK);  // stage's gain registers, one gather batch
   LLJ_REQUIRE(P.C <= eng::AREG_C * eng::NC * 128);  // A fragments of the K = C ops in registers
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
