@@ -705,23 +705,19 @@ __device__ __forceinline__ void attention_dims(Ctx& X, const Lds& L, const llj_e
     for (int jj = 0; jj < J; ++jj) a += __uint_as_float((uint32_t)v[jj]);
     sfull[r] = kk < NK ? a : -INFINITY;
   }
-  // softmax over the NK keys (every consumer wave), then P.V over this CU's 16 dims
+  // softmax over the NK keys and P.V over this CU's 16 dims: every wave against its own running max
+  // (flash-style partials (max, sum, o[16]) in LDS), merged by wave 0 in wave order -- one barrier
   float mx = -INFINITY;
 #pragma unroll
   for (int r = 0; r < kKPT; ++r) mx = fmaxf(mx, sfull[r]);
   mx = wave_max(mx);
-  if (X.lane == 0) s_m[X.wave] = mx;
-  cbarrier(X, L);
-  float M = -INFINITY;
-#pragma unroll
-  for (int w = 0; w < NC; ++w) M = fmaxf(M, s_m[w]);
   float lsum = 0.f, o[16];
 #pragma unroll
   for (int d = 0; d < 16; ++d) o[d] = 0.f;
 #pragma unroll
   for (int r = 0; r < kKPT; ++r) {
     const int kk = t + 64 * NC * r;
-    const float e = kk < NK ? exp2f(sfull[r] - M) : 0.f;
+    const float e = kk < NK ? exp2f(sfull[r] - mx) : 0.f;
     lsum += e;
     if (kk == nprev) {
 #pragma unroll
@@ -739,6 +735,7 @@ __device__ __forceinline__ void attention_dims(Ctx& X, const Lds& L, const llj_e
 #pragma unroll
   for (int d = 0; d < 16; ++d) o[d] = wave_sum(o[d]);
   if (X.lane == 0) {
+    s_m[X.wave] = mx;
     s_l[X.wave] = lsum;
 #pragma unroll
     for (int d = 0; d < 16; ++d) s_o[X.wave * 16 + d] = o[d];
@@ -746,11 +743,15 @@ __device__ __forceinline__ void attention_dims(Ctx& X, const Lds& L, const llj_e
   cbarrier(X, L);
   if (X.wave == 0) {
     const int d = X.lane & 15;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NC; ++w) M = fmaxf(M, s_m[w]);
     float Ls = 0.f, O = 0.f;
 #pragma unroll
     for (int w = 0; w < NC; ++w) {
-      Ls += s_l[w];
-      O += s_o[w * 16 + d];
+      const float f = s_m[w] == -INFINITY ? 0.f : exp2f(s_m[w] - M);  // a wave without keys: -inf, weight 0
+      Ls += s_l[w] * f;
+      O += s_o[w * 16 + d] * f;
     }
     const uint32_t ob = (uint32_t)f2bf(O / Ls);
     const uint32_t pr = lane_xor1(ob);
