@@ -28,3 +28,9 @@ echo "engine tests rc=$?" >> $O/status.log
 grep -q " passed" $O/t_engine.log && ! grep -q "failed\|error" $O/t_engine.log && \
   timeout -k 10 240 python -u tools/engine_trace.py --out $O/engine_trace.json > $O/engine_trace.log 2>&1
 echo "trace rc=$?" >> $O/status.log
+cd $R
+LLJ_LIB=$R/scratch/eng_f16.so timeout -k 10 200 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread > $O/t_engine_f16.log 2>&1
+echo "engine f16 tests rc=$?" >> $O/status.log
+grep -q " passed" $O/t_engine_f16.log && ! grep -q "failed\|error" $O/t_engine_f16.log && \
+  LLJ_LIB=$R/scratch/eng_f16.so timeout -k 10 240 python -u tools/engine_trace.py --out $O/engine_trace_f16.json > $O/engine_trace_f16.log 2>&1
+echo "trace f16 rc=$?" >> $O/status.log

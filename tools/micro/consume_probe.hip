@@ -55,7 +55,7 @@ __global__ __launch_bounds__(512, 1) void probe(const uint4* __restrict__ fill, 
       ar[ci][t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(A + 256 * (ci * 7 + w) + 64 * (lane >> 4) + 16 * t));
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
   uint32_t xo = 0;
-  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int j = 0; j < tiles; ++j) {
     const int tb = (j * kc * NM) % 96;
     u32x4 wt[AREG_C][NM];
@@ -122,8 +122,11 @@ __global__ __launch_bounds__(512, 1) void probe(const uint4* __restrict__ fill, 
     acc0 += a0;
     acc1 += a1;
   }
-  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-  if (lane == 0) out[(size_t)blockIdx.x * 16 + w] = t1 - t0;
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) {
+    out[(size_t)blockIdx.x * 16 + w] = t1 - t0;
+    out[(size_t)blockIdx.x * 16 + 8 + w] = r1 - r0;  // 100 MHz ticks: the clock the loop ran at
+  }
   sink[(size_t)blockIdx.x * 512 + tid] = acc0[0] + acc1[1] + (float)(xo & 1);
 }
 
@@ -163,16 +166,18 @@ int main(int argc, char** argv) {
   std::vector<unsigned long long> ho(256 * 16);
   hipMemcpy(ho.data(), out, ho.size() * 8, hipMemcpyDeviceToHost);
   // per wave: cycles per block; per SIMD (waves w and w + 4 share SIMD w % 4): busiest
-  double sum = 0, worst = 0;
+  double sum = 0, worst = 0, ghz = 0;
   int n = 0;
   for (int b = 0; b < 256; ++b)
     for (int w = 0; w < ncw; ++w) {
       const int nch = (32 - w + ncw - 1) / ncw;
       const double c = (double)ho[b * 16 + w] / ((double)tiles * nch * nm);
       sum += c;
+      ghz += (double)ho[b * 16 + w] / ((double)ho[b * 16 + 8 + w] * 10.0);  // cycles per ns
       ++n;
       worst = std::max(worst, (double)ho[b * 16 + w]);
     }
+  printf("clock %.2f GHz; ", ghz / n);
   const double tot_blocks = 32.0 * nm * tiles;  // per CU
   printf("variant %d consumers %d NM %d tiles %d: cycles/block/wave avg %.1f; CU wall %.0f cycles = %.1f cycles per block per CU "
          "(%.1f per SIMD)\n",
