@@ -341,6 +341,10 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
 #pragma unroll
   for (int d = 0; d < GDEPTH; ++d) load_chunk(d, d);
   int c = 0;  // KC is a multiple of 2 (K % 128 == 0); the ring slots are static inside the unrolled body
+  // 64-deep chunks (all but LLM.int8): KC = K / 64 is even and >= 2, so with GDEPTH <= 2 the loop
+  // runs at least once and no tail step is left (without this the compiler keeps the prologue's
+  // chunk live across the loop for the tail and spills it at 256 VGPRs)
+  if constexpr (!I8 && GDEPTH <= 2) __builtin_assume(KC >= 2 && KC % 2 == 0);
   for (; c + GDEPTH <= KC; c += GDEPTH) {
 #pragma unroll
     for (int d = 0; d < GDEPTH; ++d) step(d, c + d);
