@@ -323,6 +323,42 @@ def time_dominant_kernel(model, B, iters=10):
     return avg_s, abytes
 
 
+def time_dominant_in_chain(sess, steps: int = 8, entry: str = "llj_norm_swiglu"):
+    """Average duration of the dominant launch INSIDE the decode chain: `steps` eager decode steps
+    of the session (the graph's kernels in the graph's order, with their real activation
+    dependencies and cache state), HIP events recorded on the launch stream right before and after
+    every `entry` launch. Beside time_dominant_kernel's isolated back-to-back loop (no dependency
+    between launches). The steps advance the session into the room ENGINE_TIMING_STEPS reserves."""
+    from lit_llama import _hip
+
+    orig = _hip.call
+    evs = []
+
+    def call(name, *args):
+        if name != entry:
+            return orig(name, *args)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = orig(name, *args)
+        e1.record()
+        evs.append((e0, e1))
+        return r
+
+    torch.cuda.synchronize()
+    _hip.call = call
+    try:
+        with torch.no_grad():
+            for _ in range(steps):
+                sess._step()
+        sess.steps_done += steps
+    finally:
+        _hip.call = orig
+    torch.cuda.synchronize()
+    if not evs:
+        return None
+    return sum(a.elapsed_time(b) for a, b in evs) / 1e3 / len(evs)
+
+
 def time_engine_kernel(sess, iters: int = 20):
     """Average duration of the persistent engine's step kernel (llj_engine_step: the whole decode
     step in ONE launch) over `iters` back-to-back eager launches on the session's stream, HIP
@@ -551,6 +587,14 @@ def main():
         k_s = time_engine_kernel(sess, iters=min(20, room - 3))
         k_bytes = sb
         k_gbs = k_bytes / k_s / 1e9
+    iso_s = None
+    if not engine:  # the chain's dominant launch timed inside eager decode steps (its in-graph neighbours)
+        sess = r["session"]
+        room = sess.total - (sess.t_prompt + sess.steps_done) - 1
+        in_s = time_dominant_in_chain(sess, steps=min(8, room - 1)) if room >= 2 else None
+        if in_s is not None:
+            iso_s, k_s = k_s, in_s
+            k_gbs = k_bytes / k_s / 1e9
     ach = achievable_read_gbs()
 
     pmc = pmc_traffic()
@@ -607,6 +651,9 @@ def main():
                          "kernel": ("engine_step_kernel (the whole decode step, csrc/engine.hip)" if engine else
                                     "gemv_kernel<W4,NORM,SWIGLU> (rms_2 + c_fc1/c_fc2 + silu*mul)"),
                          "bytes_per_launch": k_bytes, "avg_launch_us": round(k_s * 1e6, 2),
+                         **({"timing": "in the decode chain (eager steps, HIP events around each launch)",
+                             "isolated_avg_launch_us": round(iso_s * 1e6, 2),
+                             "isolated_frac": round(k_bytes / iso_s / 1e9 / HBM_PEAK_GBS, 4)} if iso_s else {}),
                          **({"chain_dominant_gemv": {"kernel": "gemv_kernel<W4,NORM,SWIGLU>", "avg_launch_us":
                                                      round(g_s * 1e6, 2), "bytes_per_launch": g_bytes,
                                                      "frac": round(g_gbs / HBM_PEAK_GBS, 4)}} if engine else {})},
