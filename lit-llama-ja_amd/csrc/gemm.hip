@@ -40,6 +40,8 @@
 // Tile order is XCD-aware: the 8 XCDs take contiguous ranges of tiles; inside a range bf16 weights
 // go m fastest (the row tiles of one weight panel run together on one XCD and share it through its
 // L2), int4 weights n fastest (one 128-row A panel shared while the XCD sweeps the columns).
+#include <cstdlib>
+
 #include "common.h"
 #include "i8ws.h"
 #include "lit_llama_amd.h"
@@ -74,6 +76,60 @@ struct GemmParams {
   const _Float16* w16;
   int kpad;
 };
+
+// One output element of a tile epilogue: y (the dequantized accumulator, fp32) at row m (live: m < M;
+// rows past M are computed on a clamped copy and never stored), column n of the 16-column block nblk;
+// row = lane & 15 (the column within the block). Every lane of the wave calls it (lane_xor1 pairs
+// neighbouring columns into one 4-byte store).
+template <int EP>
+__device__ __forceinline__ void gemm_store_elem(const GemmParams& p, float y, int m, int n, int nblk, bool live, int row,
+                                                int Cd) {
+  const int M = p.M;
+  if constexpr (EP == GEP_QKV) {
+    const float v = round_bf(y);  // c_attn output in bf16 (model.py:204), RoPE in fp32
+    const float partner = lane_xor1(v);
+    const int region = nblk / Cd;  // 0 q, 1 k, 2 v: uniform per 16-column block
+    const int nc = n - region * Cd;
+    const int h = nc / p.head_size, dd = nc % p.head_size;
+    const int mm = live ? m : M - 1;
+    const int b = mm / p.T, ps = p.pos[mm % p.T];
+    float out = v;
+    if (region < 2) {
+      const float2 cs = *reinterpret_cast<const float2*>(p.rope + ((size_t)ps * (p.head_size >> 1) + (dd >> 1)) * 2);
+      out = (dd & 1) ? (v * cs.x + partner * cs.y) : (v * cs.x - partner * cs.y);
+    }
+    const uint32_t ob = (uint32_t)f2bf(out);
+    const uint32_t pr = lane_xor1(ob);
+    if (live && !(dd & 1)) {
+      bf16_t* dst;
+      size_t ei;
+      if (region == 0) {
+        dst = p.q_out;
+        ei = (size_t)mm * Cd + nc;
+      } else {
+        const int slot = ps < p.S ? ps : ps % p.S;
+        dst = region == 1 ? p.kcache : p.vcache;
+        ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
+      }
+      *reinterpret_cast<uint32_t*>(dst + ei) = ob | (pr << 16);
+    }
+  } else {
+    bf16_t* cp = p.C + (size_t)(live ? m : M - 1) * p.ldc + n;
+    float o;
+    if constexpr (EP == GEP_RESID) {
+      o = round_bf(bf2f(*cp) + round_bf(y));  // x + y in bf16 (model.py:172-173)
+    } else if constexpr (EP == GEP_SILU_MUL) {
+      const float a1 = bf2f(*cp);  // bf16(c_fc1 x), stored by the first pass
+      const float sl = round_bf(a1 / (1.f + __expf(-a1)));  // F.silu in bf16
+      o = sl * round_bf(y);
+    } else {
+      o = y;
+    }
+    const uint32_t ob = (uint32_t)f2bf(o);
+    const uint32_t pr = lane_xor1(ob);
+    if (live && !(row & 1)) *reinterpret_cast<uint32_t*>(cp) = ob | (pr << 16);
+  }
+}
 
 constexpr int kGBM = 128, kGBN = 128, kGBK = 64, kGNT = 256;
 #ifndef LLJ_GEMM_PRIO
@@ -500,50 +556,7 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
           y = (float)iacc[i][j][r] * (sa * szn.x * (1.f / (127.f * 127.f)));
           y = (float)(_Float16)((float)(_Float16)y + sacc[i][j][r]);
         }
-        if constexpr (EP == GEP_QKV) {
-          const float v = round_bf(y);  // c_attn output in bf16 (model.py:204), RoPE in fp32
-          const float partner = lane_xor1(v);
-          const int region = nblk / Cd;  // 0 q, 1 k, 2 v: uniform per 16-column block
-          const int nc = n - region * Cd;
-          const int h = nc / p.head_size, dd = nc % p.head_size;
-          const int mm = live ? m : M - 1;
-          const int b = mm / p.T, ps = p.pos[mm % p.T];
-          float out = v;
-          if (region < 2) {
-            const float2 cs = *reinterpret_cast<const float2*>(p.rope + ((size_t)ps * (p.head_size >> 1) + (dd >> 1)) * 2);
-            out = (dd & 1) ? (v * cs.x + partner * cs.y) : (v * cs.x - partner * cs.y);
-          }
-          const uint32_t ob = (uint32_t)f2bf(out);
-          const uint32_t pr = lane_xor1(ob);
-          if (live && !(dd & 1)) {
-            bf16_t* dst;
-            size_t ei;
-            if (region == 0) {
-              dst = p.q_out;
-              ei = (size_t)mm * Cd + nc;
-            } else {
-              const int slot = ps < p.S ? ps : ps % p.S;
-              dst = region == 1 ? p.kcache : p.vcache;
-              ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
-            }
-            *reinterpret_cast<uint32_t*>(dst + ei) = ob | (pr << 16);
-          }
-        } else {
-          bf16_t* cp = p.C + (size_t)(live ? m : M - 1) * p.ldc + n;
-          float o;
-          if constexpr (EP == GEP_RESID) {
-            o = round_bf(bf2f(*cp) + round_bf(y));  // x + y in bf16 (model.py:172-173)
-          } else if constexpr (EP == GEP_SILU_MUL) {
-            const float a1 = bf2f(*cp);  // bf16(c_fc1 x), stored by the first pass
-            const float sl = round_bf(a1 / (1.f + __expf(-a1)));  // F.silu in bf16
-            o = sl * round_bf(y);
-          } else {
-            o = y;
-          }
-          const uint32_t ob = (uint32_t)f2bf(o);
-          const uint32_t pr = lane_xor1(ob);
-          if (live && !(row & 1)) *reinterpret_cast<uint32_t*>(cp) = ob | (pr << 16);
-        }
+        gemm_store_elem<EP>(p, y, m, n, nblk, live, row, Cd);
       }
     }
   }
@@ -565,6 +578,259 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
   return 0;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// 256-row LDS-DMA GEMM (bf16 and int4 W4P weights, M >= 256): a 512-thread workgroup (8 waves, one
+// per CU) owns a 256 x BN output tile (BN 256: waves 2 x 4 of 128 x 64; BN 128: 4 x 2 of 64 x 64)
+// and walks K in 64-deep chunks. A chunk's A tile (256 rows x 128 B) and B tile (bf16: BN rows x
+// 128 B; W4P: the 512-B half of each of its BN / 16 tiles that holds the chunk) go global -> LDS
+// by global_load_lds_dwordx4 (no VGPR staging, no ds_write), NST stages deep: the loads of chunks
+// t + 1 .. t + NST - 1 stay in flight across the barrier while chunk t is multiplied; the wait for
+// chunk t is a counted vmcnt (never 0 while a later chunk is outstanding) and the barrier a raw
+// s_barrier (a __syncthreads() would drain every DMA in flight). The LDS image is lane-linear (the
+// DMA writes base + 16 * lane) with the 16-B segments of a 128-B row permuted by
+// seg ^ ((row >> 1) & 7) on the SOURCE side, so a fragment read (16 rows x 16 B per lane group)
+// hits 16 distinct bank slots. int4: the 128 + zero offset is removed with the row sums of A,
+// which the waves form from the A fragments they already hold (v_dot2 with (1, 1); wave column wc
+// sums the 16-row blocks i = wc mod WN) and combine through LDS after the loop.
+#ifndef LLJ_GEMM_GLDS
+#define LLJ_GEMM_GLDS 0  // default until measured; LLJ_GEMM_GLDS=1 / 0 in the environment overrides
+#endif
+#ifndef LLJ_GLDS_COST128
+#define LLJ_GLDS_COST128 55  // time of a 256 x 128 tile in % of a 256 x 256 one (tile-shape choice)
+#endif
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int WF, int BN>
+struct GldsGeo {
+  static constexpr int WN = BN == 256 ? 4 : 2, WM = 8 / WN;
+  static constexpr int MI = 256 / WM / 16, NJ = BN / WN / 16;
+  static constexpr size_t SA = 256 * 128;
+  static constexpr size_t SB = WF == GWF_W4 ? 8192 : (size_t)BN * 128;  // W4 at BN 128: waves 4-7 stage a copy
+  static constexpr size_t STAGE = SA + SB;
+  static constexpr int NST = 3 * STAGE + 1024 <= 160 * 1024 ? 3 : 2;
+  static constexpr size_t LDS = NST * STAGE + 1024;  // + the row sums (W4)
+  static constexpr int NG = 4 + (WF == GWF_W4 ? 1 : BN / 64);  // glds per thread per chunk
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int WF, int EP, int BN>
+__global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
+  static_assert(WF == GWF_BF16 || WF == GWF_W4, "LDS-DMA GEMM: bf16 and int4 W4P");
+  using G = GldsGeo<WF, BN>;
+  constexpr int MI = G::MI, NJ = G::NJ, WN = G::WN, NST = G::NST;
+  constexpr bool NIB = WF == GWF_W4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w / WN, wc = w % WN;
+  const int row = lane & 15, g = lane >> 4;
+  const int M = p.M, K = p.K, KC = K / 64, KC128 = K / 128;
+  const int mtiles = (M + 255) / 256, ntiles = p.N / BN, total = mtiles * ntiles;
+  int t = blockIdx.x;
+  {  // contiguous tile ranges per XCD (bijective for any total)
+    const int q = total / 8, r = total % 8, x = t % 8;
+    t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + t / 8;
+  }
+  const int nb = t / mtiles, mb = t % mtiles;  // m fastest: a weight panel's row tiles run together
+  const int m0 = mb * 256, n0 = nb * BN;
+  float* rs_lds = reinterpret_cast<float*>(smem + NST * G::STAGE);
+
+  // ---- DMA sources: A rows q * 64 + 8 w + lane / 8 (q < 4), physical segment lane % 8 holds the
+  // logical segment (lane % 8) ^ ((row >> 1) & 7); bf16 B the same over BN rows
+  const int drow = 8 * w + (lane >> 3), dseg = (lane & 7) ^ ((drow >> 1) & 7);  // (row >> 1) & 7 same for +64 q
+  const bf16_t* asrc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int m = m0 + 64 * q + drow;
+    asrc[q] = p.A + (size_t)(m < M ? m : M - 1) * p.lda + 8 * dseg;
+  }
+  const char* bsrc;
+  if constexpr (NIB) {  // W4P: wave w stages tiles 2 w, 2 w + 1 (BN 128: waves 4-7 a copy of 0-3's)
+    const int tl = (2 * w + (lane >> 5)) % (BN / 16);
+    bsrc = reinterpret_cast<const char*>(p.W) + (size_t)(n0 / 16 + tl) * KC128 * 1024 + 16 * (lane & 31);
+  } else {
+    bsrc = reinterpret_cast<const char*>(reinterpret_cast<const bf16_t*>(p.W) + (size_t)(n0 + drow) * K + 8 * dseg);
+  }
+  auto stage = [&](int buf, int c) {
+    unsigned char* base = smem + (size_t)buf * G::STAGE;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds(asrc[q] + (size_t)c * 64, (lds_void_t*)(base + (64 * q + 8 * w) * 128), 16, 0, 0);
+    if constexpr (NIB) {
+      __builtin_amdgcn_global_load_lds(bsrc + (size_t)(c >> 1) * 1024 + 512 * (c & 1),
+                                       (lds_void_t*)(base + G::SA + 1024 * w), 16, 0, 0);
+    } else {
+#pragma unroll
+      for (int q = 0; q < BN / 64; ++q)
+        __builtin_amdgcn_global_load_lds(bsrc + ((size_t)64 * q * K + (size_t)c * 64) * 2,
+                                         (lds_void_t*)(base + G::SA + (64 * q + 8 * w) * 128), 16, 0, 0);
+    }
+  };
+
+  // ---- fragment reads: A row wr * 16 MI + 16 i + row, B row (column) wc * 16 NJ + 16 j + row; MFMA
+  // step s reads logical segment 4 s + g at physical (4 s + g) ^ sw
+  const int sw = (row >> 1) & 7;
+  const int aoff0 = (wr * 16 * MI + row) * 128, boff0 = (wc * 16 * NJ + row) * 128;
+  uint32_t msk = 0x000F000Fu, mag = 0x43004300u;
+  asm volatile("" : "+s"(msk));
+  asm volatile("" : "+v"(mag));
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // W4: partial row sums of A. The WN waves of a row group split the chunk's (block, k) pairs: WN 4
+  // -> wave wc sums the blocks of parity wc >> 1 in MFMA step wc & 1; WN 2 -> every block in step wc
+  float rsp[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) rsp[i] = 0.f;
+  if constexpr (NIB) {
+    if (tid < 256) rs_lds[tid] = 0.f;  // ordered before the adds by the K loop's barriers
+  }
+
+  auto compute = [&](int buf) {
+    const unsigned char* Ab = smem + (size_t)buf * G::STAGE;
+    const unsigned char* Bb = Ab + G::SA;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int so = ((4 * s + g) ^ sw) * 16;
+      bf16x8 af[MI], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + aoff0 + 16 * i * 128 + so);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (NIB) {  // word g of W4P lane 16 s + column of tile wc * NJ + j (the chunk's half)
+          const uint32_t wv = reinterpret_cast<const uint32_t*>(Bb)[((wc * NJ + j) * 32 + 16 * s + row) * 4 + g];
+          bfr[j] = __builtin_bit_cast(bf16x8, make_uint4(and_or(wv, msk, mag), and_or(wv >> 4, msk, mag),
+                                                         and_or(wv >> 8, msk, mag), and_or(wv >> 12, msk, mag)));
+        } else {
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bb + boff0 + 16 * j * 128 + so);
+        }
+      }
+      if constexpr (NIB) {
+        typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+        const bf16x2_t one2 = {(__bf16)1.0f, (__bf16)1.0f};
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const bool mine = WN == 4 ? ((i & 1) == (wc >> 1) && s == (wc & 1)) : s == wc;
+          if (mine) {
+            const u32x4 a = __builtin_bit_cast(u32x4, af[i]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              rsp[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a[e]), one2, rsp[i], false);
+          }
+        }
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  // ---- K loop: NST - 1 chunks staged ahead
+#pragma unroll
+  for (int c = 0; c < NST - 1; ++c)
+    if (c < KC) stage(c, c);
+  int cb = 0;  // buffer of chunk t
+  for (int tc = 0; tc < KC; ++tc) {
+    if constexpr (NST == 3) {
+      if (tc + 1 < KC) wait_vm<G::NG>(); else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of chunk t - 1 are done
+    __builtin_amdgcn_s_barrier();  // chunk t landed for every wave; chunk t - 1's buffer is free
+    if (tc + NST - 1 < KC) stage(cb == 0 ? NST - 1 : cb - 1, tc + NST - 1);
+    compute(cb);
+    cb = cb + 1 == NST ? 0 : cb + 1;
+  }
+
+  // ---- epilogue: lane holds rows m0 + wr * 16 MI + 16 i + 4 g + r, column n0 + wc * 16 NJ + 16 j + row
+  if constexpr (NIB) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {  // two waves hold parts of each row: 0 + a + b is order-free
+      if (WN == 4 && (i & 1) != (wc >> 1)) continue;
+      float v = rsp[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) atomicAdd(rs_lds + wr * 16 * MI + 16 * i + row, v);
+    }
+    __syncthreads();
+  }
+  const int Cd = p.n_head * p.head_size;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nblk = n0 + wc * 16 * NJ + 16 * j;
+    const int n = nblk + row;
+    float2 szn = make_float2(1.f, 0.f);
+    if constexpr (NIB) szn = p.sz[n];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ml = wr * 16 * MI + 16 * i + 4 * g + r;
+        const int m = m0 + ml;
+        float y = acc[i][j][r];
+        if constexpr (NIB) y = szn.x * (y - szn.y * rs_lds[ml]);
+        gemm_store_elem<EP>(p, y, m, n, nblk, m < M, row, Cd);
+      }
+    }
+  }
+}
+
+template <int WF, int EP, int BN>
+static int gemm_glds_launch(const GemmParams& p, hipStream_t s) {
+  auto kern = gemm_glds_kernel<WF, EP, BN>;
+  static bool attr_set = false;  // per instantiation, before any graph capture
+  const size_t lds = GldsGeo<WF, BN>::LDS;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  const int tiles = ((p.M + 255) / 256) * (p.N / BN);
+  hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), lds, s, p);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+// LLJ_GEMM_GLDS=1 / 0 in the environment: the LDS-DMA / the register-staged kernels (A/B in one process)
+static bool glds_enabled() {
+  const char* e = getenv("LLJ_GEMM_GLDS");
+  return e && e[0] ? e[0] != '0' : LLJ_GEMM_GLDS != 0;
+}
+
+// 256 x 256 or 256 x 128 tiles: the shape with the fewer tile-time units over the CUs (waves of
+// tiles rounded up, a 256 x 128 tile costing LLJ_GLDS_COST128 % of a 256 x 256 one)
+template <int WF, int EP>
+static int gemm_glds_run(const GemmParams& p, hipStream_t s) {
+  int cus = 256;
+  {
+    static int cached = 0;
+    if (!cached) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cached, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cached <= 0) cached = 256;
+    }
+    cus = cached;
+  }
+  const long mt = (p.M + 255) / 256;
+  const long w256 = p.N % 256 == 0 ? (mt * (p.N / 256) + cus - 1) / cus : -1;
+  const long w128 = (mt * (p.N / 128) + cus - 1) / cus;
+  const char* e = getenv("LLJ_GLDS_COST128");  // A/B and tests: 0 forces 256 x 128, >= 100 prefers 256 x 256
+  const long cost = e ? atol(e) : LLJ_GLDS_COST128;
+  if (w256 > 0 && 100 * w256 <= cost * w128) return gemm_glds_launch<WF, EP, 256>(p, s);
+  return gemm_glds_launch<WF, EP, 128>(p, s);
+}
+
 template <int EP>
 static int gemm_run(int wfmt, GemmParams& p, void* stream) {
   if (p.M < 1 || p.N % kGBN || p.K % kGBK || p.K < kGBK || (p.lda & 7)) return LLJ_EINVAL;
@@ -572,6 +838,7 @@ static int gemm_run(int wfmt, GemmParams& p, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (wfmt == GWF_W4) {
     if (!p.sz) return LLJ_EINVAL;
+    if (p.M >= 256 && p.K % 128 == 0 && glds_enabled()) return gemm_glds_run<GWF_W4, EP>(p, s);
     if (LLJ_GEMM_BM256_W4 && p.M >= 256) return gemm_launch<GWF_W4, EP, 256>(p, s);
     return gemm_launch<GWF_W4, EP>(p, s);
   }
@@ -581,6 +848,7 @@ static int gemm_run(int wfmt, GemmParams& p, void* stream) {
     return (p.sz && p.gch >= 1 && p.K % 128 == 0) ? gemm_launch<GWF_W4G, EP>(p, s) : LLJ_EINVAL;
   }
   if (wfmt == GWF_BF16) {
+    if (p.M >= 256 && glds_enabled()) return gemm_glds_run<GWF_BF16, EP>(p, s);
     if (LLJ_GEMM_BM256 && p.M >= 256) return gemm_launch<GWF_BF16, EP, 256>(p, s);
     return gemm_launch<GWF_BF16, EP>(p, s);
   }

@@ -901,6 +901,86 @@ def test_gemm_linear_and_resid(hip, wfmt, M, N, K):
     assert_bf16_close(xr.float().cpu().numpy(), x0 + bf16(y), f"gemm resid wfmt={wfmt}")
 
 
+GLDS_TILES = {"256x256": {"LLJ_GEMM_GLDS": "1", "LLJ_GLDS_COST128": "1000"},
+              "256x128": {"LLJ_GEMM_GLDS": "1", "LLJ_GLDS_COST128": "0"}, "regstaged": {"LLJ_GEMM_GLDS": "0"}}
+
+
+@pytest.fixture
+def glds_tile(request, monkeypatch):
+    """The prefill GEMM's M >= 256 kernel forced through its host-side knobs (read per call): the
+    LDS-DMA kernel's 256 x 256 or 256 x 128 tiles, or the register-staged kernel."""
+    for k, v in GLDS_TILES[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+@pytest.mark.parametrize("glds_tile", list(GLDS_TILES), indirect=True)
+@pytest.mark.parametrize("wfmt", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(256, 512, 256), (300, 4096, 4096), (520, 11008, 4096), (257, 4096, 11008)])
+def test_gemm_glds_tiles(hip, glds_tile, wfmt, M, N, K):
+    """The LDS-DMA prefill GEMM (global_load_lds staging, counted vmcnt, source-swizzled LDS image,
+    int4 row sums from the A fragments) in both tile shapes and the register-staged kernel, int4
+    W4P and bf16 weights, against the oracle: store and residual epilogues, ragged M (a partial
+    last row tile: rows past M clamped, never stored), K from 4 to 172 chunks."""
+    rng = np.random.default_rng(M + N + K + wfmt)
+    Wref, Wd, szd = quant_operands(hip, rng, wfmt, N, K)
+    x = bf16(rng.standard_normal((M, K)).astype(np.float32))
+    xd = T(x, torch.bfloat16)
+    out = torch.full((M + 1, N), 7.0, dtype=torch.bfloat16, device=dev)  # row M: canary
+    call(hip, "llj_gemm_linear", wfmt, xd.data_ptr(), K, Wd.data_ptr(), None if szd is None else szd.data_ptr(),
+         out.data_ptr(), N, M, N, K, st())
+    x0 = bf16(rng.standard_normal((M, N)).astype(np.float32))
+    xr = T(x0, torch.bfloat16)
+    call(hip, "llj_gemm_resid", wfmt, xd.data_ptr(), K, Wd.data_ptr(), None if szd is None else szd.data_ptr(),
+         xr.data_ptr(), N, M, N, K, st())
+    torch.cuda.synchronize()
+    y = x @ Wref.T
+    o = out.float().cpu().numpy()
+    assert_bf16_close(o[:M], y, f"gemm {glds_tile} wfmt={wfmt} M={M} N={N} K={K}")
+    assert (o[M] == 7.0).all(), "wrote past row M"
+    assert_bf16_close(xr.float().cpu().numpy(), x0 + bf16(y), f"gemm resid {glds_tile} wfmt={wfmt}")
+
+
+@pytest.mark.parametrize("glds_tile", ["256x256", "256x128"], indirect=True)
+@pytest.mark.parametrize("wfmt", [0, 1])
+def test_gemm_glds_qkv_swiglu(hip, glds_tile, wfmt):
+    """The LDS-DMA GEMM's QKV + RoPE + KV-write and silu * mul epilogues in both tile shapes
+    (M = 2 x 150 prompt rows, 8 heads of 128; SwiGLU hidden 2816 = 11 x 256)."""
+    rng = np.random.default_rng(90 + wfmt)
+    B, T_, nh, hs, S = 2, 150, 8, 128, 256
+    C, M = nh * hs, B * T_
+    x = bf16(rng.standard_normal((M, C)).astype(np.float32))
+    xd = T(x, torch.bfloat16)
+    rope = O.build_rope_cache(512, hs)
+    pos = np.arange(5, 5 + T_, dtype=np.int32)
+    Wref, Wd, szd = quant_operands(hip, rng, wfmt, 3 * C, C)
+    q = torch.zeros(M, C, dtype=torch.bfloat16, device=dev)
+    kc = torch.zeros(B, nh, S, hs, dtype=torch.bfloat16, device=dev)
+    vc = torch.zeros_like(kc)
+    rd, pd = T(rope), T(pos)
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    call(hip, "llj_gemm_qkv_rope", wfmt, xd.data_ptr(), Wd.data_ptr(), P(szd), q.data_ptr(), kc.data_ptr(),
+         vc.data_ptr(), rd.data_ptr(), pd.data_ptr(), B, T_, C, nh, S, st())
+    H = 2816
+    W1, W1d, s1 = quant_operands(hip, rng, wfmt, H, C)
+    W2, W2d, s2 = quant_operands(hip, rng, wfmt, H, C)
+    h = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+    call(hip, "llj_gemm_linear", wfmt, xd.data_ptr(), C, W1d.data_ptr(), P(s1), h.data_ptr(), H, M, H, C, st())
+    call(hip, "llj_gemm_silu_mul", wfmt, xd.data_ptr(), C, W2d.data_ptr(), P(s2), h.data_ptr(), H, M, H, C, st())
+    torch.cuda.synchronize()
+    qkv = bf16(x @ Wref.T)
+    qe = O.apply_rope(qkv[:, :C].reshape(B, T_, nh, hs), rope[pos]).reshape(M, C)
+    ke = O.apply_rope(qkv[:, C:2 * C].reshape(B, T_, nh, hs), rope[pos])
+    ve = qkv[:, 2 * C:].reshape(B, T_, nh, hs)
+    assert_bf16_close(q.float().cpu().numpy(), qe, f"gemm q {glds_tile}")
+    kcn, vcn = kc.float().cpu().numpy(), vc.float().cpu().numpy()
+    slots = pos % S
+    assert_bf16_close(kcn[:, :, slots].transpose(0, 2, 1, 3), ke, f"gemm k cache {glds_tile}")
+    assert_bf16_close(vcn[:, :, slots].transpose(0, 2, 1, 3), ve, f"gemm v cache {glds_tile}")
+    hexp = bf16(bf16(O.silu(bf16(x @ W1.T))) * bf16(x @ W2.T))
+    assert_bf16_close(h.float().cpu().numpy(), hexp, f"gemm swiglu {glds_tile}", rel=3e-2)
+
+
 def _i8_operands(hip, W):
     """CB / SCB of an LLM.int8 weight (llj_i8_quant_weight, checked against the oracle's rule) and
     CB re-tiled into I8P (what Linear8bitLt holds on the device)."""

@@ -29,10 +29,15 @@ if grep -q " passed" $O/t_engine_f16.log && ! grep -q "failed\|error" $O/t_engin
 fi
 timeout -k 10 200 python -u -m pytest tests/test_generic_gpu.py -k "int8" -q --timeout 120 --timeout-method thread > $O/t_generic_i8.log 2>&1
 chk "generic int8" $?
-timeout -k 10 200 python -u -m pytest tests/test_model_7b_gpu.py -k "prefill" -q --timeout 150 --timeout-method thread > $O/t_prefill.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "gemm" -q --timeout 120 --timeout-method thread > $O/t_gemm.log 2>&1
+chk "gemm tests" $?
+LLJ_GEMM_GLDS=1 timeout -k 10 200 python -u -m pytest tests/test_model_7b_gpu.py -k "prefill" -q --timeout 150 --timeout-method thread > $O/t_prefill.log 2>&1
 chk "prefill tests" $?
-timeout -k 10 300 python -u tools/prefill_bench.py --T 512 2048 --modes gptq.int4 none llm.int8 > $O/prefill_bench.log 2>&1
-chk "prefill bench" $?
+for cfg in "LLJ_GEMM_GLDS=0" "LLJ_GLDS_COST128=55" "LLJ_GLDS_COST128=0" "LLJ_GLDS_COST128=1000"; do
+  echo "== $cfg" >> $O/prefill_bench.log
+  env LLJ_GEMM_GLDS=1 $cfg timeout -k 10 200 python -u tools/prefill_bench.py --T 2048 --modes gptq.int4 none >> $O/prefill_bench.log 2>&1
+  chk "prefill bench $cfg" $?
+done
 (cd /tmp && timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1); chk list $?
 bash tools/engine_pmc.sh r04c_engine_pmc >> $O/status.log 2>&1; chk "engine pmc" $?
 for reg in random none 6x20; do
