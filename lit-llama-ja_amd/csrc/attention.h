@@ -55,9 +55,12 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   const int C = nh * HS;
   const size_t base = ((size_t)(b * nh + h) * S) * HS + sub * DPL;  // elements
   // K/V rows of one pass (U keys of this group): every load first, rows clamped into the cache
-  auto load_pass = [&](int j0, int jlim, uint32_t (&kw)[U][DPL / 2], uint32_t (&vw)[U][DPL / 2]) {
+  // keys u in [u0, u1) of a pass; past jlim: row 0 (an L2 hit after the first pass, never used)
+  auto load_pass = [&](int j0, int jlim, uint32_t (&kw)[U][DPL / 2], uint32_t (&vw)[U][DPL / 2], int u0 = 0,
+                       int u1 = U) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      if (u < u0 || u >= u1) continue;
       const int j = j0 + NG * u < jlim ? j0 + NG * u : 0;
       const size_t eo = base + (size_t)j * HS;
       if constexpr (DPL == 8) {
@@ -74,13 +77,15 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
     }
   };
   uint32_t kw[U][DPL / 2], vw[U][DPL / 2];
-  // the first pass (keys kg + NG u of slots 0 .. NG U - 1) is loaded before the position is
-  // known: the cache rows exist whatever p is, and keys past the valid range are masked below,
-  // so the position read and the first K/V reads are one memory latency instead of two. Only
+  // the first half of the first pass (keys kg + NG u, u < U / 2: slots 0 .. NG U / 2 - 1) is
+  // loaded before the position is known: the cache rows exist whatever p is, and keys past the
+  // valid range are masked below, so the position read and the first K/V reads are one memory
+  // latency instead of two; the second half waits for the position and reads only valid rows
+  // (a whole speculative pass read 128 rows at p = 80: 1.6x the K/V bytes the step uses). Only
   // for small grids (bs = 1: 32 blocks), where the launch is latency-bound; with many blocks the
   // extra rows past p cost more bandwidth than the latency saved (7B bs=8: 1.79 -> 1.87 ms)
   const bool spec = !PART && gridDim.x * gridDim.y <= 64;
-  if (spec) load_pass(kg, S, kw, vw);
+  if (spec) load_pass(kg, S, kw, vw, 0, U / 2);
   const int ps = pos[t];
   const int nvalid = ps < S ? ps + 1 : S;
   // key range of this block (the whole valid range unless split)
@@ -117,6 +122,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   bool first = spec;
   for (int j0 = jbeg + kg; j0 < jend; j0 += NG * U) {
     if (!first) load_pass(j0, jend, kw, vw);
+    else load_pass(j0, jend, kw, vw, U / 2, U);  // the speculative pass's second half
     first = false;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -240,9 +246,12 @@ __device__ __forceinline__ void attention_fsplit_body(const bf16_t* __restrict__
   const int sub = threadIdx.x & 15, kg = threadIdx.x >> 4;
   const int C = nh * HS;
   const size_t base = ((size_t)(b * nh + h) * S) * HS + sub * DPL;
-  auto load_pass = [&](int j0, int jlim, uint32_t (&kw)[U][DPL / 2], uint32_t (&vw)[U][DPL / 2]) {
+  // keys u in [u0, u1) of a pass; past jlim: row 0 (an L2 hit after the first pass, never used)
+  auto load_pass = [&](int j0, int jlim, uint32_t (&kw)[U][DPL / 2], uint32_t (&vw)[U][DPL / 2], int u0 = 0,
+                       int u1 = U) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      if (u < u0 || u >= u1) continue;
       const int j = j0 + NG * u < jlim ? j0 + NG * u : 0;
       const size_t eo = base + (size_t)j * HS;
       if constexpr (DPL == 8) {
