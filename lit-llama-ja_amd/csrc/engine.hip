@@ -580,11 +580,18 @@ __device__ __forceinline__ void consume_t(Ctx& X, const Lds& L, const float2* eo
 #pragma unroll
         for (int ci = 0; ci < AREG_C; ++ci) {
           if (ci < nch) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) a0 = mfma_a(ar[ci][t], LLJ_DQ(wt[ci][0][t]), a0);
             if constexpr (NM == 2) {
 #pragma unroll
-              for (int t = 0; t < 4; ++t) a1 = mfma_a(ar[ci][t], LLJ_DQ(wt[ci][1][t]), a1);
+              for (int t = 0; t < 4; ++t) {
+                a0 = mfma_a(ar[ci][t], LLJ_DQ(wt[ci][0][t]), a0);
+                a1 = mfma_a(ar[ci][t], LLJ_DQ(wt[ci][1][t]), a1);
+              }
+            } else {  // two independent chains (odd fragments into a1): no MFMA waits on its predecessor
+#pragma unroll
+              for (int t = 0; t < 4; t += 2) {
+                a0 = mfma_a(ar[ci][t], LLJ_DQ(wt[ci][0][t]), a0);
+                a1 = mfma_a(ar[ci][t + 1], LLJ_DQ(wt[ci][0][t + 1]), a1);
+              }
             }
           }
         }
@@ -607,16 +614,24 @@ __device__ __forceinline__ void consume_t(Ctx& X, const Lds& L, const float2* eo
 #pragma unroll
           for (int u = 0; u < KB; ++u) {
             if (u < nbat) {
-#pragma unroll
-              for (int t = 0; t < 4; ++t) a0 = mfma_a(af[u][t], LLJ_DQ(wt[u][0][t]), a0);
               if constexpr (NM == 2) {
 #pragma unroll
-                for (int t = 0; t < 4; ++t) a1 = mfma_a(af[u][t], LLJ_DQ(wt[u][1][t]), a1);
+                for (int t = 0; t < 4; ++t) {
+                  a0 = mfma_a(af[u][t], LLJ_DQ(wt[u][0][t]), a0);
+                  a1 = mfma_a(af[u][t], LLJ_DQ(wt[u][1][t]), a1);
+                }
+              } else {
+#pragma unroll
+                for (int t = 0; t < 4; t += 2) {
+                  a0 = mfma_a(af[u][t], LLJ_DQ(wt[u][0][t]), a0);
+                  a1 = mfma_a(af[u][t + 1], LLJ_DQ(wt[u][0][t + 1]), a1);
+                }
               }
             }
           }
         }
       }
+      if constexpr (NM == 1) a0 += a1;
       if (lane < 16) {  // partial sums of output row 0 (lanes 0..15, register 0)
         red[((w * TG + jj) * 2 + 0) * 16 + lane] = a0[0];
         red[((w * TG + jj) * 2 + 1) * 16 + lane] = a1[0];

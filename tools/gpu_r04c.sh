@@ -12,7 +12,7 @@ chk() {  # chk <name> <rc>: log; stop on a crash / limit (test failures, rc 1, c
   echo "$1 rc=$2" >> $O/status.log
   case $2 in 124|134|137|139|-6|-11) echo "stopping after $1" >> $O/status.log; exit $2;; esac
 }
-for v in 0 1 2 3 4; do timeout -k 5 30 tools/micro/consume_probe $v 7 2 64 >> $O/consume_probe.log 2>&1; chk "probe $v" $?; done
+for v in 0 1 2 3 4 5 6; do timeout -k 5 30 tools/micro/consume_probe $v 7 2 64 >> $O/consume_probe.log 2>&1; chk "probe $v" $?; done
 timeout -k 5 30 tools/micro/consume_probe 0 7 1 64 >> $O/consume_probe.log 2>&1; chk "probe nm1" $?
 timeout -k 5 30 tools/micro/consume_probe 0 4 2 64 >> $O/consume_probe.log 2>&1; chk "probe c4" $?
 timeout -k 5 30 tools/micro/consume_probe 0 8 2 64 >> $O/consume_probe.log 2>&1; chk "probe c8" $?
@@ -29,7 +29,7 @@ if grep -q " passed" $O/t_engine_f16.log && ! grep -q "failed\|error" $O/t_engin
 fi
 timeout -k 10 200 python -u -m pytest tests/test_generic_gpu.py -k "int8" -q --timeout 120 --timeout-method thread > $O/t_generic_i8.log 2>&1
 chk "generic int8" $?
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "gemm" -q --timeout 120 --timeout-method thread > $O/t_gemm.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "gemm or test_attention" -q --timeout 120 --timeout-method thread > $O/t_gemm.log 2>&1
 chk "gemm tests" $?
 LLJ_GEMM_GLDS=1 timeout -k 10 200 python -u -m pytest tests/test_model_7b_gpu.py -k "prefill" -q --timeout 150 --timeout-method thread > $O/t_prefill.log 2>&1
 chk "prefill tests" $?

@@ -7,7 +7,8 @@
 // Variants: 0 the engine's loop, 1 MFMA on the raw codes (no dequant VALU), 2 dequant only (no
 // MFMA; results kept live), 3 dequant with 20 instead of 28 VALU ops per block (pairs 1/3 by
 // v_and_or on a pre-shifted word: the layout a re-packed tile would need), 4 the engine's loop with
-// the chunk's NM x 4 MFMAs issued after all its dequant.
+// the chunk's NM x 4 MFMAs issued after all its dequant, 5 the engine's loop with 4 independent
+// accumulators per matrix (fragment t into accumulator t: no dependent MFMA chain), 6 with 2.
 // Usage: consume_probe <variant> <consumer waves> <NM> <tiles>
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -66,6 +67,7 @@ __global__ __launch_bounds__(512, 1) void probe(const uint4* __restrict__ fill, 
       for (int m = 0; m < NM; ++m) wt[ci][m] = *reinterpret_cast<const u32x4*>(ring + (size_t)((b + m) % 104) * 1024 + 16 * lane);
     }
     f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+    f32x4 q0[4] = {a0, a0, a0, a0}, q1[4] = {a0, a0, a0, a0};
 #pragma unroll
     for (int ci = 0; ci < AREG_C; ++ci) {
       if (ci < nch) {
@@ -104,6 +106,14 @@ __global__ __launch_bounds__(512, 1) void probe(const uint4* __restrict__ fill, 
 #pragma unroll
             for (int t = 0; t < 4; ++t) a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[ci][t], dequant5(wt[ci][1][t], msk, mag), a1, 0, 0, 0);
           }
+        } else if constexpr (VAR == 5 || VAR == 6) {
+          constexpr int NA = VAR == 5 ? 4 : 2;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            q0[t % NA] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[ci][t], dequant(wt[ci][0][t], msk, mag), q0[t % NA], 0, 0, 0);
+            if constexpr (NM == 2)
+              q1[t % NA] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[ci][t], dequant(wt[ci][1][t], msk, mag), q1[t % NA], 0, 0, 0);
+          }
         } else {
           bf16x8 d0[4], d1[4];
 #pragma unroll
@@ -119,8 +129,8 @@ __global__ __launch_bounds__(512, 1) void probe(const uint4* __restrict__ fill, 
         }
       }
     }
-    acc0 += a0;
-    acc1 += a1;
+    acc0 += a0 + (q0[0] + q0[1]) + (q0[2] + q0[3]);
+    acc1 += a1 + (q1[0] + q1[1]) + (q1[2] + q1[3]);
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   if (lane == 0) {
@@ -158,7 +168,9 @@ int main(int argc, char** argv) {
       case 1: R(1); break;
       case 2: R(2); break;
       case 3: R(3); break;
-      default: R(4); break;
+      case 4: R(4); break;
+      case 5: R(5); break;
+      default: R(6); break;
     }
 #undef R
     if (hipDeviceSynchronize() != hipSuccess) return 3;
