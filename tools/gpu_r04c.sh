@@ -33,7 +33,7 @@ timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "gemm or test
 chk "gemm tests" $?
 LLJ_GEMM_GLDS=1 timeout -k 10 200 python -u -m pytest tests/test_model_7b_gpu.py -k "prefill" -q --timeout 150 --timeout-method thread > $O/t_prefill.log 2>&1
 chk "prefill tests" $?
-for cfg in "LLJ_GEMM_GLDS=0" "LLJ_GLDS_COST128=55" "LLJ_GLDS_COST128=0" "LLJ_GLDS_COST128=1000"; do
+for cfg in "LLJ_GEMM_GLDS=0" "LLJ_GLDS_COST128=55" "LLJ_GLDS_COST128=0" "LLJ_GLDS_COST128=1000" "LLJ_FLASH_QB=2"; do
   echo "== $cfg" >> $O/prefill_bench.log
   env LLJ_GEMM_GLDS=1 $cfg timeout -k 10 200 python -u tools/prefill_bench.py --T 2048 --modes gptq.int4 none >> $O/prefill_bench.log 2>&1
   chk "prefill bench $cfg" $?
