@@ -400,7 +400,7 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
   // 64-deep chunks (all but LLM.int8): KC = K / 64 is even and >= 2, so with GDEPTH <= 2 the loop
   // runs at least once and no tail step is left (without this the compiler keeps the prologue's
   // chunk live across the loop for the tail and spills it at 256 VGPRs)
-  if constexpr (!I8 && GDEPTH <= 2) __builtin_assume(KC >= 2 && KC % 2 == 0);
+  if constexpr ((WF == GWF_W4 || WF == GWF_BF16) && GDEPTH <= 2) __builtin_assume(KC >= 2 && KC % 2 == 0);
   for (; c + GDEPTH <= KC; c += GDEPTH) {
 #pragma unroll
     for (int d = 0; d < GDEPTH; ++d) step(d, c + d);
@@ -711,17 +711,14 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
           bfr[j] = *reinterpret_cast<const bf16x8*>(Bb + boff0 + 16 * j * 128 + so);
         }
       }
-      if constexpr (NIB) {
-        typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-        const bf16x2_t one2 = {(__bf16)1.0f, (__bf16)1.0f};
+      if constexpr (NIB) {  // (not v_dot2c_f32_bf16: ROCm 7.2 clang feeds element 0 of a bit-cast vector to every call)
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const bool mine = WN == 4 ? ((i & 1) == (wc >> 1) && s == (wc & 1)) : s == wc;
           if (mine) {
             const u32x4 a = __builtin_bit_cast(u32x4, af[i]);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              rsp[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a[e]), one2, rsp[i], false);
+            const f32x2 p2 = (unpk(a[0]) + unpk(a[1])) + (unpk(a[2]) + unpk(a[3]));
+            rsp[i] += p2.x + p2.y;
           }
         }
       }
