@@ -323,40 +323,23 @@ def time_dominant_kernel(model, B, iters=10):
     return avg_s, abytes
 
 
-def time_dominant_in_chain(sess, steps: int = 8, entry: str = "llj_norm_swiglu"):
-    """Average duration of the dominant launch INSIDE the decode chain: `steps` eager decode steps
-    of the session (the graph's kernels in the graph's order, with their real activation
-    dependencies and cache state), HIP events recorded on the launch stream right before and after
-    every `entry` launch. Beside time_dominant_kernel's isolated back-to-back loop (no dependency
-    between launches). The steps advance the session into the room ENGINE_TIMING_STEPS reserves."""
-    from lit_llama import _hip
+def graph_kernel_us(kernel_prefix: str = "void llj::gemv_kernel<0, 2, 3, 4, 4, 1, 1>"):
+    """In-graph average duration of the dominant launch from the newest committed kernel trace of
+    the decode graph alone: profiles/<round>_graph_kernel_stats.csv, the rocprofv3 --kernel-trace
+    --stats summary of `bench.py --decode-only` (graph replays only: no isolated loop in the
+    process, so the average is over launches inside the captured chain). None when absent."""
+    import csv
 
-    orig = _hip.call
-    evs = []
-
-    def call(name, *args):
-        if name != entry:
-            return orig(name, *args)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        r = orig(name, *args)
-        e1.record()
-        evs.append((e0, e1))
-        return r
-
-    torch.cuda.synchronize()
-    _hip.call = call
-    try:
-        with torch.no_grad():
-            for _ in range(steps):
-                sess._step()
-        sess.steps_done += steps
-    finally:
-        _hip.call = orig
-    torch.cuda.synchronize()
-    if not evs:
-        return None
-    return sum(a.elapsed_time(b) for a, b in evs) / 1e3 / len(evs)
+    best = None
+    for p in sorted((REPO / "profiles").glob("r*_graph_kernel_stats.csv")):
+        try:
+            with open(p) as f:
+                for r in csv.DictReader(f):
+                    if r["Name"].startswith(kernel_prefix):
+                        best = (float(r["AverageNs"]) / 1e3, p.name)
+        except (OSError, KeyError, ValueError):
+            continue
+    return best
 
 
 def time_engine_kernel(sess, iters: int = 20):
@@ -525,6 +508,8 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the LLaMA-13B replica leg (C4)")
     ap.add_argument("--only-dominant", action="store_true",
                     help="profiling aid: only the dominant-kernel loop (for the PMC traffic passes)")
+    ap.add_argument("--decode-only", action="store_true",
+                    help="profiling aid: only the timed decode (graph replays), printed as a short line")
     ap.add_argument("--eager", action="store_true",
                     help="profiling aid: decode steps launched one by one instead of graph replays (PMC passes)")
     ap.add_argument("--stub", action="store_true",
@@ -568,6 +553,11 @@ def main():
         return
     r = time_decode(model, args.batch, args.prompt_len, S, args.warmup, args.steps, ws, use_graph=not args.eager)
     t_max, tokens = aggregate(r["seconds"], r["tokens"], ws)
+    if args.decode_only:
+        if rank == 0:
+            print(json.dumps({"decode_only": True, "tokens_per_s": round(tokens / t_max, 2),
+                              "ms_per_step": round(t_max / args.steps * 1e3, 4)}), flush=True)
+        return
     value = tokens / t_max
     ms_per_step = t_max / args.steps * 1e3
     sb = step_bytes(model, args.batch, r["pos_mean"])
@@ -587,14 +577,7 @@ def main():
         k_s = time_engine_kernel(sess, iters=min(20, room - 3))
         k_bytes = sb
         k_gbs = k_bytes / k_s / 1e9
-    iso_s = None
-    if not engine:  # the chain's dominant launch timed inside eager decode steps (its in-graph neighbours)
-        sess = r["session"]
-        room = sess.total - (sess.t_prompt + sess.steps_done) - 1
-        in_s = time_dominant_in_chain(sess, steps=min(8, room - 1)) if room >= 2 else None
-        if in_s is not None:
-            iso_s, k_s = k_s, in_s
-            k_gbs = k_bytes / k_s / 1e9
+    in_graph = graph_kernel_us() if not engine else None
     ach = achievable_read_gbs()
 
     pmc = pmc_traffic()
@@ -651,9 +634,10 @@ def main():
                          "kernel": ("engine_step_kernel (the whole decode step, csrc/engine.hip)" if engine else
                                     "gemv_kernel<W4,NORM,SWIGLU> (rms_2 + c_fc1/c_fc2 + silu*mul)"),
                          "bytes_per_launch": k_bytes, "avg_launch_us": round(k_s * 1e6, 2),
-                         **({"timing": "in the decode chain (eager steps, HIP events around each launch)",
-                             "isolated_avg_launch_us": round(iso_s * 1e6, 2),
-                             "isolated_frac": round(k_bytes / iso_s / 1e9 / HBM_PEAK_GBS, 4)} if iso_s else {}),
+                         **({"in_graph_avg_launch_us": round(in_graph[0], 2),
+                             "in_graph_frac": round(k_bytes / (in_graph[0] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                             "in_graph_source": f"profiles/{in_graph[1]} (rocprofv3 kernel trace of bench.py --decode-only)"}
+                            if in_graph and head7 else {}),
                          **({"chain_dominant_gemv": {"kernel": "gemv_kernel<W4,NORM,SWIGLU>", "avg_launch_us":
                                                      round(g_s * 1e6, 2), "bytes_per_launch": g_bytes,
                                                      "frac": round(g_gbs / HBM_PEAK_GBS, 4)}} if engine else {})},

@@ -593,8 +593,11 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
 // hits 16 distinct bank slots. int4: the 128 + zero offset is removed with the row sums of A,
 // which the waves form from the A fragments they already hold (v_dot2 with (1, 1); wave column wc
 // sums the 16-row blocks i = wc mod WN) and combine through LDS after the loop.
-#ifndef LLJ_GEMM_GLDS
-#define LLJ_GEMM_GLDS 0  // default until measured; LLJ_GEMM_GLDS=1 / 0 in the environment overrides
+#ifndef LLJ_GEMM_GLDS_BF16
+#define LLJ_GEMM_GLDS_BF16 1  // 7B 2048-token bf16 window 43.1 -> 36.5 ms (profiles/r04_prefill_ab.json)
+#endif
+#ifndef LLJ_GEMM_GLDS_W4
+#define LLJ_GEMM_GLDS_W4 0  // int4: 42.5 ms vs 37.6 with the register-staged 256-row kernel
 #endif
 #ifndef LLJ_GLDS_COST128
 #define LLJ_GLDS_COST128 55  // time of a 256 x 128 tile in % of a 256 x 256 one (tile-shape choice)
@@ -798,10 +801,12 @@ static int gemm_glds_launch(const GemmParams& p, hipStream_t s) {
   return 0;
 }
 
-// LLJ_GEMM_GLDS=1 / 0 in the environment: the LDS-DMA / the register-staged kernels (A/B in one process)
-static bool glds_enabled() {
+// LLJ_GEMM_GLDS=1 / 0 in the environment: the LDS-DMA / the register-staged kernels for every
+// format (A/B in one process); otherwise the per-format default
+static bool glds_enabled(int wf) {
   const char* e = getenv("LLJ_GEMM_GLDS");
-  return e && e[0] ? e[0] != '0' : LLJ_GEMM_GLDS != 0;
+  if (e && e[0]) return e[0] != '0';
+  return wf == GWF_BF16 ? LLJ_GEMM_GLDS_BF16 != 0 : LLJ_GEMM_GLDS_W4 != 0;
 }
 
 // 256 x 256 or 256 x 128 tiles: the shape with the fewer tile-time units over the CUs (waves of
@@ -835,7 +840,7 @@ static int gemm_run(int wfmt, GemmParams& p, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (wfmt == GWF_W4) {
     if (!p.sz) return LLJ_EINVAL;
-    if (p.M >= 256 && p.K % 128 == 0 && glds_enabled()) return gemm_glds_run<GWF_W4, EP>(p, s);
+    if (p.M >= 256 && p.K % 128 == 0 && glds_enabled(GWF_W4)) return gemm_glds_run<GWF_W4, EP>(p, s);
     if (LLJ_GEMM_BM256_W4 && p.M >= 256) return gemm_launch<GWF_W4, EP, 256>(p, s);
     return gemm_launch<GWF_W4, EP>(p, s);
   }
@@ -845,7 +850,7 @@ static int gemm_run(int wfmt, GemmParams& p, void* stream) {
     return (p.sz && p.gch >= 1 && p.K % 128 == 0) ? gemm_launch<GWF_W4G, EP>(p, s) : LLJ_EINVAL;
   }
   if (wfmt == GWF_BF16) {
-    if (p.M >= 256 && glds_enabled()) return gemm_glds_run<GWF_BF16, EP>(p, s);
+    if (p.M >= 256 && glds_enabled(GWF_BF16)) return gemm_glds_run<GWF_BF16, EP>(p, s);
     if (LLJ_GEMM_BM256 && p.M >= 256) return gemm_launch<GWF_BF16, EP, 256>(p, s);
     return gemm_launch<GWF_BF16, EP>(p, s);
   }

@@ -1219,7 +1219,12 @@ template <int WF, int AM>
 constexpr bool tpw_ok() { return (WF == WF_W4 || WF == WF_W8) && AM != AM_GLOBAL && LLJ_TPW_MAX > 1; }
 
 // the LDS A image must leave room for the reduction scratch: <= 96 KiB, M <= 8 rows
-static inline bool lds_fits(int wf, int M, int K) { return M <= 8 && a_image_bytes(wf, AM_LDS, M, K) <= 96 * 1024; }
+#ifndef LLJ_GEMV_LDS_A_MAX
+#define LLJ_GEMV_LDS_A_MAX (96 * 1024)  // profiling variant: 56 KiB keeps every non-int8 launch under 64 KiB
+#endif
+static inline bool lds_fits(int wf, int M, int K) {
+  return M <= 8 && a_image_bytes(wf, AM_LDS, M, K) <= (wf == WF_I8 ? 96 * 1024 : LLJ_GEMV_LDS_A_MAX);
+}
 
 // waves per workgroup: the global-A form (rows whose A image does not fit the LDS) keeps twice
 // as many waves, each with fewer chunks, for more A-fragment loads in flight
@@ -1245,30 +1250,16 @@ constexpr int d_of() {
                 : (EP == EP_SWIGLU ? kD : EP == EP_RESID ? LLJ_DR : LLJ_D1);
 }
 
-#ifndef LLJ_GEMV_ATTR_EXACT
-#define LLJ_GEMV_ATTR_EXACT 0  // profiling variant: the dynamic-LDS attribute set to each launch's own size
-#endif
 template <int WF, int AM, int EP, int MB, int NW, int TPW>
 static int launch_t(const GemvParams& p, hipStream_t s) {
   const size_t sm = gemv_smem(WF, AM, p.M, p.K, NW, TPW);
   auto kern = gemv_kernel<WF, AM, EP, NW, d_of<EP, MB>(), MB, TPW>;
-#if LLJ_GEMV_ATTR_EXACT
-  // eager runs only (a captured node needs the attribute >= its size at every replay): rocprofv3
-  // --pmc passes over launches whose size is below a larger attribute ended in a host SIGSEGV
-  static size_t attr_sz = 0;
-  if (sm > 64 * 1024 && sm != attr_sz) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    if (e != hipSuccess) return (int)e;
-    attr_sz = sm;
-  }
-#else
   static bool attr_set = false;  // per instantiation; set before any graph capture
   if (sm > 64 * 1024 && !attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-#endif
   const int ntiles = p.N / 16;
   hipLaunchKernelGGL(kern, dim3((ntiles + TPW - 1) / TPW), dim3(NW * 64), sm, s, p);
   LLJ_CHECK_LAUNCH();

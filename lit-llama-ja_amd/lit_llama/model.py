@@ -93,6 +93,8 @@ llama_configs = {
 QKV_ROWS = 8    # fused-norm kernels stage <= 8 rows in LDS
 LIN_ROWS = 16   # plain linear kernels take <= 16 rows per launch
 I8_ROWS = 8     # int8 kernels quantize <= 8 rows in LDS
+if os.environ.get("LLJ_I8_ROWS"):  # profiling only: smaller int8 row slices (A images under 64 KiB of LDS)
+    I8_ROWS = max(1, min(8, int(os.environ["LLJ_I8_ROWS"])))
 # long caches: attention split over the keys (llj_attention_split) into ATTN_SPLIT_KEYS-key
 # ranges once the cache holds >= ATTN_SPLIT_MIN_S slots (32 heads x 1 row leave most CUs idle)
 ATTN_SPLIT_MIN_S = 512
