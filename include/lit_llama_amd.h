@@ -120,32 +120,12 @@ size_t llj_attention_ws_bytes(int rows, int n_head, int head_size, int nsplit);
 int llj_attention_split(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
                         int n_head, int head_size, int S, int nsplit, void* part_ws, void* stream);
 
-/* Decode attention in ONE launch (replaces the one-block-per-head llj_attention at bs = 1 and the
- * two-launch llj_attention_split; reference model.py:237 via CausalSelfAttention.forward): nsplit
- * blocks per (row, head), block s over the key chunks s, s + nsplit, ...; each writes its
- * unnormalized softmax partial and the last to arrive (per-(row, head) ticket) merges the nsplit
- * partials in a fixed order (result independent of arrival order) and writes y. ws:
- * llj_attention_decode_ws_bytes(B*T, n_head, head_size, nsplit) bytes, ZERO-FILLED before the
- * first launch (its tickets); every launch leaves them at zero again. Not concurrent-safe on one ws. */
-size_t llj_attention_decode_ws_bytes(int rows, int n_head, int head_size, int nsplit);
-int llj_attention_decode(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
-                         int n_head, int head_size, int S, int nsplit, void* ws, void* stream);
-
 /* x[M, N] += A[M, K] . W^T (attn.c_proj / mlp.c_proj + residual add, model.py:172-173).
  * nstat_out (optional, M <= 16, not int8): per 16-column tile t of the new x, the bf16-rounded
  * squares summed over the tile's columns, nstat_out[t * 16 + m] (fp32; N / 16 partials): the
  * statistics of the next RMSNorm (model.py:281), handed to the norm-fused op that follows. */
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
                      int N, int K, const void* i8ws, int i8_row0, float* nstat_out, void* stream);
-/* llj_linear_resid (M <= 8, not int8) + the NEXT RMSNorm (model.py:276-283) of the updated x, done
- * by the last M workgroups to finish, one row each: xn (M, N) = RMSNorm(x) * norm_w and rowsum[m]
- * = fp32 sum of xn's bf16 row (the int4 offset term of the GEMV that reads xn). sync: two
- * unsigned counters, zero before the first call; the kernel leaves them zero (graph-replay safe).
- * Replaces a separate llj_rmsnorm_rows launch per norm at batched decode. N <= 8192. */
-int llj_linear_resid_norm(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
-                          int N, int K, const void* norm_w, float eps, void* xn, float* rowsum, unsigned* sync,
-                          void* stream);
-
 /* h[M, H] = silu(rms_2(x) . W1^T) * (rms_2(x) . W2^T)  (model.py:173, 258). M <= 8. */
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,

@@ -203,242 +203,6 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   LLJ_STAMP(5);
 }
 
-// ---- decode attention in ONE launch over nsplit blocks per (row, head) (short caches: 32 heads
-// x 1 row would leave 224 CUs idle while 32 of them pull 64 KB each). Block `split` takes the
-// CH-key chunks split, split + nsplit, ... (CH = NG * U keys, one pass each); its first chunk is
-// loaded before the position is known (slots exist whatever p is; keys past p are masked). Each
-// block writes its unnormalized partial (max, sum, HS outputs) with agent-scope 8-byte stores
-// (sc1, write-through), waits for them (vmcnt(0)), and one lane adds to the (row, head) ticket;
-// the block whose add returns nsplit - 1 loads the nsplit partials with sc1 loads (the hand-off of
-// MI355X_MICROARCH.md's table row 1: one adding lane per storing workgroup, last adder told by the
-// returned value, every store and load sc1), merges them in a FIXED order (lane group g takes
-// splits g, g + 4, ... in increasing order; then groups 0+1, 2+3, then the halves) so the result
-// does not depend on which block came last, writes y and puts the ticket back to 0 for the next
-// launch. Workspace: tickets (rows * nh u32, zero before the first launch), then the partials.
-__host__ __device__ constexpr size_t attention_fsplit_ticket_bytes(int rows, int nh) {
-  return ((size_t)rows * nh * 4 + 255) / 256 * 256;
-}
-
-__device__ __forceinline__ void st_sc1_f2(float* p, float a, float b) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
-                     (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ f32x2 ld_sc1_f2(const float* p) {
-  const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-  return f32x2{__uint_as_float((uint32_t)v), __uint_as_float((uint32_t)(v >> 32))};
-}
-
-template <int HS, int U, int NTH>
-__device__ __forceinline__ void attention_fsplit_body(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
-                                                      const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
-                                                      const int* __restrict__ pos, int T, int S, int nh,
-                                                      float scale_log2, int h, int m, int split, int nsplit,
-                                                      unsigned* __restrict__ tickets, float* __restrict__ part,
-                                                      float* lds) {
-  constexpr int DPL = HS / 16;
-  constexpr int NG = NTH / 16;
-  constexpr int NWV = NTH / 64;
-  constexpr int CH = NG * U;  // keys per chunk (one pass)
-  constexpr int PSTR = HS + 2;  // floats per partial: outputs, max, sum (8-byte aligned: HS even)
-  const int b = m / T, t = m % T;
-  const int sub = threadIdx.x & 15, kg = threadIdx.x >> 4;
-  const int C = nh * HS;
-  const size_t base = ((size_t)(b * nh + h) * S) * HS + sub * DPL;
-  // keys u in [u0, u1) of a pass; past jlim: row 0 (an L2 hit after the first pass, never used)
-  auto load_pass = [&](int j0, int jlim, uint32_t (&kw)[U][DPL / 2], uint32_t (&vw)[U][DPL / 2], int u0 = 0,
-                       int u1 = U) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u < u0 || u >= u1) continue;
-      const int j = j0 + NG * u < jlim ? j0 + NG * u : 0;
-      const size_t eo = base + (size_t)j * HS;
-      if constexpr (DPL == 8) {
-        const uint4 a = *reinterpret_cast<const uint4*>(kc + eo);
-        const uint4 c = *reinterpret_cast<const uint4*>(vc + eo);
-        kw[u][0] = a.x; kw[u][1] = a.y; kw[u][2] = a.z; kw[u][3] = a.w;
-        vw[u][0] = c.x; vw[u][1] = c.y; vw[u][2] = c.z; vw[u][3] = c.w;
-      } else {
-        const uint2 a = *reinterpret_cast<const uint2*>(kc + eo);
-        const uint2 c = *reinterpret_cast<const uint2*>(vc + eo);
-        kw[u][0] = a.x; kw[u][1] = a.y;
-        vw[u][0] = c.x; vw[u][1] = c.y;
-      }
-    }
-  };
-  uint32_t kw[U][DPL / 2], vw[U][DPL / 2];
-  load_pass(split * CH + kg, S, kw, vw);  // chunk `split`, before the position is known
-  const int ps = pos[t];
-  const int nvalid = ps < S ? ps + 1 : S;
-  float qf[DPL];
-  {
-    const size_t qo = (size_t)m * C + h * HS + sub * DPL;
-    if constexpr (DPL == 8) {
-      const uint4 a = *reinterpret_cast<const uint4*>(q + qo);
-      const uint32_t w[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        qf[2 * i] = bflo(w[i]) * scale_log2;
-        qf[2 * i + 1] = bfhi(w[i]) * scale_log2;
-      }
-    } else {
-      const uint2 a = *reinterpret_cast<const uint2*>(q + qo);
-      qf[0] = bflo(a.x) * scale_log2;
-      qf[1] = bfhi(a.x) * scale_log2;
-      qf[2] = bflo(a.y) * scale_log2;
-      qf[3] = bfhi(a.y) * scale_log2;
-    }
-  }
-  float mx = -INFINITY, l = 0.f, o[DPL];
-#pragma unroll
-  for (int i = 0; i < DPL; ++i) o[i] = 0.f;
-  for (int c = split; c * CH < nvalid; c += nsplit) {
-    const int j0 = c * CH + kg;
-    if (c != split) load_pass(j0, nvalid, kw, vw);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < DPL / 2; ++i) s += qf[2 * i] * bflo(kw[u][i]) + qf[2 * i + 1] * bfhi(kw[u][i]);
-      s = row16_sum(s);
-      if (j0 + NG * u >= nvalid) continue;
-      const float mn = fmaxf(mx, s);
-      const float corr = exp2f(mx - mn);
-      const float pj = exp2f(s - mn);
-      l = l * corr + pj;
-#pragma unroll
-      for (int i = 0; i < DPL / 2; ++i) {
-        o[2 * i] = o[2 * i] * corr + pj * bflo(vw[u][i]);
-        o[2 * i + 1] = o[2 * i + 1] * corr + pj * bfhi(vw[u][i]);
-      }
-      mx = mn;
-    }
-  }
-  // the four key groups of each wave (lane swaps; every lane ends with its group's merge)
-  {
-    float mlo, mhi, llo, lhi, olo[DPL], ohi[DPL];
-    lane_halves<false>(mx, mlo, mhi);
-    lane_halves<false>(l, llo, lhi);
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) lane_halves<false>(o[i], olo[i], ohi[i]);
-    softmax_merge<DPL>(mx, l, o, mlo, mhi, llo, lhi, olo, ohi);
-    lane_halves<true>(mx, mlo, mhi);
-    lane_halves<true>(l, llo, lhi);
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) lane_halves<true>(o[i], olo[i], ohi[i]);
-    softmax_merge<DPL>(mx, l, o, mlo, mhi, llo, lhi, olo, ohi);
-  }
-  const int rh = m * nh + h;
-  float* mine = part + ((size_t)rh * nsplit + split) * PSTR;
-  if constexpr (NWV == 1) {
-    if (kg == 0) {
-#pragma unroll
-      for (int i = 0; i < DPL; i += 2) st_sc1_f2(mine + sub * DPL + i, o[i], o[i + 1]);
-      if (sub == 0) st_sc1_f2(mine + HS, mx, l);
-    }
-  } else {
-    float* s_m = lds;
-    float* s_l = s_m + NWV;
-    float* s_o = s_l + NWV;
-    const int wv = threadIdx.x >> 6;
-    if (kg % 4 == 0) {
-#pragma unroll
-      for (int i = 0; i < DPL; ++i) s_o[wv * HS + sub * DPL + i] = o[i];
-      if (sub == 0) {
-        s_m[wv] = mx;
-        s_l[wv] = l;
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x < HS) {
-      const int d = threadIdx.x;
-      float M = -INFINITY;
-#pragma unroll
-      for (int w = 0; w < NWV; ++w) M = fmaxf(M, s_m[w]);
-      float L = 0.f, O = 0.f;
-#pragma unroll
-      for (int w = 0; w < NWV; ++w) {
-        const float f = s_m[w] == -INFINITY ? 0.f : exp2f(s_m[w] - M);
-        L += s_l[w] * f;
-        O += s_o[w * HS + d] * f;
-      }
-      const float On = lane_xor1(O);
-      if (!(d & 1)) st_sc1_f2(mine + d, O, On);
-      if (d == 0) st_sc1_f2(mine + HS, M, L);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its partial has left
-  __shared__ unsigned s_last;
-  if constexpr (NWV > 1) __syncthreads();
-  unsigned old = 0;
-  if (threadIdx.x == 0) old = __hip_atomic_fetch_add(tickets + rh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  bool last;
-  if constexpr (NWV == 1) {
-    last = (unsigned)__builtin_amdgcn_readfirstlane((int)old) == (unsigned)(nsplit - 1);
-  } else {
-    if (threadIdx.x == 0) s_last = old;
-    __syncthreads();
-    last = s_last == (unsigned)(nsplit - 1);
-  }
-  if (!last || threadIdx.x >= 64) return;
-  // wave 0 of the last block: lane group g merges splits g, g + 4, ... in order, then the groups
-  const float* pr = part + (size_t)rh * nsplit * PSTR;
-  mx = -INFINITY;
-  l = 0.f;
-#pragma unroll
-  for (int i = 0; i < DPL; ++i) o[i] = 0.f;
-  for (int s0 = kg; s0 < nsplit; s0 += 16) {  // up to 4 splits per lane group per round, loads first
-    f32x2 ml[4], ov[4][DPL / 2];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int s = s0 + 4 * r < nsplit ? s0 + 4 * r : s0;
-      const float* ps_ = pr + (size_t)s * PSTR;
-      ml[r] = ld_sc1_f2(ps_ + HS);
-#pragma unroll
-      for (int i = 0; i < DPL / 2; ++i) ov[r][i] = ld_sc1_f2(ps_ + sub * DPL + 2 * i);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (s0 + 4 * r >= nsplit) break;
-      float on[DPL];
-#pragma unroll
-      for (int i = 0; i < DPL / 2; ++i) {
-        on[2 * i] = ov[r][i].x;
-        on[2 * i + 1] = ov[r][i].y;
-      }
-      float om[DPL];
-#pragma unroll
-      for (int i = 0; i < DPL; ++i) om[i] = o[i];
-      softmax_merge<DPL>(mx, l, o, mx, ml[r].x, l, ml[r].y, om, on);
-    }
-  }
-  {
-    float mlo, mhi, llo, lhi, olo[DPL], ohi[DPL];
-    lane_halves<false>(mx, mlo, mhi);
-    lane_halves<false>(l, llo, lhi);
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) lane_halves<false>(o[i], olo[i], ohi[i]);
-    softmax_merge<DPL>(mx, l, o, mlo, mhi, llo, lhi, olo, ohi);
-    lane_halves<true>(mx, mlo, mhi);
-    lane_halves<true>(l, llo, lhi);
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) lane_halves<true>(o[i], olo[i], ohi[i]);
-    softmax_merge<DPL>(mx, l, o, mlo, mhi, llo, lhi, olo, ohi);
-  }
-  if (kg == 0) {
-    uint32_t w[DPL / 2];
-#pragma unroll
-    for (int i = 0; i < DPL / 2; ++i) w[i] = pack2bf(o[2 * i] / l, o[2 * i + 1] / l);
-    unsigned long long* dst = reinterpret_cast<unsigned long long*>(y + (size_t)m * C + h * HS + sub * DPL);
-#pragma unroll
-    for (int i = 0; i < DPL / 4; ++i)
-      __hip_atomic_store(dst + i, (unsigned long long)w[2 * i] | ((unsigned long long)w[2 * i + 1] << 32),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (sub == 0) __hip_atomic_store(tickets + rh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // Merge the nsplit partials of one (head, row) in split order: y = sum_s O_s f_s / sum_s L_s f_s
 // with f_s = exp2(M_s - max_s M_s) (empty ranges have M = -inf and contribute nothing).
 template <int HS>

@@ -83,20 +83,6 @@ int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void
   return run<EP_RESID>(wfmt, p, stream);
 }
 
-// llj_linear_resid + the next RMSNorm of the updated x by its last M workgroups (one row each).
-int llj_linear_resid_norm(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
-                          int N, int K, const void* norm_w, float eps, void* xn, float* rowsum, unsigned* sync,
-                          void* stream) {
-  if (!norm_w || !xn || !rowsum || !sync || M < 1 || M > 8 || N % 4 || N > 4 * 256 * 8) return LLJ_EINVAL;
-  GemvParams p{};
-  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K;
-  p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)x; p.ldc = ldx;
-  p.post_w = (const bf16_t*)norm_w; p.post_eps = eps; p.post_xn = (bf16_t*)xn; p.post_rs = rowsum;
-  p.post_sync = sync;
-  if ((wfmt & 0xFF) == 2) return LLJ_EINVAL;  // int8 takes its own statistics
-  return run<EP_RESID>(wfmt, p, stream);
-}
-
 // h[M,H] = silu(RMSNorm(x) . W1^T) * (RMSNorm(x) . W2^T)  (rms_2 + model.py:258).
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,

@@ -87,15 +87,6 @@ struct GemvParams {
   int npart;
   float* nstat_out;
   int gch;  // WF_W4G: group size in 128-deep chunks (tile_cols / 128)
-  // EP_RESID post-norm (llj_linear_resid_norm): the next RMSNorm of the updated x, done by the
-  // last M workgroups to finish (one row each): post_xn (M, N) = RMSNorm(x) * post_w, post_rs[m]
-  // = fp32 sum of that bf16 row; post_sync = two zeroed counters (arrivals, rows done), reset by
-  // the kernel itself
-  const bf16_t* post_w;
-  float post_eps;
-  bf16_t* post_xn;
-  float* post_rs;
-  unsigned* post_sync;
 };
 constexpr int kNstRows = 16;
 #ifndef LLJ_SACC_NORM
@@ -1055,92 +1046,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   LLJ_STAMP(5);
 }
 
-// EP_RESID post-norm: after this workgroup's stores of x, take an arrival ticket; the last M
-// workgroups wait for every arrival, then each normalizes one row of the new x (model.py:276-283
-// with the bf16 rounding points of rmsnorm_kernel) into post_xn and its row sum into post_rs. x
-// comes from other workgroups (other XCDs): written with agent-scope stores (st_out32), read back
-// with agent-scope loads after the acquire. No spin can wait on an undispatched workgroup: a
-// waiter's ticket says all but fewer than M of the grid have already finished.
-template <int NW>
-__device__ __forceinline__ void resid_post_norm(const GemvParams& p, unsigned char* smem) {
-  constexpr int NT = NW * 64;
-  float* red = reinterpret_cast<float*>(smem);
-  unsigned* tk = reinterpret_cast<unsigned*>(smem) + 2 * NW;
-  // x went out as agent-scope write-through stores (st_out32): each wave waits for its own to
-  // complete, then one ticket per workgroup (relaxed: a release fence here would write back the
-  // whole L2 in every workgroup -- measured 1.80 -> 2.13 ms per bs=8 step)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) tk[0] = __hip_atomic_fetch_add(p.post_sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const unsigned nwg = gridDim.x, M = (unsigned)p.M;
-  const unsigned t = tk[0];
-  if (t + M < nwg) return;  // not among the last M
-  const int row = (int)(t + M - nwg);
-  if (threadIdx.x == 0) {
-    while (__hip_atomic_load(p.post_sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nwg) __builtin_amdgcn_s_sleep(2);
-  }
-  __syncthreads();
-  const int C = p.N, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const unsigned long long* xr = reinterpret_cast<const unsigned long long*>(p.C + (size_t)row * p.ldc);
-  const uint2* g2 = reinterpret_cast<const uint2*>(p.post_w);
-  uint2* yr = reinterpret_cast<uint2*>(p.post_xn + (size_t)row * C);
-  constexpr int MAXQ = 8;  // 4-element quads per thread held in registers (C <= 4 * NT * MAXQ)
-  unsigned long long xa[MAXQ];
-  float ss = 0.f;
-#pragma unroll
-  for (int k = 0; k < MAXQ; ++k) {
-    const int q = threadIdx.x + NT * k;
-    xa[k] = q < C / 4 ? __hip_atomic_load(xr + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-  }
-#pragma unroll
-  for (int k = 0; k < MAXQ; ++k) {
-    const uint32_t lo = (uint32_t)xa[k], hi = (uint32_t)(xa[k] >> 32);
-    ss += round_bf(bflo(lo) * bflo(lo)) + round_bf(bfhi(lo) * bfhi(lo)) + round_bf(bflo(hi) * bflo(hi)) +
-          round_bf(bfhi(hi) * bfhi(hi));  // x * x in bf16 (model.py:281)
-  }
-  ss = wave_sum(ss);
-  if (lane == 0) red[wave] = ss;
-  __syncthreads();
-  float tot = 0.f;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) tot += red[w];
-  const float r = rms_rstd(tot / (float)C, p.post_eps);
-  float rs = 0.f;
-#pragma unroll
-  for (int k = 0; k < MAXQ; ++k) {
-    const int q = threadIdx.x + NT * k;
-    if (q < C / 4) {
-      const uint2 g = g2[q];
-      const uint32_t o0 = norm_pair((uint32_t)xa[k], g.x, r), o1 = norm_pair((uint32_t)(xa[k] >> 32), g.y, r);
-      yr[q] = make_uint2(o0, o1);
-      rs += bflo(o0) + bfhi(o0) + bflo(o1) + bfhi(o1);
-    }
-  }
-  rs = wave_sum(rs);
-  __syncthreads();
-  if (lane == 0) red[NW + wave] = rs;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float a = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) a += red[NW + w];
-    p.post_rs[row] = a;
-    // the last row done resets both counters for the next launch (every waiter has passed)
-    if (__hip_atomic_fetch_add(p.post_sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == M) {
-      __hip_atomic_store(p.post_sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p.post_sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 template <int WF, int AM, int EP, int NW, int D, int MB, int TPW>
 __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   gemv_body<WF, AM, EP, NW, D, MB, TPW>(p, blockIdx.x * TPW, smem);
-  if constexpr (EP == EP_RESID) {
-    if (p.post_xn) resid_post_norm<NW>(p, smem);  // uniform
-  }
 }
 
 // ------------------------------------------------------------------------------------

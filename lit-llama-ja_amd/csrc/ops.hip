@@ -130,21 +130,6 @@ __global__ __launch_bounds__(NTH) void attention_part_kernel(const bf16_t* __res
                                    blockIdx.z, part);
 }
 
-// one-launch split decode attention (attention.h attention_fsplit_body): block (split * nh + h, row),
-// so with nh % 8 == 0 the nsplit blocks of a head are dispatched to the same XCD
-template <int HS, int U, int NTH>
-__global__ __launch_bounds__(NTH) void attention_fsplit_kernel(const bf16_t* __restrict__ q,
-                                                               const bf16_t* __restrict__ kc,
-                                                               const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
-                                                               const int* __restrict__ pos, int T, int S, int nh,
-                                                               float scale_log2, int nsplit, unsigned* tickets,
-                                                               float* part) {
-  __shared__ float lds[NTH > 64 ? attention_lds_floats<HS, NTH>() : 1];
-  const int h = blockIdx.x % nh, split = blockIdx.x / nh;
-  attention_fsplit_body<HS, U, NTH>(q, kc, vc, y, pos, T, S, nh, scale_log2, h, blockIdx.y, split, nsplit, tickets,
-                                    part, lds);
-}
-
 // ---- greedy next token: argmax over bf16 logits (lowest index on ties). Reference
 // generate.py:66-74 with top_k = 1 (multinomial over the kept maximum).
 __global__ __launch_bounds__(1024) void argmax_kernel(const bf16_t* __restrict__ logits, int ldl, int V,
@@ -487,39 +472,6 @@ int llj_attention_split(const void* q, const void* kcache, const void* vcache, v
   } else {
     return LLJ_EINVAL;
   }
-  LLJ_CHECK_LAUNCH();
-  return 0;
-}
-
-size_t llj_attention_decode_ws_bytes(int rows, int n_head, int head_size, int nsplit) {
-  return attention_fsplit_ticket_bytes(rows, n_head) +
-         (size_t)rows * n_head * (nsplit < 1 ? 1 : nsplit) * (head_size + 2) * sizeof(float);
-}
-
-// caches whose keys per split fit one 64-key pass of a wave run 64-thread blocks (16-key chunks),
-// longer ones 256-thread blocks (128-key chunks)
-int llj_attention_decode(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
-                         int n_head, int head_size, int S, int nsplit, void* ws, void* stream) {
-  LLJ_REQUIRE(B > 0 && T > 0 && n_head > 0 && S > 0 && ws && nsplit >= 1 && nsplit <= 1024 &&
-              (size_t)n_head * nsplit < 65536);
-  const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
-  const dim3 grid(n_head * nsplit, B * T);
-  hipStream_t st = (hipStream_t)stream;
-  unsigned* tickets = (unsigned*)ws;
-  float* part = (float*)((char*)ws + attention_fsplit_ticket_bytes(B * T, n_head));
-  const bool wide = (S + nsplit - 1) / nsplit > 64;
-#define LLJ_FSPLIT(HS, U, NTH)                                                                                   \
-  hipLaunchKernelGGL((attention_fsplit_kernel<HS, U, NTH>), grid, dim3(NTH), 0, st, (const bf16_t*)q,            \
-                     (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2, nsplit, \
-                     tickets, part)
-  if (head_size == 128) {
-    if (wide) LLJ_FSPLIT(128, 8, 256); else LLJ_FSPLIT(128, 4, 64);
-  } else if (head_size == 64) {
-    if (wide) LLJ_FSPLIT(64, 8, 256); else LLJ_FSPLIT(64, 4, 64);
-  } else {
-    return LLJ_EINVAL;
-  }
-#undef LLJ_FSPLIT
   LLJ_CHECK_LAUNCH();
   return 0;
 }

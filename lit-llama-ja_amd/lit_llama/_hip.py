@@ -34,7 +34,6 @@ SIGNATURES = {
     "llj_norm_qkv_rope": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I,
                           _P],
     "llj_attention_split": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
-    "llj_attention_decode": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
     "llj_gemm_i8_linear": [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P],
     "llj_gemm_i8_resid": [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P],
     "llj_gemm_i8_silu_mul": [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P],
@@ -46,7 +45,6 @@ SIGNATURES = {
     "llj_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_attention_prefill": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_linear_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
-    "llj_linear_resid_norm": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _F, _P, _P, _P, _P],
     "llj_norm_swiglu": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _I, _P],
     "llj_norm_linear": [_I, _P, _P, _F, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P],
     "llj_i8_stats": [_P, _I, _I, _I, _F, _P, _P],
@@ -98,8 +96,6 @@ def lib() -> ctypes.CDLL:
         L.llj_i8_ws_bytes.restype = ctypes.c_size_t
         L.llj_attention_ws_bytes.argtypes = [_I, _I, _I, _I]
         L.llj_attention_ws_bytes.restype = ctypes.c_size_t
-        L.llj_attention_decode_ws_bytes.argtypes = [_I, _I, _I, _I]
-        L.llj_attention_decode_ws_bytes.restype = ctypes.c_size_t
         L.llj_engine_arena_bytes.argtypes = [_I, _I]
         L.llj_engine_arena_bytes.restype = ctypes.c_size_t
         L.llj_g_i8_ws_bytes.argtypes = [_I, _I]

@@ -106,16 +106,6 @@ ATTN_SPLIT_KEYS = 256  # 7B bs=1 at p = 2000 (S = 2048): 33.1 us one block, 14.4
 FLASH_MIN_T = 32
 
 
-# decode attention in ONE launch (llj_attention_decode): ATTN_DEC_SPLIT blocks per (row, head) over
-# interleaved key chunks and an in-kernel last-arriver merge, for short caches when rows * n_head
-# <= ATTN_DEC_MAX_RH (bs = 1: 32 blocks of one head each would leave most CUs idle), and for long
-# caches in place of the part + combine launches (ATTN_DEC_LONG)
-ATTN_DEC = os.environ.get("LLJ_ATTN_DEC", "0") != "0"  # (A/B switch; measured slower at bs=1)
-ATTN_DEC_SPLIT = 8
-ATTN_DEC_MAX_RH = 64
-ATTN_DEC_LONG = True
-
-
 def attn_splits(S: int) -> int:
     """key ranges per (row, head) for a cache of S slots (1 = the one-block attention)."""
     if S < ATTN_SPLIT_MIN_S:
@@ -132,13 +122,6 @@ PRE_NORM_MIN_M = 2  # smallest batch that takes the separate launch (measured be
 # 1.788 (every workgroup normalizes all rows: 768 of them at bs=4) -> bs=2 only
 HAND_NORM = True
 HAND_NORM_MAX_M = 2
-# batched decode rows (PRE_NORM_MIN_M <= M <= 8, not int8): each residual op (c_proj, mlp.c_proj)
-# can also produce the next RMSNorm of the updated x (llj_linear_resid_norm: its last M workgroups
-# normalize one row each), removing the separate llj_rmsnorm_rows launches (two per layer). Measured
-# 7B gptq.int4 bs=8 (bench.py, 100 steps, two runs each): 2.021 ms with it vs 1.803 ms without (2.13
-# with a release fence per workgroup): the 256 arrivals on one counter, each after its own stores
-# completed, and the row pass on the critical path cost more than the ~4.9 us launch. Off.
-POST_NORM = os.environ.get("LLJ_POST_NORM", "0") != "0"  # (A/B switch)
 
 
 # prefill / no-cache calls with at least this many rows (B * T) run the MFMA-tiled GEMMs
@@ -230,9 +213,8 @@ class _Work:
             self.a1 = torch.empty(M, H, dtype=bf, device=device)
             self.a2 = torch.empty(M, H, dtype=bf, device=device)
             self.h = torch.empty(M, H, dtype=bf, device=device)
-            self.gemm = self.flash = self.pre = self.hand = self.post = False
-            self.i8ws = self.att_ws = self.nst = self.rs = self.sync = None
-            self.att_dec = 0
+            self.gemm = self.flash = self.pre = self.hand = False
+            self.i8ws = self.att_ws = self.nst = self.rs = None
             return
         self.gemm = gemm  # many rows: the prefill GEMMs (LLaMA._blocks_gemm)
         self.flash = False  # T-row prompt attention on the MFMA flash kernel (set by LLaMA._run)
@@ -245,13 +227,10 @@ class _Work:
         self.pre = M >= max(2, PRE_NORM_MIN_M) and not need_i8 and PRE_NORM_ROWS
         self.xn = torch.empty(M, C, dtype=bf, device=device) if (need_i8 or self.pre or gemm) else None
         self.rs = torch.empty(M, dtype=torch.float32, device=device) if self.pre else None
-        self.post = self.pre and POST_NORM and M <= 8 and not gemm
         # norm statistics hand-off (HAND_NORM): partials [C / 16 tiles][16 rows]
         self.hand = (HAND_NORM and not need_i8 and not gemm and 2 <= M <= HAND_NORM_MAX_M
                      and C % 16 == 0 and C // 16 <= 512)
         self.npart = C // 16
-        self.post = self.post and not self.hand  # bs=2 keeps the partial-sums hand-off
-        self.sync = torch.zeros(2, dtype=torch.int32, device=device) if self.post else None
         self.nst = torch.empty(self.npart * 16, dtype=torch.float32, device=device) if self.hand else None
         if need_i8:
             L = _hip.lib()
@@ -262,16 +241,7 @@ class _Work:
         # split-K attention partials for long caches (llj_attention_split)
         self.nsplit = attn_splits(S)
         self.att_ws = None
-        self.att_dec = 0  # > 0: llj_attention_decode with this many blocks per (row, head)
-        if ATTN_DEC:
-            if self.nsplit > 1 and ATTN_DEC_LONG:
-                self.att_dec = self.nsplit
-            elif self.nsplit == 1 and M * cfg.n_head <= ATTN_DEC_MAX_RH:
-                self.att_dec = ATTN_DEC_SPLIT
-        if self.att_dec:  # zero-filled: the per-(row, head) tickets start (and every launch ends) at 0
-            nb = _hip.lib().llj_attention_decode_ws_bytes(M, cfg.n_head, C // cfg.n_head, self.att_dec)
-            self.att_ws = torch.zeros(nb, dtype=torch.uint8, device=device)
-        elif self.nsplit > 1:
+        if self.nsplit > 1:
             nb = _hip.lib().llj_attention_ws_bytes(M, cfg.n_head, C // cfg.n_head, self.nsplit)
             self.att_ws = torch.empty(nb, dtype=torch.uint8, device=device)
 
@@ -473,9 +443,6 @@ class LLaMA(nn.Module):
         if w.flash:
             _hip.call("llj_attention_prefill", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
                       pos.data_ptr(), B, T, nh, C // nh, S, st)
-        elif w.att_dec:
-            _hip.call("llj_attention_decode", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
-                      pos.data_ptr(), B, T, nh, C // nh, S, w.att_dec, w.att_ws.data_ptr(), st)
         elif w.att_ws is not None:
             _hip.call("llj_attention_split", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(),
                       pos.data_ptr(), B, T, nh, C // nh, S, w.nsplit, w.att_ws.data_ptr(), st)
@@ -606,9 +573,6 @@ class LLaMA(nn.Module):
                 src, nw = w.xn, None
             elif w.hand and i > 0:  # the previous mlp.c_proj handed over the sums of squares
                 src, nw = w.x, blk.rms_1.scale.data_ptr()
-            elif w.post and i > 0:  # the previous mlp.c_proj normalized x into xn (and rs)
-                rs = w.rs if fa in _ROWSUM_FMTS else None
-                src, nw = w.xn, None
             elif w.pre:
                 rs = w.rs if fa in _ROWSUM_FMTS else None
                 _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
@@ -624,8 +588,7 @@ class LLaMA(nn.Module):
                           S, r0, r, P(w.i8ws), P(rs), P(nst), w.npart, st)
             # 2. attention, 3. c_proj + residual
             self._attention(w, kc, vc, pos, B, T, S, st)
-            self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst if w.hand else None,
-                        post=blk.rms_2 if w.post else None)
+            self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst if w.hand else None)
             # 4. rms_2 + fc1/fc2 + silu*mul
             if f1 != f2:
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")
@@ -635,9 +598,6 @@ class LLaMA(nn.Module):
                 src, nw, step = w.xn, None, I8_ROWS
             elif w.hand:  # c_proj handed over the sums of squares
                 src, nw, step = w.x, blk.rms_2.scale.data_ptr(), QKV_ROWS
-            elif w.post:  # c_proj normalized x into xn (and rs)
-                rs = w.rs if f1 in _ROWSUM_FMTS else None
-                src, nw, step = w.xn, None, QKV_ROWS
             elif w.pre:
                 rs = w.rs if f1 in _ROWSUM_FMTS else None
                 _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
@@ -652,21 +612,12 @@ class LLaMA(nn.Module):
                           w2.data_ptr(), P(s2), w.h[r0].data_ptr(), r, H, C, P(w.i8ws), r0,
                           None if rs is None else rs[r0].data_ptr(), None if nst is None else nst[r0].data_ptr(),
                           w.npart, st)
-            # 5. mlp.c_proj + residual (+ the next layer's rms_1, or ln_f after the last layer)
-            nxt = (self.transformer.h[i + 1].rms_1 if i + 1 < len(self.transformer.h)
-                   else getattr(self.transformer, "ln_f", None))  # (Block.forward: no ln_f, no norm after)
-            self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st, w.nst if w.hand else None,
-                        post=nxt if w.post else None)
+            # 5. mlp.c_proj + residual
+            self._resid(fd, w.h, wd, sd, w.x, M, C, H, w, st, w.nst if w.hand else None)
 
-    def _resid(self, f, A, W, sz, x, M, N, K, w, st, nst=None, post=None):
+    def _resid(self, f, A, W, sz, x, M, N, K, w, st, nst=None):
         """x += A . W^T; with `nst` (the norm hand-off, N / 16 tiles x 16 rows) also the next
-        RMSNorm's partial sums of squares of the new x; with `post` (an RMSNorm module, batched
-        decode rows) also that norm of the new x into w.xn / w.rs (llj_linear_resid_norm)."""
-        if post is not None:
-            _hip.call("llj_linear_resid_norm", f, A.data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz), x.data_ptr(),
-                      x.stride(0), M, N, K, post.scale.data_ptr(), post.eps, w.xn.data_ptr(), w.rs.data_ptr(),
-                      w.sync.data_ptr(), st)
-            return
+        RMSNorm's partial sums of squares of the new x."""
         if f == 2:
             self._i8_prep(A, M, K, w, st)
         step = I8_ROWS if f == 2 else LIN_ROWS
@@ -706,10 +657,6 @@ class LLaMA(nn.Module):
         elif x is w.x and w.hand and f != 2 and len(self.transformer.h) > 0:  # the last mlp.c_proj's partials
             nst = w.nst
             src, nw = x, ln.scale.data_ptr()
-        elif x is w.x and w.post and len(self.transformer.h) > 0:  # the last mlp.c_proj normalized x with ln_f
-            xn = w.xn
-            rs = w.rs if f in _ROWSUM_FMTS else None
-            src, nw = xn, None
         elif M >= 2 and w.pre:  # batched rows: normalize once (see _Work.pre)
             xn = torch.empty_like(x)
             rs = torch.empty(M, dtype=torch.float32, device=x.device) if f in _ROWSUM_FMTS else None

@@ -702,38 +702,6 @@ def test_attention_split_keys(hip, hs, nh, B, T_, S, p0, nsplit):
     assert_bf16_close(y.float().cpu().numpy(), _attn_oracle(q, kc, vc, pos, S, T_, nh, hs), "split attention")
 
 
-@pytest.mark.parametrize("hs,nh,B,T_,S,p0,nsplit", [(128, 32, 1, 1, 144, 80, 8), (128, 4, 1, 1, 144, 143, 8),
-                                                   (128, 3, 8, 1, 144, 200, 8), (64, 4, 2, 5, 16, 0, 8),
-                                                   (128, 2, 1, 1, 10, 37, 3), (128, 4, 1, 1, 2048, 2000, 8),
-                                                   (128, 3, 2, 1, 2048, 40, 16), (64, 4, 2, 5, 600, 300, 5),
-                                                   (128, 2, 8, 1, 1024, 1023, 8), (128, 2, 1, 1, 511, 17, 40)])
-def test_attention_decode_one_launch(hip, hs, nh, B, T_, S, p0, nsplit):
-    """One-launch split attention (llj_attention_decode: nsplit blocks per (row, head), in-kernel
-    last-arriver merge in a fixed order) against the oracle: short caches (16-key chunks, empty
-    splits), long caches (128-key chunks), prefill rows (T > 1), the rolled ring (p0 >= S) and more
-    than 16 splits per head. Three launches on one workspace give bitwise-equal outputs and leave the
-    tickets at zero (the merge order does not depend on which block arrives last)."""
-    rng = np.random.default_rng(hs + S + p0 + nsplit + 11)
-    C = nh * hs
-    kc = bf16(rng.standard_normal((B, nh, S, hs)))
-    vc = bf16(rng.standard_normal((B, nh, S, hs)))
-    q = bf16(rng.standard_normal((B * T_, C)) * 2)
-    pos = np.arange(p0, p0 + T_, dtype=np.int32)
-    ws = torch.zeros(hip.llj_attention_decode_ws_bytes(B * T_, nh, hs, nsplit), dtype=torch.uint8, device=dev)
-    qd, kd, vd, pd = T(q, torch.bfloat16), T(kc, torch.bfloat16), T(vc, torch.bfloat16), T(pos)
-    outs = []
-    for _ in range(3):
-        y = torch.empty(B * T_, C, dtype=torch.bfloat16, device=dev)
-        call(hip, "llj_attention_decode", qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), y.data_ptr(), pd.data_ptr(),
-             B, T_, nh, hs, S, nsplit, ws.data_ptr(), st())
-        outs.append(y)
-    torch.cuda.synchronize()
-    tickets = ws[:B * T_ * nh * 4].view(torch.int32)
-    assert int(tickets.abs().sum()) == 0, "tickets not returned to zero"
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
-    assert_bf16_close(outs[0].float().cpu().numpy(), _attn_oracle(q, kc, vc, pos, S, T_, nh, hs), "decode attention")
-
-
 @pytest.mark.parametrize("M", [1, 8])
 def test_int8_fused_ops_7b_shapes(hip, M):
     """llm.int8 (wfmt 2) through every fused entry point the model uses, at the 7B shapes (C 4096,
