@@ -599,6 +599,9 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
 #ifndef LLJ_GEMM_GLDS_W4
 #define LLJ_GEMM_GLDS_W4 0  // int4: 42.5 ms vs 37.6 with the register-staged 256-row kernel
 #endif
+#ifndef LLJ_GLDS_PRE
+#define LLJ_GLDS_PRE 0  // 256 x 128 tiles: read both MFMA steps' fragments of a chunk before its MFMAs
+#endif
 #ifndef LLJ_GLDS_COST128
 #define LLJ_GLDS_COST128 55  // time of a 256 x 128 tile in % of a 256 x 256 one (tile-shape choice)
 #endif
@@ -695,42 +698,56 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     if (tid < 256) rs_lds[tid] = 0.f;  // ordered before the adds by the K loop's barriers
   }
 
+  auto frags = [&](const unsigned char* Ab, const unsigned char* Bb, int s, bf16x8 (&af)[MI], bf16x8 (&bfr)[NJ]) {
+    const int so = ((4 * s + g) ^ sw) * 16;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + aoff0 + 16 * i * 128 + so);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      if constexpr (NIB) {  // word g of W4P lane 16 s + column of tile wc * NJ + j (the chunk's half)
+        const uint32_t wv = reinterpret_cast<const uint32_t*>(Bb)[((wc * NJ + j) * 32 + 16 * s + row) * 4 + g];
+        bfr[j] = __builtin_bit_cast(bf16x8, make_uint4(and_or(wv, msk, mag), and_or(wv >> 4, msk, mag),
+                                                       and_or(wv >> 8, msk, mag), and_or(wv >> 12, msk, mag)));
+      } else {
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bb + boff0 + 16 * j * 128 + so);
+      }
+    }
+  };
+  auto mma = [&](int s, const bf16x8 (&af)[MI], const bf16x8 (&bfr)[NJ]) {
+    if constexpr (NIB) {  // (not v_dot2c_f32_bf16: ROCm 7.2 clang feeds element 0 of a bit-cast vector to every call)
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const bool mine = WN == 4 ? ((i & 1) == (wc >> 1) && s == (wc & 1)) : s == wc;
+        if (mine) {
+          const u32x4 a = __builtin_bit_cast(u32x4, af[i]);
+          const f32x2 p2 = (unpk(a[0]) + unpk(a[1])) + (unpk(a[2]) + unpk(a[3]));
+          rsp[i] += p2.x + p2.y;
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
   auto compute = [&](int buf) {
     const unsigned char* Ab = smem + (size_t)buf * G::STAGE;
     const unsigned char* Bb = Ab + G::SA;
+    if constexpr (LLJ_GLDS_PRE && BN == 128) {  // both MFMA steps' fragments read before either's MFMAs
+      bf16x8 af0[MI], bf0[NJ], af1[MI], bf1[NJ];
+      frags(Ab, Bb, 0, af0, bf0);
+      frags(Ab, Bb, 1, af1, bf1);
+      mma(0, af0, bf0);
+      mma(1, af1, bf1);
+    } else {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int so = ((4 * s + g) ^ sw) * 16;
-      bf16x8 af[MI], bfr[NJ];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + aoff0 + 16 * i * 128 + so);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        if constexpr (NIB) {  // word g of W4P lane 16 s + column of tile wc * NJ + j (the chunk's half)
-          const uint32_t wv = reinterpret_cast<const uint32_t*>(Bb)[((wc * NJ + j) * 32 + 16 * s + row) * 4 + g];
-          bfr[j] = __builtin_bit_cast(bf16x8, make_uint4(and_or(wv, msk, mag), and_or(wv >> 4, msk, mag),
-                                                         and_or(wv >> 8, msk, mag), and_or(wv >> 12, msk, mag)));
-        } else {
-          bfr[j] = *reinterpret_cast<const bf16x8*>(Bb + boff0 + 16 * j * 128 + so);
-        }
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 af[MI], bfr[NJ];
+        frags(Ab, Bb, s, af, bfr);
+        mma(s, af, bfr);
       }
-      if constexpr (NIB) {  // (not v_dot2c_f32_bf16: ROCm 7.2 clang feeds element 0 of a bit-cast vector to every call)
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const bool mine = WN == 4 ? ((i & 1) == (wc >> 1) && s == (wc & 1)) : s == wc;
-          if (mine) {
-            const u32x4 a = __builtin_bit_cast(u32x4, af[i]);
-            const f32x2 p2 = (unpk(a[0]) + unpk(a[1])) + (unpk(a[2]) + unpk(a[3]));
-            rsp[i] += p2.x + p2.y;
-          }
-        }
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
     }
   };
 
