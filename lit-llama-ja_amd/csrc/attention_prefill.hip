@@ -29,12 +29,15 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 #ifndef LLJ_FLASH_OCC
 #define LLJ_FLASH_OCC 3  // workgroups per CU the QB = 1 register budget is sized for (152 VGPRs, no spill; 2: 7B T=2048 window 40.0 vs 39.5 ms)
 #endif
+#ifndef LLJ_FLASH_PAIR
+#define LLJ_FLASH_PAIR 0  // causal balance: one workgroup per (long, short) pair of query blocks
+#endif
 #ifndef LLJ_FLASH_QB
 #define LLJ_FLASH_QB 2  // 16-query blocks per wave (2: every K / V fragment read feeds two MFMAs; 7B window -0.1..-0.4 ms, profiles/r04_prefill_ab.json)
 #endif
 // QB 16-query blocks per wave: 64 QB queries per workgroup; a K fragment (S^T) and a V^T fragment
 // (O^T) read from LDS feed QB MFMAs, and the tile's staging and barriers are shared by 4 x 16 QB queries
-template <int HS, int QB>
+template <int HS, int QB, bool PAIR>
 __global__ __launch_bounds__(256, QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefill_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                             const int* __restrict__ pos, int T, int S, int nh,
@@ -48,169 +51,186 @@ __global__ __launch_bounds__(256, QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefil
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, g = lane >> 4;
   constexpr int kFQ = 64 * QB;  // queries per workgroup
-  const int qb = gridDim.x - 1 - blockIdx.x;  // long (late) query blocks first
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int C = nh * HS;
-  const int p0 = pos[0];
-  int t[QB], qpos[QB];  // this lane's query rows (rows past T are computed on a copy, never stored)
-  // Q^T fragments: lane holds Q[t][32 kk + 8 g .. + 8]
-  u32x4 qf[QB][KS];
-#pragma unroll
-  for (int qi = 0; qi < QB; ++qi) {
-    t[qi] = qb * kFQ + wave * 16 * QB + 16 * qi + col;
-    qpos[qi] = p0 + t[qi];
-    const int tq = t[qi] < T ? t[qi] : T - 1;
-    const bf16_t* qrow = q + ((size_t)b * T + tq) * C + h * HS;
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) qf[qi][kk] = *reinterpret_cast<const u32x4*>(qrow + 32 * kk + 8 * g);
-  }
-  const int tlast = min(T, qb * kFQ + kFQ) - 1;
-  const int kmax = p0 + tlast;  // last key any query of the block attends
-  const int ntile = kmax / kFK + 1;
-  const bf16_t* kbase = kc + ((size_t)(b * nh + h) * S) * HS;
-  const bf16_t* vbase = vc + ((size_t)(b * nh + h) * S) * HS;
-  // staging map: 64 keys x HS/8 vectors = 64 * HS / 8 16-B pieces over 256 threads
-  constexpr int PV = kFK * HS / 8 / 256;
-  u32x4 kreg[PV], vreg[PV];
-  auto load_tile = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < PV; ++i) {
-      const int piece = tid + 256 * i;
-      const int key = piece / (HS / 8), v8 = piece % (HS / 8);
-      int slot = kt * kFK + key;
-      slot = slot <= kmax ? slot : kmax;  // clamped: masked below
-      kreg[i] = *reinterpret_cast<const u32x4*>(kbase + (size_t)slot * HS + 8 * v8);
-      vreg[i] = *reinterpret_cast<const u32x4*>(vbase + (size_t)slot * HS + 8 * v8);
+  auto run = [&](const int qb) {
+    const int h = blockIdx.y, b = blockIdx.z;
+    const int C = nh * HS;
+    const int p0 = pos[0];
+    int t[QB], qpos[QB];  // this lane's query rows (rows past T are computed on a copy, never stored)
+    // Q^T fragments: lane holds Q[t][32 kk + 8 g .. + 8]
+    u32x4 qf[QB][KS];
+  #pragma unroll
+    for (int qi = 0; qi < QB; ++qi) {
+      t[qi] = qb * kFQ + wave * 16 * QB + 16 * qi + col;
+      qpos[qi] = p0 + t[qi];
+      const int tq = t[qi] < T ? t[qi] : T - 1;
+      const bf16_t* qrow = q + ((size_t)b * T + tq) * C + h * HS;
+  #pragma unroll
+      for (int kk = 0; kk < KS; ++kk) qf[qi][kk] = *reinterpret_cast<const u32x4*>(qrow + 32 * kk + 8 * g);
+    }
+    const int tlast = min(T, qb * kFQ + kFQ) - 1;
+    const int kmax = p0 + tlast;  // last key any query of the block attends
+    const int ntile = kmax / kFK + 1;
+    const bf16_t* kbase = kc + ((size_t)(b * nh + h) * S) * HS;
+    const bf16_t* vbase = vc + ((size_t)(b * nh + h) * S) * HS;
+    // staging map: 64 keys x HS/8 vectors = 64 * HS / 8 16-B pieces over 256 threads
+    constexpr int PV = kFK * HS / 8 / 256;
+    u32x4 kreg[PV], vreg[PV];
+    auto load_tile = [&](int kt) {
+  #pragma unroll
+      for (int i = 0; i < PV; ++i) {
+        const int piece = tid + 256 * i;
+        const int key = piece / (HS / 8), v8 = piece % (HS / 8);
+        int slot = kt * kFK + key;
+        slot = slot <= kmax ? slot : kmax;  // clamped: masked below
+        kreg[i] = *reinterpret_cast<const u32x4*>(kbase + (size_t)slot * HS + 8 * v8);
+        vreg[i] = *reinterpret_cast<const u32x4*>(vbase + (size_t)slot * HS + 8 * v8);
+      }
+    };
+    float m_run[QB], l_run[QB];
+    f32x4 acc_o[QB][DB];
+  #pragma unroll
+    for (int qi = 0; qi < QB; ++qi) {
+      m_run[qi] = -INFINITY;
+      l_run[qi] = 0.f;
+  #pragma unroll
+      for (int d = 0; d < DB; ++d) acc_o[qi][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    load_tile(0);
+    for (int kt = 0; kt < ntile; ++kt) {
+      __syncthreads();  // the previous tile's readers are done with Ks / Vt
+  #pragma unroll
+      for (int i = 0; i < PV; ++i) {
+        const int piece = tid + 256 * i;
+        const int key = piece / (HS / 8), v8 = piece % (HS / 8);
+        *reinterpret_cast<u32x4*>(Ks + key * KP + 8 * v8) = kreg[i];
+        *reinterpret_cast<u32x4*>(Vs + key * VP + 8 * v8) = vreg[i];
+      }
+      __syncthreads();
+      if (kt + 1 < ntile) load_tile(kt + 1);  // in flight during this tile's MFMAs
+      // S^T = K . Q^T for the tile's four 16-key blocks
+      f32x4 s[QB][4];
+  #pragma unroll
+      for (int j = 0; j < 4; ++j) {
+  #pragma unroll
+        for (int qi = 0; qi < QB; ++qi) s[qi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          const bf16x8 a = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Ks + (16 * j + col) * KP + 32 * kk + 8 * g));
+  #pragma unroll
+          for (int qi = 0; qi < QB; ++qi) s[qi][j] = mfma_bf16(a, __builtin_bit_cast(bf16x8, qf[qi][kk]), s[qi][j]);
+        }
+      }
+      uint32_t pb[QB][4][2];  // bf16 P^T pairs per key block: (r0, r1), (r2, r3)
+  #pragma unroll
+      for (int qi = 0; qi < QB; ++qi) {
+        // mask (key slot > query position) and scale into log2 units; per-query max
+        float mx = -INFINITY;
+  #pragma unroll
+        for (int j = 0; j < 4; ++j)
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kt * kFK + 16 * j + 4 * g + r;
+            const float v = key <= qpos[qi] ? s[qi][j][r] * sl2 : -INFINITY;
+            s[qi][j][r] = v;
+            mx = fmaxf(mx, v);
+          }
+        {  // max over the 4 lane groups holding this query's keys (lanes col, col+16, col+32, col+48)
+          float lo, hi;
+          lane_halves<false>(mx, lo, hi);
+          mx = fmaxf(lo, hi);
+          lane_halves<true>(mx, lo, hi);
+          mx = fmaxf(lo, hi);
+        }
+        const float m_new = fmaxf(m_run[qi], mx);
+        const float corr = m_run[qi] == -INFINITY ? 0.f : exp2f(m_run[qi] - m_new);
+        float psum = 0.f;
+  #pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float pr[4];
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            pr[r] = s[qi][j][r] == -INFINITY ? 0.f : exp2f(s[qi][j][r] - m_new);
+            psum += pr[r];
+          }
+          pb[qi][j][0] = pack2bf(pr[0], pr[1]);
+          pb[qi][j][1] = pack2bf(pr[2], pr[3]);
+        }
+        {
+          float lo, hi;
+          lane_halves<false>(psum, lo, hi);
+          psum = lo + hi;
+          lane_halves<true>(psum, lo, hi);
+          psum = lo + hi;
+        }
+        l_run[qi] = l_run[qi] * corr + psum;
+        m_run[qi] = m_new;
+  #pragma unroll
+        for (int d = 0; d < DB; ++d)
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) acc_o[qi][d][r] *= corr;
+      }
+      // O^T += V^T . P^T, two 32-key steps
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        bf16x8 bfrag[QB];
+  #pragma unroll
+        for (int qi = 0; qi < QB; ++qi) {
+          const u32x4 bw = {pb[qi][2 * u][0], pb[qi][2 * u][1], pb[qi][2 * u + 1][0], pb[qi][2 * u + 1][1]};
+          bfrag[qi] = __builtin_bit_cast(bf16x8, bw);
+        }
+  #pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          // lane 4q + p of group g addresses keys 32u + 4g + q (+16), dims 16d + 4p .. +3; lane col
+          // receives dim 16d + col of those 4 keys
+          const bf16_t* vr = Vs + (32 * u + 4 * g + ((lane >> 2) & 3)) * VP + 16 * d + 4 * (lane & 3);
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)vr);
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr + 16 * VP));
+          const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
+          const u32x4 aw = {l2.x, l2.y, h2.x, h2.y};
+  #pragma unroll
+          for (int qi = 0; qi < QB; ++qi) acc_o[qi][d] = mfma_bf16(__builtin_bit_cast(bf16x8, aw), bfrag[qi], acc_o[qi][d]);
+        }
+      }
+    }
+    // y[b*T + t][h*HS + d] = O / l; lane holds d = 16 db + 4 g + r of its query
+  #pragma unroll
+    for (int qi = 0; qi < QB; ++qi) {
+      if (t[qi] < T) {
+        const float inv = 1.f / l_run[qi];
+        bf16_t* yrow = y + ((size_t)b * T + t[qi]) * C + h * HS;
+  #pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          const uint2 o = make_uint2(pack2bf(acc_o[qi][d][0] * inv, acc_o[qi][d][1] * inv),
+                                     pack2bf(acc_o[qi][d][2] * inv, acc_o[qi][d][3] * inv));
+          *reinterpret_cast<uint2*>(yrow + 16 * d + 4 * g) = o;
+        }
+      }
     }
   };
-  float m_run[QB], l_run[QB];
-  f32x4 acc_o[QB][DB];
-#pragma unroll
-  for (int qi = 0; qi < QB; ++qi) {
-    m_run[qi] = -INFINITY;
-    l_run[qi] = 0.f;
-#pragma unroll
-    for (int d = 0; d < DB; ++d) acc_o[qi][d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  load_tile(0);
-  for (int kt = 0; kt < ntile; ++kt) {
-    __syncthreads();  // the previous tile's readers are done with Ks / Vt
-#pragma unroll
-    for (int i = 0; i < PV; ++i) {
-      const int piece = tid + 256 * i;
-      const int key = piece / (HS / 8), v8 = piece % (HS / 8);
-      *reinterpret_cast<u32x4*>(Ks + key * KP + 8 * v8) = kreg[i];
-      *reinterpret_cast<u32x4*>(Vs + key * VP + 8 * v8) = vreg[i];
+  const int nqb = (T + kFQ - 1) / kFQ;
+  if constexpr (PAIR) {  // block x takes query blocks nqb - 1 - x (long) and x (short): equal work per workgroup
+    const int qz = nqb - 1 - (int)blockIdx.x, qa = blockIdx.x;
+    run(qz);
+    if (qa < qz) {
+      __syncthreads();  // the first block's last readers are done with Ks / Vs
+      run(qa);
     }
-    __syncthreads();
-    if (kt + 1 < ntile) load_tile(kt + 1);  // in flight during this tile's MFMAs
-    // S^T = K . Q^T for the tile's four 16-key blocks
-    f32x4 s[QB][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#pragma unroll
-      for (int qi = 0; qi < QB; ++qi) s[qi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const bf16x8 a = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Ks + (16 * j + col) * KP + 32 * kk + 8 * g));
-#pragma unroll
-        for (int qi = 0; qi < QB; ++qi) s[qi][j] = mfma_bf16(a, __builtin_bit_cast(bf16x8, qf[qi][kk]), s[qi][j]);
-      }
-    }
-    uint32_t pb[QB][4][2];  // bf16 P^T pairs per key block: (r0, r1), (r2, r3)
-#pragma unroll
-    for (int qi = 0; qi < QB; ++qi) {
-      // mask (key slot > query position) and scale into log2 units; per-query max
-      float mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kt * kFK + 16 * j + 4 * g + r;
-          const float v = key <= qpos[qi] ? s[qi][j][r] * sl2 : -INFINITY;
-          s[qi][j][r] = v;
-          mx = fmaxf(mx, v);
-        }
-      {  // max over the 4 lane groups holding this query's keys (lanes col, col+16, col+32, col+48)
-        float lo, hi;
-        lane_halves<false>(mx, lo, hi);
-        mx = fmaxf(lo, hi);
-        lane_halves<true>(mx, lo, hi);
-        mx = fmaxf(lo, hi);
-      }
-      const float m_new = fmaxf(m_run[qi], mx);
-      const float corr = m_run[qi] == -INFINITY ? 0.f : exp2f(m_run[qi] - m_new);
-      float psum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float pr[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pr[r] = s[qi][j][r] == -INFINITY ? 0.f : exp2f(s[qi][j][r] - m_new);
-          psum += pr[r];
-        }
-        pb[qi][j][0] = pack2bf(pr[0], pr[1]);
-        pb[qi][j][1] = pack2bf(pr[2], pr[3]);
-      }
-      {
-        float lo, hi;
-        lane_halves<false>(psum, lo, hi);
-        psum = lo + hi;
-        lane_halves<true>(psum, lo, hi);
-        psum = lo + hi;
-      }
-      l_run[qi] = l_run[qi] * corr + psum;
-      m_run[qi] = m_new;
-#pragma unroll
-      for (int d = 0; d < DB; ++d)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc_o[qi][d][r] *= corr;
-    }
-    // O^T += V^T . P^T, two 32-key steps
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      bf16x8 bfrag[QB];
-#pragma unroll
-      for (int qi = 0; qi < QB; ++qi) {
-        const u32x4 bw = {pb[qi][2 * u][0], pb[qi][2 * u][1], pb[qi][2 * u + 1][0], pb[qi][2 * u + 1][1]};
-        bfrag[qi] = __builtin_bit_cast(bf16x8, bw);
-      }
-#pragma unroll
-      for (int d = 0; d < DB; ++d) {
-        // lane 4q + p of group g addresses keys 32u + 4g + q (+16), dims 16d + 4p .. +3; lane col
-        // receives dim 16d + col of those 4 keys
-        const bf16_t* vr = Vs + (32 * u + 4 * g + ((lane >> 2) & 3)) * VP + 16 * d + 4 * (lane & 3);
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)vr);
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr + 16 * VP));
-        const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
-        const u32x4 aw = {l2.x, l2.y, h2.x, h2.y};
-#pragma unroll
-        for (int qi = 0; qi < QB; ++qi) acc_o[qi][d] = mfma_bf16(__builtin_bit_cast(bf16x8, aw), bfrag[qi], acc_o[qi][d]);
-      }
-    }
-  }
-  // y[b*T + t][h*HS + d] = O / l; lane holds d = 16 db + 4 g + r of its query
-#pragma unroll
-  for (int qi = 0; qi < QB; ++qi) {
-    if (t[qi] < T) {
-      const float inv = 1.f / l_run[qi];
-      bf16_t* yrow = y + ((size_t)b * T + t[qi]) * C + h * HS;
-#pragma unroll
-      for (int d = 0; d < DB; ++d) {
-        const uint2 o = make_uint2(pack2bf(acc_o[qi][d][0] * inv, acc_o[qi][d][1] * inv),
-                                   pack2bf(acc_o[qi][d][2] * inv, acc_o[qi][d][3] * inv));
-        *reinterpret_cast<uint2*>(yrow + 16 * d + 4 * g) = o;
-      }
-    }
+  } else {
+    run(gridDim.x - 1 - blockIdx.x);  // long (late) query blocks first
   }
 }
 
 template <int HS, int QB>
 static void flash_launch(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
-                         int n_head, int S, float sl2, hipStream_t st) {
-  const dim3 grid((T + 64 * QB - 1) / (64 * QB), n_head, B);
-  hipLaunchKernelGGL((flash_prefill_kernel<HS, QB>), grid, dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)kcache,
-                     (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
+                         int n_head, int S, float sl2, bool pair, hipStream_t st) {
+  const int nqb = (T + 64 * QB - 1) / (64 * QB);
+  if (pair) {
+    hipLaunchKernelGGL((flash_prefill_kernel<HS, QB, true>), dim3((nqb + 1) / 2, n_head, B), dim3(256), 0, st,
+                       (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
+  } else {
+    hipLaunchKernelGGL((flash_prefill_kernel<HS, QB, false>), dim3(nqb, n_head, B), dim3(256), 0, st,
+                       (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
+  }
 }
 
 }  // namespace llj
@@ -226,12 +246,14 @@ int llj_attention_prefill(const void* q, const void* kcache, const void* vcache,
   hipStream_t st = (hipStream_t)stream;
   const char* e = getenv("LLJ_FLASH_QB");  // A/B in one process: 1 or 2 query blocks per wave
   const int qbw = e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : LLJ_FLASH_QB;
+  const char* ep = getenv("LLJ_FLASH_PAIR");  // 1 / 0: pair a long and a short query block per workgroup
+  const bool pair = ep && ep[0] ? ep[0] != '0' : LLJ_FLASH_PAIR != 0;
   if (head_size == 128) {
-    if (qbw == 2) flash_launch<128, 2>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, st);
-    else flash_launch<128, 1>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, st);
+    if (qbw == 2) flash_launch<128, 2>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, pair, st);
+    else flash_launch<128, 1>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, pair, st);
   } else if (head_size == 64) {
-    if (qbw == 2) flash_launch<64, 2>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, st);
-    else flash_launch<64, 1>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, st);
+    if (qbw == 2) flash_launch<64, 2>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, pair, st);
+    else flash_launch<64, 1>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, pair, st);
   } else {
     return LLJ_EINVAL;
   }

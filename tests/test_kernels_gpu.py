@@ -1140,13 +1140,16 @@ def test_gemm_qkv_rope_kv(hip, wfmt, B, T_, nh, hs):
 
 
 @pytest.mark.parametrize("hs,nh,B,T_,S,p0", [(128, 4, 1, 200, 256, 0), (64, 4, 2, 130, 160, 17), (128, 2, 1, 64, 64, 0),
-                                            (128, 3, 1, 33, 2048, 1000)])
+                                            (128, 3, 1, 33, 2048, 1000), (128, 2, 1, 700, 1024, 0)])
+@pytest.mark.parametrize("pair", ["0", "1"])
 @pytest.mark.parametrize("qb", ["1", "2"])
-def test_attention_prefill_flash(hip, hs, nh, B, T_, S, p0, qb, monkeypatch):
+def test_attention_prefill_flash(hip, hs, nh, B, T_, S, p0, qb, pair, monkeypatch):
     """The MFMA flash attention for prompt rows (llj_attention_prefill) against the oracle: causal
     over cache slots 0 .. p0 + t, partial last query block, ragged key tiles, earlier context (p0 > 0);
-    one or two 16-query blocks per wave (LLJ_FLASH_QB, read per call)."""
+    one or two 16-query blocks per wave (LLJ_FLASH_QB) and one query block or a (long, short) pair
+    per workgroup (LLJ_FLASH_PAIR; odd block counts leave the middle block alone), read per call."""
     monkeypatch.setenv("LLJ_FLASH_QB", qb)
+    monkeypatch.setenv("LLJ_FLASH_PAIR", pair)
     rng = np.random.default_rng(hs + T_ + p0)
     C = nh * hs
     kc = bf16(rng.standard_normal((B, nh, S, hs)))
