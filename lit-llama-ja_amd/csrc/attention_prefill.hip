@@ -30,10 +30,10 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 #define LLJ_FLASH_OCC 3  // workgroups per CU the QB = 1 register budget is sized for (152 VGPRs, no spill; 2: 7B T=2048 window 40.0 vs 39.5 ms)
 #endif
 #ifndef LLJ_FLASH_PAIR
-#define LLJ_FLASH_PAIR 0  // causal balance: one workgroup per (long, short) pair of query blocks
+#define LLJ_FLASH_PAIR 1  // causal balance: one workgroup per (long, short) pair of query blocks (7B window -1.0 ms)
 #endif
 #ifndef LLJ_FLASH_QB
-#define LLJ_FLASH_QB 2  // 16-query blocks per wave (2: every K / V fragment read feeds two MFMAs; 7B window -0.1..-0.4 ms, profiles/r04_prefill_ab.json)
+#define LLJ_FLASH_QB 1  // 16-query blocks per wave (2: every K / V fragment read feeds two MFMAs; with the pairing 1 is faster)
 #endif
 // QB 16-query blocks per wave: 64 QB queries per workgroup; a K fragment (S^T) and a V^T fragment
 // (O^T) read from LDS feed QB MFMAs, and the tile's staging and barriers are shared by 4 x 16 QB queries
