@@ -640,6 +640,9 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
 #ifndef LLJ_GEMM_GLDS_W4
 #define LLJ_GEMM_GLDS_W4 0  // int4: 42.5 ms vs 37.6 with the register-staged 256-row kernel
 #endif
+#ifndef LLJ_GLDS_W4_WN
+#define LLJ_GLDS_W4_WN 4
+#endif
 #ifndef LLJ_GLDS_PRE
 #define LLJ_GLDS_PRE 1  // 256 x 128 tiles: read both MFMA steps' fragments of a chunk before its MFMAs (bf16 window 35.9 -> 35.4 ms)
 #endif
@@ -650,7 +653,9 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 
 template <int WF, int BN>
 struct GldsGeo {
-  static constexpr int WN = BN == 256 ? 4 : 2, WM = 8 / WN;
+  // waves along N: 4 at BN 256; at BN 128, 2 for bf16 (64 x 64 per wave: fewer A fragment reads) and
+  // LLJ_GLDS_W4_WN for int4 (4: 128 x 32 per wave, each B fragment dequantized by 2 waves instead of 4)
+  static constexpr int WN = BN == 256 ? 4 : WF == GWF_W4 ? LLJ_GLDS_W4_WN : 2, WM = 8 / WN;
   static constexpr int MI = 256 / WM / 16, NJ = BN / WN / 16;
   static constexpr size_t SA = 256 * 128;
   static constexpr size_t SB = WF == GWF_W4 ? 8192 : (size_t)BN * 128;  // W4 at BN 128: waves 4-7 stage a copy
