@@ -37,7 +37,7 @@ __device__ __forceinline__ void softmax_merge(float& mx, float& l, float* o, con
 // PART: split-K over the keys (long contexts): this block takes key range `split` of `nsplit`
 // equal ranges (>= one pass of NG * U keys each) of the valid keys and writes its unnormalized partial (outputs, running max,
 // sum) to part[((m * nh + h) * nsplit + split) * (HS + 2)]; attention_combine_kernel merges.
-template <int HS, int U, int NTH, bool PART = false>
+template <int HS, int U, int NTH, bool PART = false, int SPECU = U / 2>
 __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                const int* __restrict__ pos, int T, int S, int nh, float scale_log2,
@@ -85,7 +85,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   // for small grids (bs = 1: 32 blocks), where the launch is latency-bound; with many blocks the
   // extra rows past p cost more bandwidth than the latency saved (7B bs=8: 1.79 -> 1.87 ms)
   const bool spec = !PART && gridDim.x * gridDim.y <= 64;
-  if (spec) load_pass(kg, S, kw, vw, 0, U / 2);
+  if (spec) load_pass(kg, S, kw, vw, 0, SPECU);
   const int ps = pos[t];
   const int nvalid = ps < S ? ps + 1 : S;
   // key range of this block (the whole valid range unless split)
@@ -122,7 +122,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   bool first = spec;
   for (int j0 = jbeg + kg; j0 < jend; j0 += NG * U) {
     if (!first) load_pass(j0, jend, kw, vw);
-    else load_pass(j0, jend, kw, vw, U / 2, U);  // the speculative pass's second half
+    else if (SPECU < U) load_pass(j0, jend, kw, vw, SPECU, U);  // the speculative pass's second half
     first = false;
 #pragma unroll
     for (int u = 0; u < U; ++u) {

@@ -1,6 +1,8 @@
 // Decode-step ops around the weight-streaming GEMVs: token embedding, standalone RMSNorm
 // (prefill rows beyond the fused-LDS limit), causal attention over the KV cache, and the
 // greedy (top_k = 1) next-token selection.
+#include <cstdlib>
+
 #include "common.h"
 #include "attention.h"
 #ifndef LLJ_NORM_SC1
@@ -110,13 +112,13 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__
 #ifndef LLJ_ATT_U
 #define LLJ_ATT_U 8  // keys per 16-lane group per pass
 #endif
-template <int HS, int U, int NTH>
+template <int HS, int U, int NTH, int SPECU>
 __global__ __launch_bounds__(NTH) void attention_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                         const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                         const int* __restrict__ pos, int T, int S, int nh,
                                                         float scale_log2) {
   __shared__ float lds[attention_lds_floats<HS, NTH>()];
-  attention_body<HS, U, NTH>(q, kc, vc, y, pos, T, S, nh, scale_log2, blockIdx.x, blockIdx.y, lds);
+  attention_body<HS, U, NTH, false, SPECU>(q, kc, vc, y, pos, T, S, nh, scale_log2, blockIdx.x, blockIdx.y, lds);
 }
 
 // split-K attention over the keys (long contexts): block (head, row, split) -> partial
@@ -431,15 +433,22 @@ int llj_attention(const void* q, const void* kcache, const void* vcache, void* y
   LLJ_REQUIRE(B > 0 && T > 0 && n_head > 0 && S > 0);
   const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
   dim3 grid(n_head, B * T);
+  // keys loaded before the position is known at small grids: half a pass (default) or a whole one
+  // (LLJ_ATT_SPEC=full: one memory latency less, more K / V rows read past the position)
+  const char* e = getenv("LLJ_ATT_SPEC");
+  const bool full = e && e[0] == 'f';
+  hipStream_t st = (hipStream_t)stream;
+#define LLJ_ATT_LAUNCH(HS_, SU_)                                                                                   \
+  hipLaunchKernelGGL((attention_kernel<HS_, LLJ_ATT_U, LLJ_ATT_NTH, SU_>), grid, dim3(LLJ_ATT_NTH), 0, st,          \
+                     (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2)
   if (head_size == 128) {
-    hipLaunchKernelGGL((attention_kernel<128, LLJ_ATT_U, LLJ_ATT_NTH>), grid, dim3(LLJ_ATT_NTH), 0, (hipStream_t)stream, (const bf16_t*)q,
-                       (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
+    if (full) LLJ_ATT_LAUNCH(128, LLJ_ATT_U); else LLJ_ATT_LAUNCH(128, LLJ_ATT_U / 2);
   } else if (head_size == 64) {
-    hipLaunchKernelGGL((attention_kernel<64, LLJ_ATT_U, LLJ_ATT_NTH>), grid, dim3(LLJ_ATT_NTH), 0, (hipStream_t)stream, (const bf16_t*)q,
-                       (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
+    if (full) LLJ_ATT_LAUNCH(64, LLJ_ATT_U); else LLJ_ATT_LAUNCH(64, LLJ_ATT_U / 2);
   } else {
     return LLJ_EINVAL;
   }
+#undef LLJ_ATT_LAUNCH
   LLJ_CHECK_LAUNCH();
   return 0;
 }

@@ -311,7 +311,9 @@ def _attn_oracle(q, kc, vc, pos, S, T_, nh, hs):
 @pytest.mark.parametrize("hs,nh,B,T_,S,p0", [(128, 4, 1, 1, 144, 80), (128, 3, 8, 1, 144, 143), (64, 4, 2, 5, 16, 0),
                                             (128, 2, 1, 1, 10, 37), (128, 2, 2, 1, 2048, 2000), (128, 32, 1, 1, 256, 90),
                                             (128, 8, 1, 1, 256, 40)])
-def test_attention(hip, hs, nh, B, T_, S, p0):
+@pytest.mark.parametrize("spec", ["half", "full"])
+def test_attention(hip, hs, nh, B, T_, S, p0, spec, monkeypatch):
+    monkeypatch.setenv("LLJ_ATT_SPEC", spec)  # keys loaded before the position is known (bs = 1 grids)
     rng = np.random.default_rng(hs + S + p0)
     C = nh * hs
     kc = bf16(rng.standard_normal((B, nh, S, hs)))

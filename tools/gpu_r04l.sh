@@ -11,13 +11,20 @@ chk() {
   echo "$1 rc=$2" >> $O/status.log
   case $2 in 124|134|137|139|-6|-11) echo "stopping after $1" >> $O/status.log; exit $2;; esac
 }
-timeout -k 10 200 python -u -m pytest tests/test_kernels_gpu.py -k "glds" -q --timeout 120 --timeout-method thread > $O/t_glds.log 2>&1
+timeout -k 10 200 python -u -m pytest tests/test_kernels_gpu.py -k "glds or test_attention" -q --timeout 120 --timeout-method thread > $O/t_glds.log 2>&1
 chk "glds tests" $?
 for rep in 1 2; do
   for cfg in "X=0" "LLJ_GEMM_GLDS=1"; do
     echo "== rep $rep $cfg" >> $O/prefill_bench.log
     env $cfg timeout -k 10 200 python -u tools/prefill_bench.py --T 2048 --modes gptq.int4 --iters 5 >> $O/prefill_bench.log 2>&1
     chk "prefill bench $cfg" $?
+  done
+done
+for rep in 1 2; do
+  for sp in half full; do
+    echo "== rep $rep LLJ_ATT_SPEC=$sp" >> $O/decode_ab.log
+    LLJ_ATT_SPEC=$sp timeout -k 10 200 python -u bench.py --decode-only --steps 300 --warmup 20 >> $O/decode_ab.log 2>&1
+    chk "decode $sp" $?
   done
 done
 D=/tmp/r04l
