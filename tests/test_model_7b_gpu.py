@@ -37,7 +37,8 @@ pytestmark = pytest.mark.gpu
 
 C7 = Cfg(block_size=128, n_layer=2, n_head=32, n_embd=4096, vocab_size=32000)
 C13 = Cfg(block_size=128, n_layer=2, n_head=40, n_embd=5120, vocab_size=32000)
-SEEDS = {4096: 4096, 5120: 5120}
+C30 = Cfg(block_size=128, n_layer=1, n_head=52, n_embd=6656, vocab_size=32000)  # mlp.c_proj K = 17920
+SEEDS = {4096: 4096, 5120: 5120, 6656: 30}
 REL = {"gptq.int4": 1.2e-2, None: 1.3e-2, "llm.int8": 5e-2}
 REL_I8 = {1: 3e-2, 2: 3e-2, 8: 5e-2}  # llm.int8 decode by batch: 2x profiles/r04_noise_floor.json
 # the 64-token prompt tests, about 2x profiles/r04_noise_floor_prefill.json: every prompt row (floor
@@ -205,3 +206,21 @@ def test_13b_width_prefill_gemm_flash_vs_oracle():
     ref, ref_rows = _oracle_steps(orc, ids, t_prompt=t, steps=2, s=96, all_rows=True)
     _check(got_rows, ref_rows, REL_PREFILL_ROWS["gptq.int4"], "13b prefill gptq.int4 rows")
     _check(got, ref, REL_PREFILL_STEPS["gptq.int4"], "13b prefill gptq.int4 steps")
+
+
+def test_30b_width_llm_int8_prefill_vs_oracle():
+    """30B width through the LLM.int8 prefill (advisor round 3): C = 6656, 52 heads of 128,
+    n_hidden 17920, so mlp.c_proj's K = 17920 exceeds the outlier gathers' LDS list capacity
+    (I8_GATHER_MAX): the model sizes the gathers by that capacity and the GEMM takes the per-tile
+    side product when a count exceeds it. A 40-token prompt (int8 GEMMs + flash) and one decode step
+    against the oracle's LLM.int8() restatement (parity unpinned: bitsandbytes absent)."""
+    from lit_llama import model as MD
+
+    t = 40
+    assert t >= MD.GEMM_MIN_ROWS and t >= MD.FLASH_MIN_T
+    model, orc = _get(C30, "llm.int8")
+    ids = np.random.default_rng(66).integers(3, C30.vocab_size, (1, t + 2))
+    got, got_rows = _gpu_steps(model, ids, t_prompt=t, steps=1, s=96, all_rows=True)
+    ref, ref_rows = _oracle_steps(orc, ids, t_prompt=t, steps=1, s=96, all_rows=True)
+    _check(got_rows, ref_rows, REL_PREFILL_ROWS["llm.int8"], "30b prefill llm.int8 rows")
+    _check(got, ref, REL_PREFILL_STEPS["llm.int8"], "30b prefill llm.int8 steps")

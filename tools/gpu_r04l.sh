@@ -13,6 +13,8 @@ chk() {
 }
 timeout -k 10 200 python -u -m pytest tests/test_kernels_gpu.py -k "glds or test_attention" -q --timeout 120 --timeout-method thread > $O/t_glds.log 2>&1
 chk "glds tests" $?
+timeout -k 10 300 python -u -m pytest tests/test_model_7b_gpu.py -k "30b" -q --timeout 280 --timeout-method thread > $O/t_30b.log 2>&1
+chk "30b int8 prefill test" $?
 for rep in 1 2; do
   for cfg in "X=0" "LLJ_GEMM_GLDS=1"; do
     echo "== rep $rep $cfg" >> $O/prefill_bench.log
