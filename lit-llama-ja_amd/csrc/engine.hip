@@ -106,27 +106,6 @@ __device__ __forceinline__ unsigned lds_ld(const unsigned* p) { return __hip_ato
 __device__ __forceinline__ void lds_st(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }  // compiler-only ordering point
 
-#ifndef LLJ_ENG_F16
-#define LLJ_ENG_F16 0  // A/B: f16 A fragments + 5-op-per-word int4 dequant (below)
-#endif
-#if LLJ_ENG_F16
-// f16 operands: the W4P word's pairs 0 / 2 (bits 0-3 | 16-19 of w and of w >> 8) become f16 1024 + q,
-// pairs 1 / 3 (bits 4-7 | 20-23) 1024 + 16 q, each by one v_and_or_b32 -- 5 VALU per word instead
-// of 7; the A fragments carry 1/16 at the k of pairs 1 / 3 (odd pair index), so the MFMA sums
-// A' (1024 + s q) = 1024 sum A' + sum A q exactly (f16 products are exact in fp32); the epilogue
-// removes 1024 sum A' + z sum A. bf16 -> f16 is exact for |A| in [2^-10, 65504] (the 1/16 pairs:
-// [2^-10, 2^-14) lose bits as f16 subnormals: <= 2^-24 absolute per element)
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef f16x8 afrag_t;
-constexpr uint32_t kDqMag = 0x64006400u;  // f16 1024
-__device__ __forceinline__ f16x8 dequant_lo(uint32_t w, uint32_t m_lo, uint32_t m_hi, uint32_t mag) {
-  const uint32_t t = w >> 8;
-  uint4 b = make_uint4(and_or(w, m_lo, mag), and_or(w, m_hi, mag), and_or(t, m_lo, mag), and_or(t, m_hi, mag));
-  return __builtin_bit_cast(f16x8, b);
-}
-__device__ __forceinline__ f32x4 mfma_a(afrag_t a, f16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
-#define LLJ_DQ(w) dequant_lo((w), msk, msk_hi, mag)
-#else
 typedef bf16x8 afrag_t;
 constexpr uint32_t kDqMag = 0x43004300u;  // bf16 128
 __device__ __forceinline__ bf16x8 dequant(uint32_t w, uint32_t msk, uint32_t mag) {
@@ -135,7 +114,6 @@ __device__ __forceinline__ bf16x8 dequant(uint32_t w, uint32_t msk, uint32_t mag
 }
 __device__ __forceinline__ f32x4 mfma_a(afrag_t a, bf16x8 b, f32x4 c) { return mfma_bf16(a, b, c); }
 #define LLJ_DQ(w) dequant((w), msk, mag)
-#endif
 __device__ __forceinline__ float rstd_bf16(float ss_over_k, float eps) {
   return round_bf(rsqrtf(round_bf(round_bf(ss_over_k) + eps)));  // model.py:281-282 on bf16 tensors
 }
@@ -343,10 +321,9 @@ __device__ __forceinline__ void stage_sz(Ctx& X, float2* eop, const llj_engine_p
 // norm ops (QKV, SwiGLU, lm_head): x (gathered, or the embedding row at layer 0) -> A raw, then
 // A = RMSNorm(x) * gain in place (model.py:276-283, bf16 rounding points) by the same threads that
 // gathered each pair, and the raw pairs of this CU's residual tile columns -> xown[buf]; plain ops
-// (c_proj, down): the gathered vector -> A. Returns sum_k A[k] (and, LLJ_ENG_F16, A rewritten as the
-// pre-scaled f16 A' with sum_k A'[k] in *asum16).
+// (c_proj, down): the gathered vector -> A. Returns sum_k A[k].
 __device__ __forceinline__ float stage(Ctx& X, const Lds& L, bool norm, int buf, const unsigned long long* g, unsigned tag,
-                                       const bf16_t* direct, const bf16_t* gain, float eps, int K, float* asum16) {
+                                       const bf16_t* direct, const bf16_t* gain, float eps, int K) {
   uint32_t* xo2 = reinterpret_cast<uint32_t*>(L.xown[buf]);
   const int own0 = 8 * X.s.g;  // first pair of the CU's c_proj / down tile (tile g: n_embd / 16 <= CUs)
   uint32_t* a2 = reinterpret_cast<uint32_t*>(L.A);
@@ -395,35 +372,12 @@ __device__ __forceinline__ float stage(Ctx& X, const Lds& L, bool norm, int buf,
       }
     }
   }
-  float a16 = 0.f;
-#if LLJ_ENG_F16
-  // the pairs this thread wrote (gathered or normalized; the same index map) -> f16 A', 1/16 on odd pairs
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {  // K / 2 <= 16 * 64 NC pairs (H <= 14336)
-    const int idx = X.lane + 64 * X.wave + 64 * NC * k;
-    if (idx < K / 2) {
-      const uint32_t v = a2[idx];
-      const float sc = (idx & 1) ? 0.0625f : 1.f;
-      const _Float16 lo = (_Float16)(bflo(v) * sc), hi = (_Float16)(bfhi(v) * sc);
-      a16 += (float)lo + (float)hi;
-      a2[idx] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
-    }
-  }
-  a16 = wave_sum(a16);
-  if (X.lane == 0) L.misc[64 + X.wave] = a16;
-#endif
   asum = wave_sum(asum);
   if (X.lane == 0) L.misc[16 + X.wave] = asum;
   cbarrier(X, L);
   float a = 0.f;
 #pragma unroll
   for (int w = 0; w < NC; ++w) a += L.misc[16 + w];
-#if LLJ_ENG_F16
-  a16 = 0.f;
-#pragma unroll
-  for (int w = 0; w < NC; ++w) a16 += L.misc[64 + w];
-#endif
-  *asum16 = a16;
   return a;
 }
 
@@ -508,18 +462,14 @@ __device__ __forceinline__ void epilogue(Ctx& X, const Lds& L, int op, Epi& E, i
 constexpr int AREG_C = 5;  // chunks per consumer whose A fragments stay in registers (K <= 4480 at NC 7)
 constexpr int KB = 3;      // chunks per read batch of the long-K form (3 x 5 reads: lgkmcnt counts to 15)
 template <int NM, bool AREG>
-__device__ __forceinline__ void consume_t(Ctx& X, const Lds& L, const float2* eop, int op, float asum, float asum16,
+__device__ __forceinline__ void consume_t(Ctx& X, const Lds& L, const float2* eop, int op, float asum,
                                           int& red_par, Epi& E) {
   const Shape& s = X.s;
   const int nt = tiles_of_cu(s, op), kc = op_kc(s, op);
   const int lane = X.lane, grp = lane >> 4, w = X.wave;
-  uint32_t msk = 0x000F000Fu, mag = kDqMag;  // 128 + q (bf16) / 1024 + q (f16) via one v_and_or_b32 per pair
+  uint32_t msk = 0x000F000Fu, mag = kDqMag;  // 128 + q (bf16) via one v_and_or_b32 per pair
   asm volatile("" : "+s"(msk));
   asm volatile("" : "+v"(mag));
-#if LLJ_ENG_F16
-  uint32_t msk_hi = 0x00F000F0u;
-  asm volatile("" : "+s"(msk_hi));
-#endif
   const int nch = kc > w ? (kc - w + NC - 1) / NC : 0;  // chunks of every tile this wave takes
   afrag_t ar[AREG ? AREG_C : 1][4];
   if constexpr (AREG) {
@@ -654,14 +604,8 @@ __device__ __forceinline__ void consume_t(Ctx& X, const Lds& L, const float2* eo
       }
       const int es = slot < kEopTiles ? slot : kEopTiles - 1;
       const float2 e1 = eop[(es * 2 + 0) * 16 + col], e2 = eop[(es * 2 + 1) * 16 + col];
-#if LLJ_ENG_F16
-      // s * (sum A' (1024 + s_k q) - 1024 sum A' - z sum A), z = (128 + z) - 128
-      y1 = e1.x * (y1 - 1024.f * asum16 - (e1.y - 128.f) * asum);
-      y2 = e2.x * (y2 - 1024.f * asum16 - (e2.y - 128.f) * asum);
-#else
       y1 = e1.x * (y1 - e1.y * asum);  // s * (sum A (128 + q) - (128 + z) sum A)
       y2 = e2.x * (y2 - e2.y * asum);
-#endif
       epilogue(X, L, op, E, slot, tile, n, y1, y2);
     }
     red_par ^= 1;
@@ -669,11 +613,11 @@ __device__ __forceinline__ void consume_t(Ctx& X, const Lds& L, const float2* eo
   X.n_used = gbase;
 }
 // (C <= AREG_C * NC * 128 is required by llj_engine_step: only the down projection takes the long-K form)
-__device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop, int op, float asum, float asum16, int& red_par,
+__device__ __forceinline__ void consume(Ctx& X, const Lds& L, const float2* eop, int op, float asum, int& red_par,
                                         Epi& E) {
-  if (op == OP_SW) consume_t<2, true>(X, L, eop, op, asum, asum16, red_par, E);
-  else if (op == OP_DOWN) consume_t<1, false>(X, L, eop, op, asum, asum16, red_par, E);
-  else consume_t<1, true>(X, L, eop, op, asum, asum16, red_par, E);
+  if (op == OP_SW) consume_t<2, true>(X, L, eop, op, asum, red_par, E);
+  else if (op == OP_DOWN) consume_t<1, false>(X, L, eop, op, asum, red_par, E);
+  else consume_t<1, true>(X, L, eop, op, asum, red_par, E);
 }
 
 // Attention of this CU's unit (head h, dims 16 j + [0, 16)) for the token at position p
@@ -1102,14 +1046,13 @@ __global__ __launch_bounds__(NTH, 1) void engine_step_kernel(llj_engine_plan P) 
     const bf16_t* direct = op == OP_QKV && l == 0 ? reinterpret_cast<const bf16_t*>(P.wte) + (size_t)tok * C : nullptr;
     const void* gain = op == OP_QKV ? Ly->rms1 : op == OP_SW ? Ly->rms2 : P.ln_f;
     const float eps = op == OP_QKV ? Ly->eps1 : op == OP_SW ? Ly->eps2 : P.eps_f;
-    float asum16 = 0.f;
     const float asum = stage(X, L, norm, op == OP_SW ? 1 : 0, g, gtag, direct, reinterpret_cast<const bf16_t*>(gain), eps,
-                             op == OP_DOWN ? H : C, &asum16);
+                             op == OP_DOWN ? H : C);
     if (X.wave == 0 && l < 8 && op != OP_HEAD) stamp(P, X.lane, sb + 2 * op + (op == OP_QKV ? 0 : 1));
     if (op == OP_HEAD && X.wave == 0) stamp(P, X.lane, 126);
     X.stamp_base = (l < 2 && (op == OP_SW || op == OP_QKV)) ? 108 + 3 * (2 * l + (op == OP_SW)) : -1;
     if (op == OP_QKV && s.unit >= 0) kv_prefetch(X, P, l, p, kvpre);  // lands while the QKV tiles run
-    consume(X, L, eop, op, asum, asum16, red_par, E);
+    consume(X, L, eop, op, asum, red_par, E);
     if (X.wave == 0 && l < 8 && op == OP_DOWN) stamp(P, X.lane, sb + 8);
   }
   if (X.wave == 0) stamp(P, X.lane, 127);
