@@ -11,10 +11,8 @@ chk() {
   echo "$1 rc=$2" >> $O/status.log
   case $2 in 124|134|137|139|-6|-11) echo "stopping after $1" >> $O/status.log; exit $2;; esac
 }
-timeout -k 10 200 python -u -m pytest tests/test_kernels_gpu.py -k "glds or test_attention" -q --timeout 120 --timeout-method thread > $O/t_glds.log 2>&1
-chk "glds tests" $?
-timeout -k 10 300 python -u -m pytest tests/test_model_7b_gpu.py -k "30b" -q --timeout 280 --timeout-method thread > $O/t_30b.log 2>&1
-chk "30b int8 prefill test" $?
+timeout -k 10 840 python -u -m pytest tests -m gpu -q --timeout 280 --timeout-method thread -p no:cacheprovider > $O/t_all.log 2>&1
+chk "gpu tests" $?
 for rep in 1 2; do
   for cfg in "X=0" "LLJ_GEMM_GLDS=1"; do
     echo "== rep $rep $cfg" >> $O/prefill_bench.log
