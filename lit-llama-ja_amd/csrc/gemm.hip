@@ -174,6 +174,9 @@ constexpr int kGBM = 128, kGBN = 128, kGBK = 64, kGNT = 256;
 #ifndef LLJ_GEMM_BM256_W4
 #define LLJ_GEMM_BM256_W4 1  // int4 W4P (39.6 -> 38.4 ms; 256 VGPRs + 64-72 B of scratch per lane)
 #endif
+#ifndef LLJ_GEMM_W4_WIDE
+#define LLJ_GEMM_W4_WIDE 0  // int4 256-row tiles as 2 x 4 waves of 128 x 32 (A/B)
+#endif
 #ifndef LLJ_GEMM_MFAST_W4
 #define LLJ_GEMM_MFAST_W4 0  // int4: m-fastest tile order too (A/B)
 #endif
@@ -216,7 +219,12 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
   constexpr bool GRP = WF == GWF_W4G;                  // grouped int4: dequantized to the weight values
   constexpr bool I8 = WF == GWF_I8;                    // LLM.int8(): int8 MFMA + fp16 outlier side product
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int WRN = BM / 64;  // row groups of waves
+  // wave grid: WRN row groups x WCN column groups of (16 MI) x (16 NJ) outputs; int4 256-row tiles
+  // optionally 2 x 4 waves of 128 x 32 (LLJ_GEMM_W4_WIDE: each B fragment dequantized by 2 waves, not 4)
+  constexpr bool WIDE = WF == GWF_W4 && BM == 256 && LLJ_GEMM_W4_WIDE;
+  constexpr int WRN = WIDE ? 2 : BM / 64;  // row groups of waves
+  constexpr int WCN = 2 * BM / 64 / WRN;   // column groups (2 * BM threads = 2 * BM / 64 waves)
+  constexpr int MI = BM / WRN / 16, NJ = kGBN / WCN / 16;
   const int wr = wave % WRN, wc = wave / WRN;
   const int row = lane & 15, g = lane >> 4;
   const int M = p.M, K = p.K, KC = I8 ? K / 128 : K / kGBK, KC128 = K / 128;
@@ -279,9 +287,9 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
       const size_t nt = (size_t)(n0 / 16 + (bt >> 5));  // (256-row tiles: threads 256.. load a copy, never stored)
       breg[slot][0] = __builtin_nontemporal_load(w + (nt * KC128 + (c >> 1)) * 64 + 32 * (c & 1) + (bt & 31));
       if constexpr (GRP) {
-        const size_t go = (size_t)((c >> 1) / p.gch) * p.N + n0 + wc * 64 + row;
+        const size_t go = (size_t)((c >> 1) / p.gch) * p.N + n0 + wc * 16 * NJ + row;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) szr[slot][j] = p.sz[go + 16 * j];
+        for (int j = 0; j < NJ; ++j) szr[slot][j] = p.sz[go + 16 * j];
       }
     } else if constexpr (WF == GWF_W8) {  // the same W4P lane of the low plane and of the high plane
       const u32x4* w = reinterpret_cast<const u32x4*>(p.W);
@@ -330,12 +338,12 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
   asm volatile("" : "+s"(msk));
   asm volatile("" : "+v"(mag));
   if constexpr (WF == GWF_W8) asm volatile("" : "+v"(mag_hi));
-  f32x4 acc[4][4];
-  i32x4 iacc[4][4];  // GWF_I8
+  f32x4 acc[MI][NJ];
+  i32x4 iacc[MI][NJ];  // GWF_I8
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       iacc[i][j] = i32x4{0, 0, 0, 0};
     }
@@ -370,17 +378,17 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
     const bf16_t* a = As(buf);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {  // MFMA k-steps of the chunk: k = 32 s + 8 g + [0, 8)
-      bf16x8 af[4], bfr[4], bhi[4];
+      bf16x8 af[MI], bfr[NJ], bhi[NJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = wr * 64 + 16 * i + row;
+      for (int i = 0; i < MI; ++i) {
+        const int r = wr * 16 * MI + 16 * i + row;
         af[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(a + r * kAP + 32 * s + 8 * g));
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         if constexpr (WF == GWF_W4) {
-          // word g of W4P lane 16 (2h + s) + column of tile wc * 4 + j (the chunk's half)
-          const uint32_t w = reinterpret_cast<const uint32_t*>(Bs(buf))[((wc * 4 + j) * 32 + 16 * s + row) * 4 + g];
+          // word g of W4P lane 16 (2h + s) + column of tile wc * NJ + j (the chunk's half)
+          const uint32_t w = reinterpret_cast<const uint32_t*>(Bs(buf))[((wc * NJ + j) * 32 + 16 * s + row) * 4 + g];
           const uint4 d = make_uint4(and_or(w, msk, mag), and_or(w >> 4, msk, mag), and_or(w >> 8, msk, mag),
                                      and_or(w >> 12, msk, mag));
           bfr[j] = __builtin_bit_cast(bf16x8, d);
@@ -389,7 +397,7 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
           // weight times the scale in the scale's precision, then stored to bf16): (128 + q) - (128 + z)
           // is an exact small integer, its product with s rounds once to fp32 (exact for bf16 / fp16
           // scales, the reference's fp32 product for fp32 scales), the conversion once to bf16
-          const uint32_t w = reinterpret_cast<const uint32_t*>(Bs(buf))[((wc * 4 + j) * 32 + 16 * s + row) * 4 + g];
+          const uint32_t w = reinterpret_cast<const uint32_t*>(Bs(buf))[((wc * NJ + j) * 32 + 16 * s + row) * 4 + g];
           const f32x2 sc = {gsz[j].x, gsz[j].x}, zz = {gsz[j].y, gsz[j].y};
           uint32_t o[4];
 #pragma unroll
@@ -397,23 +405,23 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
           bfr[j] = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
         } else if constexpr (WF == GWF_W8) {
           const uint32_t* b32 = reinterpret_cast<const uint32_t*>(Bs(buf));
-          const int wi = ((wc * 4 + j) * 32 + 16 * s + row) * 4 + g;
+          const int wi = ((wc * NJ + j) * 32 + 16 * s + row) * 4 + g;
           const uint32_t wl = b32[wi], wh = b32[kGNT * 4 + wi];
           bfr[j] = __builtin_bit_cast(bf16x8, make_uint4(and_or(wl, msk, mag), and_or(wl >> 4, msk, mag),
                                                          and_or(wl >> 8, msk, mag), and_or(wl >> 12, msk, mag)));
           bhi[j] = __builtin_bit_cast(bf16x8, make_uint4(and_or(wh, msk, mag_hi), and_or(wh >> 4, msk, mag_hi),
                                                          and_or(wh >> 8, msk, mag_hi), and_or(wh >> 12, msk, mag_hi)));
         } else {
-          const int n = wc * 64 + 16 * j + row;
+          const int n = wc * 16 * NJ + 16 * j + row;
           bfr[j] = __builtin_bit_cast(
               bf16x8, *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(Bs(buf)) + n * kAP + 32 * s + 8 * g));
         }
       }
       if (LLJ_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);  // the MFMA cluster ahead of the other waves' staging
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
           if constexpr (WF == GWF_W8) acc[i][j] = mfma_bf16(af[i], bhi[j], acc[i][j]);
         }
@@ -441,11 +449,11 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
   __syncthreads();
 
   // ---- GWF_I8: fp16 outlier side product into sacc (the K loop's LDS is free now)
-  f32x4 sacc[4][4];
+  f32x4 sacc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) sacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (I8) {
     int* s_pre = reinterpret_cast<int*>(smem);  // [kNSB + 1] prefix of the per-block outlier counts
     int* s_k = s_pre + 64;                      // [kSideK] this round's columns
@@ -562,22 +570,22 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
   // ---- epilogue: lane holds rows m0 + wr*64 + 16i + 4g + r, column n0 + wc*64 + 16j + row
   const int Cd = p.n_head * p.head_size;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wc * 64 + 16 * j + row;
+  for (int j = 0; j < NJ; ++j) {
+    const int n = n0 + wc * 16 * NJ + 16 * j + row;
     float2 szn = make_float2(1.f, 0.f);
     if constexpr (NIB) szn = p.sz[n];
     if constexpr (I8) szn.x = reinterpret_cast<const float*>(p.sz)[n];  // SCB
-    const int nblk = n0 + wc * 64 + 16 * j;  // first column of this 16-column block
+    const int nblk = n0 + wc * 16 * NJ + 16 * j;  // first column of this 16-column block
     constexpr int GI = I8 ? (EP == GEP_QKV ? 1 : 2) : 4;  // row blocks whose operands are in flight together (LLM.int8: 3 accumulator sets live)
 #pragma unroll
-    for (int i0 = 0; i0 < 4; i0 += GI) {
+    for (int i0 = 0; i0 < MI; i0 += GI) {
       int2 bps[GI][4];  // QKV: (sequence, position) per row
       float2 opv[GI][4];
 #pragma unroll
       for (int i = 0; i < GI; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wr * 64 + 16 * (i0 + i) + 4 * g + r;
+          const int m = m0 + wr * 16 * MI + 16 * (i0 + i) + 4 * g + r;
           bps[i][r] = EP == GEP_QKV ? qkv_row(p, m) : make_int2(0, 0);
           opv[i][r] = gemm_operand<EP>(p, m, n, bps[i][r].y, Cd);
         }
@@ -585,7 +593,7 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
       for (int i = 0; i < GI; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int ml = wr * 64 + 16 * (i0 + i) + 4 * g + r;
+          const int ml = wr * 16 * MI + 16 * (i0 + i) + 4 * g + r;
           const int m = m0 + ml;
           float y = acc[i0 + i][j][r];
           if constexpr (NIB) y = szn.x * (y - szn.y * rs_lds[ml]);

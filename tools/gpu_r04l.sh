@@ -13,8 +13,10 @@ chk() {
 }
 timeout -k 10 840 python -u -m pytest tests -m gpu -q --timeout 280 --timeout-method thread -p no:cacheprovider > $O/t_all.log 2>&1
 chk "gpu tests" $?
+LLJ_LIB=$R/scratch/w4wide.so timeout -k 10 200 python -u -m pytest tests/test_kernels_gpu.py -k "gemm" -q --timeout 120 --timeout-method thread > $O/t_wide.log 2>&1
+chk "w4 wide gemm tests" $?
 for rep in 1 2; do
-  for cfg in "X=0" "LLJ_GEMM_GLDS=1"; do
+  for cfg in "X=0" "LLJ_GEMM_GLDS=1" "LLJ_LIB=$R/scratch/w4wide.so"; do
     echo "== rep $rep $cfg" >> $O/prefill_bench.log
     env $cfg timeout -k 10 200 python -u tools/prefill_bench.py --T 2048 --modes gptq.int4 --iters 5 >> $O/prefill_bench.log 2>&1
     chk "prefill bench $cfg" $?
