@@ -42,6 +42,8 @@
 #pragma once
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "i8ws.h"
 #include "attention.h"
@@ -987,7 +989,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
               dst = p.q_out;
               ei = (size_t)mg * Cd + nc;
             } else {
-              const int slot = ps < p.S ? ps : ps % p.S;
+              int slot = ps;
+              if (slot >= p.S) slot %= p.S;  // ring wrap only (no division on the common path)
               dst = region == 1 ? p.kcache : p.vcache;
               ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
             }
@@ -1131,8 +1134,12 @@ constexpr bool tpw_ok() { return (WF == WF_W4 || WF == WF_W8) && AM != AM_GLOBAL
 #ifndef LLJ_GEMV_LDS_A_MAX
 #define LLJ_GEMV_LDS_A_MAX (96 * 1024)  // profiling variant: 56 KiB keeps every non-int8 launch under 64 KiB
 #endif
+static inline size_t lds_a_max() {  // LLJ_GEMV_LDS_A_KB in the environment: A/B of the A-image cap (KiB)
+  const char* e = getenv("LLJ_GEMV_LDS_A_KB");
+  return e && e[0] ? (size_t)atol(e) * 1024 : (size_t)(LLJ_GEMV_LDS_A_MAX);
+}
 static inline bool lds_fits(int wf, int M, int K) {
-  return M <= 8 && a_image_bytes(wf, AM_LDS, M, K) <= (wf == WF_I8 ? 96 * 1024 : LLJ_GEMV_LDS_A_MAX);
+  return M <= 8 && a_image_bytes(wf, AM_LDS, M, K) <= (wf == WF_I8 ? 96 * 1024 : lds_a_max());
 }
 
 // waves per workgroup: the global-A form (rows whose A image does not fit the LDS) keeps twice
