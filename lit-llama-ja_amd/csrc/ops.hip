@@ -106,11 +106,14 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__
 }
 
 // ---- attention (attention.h): one block per (head, query row)
+// 512 x 4 (128 keys per pass, half the serial score / softmax chain per lane of 256 x 8): 7B
+// gptq.int4 decode-only at position ~80, bs=1 847.4 -> 857.8 tok/s, bs=8 4321 -> 4355
+// (profiles/r04_attention_block_ab.json; 512 x 8 and 1024 x 2 in between)
 #ifndef LLJ_ATT_NTH
-#define LLJ_ATT_NTH 256  // threads per (row, head) block
+#define LLJ_ATT_NTH 512  // threads per (row, head) block
 #endif
 #ifndef LLJ_ATT_U
-#define LLJ_ATT_U 8  // keys per 16-lane group per pass
+#define LLJ_ATT_U 4  // keys per 16-lane group per pass
 #endif
 template <int HS, int U, int NTH, int SPECU>
 __global__ __launch_bounds__(NTH) void attention_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
