@@ -323,7 +323,11 @@ def time_dominant_kernel(model, B, iters=10):
     return avg_s, abytes
 
 
-def graph_kernel_us(kernel_prefix: str = "void llj::gemv_kernel<0, 2, 3, 4, 4, 1, 1>"):
+# the dominant decode launch (W4, fused RMSNorm, SwiGLU; 4 waves, 2 chunks in flight, one row)
+DOMINANT = "llj::gemv_kernel<0, 2, 3, 4, 2, 1, 1>"
+
+
+def graph_kernel_us(kernel_prefix: str = "void " + DOMINANT):
     """In-graph average duration of the dominant launch from the newest committed kernel trace of
     the decode graph alone: profiles/<round>_graph_kernel_stats.csv, the rocprofv3 --kernel-trace
     --stats summary of `bench.py --decode-only` (graph replays only: no isolated loop in the
@@ -387,7 +391,7 @@ def achievable_read_gbs(gb: float = 4.0, iters: int = 5):
     return best
 
 
-def pmc_traffic(kernel_prefix: str = "llj::gemv_kernel<0, 2, 3, 4, 4, 1, 1>"):
+def pmc_traffic(kernel_prefix: str = DOMINANT):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC summary:
     profiles/<round>_pmc_summary.json (tools/profile_summary.py over separate rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE passes of the 7B gptq.int4 bs=1 decode, gfx950 correction

@@ -1059,11 +1059,14 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
 #ifndef LLJ_NW
 #define LLJ_NW 4  // waves per workgroup (K split across them)
 #endif
+// weight chunks in flight per wave of the one-row SwiGLU (two matrices, so 2 D chunks): 2 vs 4,
+// 7B gptq.int4 bs=1 decode-only 866 -> 892 tokens/s (dominant launch 11.3 -> 10.3 us), 13B 488 ->
+// 514, gptq.int8 575 -> 590, bf16 321 -> 323 (profiles/r04_swiglu_depth_ab.json; 3: 871, 1: 885)
 #ifndef LLJ_D
-#define LLJ_D 4  // weight chunks in flight per wave
+#define LLJ_D 2
 #endif
 #ifndef LLJ_D1
-#define LLJ_D1 LLJ_D  // chunks in flight per wave for the single-matrix ops (QKV, c_proj, down, head)
+#define LLJ_D1 4  // chunks in flight per wave for the single-matrix ops (QKV, c_proj, down, head)
 #endif
 // The residual ops have only N / 16 = C / 16 workgroups (256 at 7B, one per CU); with a long K
 // (mlp.c_proj, K = n_hidden) twice the waves keep twice the weight chunks in flight per CU
@@ -1155,7 +1158,7 @@ constexpr int nw_of() { return AM == AM_GLOBAL ? 2 * kNW : kNW; }
 #define LLJ_DM LLJ_D1  // single-matrix ops (QKV, lm_head)
 #endif
 #ifndef LLJ_DMS
-#define LLJ_DMS LLJ_D  // SwiGLU (two matrices)
+#define LLJ_DMS 4  // SwiGLU (two matrices)
 #endif
 #ifndef LLJ_NWM
 #define LLJ_NWM LLJ_NW
