@@ -224,7 +224,6 @@ def step_bytes(model, B: int, pos_mean: float) -> float:
 
 # ----------------------------------------------------------------------------- timing
 POS_CENTER = 80  # a 128-token generation after a 16-token prompt has mean position 80
-ENGINE_TIMING_STEPS = 24  # decode steps after the timed region reserved for time_engine_kernel
 
 
 def untimed_steps(prompt_len: int, S: int, warmup: int, steps: int) -> int:
@@ -240,7 +239,7 @@ def time_decode(model, B, prompt_len, S, warmup, steps, ws, seed=1234, use_graph
 
     cfg = model.config
     skip = untimed_steps(prompt_len, S, warmup, steps)
-    total = prompt_len + 1 + skip + steps + ENGINE_TIMING_STEPS  # room for time_engine_kernel's launches
+    total = prompt_len + 1 + skip + steps
     assert total <= cfg.block_size, "positions beyond block_size"
     g = torch.Generator().manual_seed(seed)
     prompts = torch.randint(3, cfg.vocab_size, (B, prompt_len), generator=g).cuda()
@@ -344,24 +343,6 @@ def graph_kernel_us(kernel_prefix: str = "void " + DOMINANT):
         except (OSError, KeyError, ValueError):
             continue
     return best
-
-
-def time_engine_kernel(sess, iters: int = 20):
-    """Average duration of the persistent engine's step kernel (llj_engine_step: the whole decode
-    step in ONE launch) over `iters` back-to-back eager launches on the session's stream, HIP
-    events on that stream. The steps advance the session (positions past the timed region)."""
-    from lit_llama import _hip
-
-    st = _hip.stream()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    sess.engine.step(st)
-    torch.cuda.synchronize()
-    ev0.record()
-    for _ in range(iters):
-        sess.engine.step(st)
-    ev1.record()
-    torch.cuda.synchronize()
-    return ev0.elapsed_time(ev1) / 1e3 / iters
 
 
 def achievable_read_gbs(gb: float = 4.0, iters: int = 5):
@@ -572,16 +553,7 @@ def main():
 
     k_s, k_bytes = time_dominant_kernel(model, args.batch)
     k_gbs = k_bytes / k_s / 1e9
-    engine = r["session"].engine is not None
-    if engine:  # the step is ONE kernel: its roofline is the step's algorithmic bytes per launch
-        g_s, g_bytes, g_gbs = k_s, k_bytes, k_gbs
-        sess = r["session"]
-        room = sess.total - (sess.t_prompt + sess.steps_done) - 1  # launches the output buffer still has room for
-        assert room >= 4, room
-        k_s = time_engine_kernel(sess, iters=min(20, room - 3))
-        k_bytes = sb
-        k_gbs = k_bytes / k_s / 1e9
-    in_graph = graph_kernel_us() if not engine else None
+    in_graph = graph_kernel_us()
     ach = achievable_read_gbs()
 
     pmc = pmc_traffic()
@@ -635,17 +607,13 @@ def main():
                          "traffic": round(pmc[0]) if pmc and head7 else None,
                          "traffic_source": (f"profiles/{pmc[1]} (PMC FETCH_SIZE/WRITE_SIZE passes, "
                                             f"profiled {pmc[2]:.2f} us)" if pmc and head7 else None),
-                         "kernel": ("engine_step_kernel (the whole decode step, csrc/engine.hip)" if engine else
-                                    "gemv_kernel<W4,NORM,SWIGLU> (rms_2 + c_fc1/c_fc2 + silu*mul)"),
+                         "kernel": "gemv_kernel<W4,NORM,SWIGLU> (rms_2 + c_fc1/c_fc2 + silu*mul)",
                          "bytes_per_launch": k_bytes, "avg_launch_us": round(k_s * 1e6, 2),
                          **({"in_graph_avg_launch_us": round(in_graph[0], 2),
                              "in_graph_frac": round(k_bytes / (in_graph[0] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                              "in_graph_source": f"profiles/{in_graph[1]} (rocprofv3 kernel trace of bench.py --decode-only)"}
-                            if in_graph and head7 else {}),
-                         **({"chain_dominant_gemv": {"kernel": "gemv_kernel<W4,NORM,SWIGLU>", "avg_launch_us":
-                                                     round(g_s * 1e6, 2), "bytes_per_launch": g_bytes,
-                                                     "frac": round(g_gbs / HBM_PEAK_GBS, 4)}} if engine else {})},
-            "decode_path": "persistent engine (one launch per token)" if engine else "launch chain (5 fused launches per layer)",
+                            if in_graph and head7 else {})},
+            "decode_path": "launch chain (5 fused launches per layer)",
             "step_roofline": {"bytes_per_step": sb, "achieved": round(step_gbs, 1), "frac": round(step_gbs / HBM_PEAK_GBS, 4),
                               "frac_of_achievable": round(step_gbs / ach, 4)},
             "reference_formula_tokens_per_s": round(r["tokens"] / (r["seconds"] + r["t_prefill"]), 2),

@@ -58,6 +58,32 @@ int llj_i8_unpack(const void* packed, void* cb, int N, int K, void* stream);
  * (tested bitwise). Returns the previous value. */
 int llj_set_tpw_max(int tiles);
 
+/* Host-side switch (no device work): 1 (default) = batched decode rows (2 <= M <= 8) of the
+ * int4 / gptq.int8 / bf16 GEMVs stream their activation rows per K chunk (the fused RMSNorm then
+ * takes the residual op's handed-over sums of squares, `nstat`); 0 = the LDS-image forms. Same
+ * rounding points either way. Returns the previous value. */
+int llj_set_stream_a(int on);
+
+/* Host-side A/B options (no device work). Each starts from its environment variable (read once, at
+ * first use; -1 = unset = the build default) and can be set per process; launches never read the
+ * environment. Returns the previous value, or -1000 for an unknown option / out-of-range value.
+ *   LLJ_OPT_ATT_SPEC_FULL  0..1  decode attention loads a whole (1) or half (0) key pass before the position (LLJ_ATT_SPEC)
+ *   LLJ_OPT_FLASH_QB       1..2  flash prefill: 16-query blocks per wave (LLJ_FLASH_QB)
+ *   LLJ_OPT_FLASH_PAIR     0..1  flash prefill: (long, short) query-block pairs per workgroup (LLJ_FLASH_PAIR)
+ *   LLJ_OPT_GEMM_GLDS      0..1  prefill GEMMs: LDS-DMA (1) or register-staged (0) kernel for every format (LLJ_GEMM_GLDS)
+ *   LLJ_OPT_GLDS_COST128   0..   LDS-DMA GEMM: cost of a 256 x 128 tile in % of a 256 x 256 one (LLJ_GLDS_COST128)
+ *   LLJ_OPT_GEMV_LDS_A_KB  56..96 decode GEMVs: cap of the staged A image in KiB (LLJ_GEMV_LDS_A_KB) */
+enum {
+  LLJ_OPT_ATT_SPEC_FULL = 0,
+  LLJ_OPT_FLASH_QB = 1,
+  LLJ_OPT_FLASH_PAIR = 2,
+  LLJ_OPT_GEMM_GLDS = 3,
+  LLJ_OPT_GLDS_COST128 = 4,
+  LLJ_OPT_GEMV_LDS_A_KB = 5,
+  LLJ_OPT_COUNT = 6
+};
+int llj_set_option(int which, int value);
+
 /* ---------------------------------------------------------------- linear layers
  * wfmt: 0 = int4 W4P (sz = (scale, 128+zero) pairs required), 1 = bf16 (N, K) row-major
  * (torch.nn.Linear.weight), 2 = LLM.int8() CB in the I8P tiling (llj_i8_repack) with sz = SCB (N) fp32,
@@ -269,15 +295,22 @@ int llj_g_attention(const void* q, const void* kcache, const void* vcache, void*
 /* h[i] = silu(a1[i]) * a2[i], i < n (model.py:258-259; dt 0: bf16(bf16(silu(a1)) * a2)). */
 int llj_g_silu_mul(const void* a1, const void* a2, void* h, size_t n, int dt, void* stream);
 /* LLM.int8() (Linear8bitLt, quantization.py:36-75, threshold 6.0; bitsandbytes' algorithm restated)
- * for any K with bf16 rows: outlier columns, row scales and the int8 / fp16 products in three plain
- * launches; CB (N, K) int8 row-major, SCB (N) fp32; y (or resid + y, resid may be y) bf16.
+ * for any K: outlier columns, row scales and the int8 / fp16 products in three plain launches; CB
+ * (N, K) int8 row-major, SCB (N) fp32; x, y (or resid + y, resid may be y) of the activation type
+ * dt (0 bf16, 1 fp32: as bitsandbytes, the input is cast to fp16 and the fp16 result back to fp32 --
+ * a float32 model under --quantize llm.int8, evaluate/full.py's default dtype).
  * ws: llj_g_i8_ws_bytes(M, K) bytes. */
 size_t llj_g_i8_ws_bytes(int M, int K);
 int llj_g_i8_linear(const void* x, int ldx, int M, int K, const void* CB, const float* SCB, float threshold, void* ws, int N,
-                    void* y, int ldy, const void* resid, int ldr, void* stream);
+                    void* y, int ldy, const void* resid, int ldr, int dt, void* stream);
 /* Greedy next token over fp32 logits (generate.py:66-74, top_k = 1), as llj_argmax. */
 int llj_g_argmax(const float* logits, int ldl, int M, int V, int* out_idx, int* tokens_out, int tok_stride, const int* pos,
                  void* stream);
+/* Sampled next token over fp32 logits (generate.py:66-74 on the reference's float32 model: x =
+ * logits / temperature, the top_k threshold (ties kept), fp32 softmax, one inverse-CDF draw), as
+ * llj_sample. */
+int llj_g_sample(const float* logits, int ldl, int M, int V, float temperature, int top_k, const float* u,
+                 unsigned long long seed, int* out_idx, int* tokens_out, int tok_stride, const int* pos, void* stream);
 
 /* Measurement aid (no reference counterpart): reads `bytes` (a multiple of 16) at p once with
  * non-temporal 16-byte loads over `grid` workgroups of 256 and writes one float per workgroup to
@@ -285,47 +318,6 @@ int llj_g_argmax(const float* logits, int ldl, int M, int V, int* out_idx, int* 
  * achievable HBM read bandwidth beside the 8 TB/s peak (roofline.achievable). */
 int llj_stream_read(const void* p, size_t bytes, float* out, int grid, void* stream);
 
-/* ---------------------------------------------------------------- persistent decode engine
- * One launch per decode token (batch 1, every Linear int4 W4P with per-row (scale, zero); head
- * size 64 / 128): the whole of LLaMA.forward for the token at position *pos + 1 (model.py:84-128)
- * plus, with flags bit 0, the greedy next-token choice (generate.py:66-74, top_k = 1). Weights
- * stream through an LDS ring by LDS-DMA across op boundaries; op outputs travel between CUs as
- * 8-byte {tag, data} granules in `arena` (csrc/engine.hip). Same results as the launch chain
- * (llj_embedding + the fused ops + llj_norm_linear + llj_argmax) up to fp32 summation order.
- * At the end of a step: logits (V bf16) written, *pos advanced by one; greedy: *cur = next token and
- * tokens[*pos + 1] = next (tokens may be NULL). The plan is passed by host pointer and copied into
- * the launch (graph-capturable); every pointer inside it is a device pointer. `arena` holds
- * llj_engine_arena_bytes(C, H) bytes, zeroed once before the first step; its control words carry
- * an error bit (word 2 of the 16 behind the granules) that a step sets on a timed-out wait. */
-#define LLJ_ENGINE_MAX_CUS 1024
-typedef struct llj_engine_layer {
-  const void* w_qkv; const void* sz_qkv;   /* attn.c_attn: W4P codes, (scale, 128 + zero) fp32 pairs */
-  const void* w_o; const void* sz_o;       /* attn.c_proj */
-  const void* w_fc1; const void* sz_fc1;   /* mlp.c_fc1 */
-  const void* w_fc2; const void* sz_fc2;   /* mlp.c_fc2 */
-  const void* w_down; const void* sz_down; /* mlp.c_proj */
-  const void* rms1; const void* rms2;      /* RMSNorm scales, bf16 (C) */
-  void* kcache; void* vcache;              /* bf16 (1, n_head, S, head_size), slot p % S */
-  float eps1, eps2;
-} llj_engine_layer;
-typedef struct llj_engine_plan {
-  const llj_engine_layer* layers;          /* device array of n_layer entries */
-  int n_layer, C, H, V, n_head, S;         /* V: lm_head rows (padded vocab), < 65536 */
-  const void* wte;                         /* bf16 (V, C) embedding */
-  const void* ln_f; float eps_f;           /* bf16 (C) */
-  const void* w_head; const void* sz_head; /* lm_head W4P + pairs */
-  const float* rope;                       /* (block_size, hs / 2, 2) fp32 */
-  int* pos; int* cur; int* tokens;         /* device step state (int32) */
-  void* logits;                            /* bf16 (V) */
-  void* arena;
-  int flags;                               /* bit 0: greedy token choice inside the step */
-  int grid;                                /* workgroups (0 = every CU) */
-  int ring_blocks;                         /* LDS ring slots (1 KiB), <= llj_engine_ring_blocks() */
-  unsigned long long* trace;               /* profiling only: NULL, or grid x 128 phase stamps (s_memrealtime) */
-} llj_engine_plan;
-size_t llj_engine_arena_bytes(int C, int H);
-int llj_engine_ring_blocks(int C, int H, int n_head);
-int llj_engine_step(const llj_engine_plan* plan, void* stream);
 
 #ifdef __cplusplus
 }

@@ -244,10 +244,9 @@ int llj_attention_prefill(const void* q, const void* kcache, const void* vcache,
   LLJ_REQUIRE(B > 0 && T > 0 && n_head > 0 && S > 0 && pos);
   const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
   hipStream_t st = (hipStream_t)stream;
-  const char* e = getenv("LLJ_FLASH_QB");  // A/B in one process: 1 or 2 query blocks per wave
-  const int qbw = e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : LLJ_FLASH_QB;
-  const char* ep = getenv("LLJ_FLASH_PAIR");  // 1 / 0: pair a long and a short query block per workgroup
-  const bool pair = ep && ep[0] ? ep[0] != '0' : LLJ_FLASH_PAIR != 0;
+  const int oq = opt(LLJ_OPT_FLASH_QB), op = opt(LLJ_OPT_FLASH_PAIR);  // A/B options (llj_set_option)
+  const int qbw = oq > 0 ? oq : LLJ_FLASH_QB;  // 1 or 2 query blocks per wave
+  const bool pair = op >= 0 ? op != 0 : LLJ_FLASH_PAIR != 0;  // a long and a short query block per workgroup
   if (head_size == 128) {
     if (qbw == 2) flash_launch<128, 2>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, pair, st);
     else flash_launch<128, 1>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, pair, st);

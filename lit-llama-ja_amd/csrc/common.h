@@ -89,6 +89,9 @@ __device__ __forceinline__ void st_out32(void* dst, uint32_t v) {
 #endif
 }
 
+// host-side A/B options (options.hip, llj_set_option): -1 = the site's build default
+int opt(int which);
+
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Cross-lane moves inside a DPP row (16 lanes) as one VALU op each, instead of __shfl_xor's

@@ -887,11 +887,11 @@ static int gemm_glds_launch(const GemmParams& p, hipStream_t s) {
   return 0;
 }
 
-// LLJ_GEMM_GLDS=1 / 0 in the environment: the LDS-DMA / the register-staged kernels for every
-// format (A/B in one process); otherwise the per-format default
+// option LLJ_OPT_GEMM_GLDS (llj_set_option / LLJ_GEMM_GLDS) 1 / 0: the LDS-DMA / the register-staged
+// kernels for every format (A/B in one process); unset: the per-format default
 static bool glds_enabled(int wf) {
-  const char* e = getenv("LLJ_GEMM_GLDS");
-  if (e && e[0]) return e[0] != '0';
+  const int o = opt(LLJ_OPT_GEMM_GLDS);
+  if (o >= 0) return o != 0;
   return wf == GWF_BF16 ? LLJ_GEMM_GLDS_BF16 != 0 : LLJ_GEMM_GLDS_W4 != 0;
 }
 
@@ -913,8 +913,8 @@ static int gemm_glds_run(const GemmParams& p, hipStream_t s) {
   const long mt = (p.M + 255) / 256;
   const long w256 = p.N % 256 == 0 ? (mt * (p.N / 256) + cus - 1) / cus : -1;
   const long w128 = (mt * (p.N / 128) + cus - 1) / cus;
-  const char* e = getenv("LLJ_GLDS_COST128");  // A/B and tests: 0 forces 256 x 128, >= 100 prefers 256 x 256
-  const long cost = e ? atol(e) : LLJ_GLDS_COST128;
+  const int oc = opt(LLJ_OPT_GLDS_COST128);  // A/B and tests: 0 forces 256 x 128, >= 100 prefers 256 x 256
+  const long cost = oc >= 0 ? oc : LLJ_GLDS_COST128;
   if (w256 > 0 && 100 * w256 <= cost * w128) return gemm_glds_launch<WF, EP, 256>(p, s);
   return gemm_glds_launch<WF, EP, 128>(p, s);
 }

@@ -5,6 +5,7 @@
 namespace llj {
 
 int g_tpw_max = LLJ_TPW_MAX;
+int g_stream_a = 1;
 
 template <int EP>
 static int dispatch(int wf, int am, const GemvParams& p, hipStream_t s) {
@@ -45,6 +46,14 @@ extern "C" {
 int llj_set_tpw_max(int tiles) {
   const int old = g_tpw_max;
   g_tpw_max = tiles < 1 ? 1 : tiles;
+  return old;
+}
+
+// Streamed-A forms of the batched-row GEMVs (2 <= M <= 8; gemv_impl.h AM_STREAM / AM_SNORM) on
+// (1, default) or off (0: the LDS-image forms); returns the previous setting. Host-side only.
+int llj_set_stream_a(int on) {
+  const int old = g_stream_a;
+  g_stream_a = on ? 1 : 0;
   return old;
 }
 

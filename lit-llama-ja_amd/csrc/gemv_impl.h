@@ -42,8 +42,6 @@
 #pragma once
 #include <algorithm>
 
-#include <cstdlib>
-
 #include "common.h"
 #include "i8ws.h"
 #include "attention.h"
@@ -52,7 +50,18 @@
 namespace llj {
 
 enum : int { WF_W4 = 0, WF_BF16 = 1, WF_I8 = 2, WF_W8 = 3, WF_W4G = 4 };
-enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2 };
+// A operand modes: AM_GLOBAL fragments straight from global memory; AM_LDS / AM_NORM one LDS
+// image of all M rows staged (and RMS-normalised) before the weight stream is consumed;
+// AM_STREAM / AM_SNORM (batched rows, 2 <= M <= 8): each wave loads the M rows of ITS OWN
+// 128-deep chunks together with the chunk's weights (16 B per lane per row group: only real
+// rows travel), normalises them in registers with the row statistics handed over by the
+// producer (nstat, AM_SNORM) and passes them through a 2-slot per-wave LDS ring into the MFMA
+// fragments -- no workgroup-wide A image, no prologue barrier, no separate RMSNorm launch.
+enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2, AM_STREAM = 3, AM_SNORM = 4 };
+// streamed A: elements per staged row (128 + 8 pad: rows land on distinct bank groups) and per slot
+constexpr int kSRow = 136;
+constexpr int kSSlot = 8 * kSRow;
+__host__ __device__ constexpr bool am_stream(int am) { return am == AM_STREAM || am == AM_SNORM; }
 enum : int { EP_STORE = 0, EP_RESID = 1, EP_QKV = 2, EP_SWIGLU = 3 };
 
 // int8 activation workspace written by llj_i8_stats (int8.hip): i8ws.h
@@ -402,7 +411,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   constexpr bool I8 = (WF == WF_I8);
   constexpr bool W4L = (WF == WF_W4 || WF == WF_W8);  // nibble-coded: offset removed with row sums
   constexpr bool GRP = (WF == WF_W4G);  // grouped int4: offset and scale removed per chunk
-  constexpr bool ALDS = I8 || (AM != AM_GLOBAL);
+  constexpr bool STRM = am_stream(AM);  // A rows streamed per chunk (see AM_STREAM)
+  constexpr bool SNRM = (AM == AM_SNORM);
+  static_assert(!STRM || (MB == 8 && !I8), "streamed A: batched rows, non-int8 formats");
+  constexpr bool ALDS = I8 || (AM != AM_GLOBAL && !STRM);
   // row sums of A for the nibble offset: an extra MFMA against a ones fragment for the global-A
   // form and for batched norm-fused rows (LLJ_SACC_NORM; the VALU sums + 8 wave reductions of the
   // prologue sit on its critical path), else summed while the LDS image is written
@@ -424,7 +436,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   // LDS carve: [A image, aliased after the main loop by the NW x 64 x 12-word reduction
   // scratch] [tail: 128 words for staging scratch / int8 SCA]
   const int a_stride = I8 ? K + 16 : K + 8;  // elements (bytes for int8)
-  const size_t a_bytes = ALDS ? (((size_t)M * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15) : 0;
+  const size_t a_bytes = ALDS ? (((size_t)M * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15)
+                              : STRM ? (size_t)NW * 2 * kSSlot * 2 : 0;
   constexpr int NV = 8 * TPW + 4;  // reduction words per lane: acc, acc2 of every tile, sacc
   constexpr size_t kRedBytes = (size_t)NW * 64 * NV * 4;
   constexpr size_t kScratch = kRedBytes + (I8 ? (size_t)2 * NW * 8 * 16 * 4 : 0);  // + int8 side partials
@@ -488,9 +501,28 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   u32x4 r1[D][TPW][WV], r2[D][TPW][WV];
   u32x4 ra[D][4];
   float2 rg[D][TPW], rg2[D][TPW];  // WF_W4G: (scale, 128 + zero) of the chunk's group, this lane's column
+  // streamed A: lane l carries 16-B segment (l & 15) of rows (l >> 4) and (l >> 4) + 4 of each of
+  // its chunks (rows past M: clamped copies of row M - 1, never stored), plus the norm weights'
+  // segment (AM_SNORM); rn0 / rn1 = the RMSNorm rstd of those two rows
+  u32x4 sa[STRM ? D : 1][2], sg[SNRM ? D : 1];
+  const bf16_t* aptr[2];
+  const bf16_t* gptr = p.norm_w + 8 * (lane & 15);
+  float rn0 = 1.f, rn1 = 1.f;
+  if constexpr (STRM) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rr = (lane >> 4) + 4 * h;
+      aptr[h] = p.A + (size_t)(rr < M ? rr : M - 1) * p.lda + 8 * (lane & 15);
+    }
+  }
   auto load = [&](int d, int i) {
     int c = wave + NW * (i < nmy ? i : nmy - 1);
     c = c < 0 ? 0 : (c >= KC ? KC - 1 : c);  // always a valid chunk (loads past the end are unused)
+    if constexpr (STRM) {  // the chunk's activation rows first: they arrive before its weights
+#pragma unroll
+      for (int h = 0; h < 2; ++h) sa[d][h] = *reinterpret_cast<const u32x4*>(aptr[h] + 128 * c);
+      if constexpr (SNRM) sg[d] = *reinterpret_cast<const u32x4*>(gptr + 128 * c);
+    }
     if constexpr (GRP) {
       const size_t go = (size_t)(c / p.gch) * p.N + row;
 #pragma unroll
@@ -525,11 +557,25 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     f32x4 gt[TPW], gt2[TPW], gs = {0, 0, 0, 0};  // WF_W4G: this chunk's sums
 #pragma unroll
     for (int j = 0; j < TPW; ++j) gt[j] = gt2[j] = gs;
+    // streamed A: this chunk's rows (normalised: g * bf16(x * r), model.py:283 in bf16) into the
+    // wave's ring slot d % 2, read back as MFMA fragments (one wave writes and reads its own slot:
+    // LDS keeps a wave's accesses in order, no barrier)
+    bf16_t* slot = reinterpret_cast<bf16_t*>(smem) + (size_t)(wave * 2 + (d & 1)) * kSSlot;
+    if constexpr (STRM) {
+      u32x4 x0 = sa[d][0], x1 = sa[d][1];
+      if constexpr (SNRM) {
+        x0 = __builtin_bit_cast(u32x4, norm8(__builtin_bit_cast(uint4, x0), __builtin_bit_cast(uint4, sg[d]), rn0));
+        x1 = __builtin_bit_cast(u32x4, norm8(__builtin_bit_cast(uint4, x1), __builtin_bit_cast(uint4, sg[d]), rn1));
+      }
+      *reinterpret_cast<u32x4*>(slot + (lane >> 4) * kSRow + 8 * (lane & 15)) = x0;
+      *reinterpret_cast<u32x4*>(slot + ((lane >> 4) + 4) * kSRow + 8 * (lane & 15)) = x1;
+    }
 #pragma unroll
     for (int t = 0; t < NSTEP; ++t) {
       // LDS lanes of rows >= M read row 0 (abase clamped): their output rows are never stored, and
       // an unconditional read keeps the hot loop free of divergent LDS accesses
-      const u32x4 av = ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
+      const u32x4 av = STRM ? *reinterpret_cast<const u32x4*>(slot + (row & 7) * kSRow + kofs<WF>(t, grp))
+                       : ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
       if constexpr (WF == WF_W4) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
@@ -797,8 +843,44 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
 #if LLJ_ABAR
   __builtin_amdgcn_s_barrier();  // experiment: every wave's A loads ahead of any weight load
 #endif
+  // AM_SNORM: the producer's partial sums of squares, partials q = lane + 64 i (i < kSnQ) of rows
+  // 0..7 (two 16-B loads per partial), issued before the weight stream
+  constexpr int kSnQ = 4;
+  float4 snv[SNRM ? kSnQ : 1][2];
+  if constexpr (SNRM) {
+#pragma unroll
+    for (int i = 0; i < kSnQ; ++i) {
+      const int q = lane + 64 * i < p.npart ? lane + 64 * i : p.npart - 1;
+      snv[i][0] = *reinterpret_cast<const float4*>(p.nstat + (size_t)q * kNstRows);
+      snv[i][1] = *reinterpret_cast<const float4*>(p.nstat + (size_t)q * kNstRows + 4);
+    }
+  }
 #pragma unroll
   for (int d = 0; d < D; ++d) load(d, d);  // the weight stream starts before any A wait
+  if constexpr (SNRM) {  // every wave reduces the partials itself (same order everywhere: one rstd per row)
+    float ss[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) ss[m] = 0.f;
+#pragma unroll
+    for (int i = 0; i < kSnQ; ++i) {
+      if (lane + 64 * i < p.npart) {
+        ss[0] += snv[i][0].x; ss[1] += snv[i][0].y; ss[2] += snv[i][0].z; ss[3] += snv[i][0].w;
+        ss[4] += snv[i][1].x; ss[5] += snv[i][1].y; ss[6] += snv[i][1].z; ss[7] += snv[i][1].w;
+      }
+    }
+    for (int q = lane + 64 * kSnQ; q < p.npart; q += 64) {  // n_embd > 4096 (rare: one more latency)
+#pragma unroll
+      for (int m = 0; m < 8; ++m) ss[m] += p.nstat[(size_t)q * kNstRows + m];
+    }
+    const int r0 = lane >> 4, r1i = (lane >> 4) + 4;
+    const int m0c = r0 < M ? r0 : M - 1, m1c = r1i < M ? r1i : M - 1;  // clamped rows: copies of row M - 1
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const float r = rms_rstd(wave_sum(ss[m]) / (float)K, p.eps);
+      if (m == m0c) rn0 = r;
+      if (m == m1c) rn1 = r;
+    }
+  }
   // int8: the per-k-block outlier counts the side product starts from, loaded now (one memory
   // latency less in the tail; needed once the stream is done)
   int i8cnt = 0, i8spk[kSpE<NW>] = {};
@@ -880,7 +962,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   // int8 side products in the LDS beyond the reduction scratch (the A image is no longer read)
   float* side = reinterpret_cast<float*>(smem + kRedBytes);
   if (NW > 1) {
-    if (ALDS) __syncthreads();  // every wave is done reading the A image it aliases
+    if (ALDS || STRM) __syncthreads();  // every wave is done reading the A image / ring it aliases
     if constexpr (I8) {
       i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W), reinterpret_cast<const float*>(p.sz), ntj[0] * 16,
                        side, smem, i8cnt, i8spk);
@@ -1080,13 +1162,14 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvParams p) {
 constexpr int kNW = LLJ_NW;
 constexpr int kD = LLJ_D;
 
-static inline size_t a_image_bytes(int wf, int am, int M, int K) {
+static inline size_t a_image_bytes(int wf, int am, int M, int K, int nw = kNW) {
   if (wf == WF_I8) return (((size_t)M * (K + 16)) + 15) & ~(size_t)15;
   if (am == AM_GLOBAL) return 0;
+  if (am_stream(am)) return (size_t)nw * 2 * kSSlot * 2;  // per-wave 2-slot rings
   return (((size_t)M * (K + 8) * 2) + 15) & ~(size_t)15;
 }
 static inline size_t gemv_smem(int wf, int am, int M, int K, int nw = kNW, int tpw = 1) {
-  const size_t a = a_image_bytes(wf, am, M, K);
+  const size_t a = a_image_bytes(wf, am, M, K, nw);
   // reduction scratch (8 words per tile slot + 4 per lane); int8: the side-product partials
   // (2 matrices x NW x 8 rows x 16 columns) follow it
   const size_t red = (size_t)nw * 64 * (8 * tpw + 4) * 4 + (wf == WF_I8 ? (size_t)2 * nw * 8 * 16 * 4 : 0);
@@ -1129,17 +1212,20 @@ static inline int pick_tpw(int ntiles, int M) {
   const int t = (ntiles + cu - 1) / cu;
   return t < 1 ? 1 : (t > cap ? cap : t);
 }
-// multi-tile instantiations: nibble-coded weights with the LDS A image
+// multi-tile instantiations: nibble-coded weights with the LDS A image or streamed A
 template <int WF, int AM>
 constexpr bool tpw_ok() { return (WF == WF_W4 || WF == WF_W8) && AM != AM_GLOBAL && LLJ_TPW_MAX > 1; }
+// run-time switch of the streamed-A forms for batched rows (llj_set_stream_a, gemv.hip; A/B and
+// equality tests): 1 = on (default)
+extern int g_stream_a;
 
 // the LDS A image must leave room for the reduction scratch: <= 96 KiB, M <= 8 rows
 #ifndef LLJ_GEMV_LDS_A_MAX
 #define LLJ_GEMV_LDS_A_MAX (96 * 1024)  // profiling variant: 56 KiB keeps every non-int8 launch under 64 KiB
 #endif
-static inline size_t lds_a_max() {  // LLJ_GEMV_LDS_A_KB in the environment: A/B of the A-image cap (KiB)
-  const char* e = getenv("LLJ_GEMV_LDS_A_KB");
-  return e && e[0] ? (size_t)atol(e) * 1024 : (size_t)(LLJ_GEMV_LDS_A_MAX);
+static inline size_t lds_a_max() {  // option LLJ_OPT_GEMV_LDS_A_KB (56..96 KiB): A/B of the A-image cap
+  const int kb = opt(LLJ_OPT_GEMV_LDS_A_KB);
+  return kb > 0 ? (size_t)kb * 1024 : (size_t)(LLJ_GEMV_LDS_A_MAX);
 }
 static inline bool lds_fits(int wf, int M, int K) {
   return M <= 8 && a_image_bytes(wf, AM_LDS, M, K) <= (wf == WF_I8 ? 96 * 1024 : lds_a_max());
@@ -1173,11 +1259,15 @@ template <int WF, int AM, int EP, int MB, int NW, int TPW>
 static int launch_t(const GemvParams& p, hipStream_t s) {
   const size_t sm = gemv_smem(WF, AM, p.M, p.K, NW, TPW);
   auto kern = gemv_kernel<WF, AM, EP, NW, d_of<EP, MB>(), MB, TPW>;
-  static bool attr_set = false;  // per instantiation; set before any graph capture
-  if (sm > 64 * 1024 && !attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
+  static bool attr_set[16] = {};  // per instantiation and device; set before any graph capture
+  if (sm > 64 * 1024) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+    if (dev >= 16 || !attr_set[dev]) {
+      hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return (int)e;
+      if (dev < 16) attr_set[dev] = true;
+    }
   }
   const int ntiles = p.N / 16;
   hipLaunchKernelGGL(kern, dim3((ntiles + TPW - 1) / TPW), dim3(NW * 64), sm, s, p);
@@ -1188,10 +1278,13 @@ static int launch_t(const GemvParams& p, hipStream_t s) {
 template <int WF, int AM, int EP, int MB, int NW = nw_of<AM>()>
 static int launch_mb(const GemvParams& p, hipStream_t s) {
   if constexpr (tpw_ok<WF, AM>() && MB > 1) {  // M == 1 (MB 1) always one tile: pick_tpw
-    switch (pick_tpw(p.N / 16, p.M)) {
+    // the residual ops (8 chunks in flight) take at most 2 tiles per workgroup (3 and 4 spill;
+    // C / 16 tiles need 2 only past 256 CUs' worth: 13B / 30B / 65B)
+    const int t = pick_tpw(p.N / 16, p.M);
+    switch (EP == EP_RESID && t > 2 ? 2 : t) {
       case 2: return launch_t<WF, AM, EP, MB, NW, 2>(p, s);
-      case 3: return launch_t<WF, AM, EP, MB, NW, 3>(p, s);
-      case 4: return launch_t<WF, AM, EP, MB, NW, 4>(p, s);
+      case 3: if constexpr (EP != EP_RESID) return launch_t<WF, AM, EP, MB, NW, 3>(p, s); break;
+      case 4: if constexpr (EP != EP_RESID) return launch_t<WF, AM, EP, MB, NW, 4>(p, s); break;
       default: break;
     }
   }
@@ -1200,21 +1293,35 @@ static int launch_mb(const GemvParams& p, hipStream_t s) {
 
 template <int WF, int AM, int EP>
 static int launch(const GemvParams& p, hipStream_t s) {
+  if constexpr (am_stream(AM)) {  // batched rows only (M <= 8)
+    if constexpr (EP == EP_RESID && LLJ_NWR != kNW)
+      if (p.K >= LLJ_NWR_KMIN) return launch_mb<WF, AM, EP, 8, LLJ_NWR>(p, s);
+    return launch_mb<WF, AM, EP, 8, LLJ_NWM>(p, s);
+  } else {
   // the register-staged prologue has an M == 1 class (bs = 1 decode) and an M <= 8 class
   if constexpr (EP == EP_RESID && AM != AM_GLOBAL && LLJ_NWR != kNW) {
     if (p.K >= LLJ_NWR_KMIN) {  // residual ops: 256 workgroups, more waves each
       if (WF != WF_I8 && p.M == 1) return launch_mb<WF, AM, EP, 1, LLJ_NWR>(p, s);
-      return launch_mb<WF, AM, EP, 8, LLJ_NWR>(p, s);
+      // one tile per workgroup: an 8-row image of K >= 8192 exceeds the LDS cap, so the multi-tile
+      // forms (M >= 7) were unreachable here (and spilled: 256 VGPRs + scratch)
+      return launch_t<WF, AM, EP, 8, LLJ_NWR, 1>(p, s);
     }
   }
   if (WF != WF_I8 && AM != AM_GLOBAL && p.M == 1) return launch_mb<WF, AM, EP, 1>(p, s);
   if constexpr (AM != AM_GLOBAL && WF != WF_I8) return launch_mb<WF, AM, EP, 8, LLJ_NWM>(p, s);
   return launch_mb<WF, AM, EP, 8>(p, s);
+  }
 }
 
-// A mode for a call: fused RMSNorm needs the LDS image; otherwise stage when it fits.
+// A mode for a call: batched rows (2..8) stream A per chunk (the fused RMSNorm then takes the
+// producer's statistics, nstat); otherwise the fused RMSNorm needs the LDS image, and plain rows
+// are staged when they fit.
 static int pick_am(int wf, const GemvParams& p) {
   if (wf == WF_I8) return (p.norm_w || !p.i8ws || !lds_fits(wf, p.M, p.K)) ? -1 : AM_LDS;
+  if (g_stream_a && p.M >= 2 && p.M <= 8) {
+    if (!p.norm_w) return AM_STREAM;
+    if (p.nstat && (reinterpret_cast<uintptr_t>(p.nstat) & 15) == 0) return AM_SNORM;
+  }
   if (p.norm_w) return lds_fits(wf, p.M, p.K) ? AM_NORM : -1;
   return lds_fits(wf, p.M, p.K) ? AM_LDS : AM_GLOBAL;
 }
@@ -1251,6 +1358,8 @@ static int launch_fmt(int am, int ep, const GemvParams& p, hipStream_t s) {
   if constexpr (WF == WF_I8) {
     return launch_ep<WF_I8, AM_LDS>(ep, p, s);
   } else {
+    if (am == AM_SNORM) return launch_ep<WF, AM_SNORM>(ep, p, s);
+    if (am == AM_STREAM) return launch_ep<WF, AM_STREAM>(ep, p, s);
     if (am == AM_NORM) return launch_ep<WF, AM_NORM>(ep, p, s);
     if (am == AM_LDS) return launch_ep<WF, AM_LDS>(ep, p, s);
     return launch_ep<WF, AM_GLOBAL>(ep, p, s);

@@ -235,23 +235,28 @@ using namespace llj;
 // the restated bnb MatMul8bitLt (oracle/llama_np.py int8_linear, reference quantization.py:36-75):
 // A16 = f16(A); outlier columns = {k : any row |A16[m, k]| >= thr}; SCA[m] = max |A16[m, k]| < thr; CA = rint(A16 * (127 / SCA)); y = f16(f16(sum_k CA CB (int32) * SCA SCB / 127^2)
 // + sum_{outliers} A16 f16(CB SCB / 127)), cast to bf16. ws: K flag bytes, then M fp32 SCA.
-__global__ __launch_bounds__(256) void g_i8_flags_kernel(const bf16_t* __restrict__ x, int ldx, int M, int K, float thr,
+// T: the activation type. bitsandbytes' MatMul8bitLt casts its input to fp16 (A16) whatever it is
+// and casts the fp16 result back to the input dtype, so a float32 model's Linear8bitLt computes on
+// f16(x) and returns fp32 holding fp16 values (no bf16 rounding, fp32 residual add).
+template <typename T>
+__global__ __launch_bounds__(256) void g_i8_flags_kernel(const T* __restrict__ x, int ldx, int M, int K, float thr,
                                                          unsigned char* __restrict__ flags) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   if (k >= K) return;
   bool o = false;
-  for (int m = 0; m < M; ++m) o |= fabsf((float)(_Float16)bf2f(x[(size_t)m * ldx + k])) >= thr;
+  for (int m = 0; m < M; ++m) o |= fabsf((float)(_Float16)ldv(x, (size_t)m * ldx + k)) >= thr;
   flags[k] = o ? 1 : 0;
 }
 // SCA[m]: max |A16| over the row's elements below the threshold (element-wise, as double_quant's row
 // statistics; an element under it in an outlier column still counts, its code is then dropped)
-__global__ __launch_bounds__(256) void g_i8_sca_kernel(const bf16_t* __restrict__ x, int ldx, int K, float thr,
+template <typename T>
+__global__ __launch_bounds__(256) void g_i8_sca_kernel(const T* __restrict__ x, int ldx, int K, float thr,
                                                        float* __restrict__ sca) {
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x;
   float mx = 0.f;
   for (int k = tid; k < K; k += 256) {
-    const float a = fabsf((float)(_Float16)bf2f(x[(size_t)m * ldx + k]));
+    const float a = fabsf((float)(_Float16)ldv(x, (size_t)m * ldx + k));
     if (a < thr) mx = fmaxf(mx, a);
   }
   mx = wave_max(mx);
@@ -259,11 +264,12 @@ __global__ __launch_bounds__(256) void g_i8_sca_kernel(const bf16_t* __restrict_
   __syncthreads();
   if (tid == 0) sca[m] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
-__global__ __launch_bounds__(256) void g_i8_linear_kernel(const bf16_t* __restrict__ x, int ldx, int M, int K,
+template <typename T>
+__global__ __launch_bounds__(256) void g_i8_linear_kernel(const T* __restrict__ x, int ldx, int M, int K,
                                                           const int8_t* __restrict__ CB, const float* __restrict__ SCB,
                                                           const unsigned char* __restrict__ flags,
-                                                          const float* __restrict__ sca, int N, bf16_t* __restrict__ y,
-                                                          int ldy, const bf16_t* resid, int ldr) {
+                                                          const float* __restrict__ sca, int N, T* __restrict__ y,
+                                                          int ldy, const T* resid, int ldr) {
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= N) return;
@@ -290,7 +296,7 @@ __global__ __launch_bounds__(256) void g_i8_linear_kernel(const bf16_t* __restri
 #pragma unroll
     for (int r = 0; r < GL_ROWS; ++r) {
       if (r < mr) {
-        const float a16 = (float)(_Float16)bf2f(x[(size_t)(m0 + r) * ldx + k]);
+        const float a16 = (float)(_Float16)ldv(x, (size_t)(m0 + r) * ldx + k);
         if (o) side[r] += a16 * w16;
         else acc[r] += (int)rintf(fminf(fmaxf(a16 * qs[r], -127.f), 127.f)) * cb;
       }
@@ -307,9 +313,9 @@ __global__ __launch_bounds__(256) void g_i8_linear_kernel(const bf16_t* __restri
       const float sa = sca[m];
       float v = (float)a * (sa * scb * (1.f / (127.f * 127.f)));
       v = (float)(_Float16)((float)(_Float16)v + sd);
-      v = round_bf(v);
-      if (resid) v = bf2f(resid[m * ldr + n]) + v;
-      y[m * ldy + n] = f2bf(v);
+      v = rnd<T>(v);
+      if (resid) v = ldv(resid, m * ldr + n) + v;
+      stv(y, m * ldy + n, v);
     }
   }
 }
@@ -400,17 +406,23 @@ int llj_g_silu_mul(const void* a1, const void* a2, void* h, size_t n, int dt, vo
 size_t llj_g_i8_ws_bytes(int M, int K) { return (((size_t)K + 15) & ~(size_t)15) + (size_t)M * 4; }
 
 int llj_g_i8_linear(const void* x, int ldx, int M, int K, const void* CB, const float* SCB, float threshold, void* ws, int N,
-                    void* y, int ldy, const void* resid, int ldr, void* stream) {
-  LLJ_REQUIRE(x && CB && SCB && ws && y && M > 0 && K > 0 && N > 0 && ldx >= K && ldy >= N && (!resid || ldr >= N));
+                    void* y, int ldy, const void* resid, int ldr, int dt, void* stream) {
+  LLJ_REQUIRE(x && CB && SCB && ws && y && M > 0 && K > 0 && N > 0 && ldx >= K && ldy >= N && (!resid || ldr >= N) &&
+              (dt == 0 || dt == 1));
   hipStream_t s = (hipStream_t)stream;
   unsigned char* flags = (unsigned char*)ws;
   float* sca = (float*)((char*)ws + (((size_t)K + 15) & ~(size_t)15));
-  hipLaunchKernelGGL(g_i8_flags_kernel, dim3((K + 255) / 256), dim3(256), 0, s, (const bf16_t*)x, ldx, M, K, threshold, flags);
-  LLJ_CHECK_LAUNCH();
-  hipLaunchKernelGGL(g_i8_sca_kernel, dim3(M), dim3(256), 0, s, (const bf16_t*)x, ldx, K, threshold, sca);
-  LLJ_CHECK_LAUNCH();
-  hipLaunchKernelGGL(g_i8_linear_kernel, dim3((N + 3) / 4, (M + GL_ROWS - 1) / GL_ROWS), dim3(256), 0, s, (const bf16_t*)x,
-                     ldx, M, K, (const int8_t*)CB, SCB, flags, sca, N, (bf16_t*)y, ldy, (const bf16_t*)resid, ldr);
+  const dim3 grid((N + 3) / 4, (M + GL_ROWS - 1) / GL_ROWS);
+#define LLJ_GI8(T)                                                                                                   \
+  do {                                                                                                                \
+    hipLaunchKernelGGL(g_i8_flags_kernel<T>, dim3((K + 255) / 256), dim3(256), 0, s, (const T*)x, ldx, M, K, threshold, \
+                       flags);                                                                                        \
+    hipLaunchKernelGGL(g_i8_sca_kernel<T>, dim3(M), dim3(256), 0, s, (const T*)x, ldx, K, threshold, sca);            \
+    hipLaunchKernelGGL(g_i8_linear_kernel<T>, grid, dim3(256), 0, s, (const T*)x, ldx, M, K, (const int8_t*)CB, SCB,  \
+                       flags, sca, N, (T*)y, ldy, (const T*)resid, ldr);                                              \
+  } while (0)
+  LLJ_DT(dt, LLJ_GI8(bf16_t), LLJ_GI8(float));
+#undef LLJ_GI8
   LLJ_CHECK_LAUNCH();
   return 0;
 }

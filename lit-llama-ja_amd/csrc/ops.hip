@@ -236,34 +236,67 @@ __device__ __forceinline__ uint32_t block_suffix_excl(uint32_t v, uint32_t* wsum
   return x - v + above;
 }
 
-__global__ __launch_bounds__(kSampNT) void sample_kernel(const bf16_t* __restrict__ logits, int ldl, int V, float inv_t,
-                                                        int top_k, const float* __restrict__ u_in, uint64_t seed,
-                                                        int* __restrict__ out_idx, int* __restrict__ tokens_out,
-                                                        int tok_stride, const int* __restrict__ pos) {
-  constexpr int HB = 2048;  // first pass: key >> 5 (2048 bins); second: key & 31 inside the chosen bin
+// The logits type of the sampler: bf16 (the reference's GPU precision: x = bf16(logits * (1/T)),
+// probabilities rounded to bf16; 16-bit keys selected in passes of 11 + 5 bits) or fp32 (its
+// float32 model: x = logits / T, fp32 softmax; 32-bit keys in passes of 11 + 11 + 10 bits).
+template <typename T>
+struct SampTraits;
+template <>
+struct SampTraits<bf16_t> {
+  static constexpr int NP = 2;
+  static constexpr int SH[3] = {5, 0, 0}, W[3] = {11, 5, 0};
+  __device__ static uint32_t key(const bf16_t* l, int i, float inv_t, float) { return bf_key(f2bf(bf2f(l[i]) * inv_t)); }
+  __device__ static float val(uint32_t k) { return key_bf(k); }
+  __device__ static float ex(float d) { return __expf(d); }
+  __device__ static float prob(float e) { return bf2f(f2bf(e)); }
+};
+__device__ __forceinline__ uint32_t f_key(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float key_f(uint32_t k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k); }
+template <>
+struct SampTraits<float> {
+  static constexpr int NP = 3;
+  static constexpr int SH[3] = {21, 10, 0}, W[3] = {11, 11, 10};
+  __device__ static uint32_t key(const float* l, int i, float, float t) { return f_key(l[i] / t); }
+  __device__ static float val(uint32_t k) { return key_f(k); }
+  __device__ static float ex(float d) { return expf(d); }
+  __device__ static float prob(float e) { return e; }
+};
+
+template <typename T>
+__global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ logits, int ldl, int V, float inv_t,
+                                                        float temp, int top_k, const float* __restrict__ u_in,
+                                                        uint64_t seed, int* __restrict__ out_idx,
+                                                        int* __restrict__ tokens_out, int tok_stride,
+                                                        const int* __restrict__ pos) {
+  using Tr = SampTraits<T>;
+  constexpr int HB = 2048;  // the widest pass: 11 bits
   __shared__ uint32_t hist[HB];
   __shared__ float fred[kSampNT / 64];
   __shared__ uint32_t ured[kSampNT / 64];
   __shared__ float chunk_excl[kSampNT];
   __shared__ uint32_t sel[4];
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const bf16_t* lr = logits + (size_t)m * ldl;
-  auto xkey = [&](int i) -> uint32_t { return bf_key(f2bf(bf2f(lr[i]) * inv_t)); };
+  const T* lr = logits + (size_t)m * ldl;
+  auto xkey = [&](int i) -> uint32_t { return Tr::key(lr, i, inv_t, temp); };
   const int k = top_k < 1 || top_k > V ? V : top_k;
   // ---- radix select: thr = the k-th largest key; keep key >= thr
   uint32_t prefix = 0, want = (uint32_t)k;
-  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+  for (int pass = 0; pass < Tr::NP; ++pass) {
+    const int sh = Tr::SH[pass], nbins = 1 << Tr::W[pass];
     for (int b = tid; b < HB; b += kSampNT) hist[b] = 0;
     __syncthreads();
     for (int i = tid; i < V; i += kSampNT) {
       const uint32_t key = xkey(i);
-      if (pass == 0) atomicAdd(&hist[key >> 5], 1u);
-      else if ((key >> 5) == prefix) atomicAdd(&hist[key & 31u], 1u);
+      if (pass == 0 || (key >> (sh + Tr::W[pass])) == prefix) atomicAdd(&hist[(key >> sh) & (nbins - 1)], 1u);
     }
     __syncthreads();
-    // thread t owns bins 2t, 2t + 1 (pass 1: bin t < 32); counts above them by a suffix scan
-    const int nb = pass == 0 ? 2 : (tid < 32 ? 1 : 0);
-    const int b0 = pass == 0 ? 2 * tid : tid;
+    // thread t owns bins [b0, b0 + nb): counts above them by a suffix scan
+    const int nb = nbins >= kSampNT ? nbins / kSampNT : (tid < nbins ? 1 : 0);
+    const int b0 = nbins >= kSampNT ? nb * tid : tid;
     uint32_t c = 0;
     for (int q = 0; q < nb; ++q) c += hist[b0 + q];
     const uint32_t above = block_suffix_excl(c, ured);
@@ -278,7 +311,7 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const bf16_t* __restric
       sel[1] = want - a;
     }
     __syncthreads();
-    prefix = pass == 0 ? sel[0] : (prefix << 5) | sel[0];
+    prefix = pass == 0 ? sel[0] : (prefix << Tr::W[pass]) | sel[0];
     want = sel[1];
     __syncthreads();
   }
@@ -296,14 +329,14 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const bf16_t* __restric
     sel[2] = mk;
   }
   __syncthreads();
-  const float xmax = key_bf(sel[2]);
+  const float xmax = Tr::val(sel[2]);
   // each thread owns a contiguous index range (the CDF is taken in index order)
   const int per = (V + kSampNT - 1) / kSampNT;
   const int i0 = tid * per, i1 = min(V, i0 + per);
   float esum = 0.f;
   for (int i = i0; i < i1; ++i) {
     const uint32_t key = xkey(i);
-    if (key >= thr) esum += __expf(key_bf(key) - xmax);
+    if (key >= thr) esum += Tr::ex(Tr::val(key) - xmax);
   }
   float t = wave_sum(esum);
   if (lane == 0) fred[wv] = t;
@@ -312,11 +345,11 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const bf16_t* __restric
 #pragma unroll
   for (int w = 0; w < kSampNT / 64; ++w) tot += fred[w];
   const float rinv = 1.f / tot;
-  // bf16 probabilities, chunk sums, exclusive scan over the chunks (thread order = index order)
+  // probabilities, chunk sums, exclusive scan over the chunks (thread order = index order)
   float csum = 0.f;
   for (int i = i0; i < i1; ++i) {
     const uint32_t key = xkey(i);
-    if (key >= thr) csum += bf2f(f2bf(__expf(key_bf(key) - xmax) * rinv));
+    if (key >= thr) csum += Tr::prob(Tr::ex(Tr::val(key) - xmax) * rinv);
   }
   chunk_excl[tid] = csum;
   __syncthreads();
@@ -348,7 +381,7 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const bf16_t* __restric
       const uint32_t key = xkey(i);
       if (key < thr) continue;
       last = i;
-      run += bf2f(f2bf(__expf(key_bf(key) - xmax) * rinv));
+      run += Tr::prob(Tr::ex(Tr::val(key) - xmax) * rinv);
       if (run > target) { pick = i; break; }
     }
     if (pick < 0) pick = last;
@@ -437,9 +470,8 @@ int llj_attention(const void* q, const void* kcache, const void* vcache, void* y
   const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
   dim3 grid(n_head, B * T);
   // keys loaded before the position is known at small grids: half a pass (default) or a whole one
-  // (LLJ_ATT_SPEC=full: one memory latency less, more K / V rows read past the position)
-  const char* e = getenv("LLJ_ATT_SPEC");
-  const bool full = e && e[0] == 'f';
+  // (option LLJ_OPT_ATT_SPEC_FULL: one memory latency less, more K / V rows read past the position)
+  const bool full = opt(LLJ_OPT_ATT_SPEC_FULL) == 1;
   hipStream_t st = (hipStream_t)stream;
 #define LLJ_ATT_LAUNCH(HS_, SU_)                                                                                   \
   hipLaunchKernelGGL((attention_kernel<HS_, LLJ_ATT_U, LLJ_ATT_NTH, SU_>), grid, dim3(LLJ_ATT_NTH), 0, st,          \
@@ -491,8 +523,17 @@ int llj_attention_split(const void* q, const void* kcache, const void* vcache, v
 int llj_sample(const void* logits, int ldl, int M, int V, float temperature, int top_k, const float* u,
                unsigned long long seed, int* out_idx, int* tokens_out, int tok_stride, const int* pos, void* stream) {
   LLJ_REQUIRE(M > 0 && V > 0 && temperature > 0.f && (!tokens_out || pos) && (u || pos));
-  hipLaunchKernelGGL(sample_kernel, dim3(M), dim3(kSampNT), 0, (hipStream_t)stream, (const bf16_t*)logits, ldl, V,
-                     1.f / temperature, top_k, u, (uint64_t)seed, out_idx, tokens_out, tok_stride, pos);
+  hipLaunchKernelGGL(sample_kernel<bf16_t>, dim3(M), dim3(kSampNT), 0, (hipStream_t)stream, (const bf16_t*)logits, ldl,
+                     V, 1.f / temperature, temperature, top_k, u, (uint64_t)seed, out_idx, tokens_out, tok_stride, pos);
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
+int llj_g_sample(const float* logits, int ldl, int M, int V, float temperature, int top_k, const float* u,
+                 unsigned long long seed, int* out_idx, int* tokens_out, int tok_stride, const int* pos, void* stream) {
+  LLJ_REQUIRE(logits && out_idx && M > 0 && V > 0 && ldl >= V && temperature > 0.f && (!tokens_out || pos) && (u || pos));
+  hipLaunchKernelGGL(sample_kernel<float>, dim3(M), dim3(kSampNT), 0, (hipStream_t)stream, logits, ldl, V,
+                     1.f / temperature, temperature, top_k, u, (uint64_t)seed, out_idx, tokens_out, tok_stride, pos);
   LLJ_CHECK_LAUNCH();
   return 0;
 }

@@ -56,12 +56,12 @@ SIGNATURES = {
     "llj_argmax": [_P, _I, _I, _I, _P, _P, _I, _P, _P],
     "llj_sample": [_P, _I, _I, _I, _F, _I, _P, ctypes.c_ulonglong, _P, _P, _I, _P, _P],
     "llj_set_tpw_max": [_I],
+    "llj_set_stream_a": [_I],
+    "llj_set_option": [_I, _I],
     "llj_gemm_linear": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_silu_mul": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_qkv_rope": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
-    "llj_engine_step": [_P, _P],
-    "llj_engine_ring_blocks": [_I, _I, _I],
     "llj_stream_read": [_P, ctypes.c_size_t, _P, _I, _P],
     "llj_g_embedding": [_P, _P, _P, _I, _I, _P, _I, _P],
     "llj_g_rmsnorm": [_P, _I, _P, _F, _P, _I, _I, _I, _I, _P],
@@ -70,7 +70,8 @@ SIGNATURES = {
     "llj_g_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "llj_g_silu_mul": [_P, _P, _P, ctypes.c_size_t, _I, _P],
     "llj_g_argmax": [_P, _I, _I, _I, _P, _P, _I, _P, _P],
-    "llj_g_i8_linear": [_P, _I, _I, _I, _P, _P, _F, _P, _I, _P, _I, _P, _I, _P],
+    "llj_g_sample": [_P, _I, _I, _I, _F, _I, _P, ctypes.c_ulonglong, _P, _P, _I, _P, _P],
+    "llj_g_i8_linear": [_P, _I, _I, _I, _P, _P, _F, _P, _I, _P, _I, _P, _I, _I, _P],
 }
 
 _lib = None
@@ -78,6 +79,10 @@ _lib = None
 
 class HipError(RuntimeError):
     pass
+
+
+# llj_set_option indices (include/lit_llama_amd.h LLJ_OPT_*)
+OPT_ATT_SPEC_FULL, OPT_FLASH_QB, OPT_FLASH_PAIR, OPT_GEMM_GLDS, OPT_GLDS_COST128, OPT_GEMV_LDS_A_KB = range(6)
 
 
 def lib() -> ctypes.CDLL:
@@ -96,8 +101,6 @@ def lib() -> ctypes.CDLL:
         L.llj_i8_ws_bytes.restype = ctypes.c_size_t
         L.llj_attention_ws_bytes.argtypes = [_I, _I, _I, _I]
         L.llj_attention_ws_bytes.restype = ctypes.c_size_t
-        L.llj_engine_arena_bytes.argtypes = [_I, _I]
-        L.llj_engine_arena_bytes.restype = ctypes.c_size_t
         L.llj_g_i8_ws_bytes.argtypes = [_I, _I]
         L.llj_g_i8_ws_bytes.restype = ctypes.c_size_t
         _lib = L

@@ -117,11 +117,13 @@ PRE_NORM_ROWS = True
 PRE_NORM_MIN_M = 2  # smallest batch that takes the separate launch (measured best from bs=2 on)
 # batched decode rows (2 <= M <= HAND_NORM_MAX_M): the residual ops hand the next RMSNorm its sums
 # of squares (per-tile partials, llj_linear_resid's nstat_out) and the norm-fused GEMVs normalize
-# from them, so no separate RMSNorm launch remains after layer 0's rms_1. Measured 7B gptq.int4
-# ms/token, hand-off vs llj_rmsnorm_rows: bs=2 1.339 vs 1.384, bs=4 1.633 vs 1.539, bs=8 1.877 vs
-# 1.788 (every workgroup normalizes all rows: 768 of them at bs=4) -> bs=2 only
+# from them, so no separate RMSNorm launch remains after layer 0's rms_1. With the LDS-image GEMVs
+# (round 3, every workgroup normalizing all rows before its stream) this lost from bs=3 on (7B
+# gptq.int4 ms/token, hand-off vs llj_rmsnorm_rows: bs=4 1.633 vs 1.539, bs=8 1.877 vs 1.788); the
+# streamed-A GEMVs (gemv_impl.h AM_SNORM) normalize each chunk's rows as they arrive, so every batch
+# up to 8 rows takes the hand-off
 HAND_NORM = True
-HAND_NORM_MAX_M = 2
+HAND_NORM_MAX_M = 8
 
 
 # prefill / no-cache calls with at least this many rows (B * T) run the MFMA-tiled GEMMs
@@ -336,8 +338,8 @@ class LLaMA(nn.Module):
             raise TypeError("the MI355X path computes in bfloat16 or float32: build the model under "
                             "EmptyInitOnDevice(device='cuda', dtype=torch.bfloat16) or call model.to(torch.bfloat16)")
         if wte.dtype == torch.float32:  # the fp32 model: every norm / dense weight fp32 as well
-            for n, prm in self.named_parameters():
-                if prm.dtype != torch.float32:
+            for n, prm in self.named_parameters():  # (LLM.int8's CB is int8 under any activation dtype)
+                if prm.dtype != torch.float32 and not (prm.dtype == torch.int8 and n.endswith(".weight")):
                     raise TypeError(f"float32 model with a {prm.dtype} parameter {n}")
 
     def _run(self, idx, pos, S, kv, all_rows=True, last_only_out=None):
@@ -514,13 +516,12 @@ class LLaMA(nn.Module):
     @staticmethod
     def _glinear(spec, A, M, K, N, out, resid, st):
         kind, W, sc, zr, bits, group = spec
-        if kind == 2:  # LLM.int8 (Linear8bitLt._gspec): statistics + int8 / fp16 products, bf16 rows
-            if A.dtype != torch.bfloat16:
-                raise TypeError(f"Linear8bitLt computes on bfloat16 activations, got {A.dtype}")
+        if kind == 2:  # LLM.int8 (Linear8bitLt._gspec): statistics + int8 / fp16 products on f16(A)
             ws = torch.empty(_hip.lib().llj_g_i8_ws_bytes(M, K), dtype=torch.uint8, device=A.device)
             _hip.call("llj_g_i8_linear", A.data_ptr(), A.stride(0), M, K, W.data_ptr(), sc.data_ptr(),
                       Linear8bitLtThreshold, ws.data_ptr(), N, out.data_ptr(), out.stride(0),
-                      None if resid is None else resid.data_ptr(), 0 if resid is None else resid.stride(0), st)
+                      None if resid is None else resid.data_ptr(), 0 if resid is None else resid.stride(0),
+                      _dt_code(A.dtype), st)
             return
         if kind == 1 and W.dtype != A.dtype:
             raise TypeError(f"dense Linear weight {W.dtype} with {A.dtype} activations")

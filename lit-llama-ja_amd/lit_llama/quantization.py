@@ -381,9 +381,11 @@ class Linear8bitLt(torch.nn.Module):
 
     def forward(self, x):
         _hip.require_device(x, "input")
-        if x.dtype != torch.bfloat16:
-            raise TypeError(f"Linear8bitLt HIP path computes in bfloat16, got {x.dtype}")
-        if self.in_features % 128 or self.out_features % 16:  # the any-shape LLM.int8 kernels
+        if x.dtype not in (torch.bfloat16, torch.float32):
+            raise TypeError(f"Linear8bitLt HIP path computes on bfloat16 or float32 input, got {x.dtype}")
+        # the any-shape LLM.int8 kernels: shapes outside the streaming tiling, and fp32 input (cast to
+        # fp16 inside and the result back to fp32, as bitsandbytes' MatMul8bitLt does)
+        if self.in_features % 128 or self.out_features % 16 or x.dtype == torch.float32:
             from .model import LLaMA
 
             K, N = self.in_features, self.out_features

@@ -346,3 +346,21 @@ def sample_inverse_cdf(logits: np.ndarray, temperature: float, top_k: int | None
     hit = np.nonzero(cdf > target)[0]
     idx = int(hit[0]) if hit.size else int(np.nonzero(keep)[0][-1])
     return idx, p
+
+
+def sample_inverse_cdf_fp32(logits: np.ndarray, temperature: float, top_k: int | None, u: float):
+    """reference generate.py:66-74 on a float32 logits row (its float32 model, generate.py:121 on a
+    host without bf16): x = logits / temperature in fp32; keep x >= the top_k-th largest (ties kept);
+    probs = exp(x - max) * (1 / sum) in fp32 (torch's softmax up to its exp / summation rounding);
+    the inverse-CDF draw at u as sample_inverse_cdf. Returns (index, probs)."""
+    x = (logits.astype(F32) / F32(temperature)).astype(F32)
+    V = x.shape[-1]
+    k = V if top_k is None or top_k < 1 or top_k > V else top_k
+    thr = np.sort(x)[::-1][k - 1]
+    keep = x >= thr
+    e = np.where(keep, np.exp((x - x.max()).astype(F32)), F32(0)).astype(F32)
+    p = np.where(keep, e * (F32(1.0) / F32(e.sum(dtype=F32))), F32(0)).astype(F32)
+    cdf = np.cumsum(p, dtype=F32)
+    hit = np.nonzero(cdf > F32(u) * cdf[-1])[0]
+    idx = int(hit[0]) if hit.size else int(np.nonzero(keep)[0][-1])
+    return idx, p

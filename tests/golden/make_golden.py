@@ -508,6 +508,38 @@ def gen_sampled():
          u=np.array(us, np.float32), probs=np.stack(probs).astype(np.float32))
 
 
+def gen_sampled_fp32():
+    """The same sampled decoding (temperature 0.8, top_k 50, recorded uniforms) on the reference's
+    float32 model -- generate.py's own defaults (top_k 200, temperature 0.8) run fp32 on a host without
+    bf16 (generate.py:97-98, 121): logits / temperature, topk threshold, softmax and the draw in fp32.
+    Keeps the uniforms, the fp32 probability rows and the ids."""
+    cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=2048)
+    seed = 4243
+    params = make_params(cfg, seed)
+    prompt = make_prompt(8, cfg.vocab_size, seed)
+    m = ref_model(cfg, params, dtype=torch.float32)
+    rng = np.random.default_rng(seed)
+    us, probs = [], []
+
+    def inv_cdf(p, num_samples=1):
+        u = float(rng.random())
+        us.append(u)
+        probs.append(p.float().numpy().copy())
+        c = torch.cumsum(p.double(), -1)
+        i = int(torch.nonzero(c > u * c[-1])[0, 0])
+        return torch.tensor([i])
+
+    orig = torch.multinomial
+    torch.multinomial = inv_cdf
+    try:
+        with torch.no_grad():
+            out = rgen.generate(m, torch.from_numpy(prompt.astype(np.int32)), 16, temperature=0.8, top_k=50)
+    finally:
+        torch.multinomial = orig
+    save("sampled_fp32", seed=np.int64(seed), prompt=prompt, ids=out.numpy().astype(np.int32),
+         u=np.array(us, np.float32), probs=np.stack(probs).astype(np.float32))
+
+
 def gen_ppl():
     """The reference's perplexity loop (evaluate/full.py:114-128) on the tiny C0 model in fp32: a
     300-token stream cut into block_size (128) windows, logits[:-1] scored against inp[1:] with a
@@ -606,6 +638,6 @@ def gen_ref_ckpt():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq", "hf_convert",
-                             "meta_convert", "bf16_init", "sampled", "ppl", "gptq_grouped", "ref_ckpt"]
+                             "meta_convert", "bf16_init", "sampled", "sampled_fp32", "ppl", "gptq_grouped", "ref_ckpt"]
     for w in which:
         globals()[f"gen_{w}"]()

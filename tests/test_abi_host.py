@@ -81,6 +81,26 @@ def test_library_loads_and_binds_without_gpu():
     assert L.llj_i8_ws_bytes(8, 4096) > 0
 
 
+def test_host_options_read_once_and_validated():
+    """llj_set_option (host only, no GPU): the A/B options are set / restored per process, invalid
+    indices or values are refused (-1000) and never change the table; the LLJ_OPT_* enum of the
+    header matches lit_llama._hip's constants."""
+    from lit_llama import _hip
+
+    L = ctypes.CDLL(str(_lib_path()))
+    text = HEADER.read_text()
+    for name, val in re.findall(r"LLJ_OPT_(\w+) = (\d+)", text):
+        if name != "COUNT":
+            assert getattr(_hip, "OPT_" + name) == int(val), name
+    old = L.llj_set_option(_hip.OPT_FLASH_QB, 1)
+    assert old in (-1, 1, 2)
+    assert L.llj_set_option(_hip.OPT_FLASH_QB, 2) == 1
+    assert L.llj_set_option(_hip.OPT_FLASH_QB, 3) == -1000  # out of range: refused, unchanged
+    assert L.llj_set_option(_hip.OPT_FLASH_QB, old) == 2
+    assert L.llj_set_option(99, 0) == -1000
+    assert L.llj_set_option(_hip.OPT_GEMV_LDS_A_KB, 40) == -1000  # below the fused-norm floor (56 KiB)
+
+
 def test_ctypes_table_matches_header():
     from lit_llama import _hip
 
@@ -92,7 +112,7 @@ def test_ctypes_table_matches_header():
         assert ret == "int"
         assert [kind[a] for a in argt] == kinds, name
     assert set(decls) - set(_hip.SIGNATURES) == {"llj_i8_ws_bytes", "llj_attention_ws_bytes", 
-                                                   "llj_engine_arena_bytes", "llj_g_i8_ws_bytes"}
+                                                   "llj_g_i8_ws_bytes"}
 
 
 def test_library_holds_gfx950_code():

@@ -127,3 +127,105 @@ def test_fp32_modules_vs_oracle():
     assert got.dtype == np.float32
     ref = x @ ((q.astype(np.float32) - z) * sc).T
     assert _rel(got, ref) < 1e-5
+
+
+def test_fp32_llm_int8_model_and_perplexity_vs_oracle():
+    """A float32 model under --quantize llm.int8 (evaluate/full.py's default dtype with the reference's
+    llm.int8 mode): Linear8bitLt casts its fp32 input to fp16 and returns the fp16 result as fp32
+    (bitsandbytes' MatMul8bitLt), on the any-shape kernels. Against the oracle's fp32 model with
+    LLM.int8() Linears (parity unpinned: bitsandbytes is absent): logits, margin-guarded greedy ids,
+    and evaluate/full.py's perplexity loop."""
+    import sys as _s
+    from pathlib import Path as _P
+
+    _s.path.insert(0, str(_P(__file__).resolve().parents[1] / "lit-llama-ja_amd"))
+    from evaluate.full import perplexity
+    from lit_llama.quantization import Linear8bitLt
+
+    cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=2048)
+    p = make_params(cfg, 23)
+    m = build32(cfg, p, mode="llm.int8")
+    assert isinstance(m.transformer.h[0].mlp.c_fc1, Linear8bitLt) and isinstance(m.lm_head, Linear8bitLt)
+    lin = {}
+    for k, v in p.items():
+        if k.endswith(".weight") and "wte" not in k:
+            cb, scb = O.int8_quantize_weight(v.astype(np.float32))
+            lin[k[:-7]] = O.LinearSpec("int8", cb=cb, scb=scb)
+    orc = O.OracleLLaMA(cfg, {k: v.astype(np.float32) for k, v in p.items()}, linears=lin)
+    prompt = np.random.default_rng(9).integers(3, 2048, 10).astype(np.int32)
+    out = m(torch.from_numpy(prompt[None].astype(np.int64)).cuda())
+    assert out.dtype == torch.float32
+    ref = orc.forward(prompt[None])
+    rel = _rel(out[0].cpu().numpy(), ref[0])
+    print(f"[fp32 llm.int8] prefill rel {rel:.2e}")
+    assert rel < 1e-2, rel
+    oids, olog = O.generate_greedy(orc, prompt, 10, return_logits=True)
+    ids = gen(m, prompt, 10)
+    top = np.sort(olog, -1)[:, ::-1][:, :2]
+    assert guarded(ids, oids, top, len(prompt), tol=0.05) >= 8
+    toks = np.random.default_rng(4).integers(3, 2048, (1, 300)).astype(np.int64)
+    ppl, nll, n = perplexity(m, torch.from_numpy(toks).cuda(), window=128)
+    onll = 0.0
+    for i in range(0, 300, 128):
+        w = toks[:, i:i + 128]
+        if w.shape[1] < 2:
+            break
+        orc.reset_cache()
+        lg = orc.forward(w)[0][:-1].astype(np.float64)
+        lse = np.log(np.exp(lg - lg.max(-1, keepdims=True)).sum(-1)) + lg.max(-1)
+        onll += float((lse - lg[np.arange(lg.shape[0]), w[0, 1:]]).sum())
+    print(f"[fp32 llm.int8] nll {nll:.3f} oracle {onll:.3f}")
+    assert n == 297 and abs(nll - onll) / onll < 1e-3
+
+
+def test_fp32_sampled_decode_replays_reference_draws(golden):
+    """generate.py's sampled decoding on the reference's float32 model (its CLI defaults run fp32 on a
+    host without bf16, generate.py:97-98, 121): tests/golden/sampled_fp32.npz is the reference's own
+    generate() at temperature 0.8 / top_k 50 with torch.multinomial replaced by an inverse-CDF draw at
+    recorded uniforms. Teacher-forced on the reference's ids, llj_g_sample at the recorded u picks
+    what the fp32 restatement picks on our logits, our probability rows equal the reference's to
+    fp32 noise, and every id equals the reference's unless u lies within that noise of a CDF step.
+    Then the captured decode session with the uniforms table reproduces the reference's ids."""
+    from lit_llama import _hip
+    from lit_llama.engine import DecodeSession
+
+    g = golden("sampled_fp32")
+    cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=2048)
+    m = build32(cfg, make_params(cfg, int(g["seed"])))
+    T, n = len(g["prompt"]), len(g["u"])
+    ids = torch.from_numpy(g["ids"]).cuda().long().view(1, -1)
+    out = torch.empty(1, dtype=torch.int32, device="cuda")
+    m.reset_cache()
+    mism, first = 0, n
+    for s in range(n):
+        x, pos = (ids[:, :T], torch.arange(T).cuda()) if s == 0 else (ids[:, T + s - 1:T + s], torch.tensor([T + s - 1]).cuda())
+        logits = m(x, T + n, pos)[0, -1:].contiguous()
+        assert logits.dtype == torch.float32
+        u = torch.tensor([g["u"][s]], dtype=torch.float32, device="cuda")
+        _hip.call("llj_g_sample", logits.data_ptr(), logits.shape[1], 1, logits.shape[1], 0.8, 50, u.data_ptr(), 0,
+                  out.data_ptr(), None, 0, None, _hip.stream())
+        pick_o, p = O.sample_inverse_cdf_fp32(logits[0].cpu().numpy(), 0.8, 50, float(g["u"][s]))
+        got = int(out.item())
+        assert got == pick_o  # the kernel's draw is the restatement's on our logits
+        pref = g["probs"][s]
+        assert np.abs(p - pref).max() < 1e-4 * pref.max() + 1e-7, f"step {s}: probabilities differ"
+        assert ((p > 0) == (pref > 0)).all(), f"step {s}: kept sets differ"
+        if got != g["ids"][T + s]:
+            c_ref = np.cumsum(pref, dtype=np.float64)
+            gap = np.abs(c_ref / c_ref[-1] - g["u"][s]).min()
+            assert gap <= 1e-5, f"step {s}: u {g['u'][s]} is {gap:.2e} from a CDF step"
+            mism += 1
+            first = min(first, s)
+    print(f"[fp32 sampled] {n - mism} of {n} draws equal to the reference's")
+    assert mism <= 1, mism
+    # the captured session, uniforms fed by position: the reference's ids
+    table = torch.zeros(T + n, 1, dtype=torch.float32, device="cuda")
+    table[T:, 0] = torch.from_numpy(g["u"]).cuda()
+    m.reset_cache()
+    sess = DecodeSession(m, 1, T + n, T + n, temperature=0.8, top_k=50, uniforms=table)
+    sess.prefill(ids[:, :T])
+    sess.decode(n - 1)
+    got_ids = sess.output().cpu().numpy()[0]
+    agree = int((got_ids[T:] == g["ids"][T:T + n]).cumprod().sum())
+    print(f"[fp32 sampled] session: first {agree} of {n} ids equal the reference's")
+    assert agree >= first, (agree, first)

@@ -92,7 +92,6 @@ def test_125m_generate_graph_matches_eager_and_wraps():
     for graph in (True, False):
         s = DecodeSession(m, 1, 16, 28, use_graph=graph)
         s.prefill(prompt.view(1, -1))
-        assert s.engine is None
         s.decode(19)
         outs.append(s.output()[0].cpu().numpy())
     np.testing.assert_array_equal(outs[0], outs[1])
@@ -151,9 +150,25 @@ def test_generic_int8_linear_vs_oracle(M, K, N, outliers):
     y = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     yr = torch.from_numpy(res).to(dev).to(torch.bfloat16)
     _hip.call("llj_g_i8_linear", xt.data_ptr(), K, M, K, cbt.data_ptr(), scbt.data_ptr(), 6.0, ws.data_ptr(), N,
-              y.data_ptr(), N, None, 0, _hip.stream())
+              y.data_ptr(), N, None, 0, 0, _hip.stream())
     _hip.call("llj_g_i8_linear", xt.data_ptr(), K, M, K, cbt.data_ptr(), scbt.data_ptr(), 6.0, ws.data_ptr(), N,
-              yr.data_ptr(), N, yr.data_ptr(), N, _hip.stream())
+              yr.data_ptr(), N, yr.data_ptr(), N, 0, _hip.stream())
     ref = O.int8_linear(x, cb, scb)
     assert_bf16_close(y.float().cpu().numpy(), ref, f"generic int8 M={M} K={K} outliers={outliers}", rel=1e-2)
     assert_bf16_close(yr.float().cpu().numpy(), O.bf16_round(res + O.bf16_round(ref)), "generic int8 resid", rel=1e-2)
+    # fp32 activations (a float32 model under llm.int8): f16(x) in, the fp16 result back as fp32
+    x32 = x + O.bf16_round(rng.standard_normal((M, K)).astype(np.float32) * 1e-3)  # not bf16-representable
+    xt32 = torch.from_numpy(x32).to(dev)
+    y32 = torch.empty(M, N, dtype=torch.float32, device=dev)
+    r32 = torch.from_numpy(res).to(dev)
+    _hip.call("llj_g_i8_linear", xt32.data_ptr(), K, M, K, cbt.data_ptr(), scbt.data_ptr(), 6.0, ws.data_ptr(), N,
+              y32.data_ptr(), N, None, 0, 1, _hip.stream())
+    yr32 = r32.clone()
+    _hip.call("llj_g_i8_linear", xt32.data_ptr(), K, M, K, cbt.data_ptr(), scbt.data_ptr(), 6.0, ws.data_ptr(), N,
+              yr32.data_ptr(), N, yr32.data_ptr(), N, 1, _hip.stream())
+    ref32 = O.int8_linear(x32, cb, scb)
+    got = y32.cpu().numpy()
+    assert np.array_equal(got, got.astype(np.float16).astype(np.float32))  # fp16 values, cast back
+    err = np.abs(got - ref32)
+    assert (err <= 2e-3 * np.abs(ref32) + 1e-3 * np.abs(ref32).max()).all(), err.max()
+    np.testing.assert_allclose(yr32.cpu().numpy(), res + got, rtol=0, atol=1e-6)

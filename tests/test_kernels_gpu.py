@@ -26,6 +26,20 @@ def st():
     return torch.cuda.current_stream().cuda_stream
 
 
+class option:
+    """llj_set_option for the duration of a `with` block (host-side A/B options)."""
+
+    def __init__(self, hip, which, value):
+        self.hip, self.which, self.value = hip, which, value
+
+    def __enter__(self):
+        self.old = self.hip.llj_set_option(self.which, self.value)
+        assert self.old != -1000
+
+    def __exit__(self, *exc):
+        self.hip.llj_set_option(self.which, self.old)
+
+
 def call(hip, name, *args):
     rc = getattr(hip, name)(*args)
     assert rc == 0, f"{name} returned {rc}"
@@ -312,8 +326,14 @@ def _attn_oracle(q, kc, vc, pos, S, T_, nh, hs):
                                             (128, 2, 1, 1, 10, 37), (128, 2, 2, 1, 2048, 2000), (128, 32, 1, 1, 256, 90),
                                             (128, 8, 1, 1, 256, 40)])
 @pytest.mark.parametrize("spec", ["half", "full"])
-def test_attention(hip, hs, nh, B, T_, S, p0, spec, monkeypatch):
-    monkeypatch.setenv("LLJ_ATT_SPEC", spec)  # keys loaded before the position is known (bs = 1 grids)
+def test_attention(hip, hs, nh, B, T_, S, p0, spec):
+    from lit_llama import _hip
+
+    with option(hip, _hip.OPT_ATT_SPEC_FULL, 1 if spec == "full" else 0):  # keys loaded before the position (bs = 1)
+        _attention_case(hip, hs, nh, B, T_, S, p0)
+
+
+def _attention_case(hip, hs, nh, B, T_, S, p0):
     rng = np.random.default_rng(hs + S + p0)
     C = nh * hs
     kc = bf16(rng.standard_normal((B, nh, S, hs)))
@@ -516,6 +536,83 @@ def test_norm_statistics_handoff(hip, wfmt, M):
     assert hip.llj_norm_swiglu(wfmt, xd.data_ptr(), gd.data_ptr(), 1e-5, W1d.data_ptr(), P(s1),
                                W2d.data_ptr(), P(s2), bad.data_ptr(), M, H, C, None, 0, None, nst.data_ptr(), 10000,
                                st()) == 1000
+
+
+@pytest.mark.parametrize("wfmt", [0, 1, 3, W4G_128])
+@pytest.mark.parametrize("M", [2, 5, 8])
+def test_streamed_a_equals_lds_image_forms(hip, wfmt, M):
+    """Batched rows (2..8) stream their A rows per K chunk (gemv_impl.h AM_STREAM / AM_SNORM,
+    llj_set_stream_a(1), the default) instead of staging one LDS image per workgroup
+    (llj_set_stream_a(0)). The MFMA operands are the same bf16 values, so the plain ops agree
+    bitwise where both take the same row-sum route (bf16; the 8-wave long-K residual, whose image
+    does not fit the LDS), and elsewhere up to the int4 offset's fp32 row sums (MFMA against a ones
+    fragment vs VALU); the fused-norm ops normalize from the producer's partials (nstat) in both.
+    All of them match the oracle at 7B widths (K 4096 / 11008, 768 / 688 / 256-tile grids)."""
+    rng = np.random.default_rng(700 + 7 * (wfmt & 0xFF) + M)
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    C, nh, hs, H, S = 4096, 32, 128, 11008, 64
+    x0 = bf16(rng.standard_normal((M, C)))
+    hin = bf16(rng.standard_normal((M, H)))
+    yin = bf16(rng.standard_normal((M, C)))
+    g = bf16(rng.uniform(0.5, 1.5, C))
+    xd, hd, yd, gd = T(x0, torch.bfloat16), T(hin, torch.bfloat16), T(yin, torch.bfloat16), T(g, torch.bfloat16)
+    Wq, Wqd, sq = quant_operands(hip, rng, wfmt, 3 * C, C)
+    Wo, Wod, so = quant_operands(hip, rng, wfmt, C, C)
+    W1, W1d, s1 = quant_operands(hip, rng, wfmt, H, C)
+    W2, W2d, s2 = quant_operands(hip, rng, wfmt, H, C)
+    Wd_, Wdd, sd = quant_operands(hip, rng, wfmt, C, H)
+    rope, pos = T(O.build_rope_cache(128, hs)), T(np.array([41], np.int32))
+    npart = C // 16
+
+    def run(stream):
+        old = hip.llj_set_stream_a(stream)
+        try:
+            nst = torch.full((npart * 16,), float("nan"), dtype=torch.float32, device=dev)
+            x = xd.clone()
+            call(hip, "llj_linear_resid", wfmt, hd.data_ptr(), H, Wdd.data_ptr(), P(sd), x.data_ptr(), C, M, C, H, None,
+                 0, nst.data_ptr(), st())  # producer: mlp.c_proj + the next norm's partials
+            q = torch.zeros(M, C, dtype=torch.bfloat16, device=dev)
+            kc = torch.zeros(M, nh, S, hs, dtype=torch.bfloat16, device=dev)
+            vc = torch.zeros_like(kc)
+            call(hip, "llj_norm_qkv_rope", wfmt, x.data_ptr(), gd.data_ptr(), 1e-5, Wqd.data_ptr(), P(sq), q.data_ptr(),
+                 kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), M, 1, C, nh, S, 0, M, None, None,
+                 nst.data_ptr(), npart, st())
+            x2 = x.clone()
+            nst2 = torch.full_like(nst, float("nan"))
+            call(hip, "llj_linear_resid", wfmt, yd.data_ptr(), C, Wod.data_ptr(), P(so), x2.data_ptr(), C, M, C, C, None,
+                 0, nst2.data_ptr(), st())  # attn.c_proj (K = C)
+            h = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+            call(hip, "llj_norm_swiglu", wfmt, x2.data_ptr(), gd.data_ptr(), 1e-5, W1d.data_ptr(), P(s1), W2d.data_ptr(),
+                 P(s2), h.data_ptr(), M, H, C, None, 0, None, nst2.data_ptr(), npart, st())
+            lin = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+            call(hip, "llj_linear", wfmt, yd.data_ptr(), C, Wod.data_ptr(), P(so), None, lin.data_ptr(), C, M, C, C,
+                 None, 0, None, st())
+            torch.cuda.synchronize()
+        finally:
+            hip.llj_set_stream_a(old)
+        return dict(x=x, q=q, k=kc[:, :, 41], v=vc[:, :, 41], x2=x2, h=h, lin=lin)
+
+    img, strm = run(0), run(1)
+    for name in img:
+        a, b = img[name].float().cpu().numpy(), strm[name].float().cpu().numpy()
+        if wfmt in (1, W4G_128) or (name == "x" and M >= 5):  # same row-sum route (or none)
+            assert np.array_equal(a, b), name
+        else:
+            assert np.mean(a == b) > 0.99, (name, np.mean(a == b))
+    # the streamed forms against the oracle
+    xs = strm["x"].float().cpu().numpy()
+    assert_bf16_close(xs, x0 + bf16(hin @ Wd_.T), "mlp.c_proj resid")
+    hn = O.rmsnorm_bf16(xs, g)
+    qkv = bf16(hn @ Wq.T)
+    assert_bf16_close(strm["q"].float().cpu().numpy(),
+                      O.apply_rope(qkv[:, :C].reshape(M, 1, nh, hs), O.build_rope_cache(128, hs)[[41]]).reshape(M, C), "q")
+    assert_bf16_close(strm["v"].float().cpu().numpy().reshape(M, C), qkv[:, 2 * C:], "v")
+    x2 = strm["x2"].float().cpu().numpy()
+    assert_bf16_close(x2, xs + bf16(yin @ Wo.T), "attn.c_proj resid")
+    hn2 = O.rmsnorm_bf16(x2, g)
+    hexp = bf16(bf16(O.silu(bf16(hn2 @ W1.T))) * bf16(hn2 @ W2.T))
+    assert_bf16_close(strm["h"].float().cpu().numpy(), hexp, "swiglu", rel=3e-2)
+    assert_bf16_close(strm["lin"].float().cpu().numpy(), yin @ Wo.T, "linear")
 
 
 def test_rmsnorm_rows_rowsum_and_int4_rowsum_operand(hip, golden):
@@ -872,17 +969,18 @@ def test_gemm_linear_and_resid(hip, wfmt, M, N, K):
     assert_bf16_close(xr.float().cpu().numpy(), x0 + bf16(y), f"gemm resid wfmt={wfmt}")
 
 
-GLDS_TILES = {"256x256": {"LLJ_GEMM_GLDS": "1", "LLJ_GLDS_COST128": "1000"},
-              "256x128": {"LLJ_GEMM_GLDS": "1", "LLJ_GLDS_COST128": "0"}, "regstaged": {"LLJ_GEMM_GLDS": "0"}}
+GLDS_TILES = {"256x256": {3: 1, 4: 1000}, "256x128": {3: 1, 4: 0}, "regstaged": {3: 0}}  # LLJ_OPT_GEMM_GLDS / _COST128
 
 
 @pytest.fixture
-def glds_tile(request, monkeypatch):
-    """The prefill GEMM's M >= 256 kernel forced through its host-side knobs (read per call): the
+def glds_tile(request, hip):
+    """The prefill GEMM's M >= 256 kernel forced through its host-side options (llj_set_option): the
     LDS-DMA kernel's 256 x 256 or 256 x 128 tiles, or the register-staged kernel."""
-    for k, v in GLDS_TILES[request.param].items():
-        monkeypatch.setenv(k, v)
-    return request.param
+    old = {k: hip.llj_set_option(k, v) for k, v in GLDS_TILES[request.param].items()}
+    assert -1000 not in old.values()
+    yield request.param
+    for k, v in old.items():
+        hip.llj_set_option(k, v)
 
 
 @pytest.mark.parametrize("glds_tile", list(GLDS_TILES), indirect=True)
@@ -1145,13 +1243,18 @@ def test_gemm_qkv_rope_kv(hip, wfmt, B, T_, nh, hs):
                                             (128, 3, 1, 33, 2048, 1000), (128, 2, 1, 700, 1024, 0)])
 @pytest.mark.parametrize("pair", ["0", "1"])
 @pytest.mark.parametrize("qb", ["1", "2"])
-def test_attention_prefill_flash(hip, hs, nh, B, T_, S, p0, qb, pair, monkeypatch):
+def test_attention_prefill_flash(hip, hs, nh, B, T_, S, p0, qb, pair):
     """The MFMA flash attention for prompt rows (llj_attention_prefill) against the oracle: causal
     over cache slots 0 .. p0 + t, partial last query block, ragged key tiles, earlier context (p0 > 0);
-    one or two 16-query blocks per wave (LLJ_FLASH_QB) and one query block or a (long, short) pair
-    per workgroup (LLJ_FLASH_PAIR; odd block counts leave the middle block alone), read per call."""
-    monkeypatch.setenv("LLJ_FLASH_QB", qb)
-    monkeypatch.setenv("LLJ_FLASH_PAIR", pair)
+    one or two 16-query blocks per wave (LLJ_OPT_FLASH_QB) and one query block or a (long, short) pair
+    per workgroup (LLJ_OPT_FLASH_PAIR; odd block counts leave the middle block alone)."""
+    from lit_llama import _hip
+
+    with option(hip, _hip.OPT_FLASH_QB, int(qb)), option(hip, _hip.OPT_FLASH_PAIR, int(pair)):
+        _flash_case(hip, hs, nh, B, T_, S, p0)
+
+
+def _flash_case(hip, hs, nh, B, T_, S, p0):
     rng = np.random.default_rng(hs + T_ + p0)
     C = nh * hs
     kc = bf16(rng.standard_normal((B, nh, S, hs)))

@@ -97,7 +97,7 @@ def main():
     for key, cs in groups.items():
         tag, n, grid = key.split("|")
         prefix = tag.split("_")[0]  # bs1 / bs8 / c1 / c3 / c3b8 (int8 bs=8 decode in 4-row slices)
-        k = out["kernels"].setdefault(f"{n} grid {grid}", {"op": op_of(n, int(grid), multi=prefix in ("bs8", "c3b8"))})
+        k = out["kernels"].setdefault(f"{n} grid {grid}", {"op": op_of(n, int(grid), multi=prefix in ("bs8", "c3b8", "c3"))})
         ent = k.setdefault(prefix, {})
         ent["dispatches"] = max(ent.get("dispatches", 0), max(len(v) for v in cs.values()))
         for c, v in cs.items():
@@ -113,7 +113,7 @@ def main():
                     ent["algorithmic_bytes"] = algo_bytes_int4(k["op"], 8 if prefix == "bs8" else 1)
                     ent["traffic_over_algorithmic"] = round(ent["hbm_bytes"] / ent["algorithmic_bytes"], 3)
                 elif prefix in ("c3", "c3b8") and k["op"] and name.startswith("llj::gemv_kernel<2,"):
-                    ent["algorithmic_bytes"] = algo_bytes_int8(k["op"], 4 if prefix == "c3b8" else 1)
+                    ent["algorithmic_bytes"] = algo_bytes_int8(k["op"], 4 if prefix == "c3b8" else 8)
                     ent["traffic_over_algorithmic"] = round(ent["hbm_bytes"] / ent["algorithmic_bytes"], 3)
             if "SQ_VALU_MFMA_BUSY_CYCLES" in ent and ent.get("GRBM_GUI_ACTIVE"):
                 ent["mfma_busy"] = ent["SQ_VALU_MFMA_BUSY_CYCLES"] / (ent["GRBM_GUI_ACTIVE"] / 8 * 1024)
