@@ -312,6 +312,30 @@ int llj_g_argmax(const float* logits, int ldl, int M, int V, int* out_idx, int* 
 int llj_g_sample(const float* logits, int ldl, int M, int V, float temperature, int top_k, const float* u,
                  unsigned long long seed, int* out_idx, int* tokens_out, int tok_stride, const int* pos, void* stream);
 
+/* ---------------------------------------------------------------- LLM.int8() decode statistics hand-off
+ * Decode rows (M <= 8) of an llm.int8 model skip the statistics launch of the attention output y and
+ * of the SwiGLU output h (Linear8bitLt inputs of attn.c_proj / mlp.c_proj, quantization.py:36-75):
+ * the producing op writes the LLM.int8 row statistics into a small block -- words [0, 8) SCA[m] =
+ * max |f16(A[m, k])| below the threshold (the bits of the float), words [16, 16 + ceil(K / 32)) the
+ * outlier columns (any row |f16(A)| >= threshold) as bits -- with order-independent atomics (max / or:
+ * the values of llj_i8_stats exactly), and the int8 GEMV quantizes its bf16 rows per K chunk from it,
+ * taking the fp16 outlier side product from the streamed weights. A block must be zero before its
+ * producer runs: llj_attention_i8 zeroes the (previous layer's) h block and llj_i8_swiglu_stats the
+ * y block, so a decode step leaves both zero. */
+size_t llj_i8_rowstats_bytes(int K);
+/* llj_attention / llj_attention_split (nsplit <= 1: one block per (head, row)) + y's statistics. */
+int llj_attention_i8(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                     int n_head, int head_size, int S, int nsplit, void* part_ws, void* y_stats, void* clr,
+                     int clr_words, float threshold, void* stream);
+/* llj_norm_swiglu for wfmt 2 (x = the normalized rows of llj_i8_norm_stats, i8ws its workspace) + h's
+ * statistics into h_stats; zeroes clr_words words at clr. */
+int llj_i8_swiglu_stats(const void* x, const void* CB1, const void* SCB1, const void* CB2, const void* SCB2, void* h,
+                        int M, int H, int K, const void* i8ws, int i8_row0, void* h_stats, void* clr, int clr_words,
+                        float threshold, void* stream);
+/* x[M, N] += LLM.int8(A)[M, K] . CB^T (CB in I8P, SCB) with A's statistics `stats` (M <= 8). */
+int llj_i8_linear_resid(const void* A, int lda, const void* CB, const void* SCB, void* x, int ldx, int M, int N, int K,
+                        const void* stats, void* stream);
+
 /* Measurement aid (no reference counterpart): reads `bytes` (a multiple of 16) at p once with
  * non-temporal 16-byte loads over `grid` workgroups of 256 and writes one float per workgroup to
  * out (grid floats). bench.py times it over a buffer far larger than the 256 MB MALL to report the

@@ -10,6 +10,7 @@
 // softmax; the groups of a wave merge through lane swaps, the waves through LDS.
 #pragma once
 #include "common.h"
+#include "i8ws.h"
 
 namespace llj {
 
@@ -17,6 +18,22 @@ template <int HS, int NTH>
 constexpr int attention_lds_floats() {
   constexpr int NWV = NTH / 64;  // waves: one (max, sum, HS outputs) partial each
   return 2 * NWV + NWV * HS;
+}
+
+// LLM.int8() statistics of attention output rows for the int8 c_proj (i8ws.h kI8StFlags): the
+// calling wave holds 64 consecutive output columns col0 .. col0 + 63 of row m (bf16 bits in ob).
+// Row maximum of |f16(y)| below the threshold (atomicMax on the float bits) and the outlier columns
+// (atomicOr); both order-independent.
+__device__ __forceinline__ void i8_emit_stats64(uint32_t* st, float thr, int m, int col0, uint32_t ob) {
+  const float a16 = fabsf(f16r(bflo(ob)));
+  const bool big = a16 >= thr;
+  const float mx = wave_max(big ? 0.f : a16);
+  const unsigned long long bal = __ballot(big);
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(st + m, __float_as_uint(mx));
+    if ((uint32_t)bal) atomicOr(st + kI8StFlags + (col0 >> 5), (uint32_t)bal);
+    if ((uint32_t)(bal >> 32)) atomicOr(st + kI8StFlags + (col0 >> 5) + 1, (uint32_t)(bal >> 32));
+  }
 }
 
 // Merge two online-softmax partials (running max, sum, outputs) of the same dims: the lanes
@@ -42,7 +59,9 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
                                                const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                const int* __restrict__ pos, int T, int S, int nh, float scale_log2,
                                                int h, int m, float* lds, int nsplit = 1,
-                                               int split = 0, float* __restrict__ part = nullptr) {
+                                               int split = 0, float* __restrict__ part = nullptr,
+                                               uint32_t* __restrict__ st = nullptr, float thr = 0.f,
+                                               uint32_t* __restrict__ clr = nullptr, int clr_words = 0) {
   constexpr int DPL = HS / 16;
   constexpr int NG = NTH / 16;
   constexpr int NWV = NTH / 64;
@@ -50,6 +69,8 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   float* s_l = s_m + NWV;               // [NWV]
   float* s_o = s_l + NWV;               // [NWV][HS]
   LLJ_STAMP(0);
+  if (clr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)  // a statistics block to zero (int8 decode)
+    for (int i = threadIdx.x; i < clr_words; i += NTH) clr[i] = 0u;
   const int b = m / T, t = m % T;
   const int sub = threadIdx.x & 15, kg = threadIdx.x >> 4;
   const int C = nh * HS;
@@ -199,6 +220,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
       const size_t eo = (size_t)m * C + h * HS + d;
       st_out32(y + eo, ob | (pr << 16));
     }
+    if (st) i8_emit_stats64(st, thr, m, h * HS + (d & ~63), ob);  // uniform
   }
   LLJ_STAMP(5);
 }
@@ -207,7 +229,9 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
 // with f_s = exp2(M_s - max_s M_s) (empty ranges have M = -inf and contribute nothing).
 template <int HS>
 __global__ __launch_bounds__(HS) void attention_combine_kernel(const float* __restrict__ part, bf16_t* __restrict__ y,
-                                                               int nh, int nsplit) {
+                                                               int nh, int nsplit, uint32_t* __restrict__ st = nullptr,
+                                                               float thr = 0.f, uint32_t* __restrict__ clr = nullptr,
+                                                               int clr_words = 0) {
   const int h = blockIdx.x, m = blockIdx.y, d = threadIdx.x;
   const float* src = part + (size_t)(m * nh + h) * nsplit * (HS + 2);
   float M = -INFINITY;
@@ -222,6 +246,9 @@ __global__ __launch_bounds__(HS) void attention_combine_kernel(const float* __re
   const uint32_t ob = (uint32_t)f2bf(O / L);
   const uint32_t pr = lane_xor1(ob);
   if (!(d & 1)) *reinterpret_cast<uint32_t*>(y + (size_t)m * nh * HS + h * HS + d) = ob | (pr << 16);
+  if (st) i8_emit_stats64(st, thr, m, h * HS + (d & ~63), ob);
+  if (clr && h == 0 && m == 0)
+    for (int i = d; i < clr_words; i += HS) clr[i] = 0u;
 }
 
 }  // namespace llj

@@ -51,6 +51,8 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+// fp32 -> fp16 -> fp32 (bitsandbytes' A16 = A.half())
+__device__ __forceinline__ float f16r(float x) { return (float)(_Float16)x; }
 
 // packed pairs: one v_pk_mul_f32 / v_cvt_pk_bf16_f32 for two values
 typedef float f32x2 __attribute__((ext_vector_type(2)));

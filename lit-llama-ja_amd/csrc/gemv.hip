@@ -125,4 +125,35 @@ int llj_norm_qkv_rope(int wfmt, const void* x, const void* norm_w, float eps, co
   return run<EP_QKV>(wfmt, p, stream);
 }
 
+// ---- LLM.int8() decode rows with handed-over statistics (i8ws.h kI8StFlags; M <= 8)
+size_t llj_i8_rowstats_bytes(int K) { return (size_t)i8st_words(K) * 4; }
+
+// x[M,N] += LLM.int8(A)[M,K] . CB^T: A bf16 rows quantized per K chunk inside the GEMV with the row
+// statistics `stats` its producer wrote (llj_attention_i8 / llj_i8_swiglu_stats), the fp16 outlier
+// side product from the streamed weights (attn.c_proj / mlp.c_proj + model.py:172-173).
+int llj_i8_linear_resid(const void* A, int lda, const void* CB, const void* SCB, void* x, int ldx, int M, int N, int K,
+                        const void* stats, void* stream) {
+  if (!stats || M > 8 || (lda & 7)) return LLJ_EINVAL;
+  GemvParams p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K;
+  p.W = CB; p.sz = (const float2*)SCB; p.C = (bf16_t*)x; p.ldc = ldx;
+  p.i8st = (const uint32_t*)stats;
+  return run<EP_RESID>(WF_I8, p, stream);
+}
+
+// h = silu(xn . CB1^T) * (xn . CB2^T) for LLM.int8 (llj_norm_swiglu, wfmt 2, i8ws from
+// llj_i8_norm_stats) that also writes the LLM.int8 statistics of h (h_stats, zeroed beforehand) and
+// zeroes clr_words words at clr (the attention output's statistics block of the next layer).
+int llj_i8_swiglu_stats(const void* x, const void* CB1, const void* SCB1, const void* CB2, const void* SCB2, void* h,
+                        int M, int H, int K, const void* i8ws, int i8_row0, void* h_stats, void* clr, int clr_words,
+                        float threshold, void* stream) {
+  if (!h_stats || M > 8 || clr_words < 0 || (clr_words && !clr)) return LLJ_EINVAL;
+  GemvParams p{};
+  p.A = (const bf16_t*)x; p.lda = K; p.M = M; p.N = H; p.K = K;
+  p.W = CB1; p.W2 = CB2; p.sz = (const float2*)SCB1; p.sz2 = (const float2*)SCB2; p.C = (bf16_t*)h; p.ldc = H;
+  p.i8ws = i8ws; p.m0 = i8_row0;
+  p.i8st_out = (uint32_t*)h_stats; p.clr = (uint32_t*)clr; p.clr_words = clr_words; p.thr = threshold;
+  return run<EP_SWIGLU>(WF_I8, p, stream);
+}
+
 }  // extern "C"

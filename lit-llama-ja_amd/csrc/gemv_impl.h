@@ -57,11 +57,19 @@ enum : int { WF_W4 = 0, WF_BF16 = 1, WF_I8 = 2, WF_W8 = 3, WF_W4G = 4 };
 // rows travel), normalises them in registers with the row statistics handed over by the
 // producer (nstat, AM_SNORM) and passes them through a 2-slot per-wave LDS ring into the MFMA
 // fragments -- no workgroup-wide A image, no prologue barrier, no separate RMSNorm launch.
-enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2, AM_STREAM = 3, AM_SNORM = 4 };
+// AM_I8Q (LLM.int8, batched decode rows): the bf16 activation rows are streamed like AM_STREAM and
+// quantized per chunk with the row statistics its producer handed over (i8st: SCA per row, outlier
+// column bits), and the fp16 outlier side product is taken from the chunk's weight registers as the
+// chunk streams -- no statistics launch, no int8 A image, no side-product pass after the stream.
+enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2, AM_STREAM = 3, AM_SNORM = 4, AM_I8Q = 5 };
 // streamed A: elements per staged row (128 + 8 pad: rows land on distinct bank groups) and per slot
 constexpr int kSRow = 136;
 constexpr int kSSlot = 8 * kSRow;
 __host__ __device__ constexpr bool am_stream(int am) { return am == AM_STREAM || am == AM_SNORM; }
+// AM_I8Q per-wave ring slot: the quantized rows (8 x 144 B) then the bf16 rows (8 x kSRow elements,
+// read only for chunks with outlier columns)
+constexpr int kQRow = 144;
+constexpr int kQSlotBytes = 8 * kQRow + kSSlot * 2;
 enum : int { EP_STORE = 0, EP_RESID = 1, EP_QKV = 2, EP_SWIGLU = 3 };
 
 // int8 activation workspace written by llj_i8_stats (int8.hip): i8ws.h
@@ -98,6 +106,14 @@ struct GemvParams {
   int npart;
   float* nstat_out;
   int gch;  // WF_W4G: group size in 128-deep chunks (tile_cols / 128)
+  // LLM.int8() decode statistics (i8ws.h kI8StFlags): i8st = the consumer's row statistics (AM_I8Q:
+  // A is the bf16 activation, quantized per chunk in the GEMV); i8st_out = the statistics of this
+  // op's output (EP_SWIGLU producer); clr / clr_words = a statistics block zeroed by workgroup 0
+  const uint32_t* i8st;
+  uint32_t* i8st_out;
+  uint32_t* clr;
+  int clr_words;
+  float thr;
 };
 constexpr int kNstRows = 16;
 #ifndef LLJ_SACC_NORM
@@ -365,6 +381,21 @@ __device__ __forceinline__ float out_value(float y, float y2) {
 }
 
 
+// LLM.int8() row quantization of 8 bf16 elements (packed in a u32x4): q = clamp(rint(f16(a) * inv))
+// with inv = 127 / SCA, outlier columns (bit e of fb) 0 -- the prep pass's quant8 (int8.hip)
+__device__ __forceinline__ uint2 quant8f(const u32x4 x, uint32_t fb, float inv) {
+  uint32_t o[2] = {0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int qa = (int)fminf(fmaxf(rintf(f16r(bflo(x[i])) * inv), -127.f), 127.f);
+    int qb = (int)fminf(fmaxf(rintf(f16r(bfhi(x[i])) * inv), -127.f), 127.f);
+    if ((fb >> (2 * i)) & 1u) qa = 0;
+    if ((fb >> (2 * i + 1)) & 1u) qb = 0;
+    o[i >> 1] |= ((uint32_t)(qa & 0xFF) | ((uint32_t)(qb & 0xFF) << 8)) << (16 * (i & 1));
+  }
+  return make_uint2(o[0], o[1]);
+}
+
 template <int V>
 struct IC {
   static constexpr int value = V;
@@ -414,7 +445,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   constexpr bool STRM = am_stream(AM);  // A rows streamed per chunk (see AM_STREAM)
   constexpr bool SNRM = (AM == AM_SNORM);
   static_assert(!STRM || (MB == 8 && !I8), "streamed A: batched rows, non-int8 formats");
-  constexpr bool ALDS = I8 || (AM != AM_GLOBAL && !STRM);
+  constexpr bool I8Q = (AM == AM_I8Q);  // int8 rows quantized per chunk from handed-over statistics
+  static_assert(!I8Q || (I8 && MB == 8 && !DUAL && TPW == 1), "AM_I8Q: int8 single-matrix ops, batched rows");
+  constexpr bool ASTR = STRM || I8Q;  // bf16 A rows streamed per chunk
+  constexpr bool ALDS = (I8 && !I8Q) || (AM != AM_GLOBAL && !STRM && !I8Q);
   // row sums of A for the nibble offset: an extra MFMA against a ones fragment for the global-A
   // form and for batched norm-fused rows (LLJ_SACC_NORM; the VALU sums + 8 wave reductions of the
   // prologue sit on its critical path), else summed while the LDS image is written
@@ -425,6 +459,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   const int wave = uniform(threadIdx.x >> 6);
   const int K = p.K, M = p.M, KC = K >> 7;
   const int ntiles = p.N >> 4;
+  if (p.clr && blockIdx.x == 0)  // a statistics block to be zeroed before its producer runs (uniform)
+    for (int i = threadIdx.x; i < p.clr_words; i += NW * 64) p.clr[i] = 0u;
   int ntj[TPW];  // tile of slot j (clamped copy of the last tile past the end)
   bool tvalid[TPW];
 #pragma unroll
@@ -437,7 +473,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   // scratch] [tail: 128 words for staging scratch / int8 SCA]
   const int a_stride = I8 ? K + 16 : K + 8;  // elements (bytes for int8)
   const size_t a_bytes = ALDS ? (((size_t)M * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15)
-                              : STRM ? (size_t)NW * 2 * kSSlot * 2 : 0;
+                              : STRM ? (size_t)NW * 2 * kSSlot * 2 : I8Q ? (size_t)NW * 2 * kQSlotBytes : 0;
   constexpr int NV = 8 * TPW + 4;  // reduction words per lane: acc, acc2 of every tile, sacc
   constexpr size_t kRedBytes = (size_t)NW * 64 * NV * 4;
   constexpr size_t kScratch = kRedBytes + (I8 ? (size_t)2 * NW * 8 * 16 * 4 : 0);  // + int8 side partials
@@ -504,11 +540,16 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   // streamed A: lane l carries 16-B segment (l & 15) of rows (l >> 4) and (l >> 4) + 4 of each of
   // its chunks (rows past M: clamped copies of row M - 1, never stored), plus the norm weights'
   // segment (AM_SNORM); rn0 / rn1 = the RMSNorm rstd of those two rows
-  u32x4 sa[STRM ? D : 1][2], sg[SNRM ? D : 1];
+  u32x4 sa[ASTR ? D : 1][2], sg[SNRM ? D : 1];
+  u32x4 sfl[I8Q ? D : 1];  // AM_I8Q: the chunk's 128 outlier-column bits (the same in every lane)
+  float qi0 = 0.f, qi1 = 0.f, i8scb = 0.f;  // AM_I8Q: 127 / SCA of the lane's two rows; SCB[n] / 127
+  float sd[I8Q ? 8 : 1];  // AM_I8Q: this lane's fp16 side-product partials of rows 0..7 (its column, its k group)
+#pragma unroll
+  for (int m = 0; m < (I8Q ? 8 : 1); ++m) sd[m] = 0.f;
   const bf16_t* aptr[2];
   const bf16_t* gptr = p.norm_w + 8 * (lane & 15);
   float rn0 = 1.f, rn1 = 1.f;
-  if constexpr (STRM) {
+  if constexpr (ASTR) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int rr = (lane >> 4) + 4 * h;
@@ -518,10 +559,11 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   auto load = [&](int d, int i) {
     int c = wave + NW * (i < nmy ? i : nmy - 1);
     c = c < 0 ? 0 : (c >= KC ? KC - 1 : c);  // always a valid chunk (loads past the end are unused)
-    if constexpr (STRM) {  // the chunk's activation rows first: they arrive before its weights
+    if constexpr (ASTR) {  // the chunk's activation rows first: they arrive before its weights
 #pragma unroll
       for (int h = 0; h < 2; ++h) sa[d][h] = *reinterpret_cast<const u32x4*>(aptr[h] + 128 * c);
       if constexpr (SNRM) sg[d] = *reinterpret_cast<const u32x4*>(gptr + 128 * c);
+      if constexpr (I8Q) sfl[d] = *reinterpret_cast<const u32x4*>(p.i8st + kI8StFlags + 4 * c);
     }
     if constexpr (GRP) {
       const size_t go = (size_t)(c / p.gch) * p.N + row;
@@ -561,6 +603,45 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     // wave's ring slot d % 2, read back as MFMA fragments (one wave writes and reads its own slot:
     // LDS keeps a wave's accesses in order, no barrier)
     bf16_t* slot = reinterpret_cast<bf16_t*>(smem) + (size_t)(wave * 2 + (d & 1)) * kSSlot;
+    unsigned char* qslot = smem + (size_t)(wave * 2 + (d & 1)) * kQSlotBytes;
+    if constexpr (I8Q) {
+      // quantize the lane's two row segments (LLM.int8 rows with the producer's SCA and outlier bits)
+      const u32x4 fw = sfl[d];
+      const int seg = lane & 15;
+      auto pick = [&](int i) {  // fw[i] for a lane-varying i (selects: no dynamic register index)
+        return i == 0 ? fw[0] : i == 1 ? fw[1] : i == 2 ? fw[2] : fw[3];
+      };
+      const uint32_t fb = (pick(seg >> 2) >> (8 * (seg & 3))) & 0xFFu;
+      *reinterpret_cast<uint2*>(qslot + (lane >> 4) * kQRow + 8 * seg) = quant8f(sa[d][0], fb, qi0);
+      *reinterpret_cast<uint2*>(qslot + ((lane >> 4) + 4) * kQRow + 8 * seg) = quant8f(sa[d][1], fb, qi1);
+      if ((fw[0] | fw[1] | fw[2] | fw[3]) != 0u) {  // uniform: the chunk has outlier columns
+        // fp16 side product from the weight registers: lane (column n, k group g) holds CB[n, k] of
+        // k = 64 t + 16 g + j (t = 0, 1; j < 16) of the chunk; f16(A) of all rows from the bf16 slot
+        bf16_t* bslot = reinterpret_cast<bf16_t*>(qslot + 8 * kQRow);
+        *reinterpret_cast<u32x4*>(bslot + (lane >> 4) * kSRow + 8 * seg) = sa[d][0];
+        *reinterpret_cast<u32x4*>(bslot + ((lane >> 4) + 4) * kSRow + 8 * seg) = sa[d][1];
+        const uint32_t m32 = ((pick(grp >> 1) >> (16 * (grp & 1))) & 0xFFFFu) |
+                             (((pick(2 + (grp >> 1)) >> (16 * (grp & 1))) & 0xFFFFu) << 16);
+        // columns j of any k group's range, in a uniform (not unrolled) loop over the set bits
+        uint32_t any = m32;
+        any |= (uint32_t)__shfl_xor((int)any, 16, 64);
+        any |= (uint32_t)__shfl_xor((int)any, 32, 64);
+        any = (uint32_t)uniform((int)any);
+        const u32x4 c0 = r1[d][0][0], c1 = r1[d][0][1];
+        for (uint32_t rem = any; rem; rem &= rem - 1u) {
+          const int j = __builtin_ctz(rem);
+          if ((m32 >> j) & 1u) {
+            const int kk = 64 * (j >> 4) + 16 * grp + (j & 15), wi = (j & 15) >> 2;
+            const u32x4 cv = (j >> 4) ? c1 : c0;
+            const uint32_t wd = wi == 0 ? cv[0] : wi == 1 ? cv[1] : wi == 2 ? cv[2] : cv[3];
+            const float cbv = (float)(int)(int8_t)((wd >> (8 * (j & 3))) & 0xFFu);
+            const float w = f16r(cbv * i8scb);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) sd[m] += f16r(bf2f(bslot[m * kSRow + kk])) * w;
+          }
+        }
+      }
+    }
     if constexpr (STRM) {
       u32x4 x0 = sa[d][0], x1 = sa[d][1];
       if constexpr (SNRM) {
@@ -575,6 +656,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       // LDS lanes of rows >= M read row 0 (abase clamped): their output rows are never stored, and
       // an unconditional read keeps the hot loop free of divergent LDS accesses
       const u32x4 av = STRM ? *reinterpret_cast<const u32x4*>(slot + (row & 7) * kSRow + kofs<WF>(t, grp))
+                       : I8Q ? *reinterpret_cast<const u32x4*>(qslot + (row & 7) * kQRow + kofs<WF>(t, grp))
                        : ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
       if constexpr (WF == WF_W4) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
@@ -845,6 +927,12 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
 #endif
   // AM_SNORM: the producer's partial sums of squares, partials q = lane + 64 i (i < kSnQ) of rows
   // 0..7 (two 16-B loads per partial), issued before the weight stream
+  // AM_I8Q: the producer's SCA of rows 0..7 (bits of non-negative floats), before the weight stream
+  float4 isc[I8Q ? 2 : 1];
+  if constexpr (I8Q) {
+    isc[0] = *reinterpret_cast<const float4*>(p.i8st);
+    isc[1] = *reinterpret_cast<const float4*>(p.i8st + 4);
+  }
   constexpr int kSnQ = 4;
   float4 snv[SNRM ? kSnQ : 1][2];
   if constexpr (SNRM) {
@@ -881,10 +969,26 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       if (m == m1c) rn1 = r;
     }
   }
+  if constexpr (I8Q) {
+    const float sv[8] = {isc[0].x, isc[0].y, isc[0].z, isc[0].w, isc[1].x, isc[1].y, isc[1].z, isc[1].w};
+    const int r0 = lane >> 4, r1i = (lane >> 4) + 4;
+    const int m0c = r0 < M ? r0 : M - 1, m1c = r1i < M ? r1i : M - 1;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const float inv = sv[m] > 0.f ? 127.f / sv[m] : 0.f;
+      if (m == m0c) qi0 = inv;
+      if (m == m1c) qi1 = inv;
+    }
+    float mine = sv[0];  // the epilogue's SCA (tail; rows >= M unused); selects, not a dynamic index
+#pragma unroll
+    for (int m = 1; m < 8; ++m) mine = tid == m ? sv[m] : mine;
+    if (tid < 8) sca[tid] = mine;
+    i8scb = e_a[0].x / 127.f;
+  }
   // int8: the per-k-block outlier counts the side product starts from, loaded now (one memory
   // latency less in the tail; needed once the stream is done)
   int i8cnt = 0, i8spk[kSpE<NW>] = {};
-  if constexpr (I8) {  // + the speculative outlier-list entries of the side product's fast path
+  if constexpr (I8 && !I8Q) {  // + the speculative outlier-list entries of the side product's fast path
     const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
     const I8Layout L8 = i8_layout(p.i8ws, h.mtot, h.K);
     i8cnt = L8.cnt[lane < kNSB ? lane : 0];
@@ -909,6 +1013,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     }
   }
   if constexpr ((LLJ_ABL & 1) != 0) {  // ablation: no A prologue (garbage A)
+  } else if constexpr (I8Q) {
   } else if constexpr (I8) {
     stage_i8<NW>(p, reinterpret_cast<int8_t*>(smem), a_stride, sca);
     __syncthreads();
@@ -962,8 +1067,16 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   // int8 side products in the LDS beyond the reduction scratch (the A image is no longer read)
   float* side = reinterpret_cast<float*>(smem + kRedBytes);
   if (NW > 1) {
-    if (ALDS || STRM) __syncthreads();  // every wave is done reading the A image / ring it aliases
-    if constexpr (I8) {
+    if (ALDS || ASTR) __syncthreads();  // every wave is done reading the A image / ring it aliases
+    if constexpr (I8Q) {  // the in-stream side partials: sum the 4 k groups, one partial per (wave, row, column)
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        float v = sd[m];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (lane < 16) side[(wave * 8 + m) * 16 + lane] = v;
+      }
+    } else if constexpr (I8) {
       i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W), reinterpret_cast<const float*>(p.sz), ntj[0] * 16,
                        side, smem, i8cnt, i8spk);
       if (DUAL)
@@ -1003,6 +1116,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       return;
     }
     const float s1 = e_a[j].x, o1 = e_a[j].y, s2 = e_b[j].x, o2 = e_b[j].y;
+    bool i8col = false;  // EP_SWIGLU int8 statistics: this lane's column has an outlier
     const float bias = p.bias ? bf2f(e_braw[j]) : 0.f;
 #pragma unroll
     for (int r = 0; r < RR; ++r) {
@@ -1096,6 +1210,24 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
           const size_t ei = (size_t)m * p.ldc + n;
           st_out32(p.C + ei, ob | (pr << 16));
         }
+        if constexpr (EP == EP_SWIGLU && I8) {
+          if (p.i8st_out) {  // uniform: LLM.int8 statistics of h for the int8 mlp.c_proj (AM_I8Q)
+            const float a16 = fabsf(f16r(bflo(ob)));
+            const bool big = m < M && a16 >= p.thr;
+            i8col |= big;
+            const float mx = row16_max(m < M && !big ? a16 : 0.f);
+            if (row == 0 && m < M) atomicMax(p.i8st_out + m, __float_as_uint(mx));
+          }
+        }
+      }
+    }
+    if constexpr (EP == EP_SWIGLU && I8) {
+      if (p.i8st_out) {  // the tile's outlier columns (any row), 16 bits of one flag word
+        uint32_t f = i8col ? 1u : 0u;
+        f |= (uint32_t)__shfl_xor((int)f, 16, 64);
+        f |= (uint32_t)__shfl_xor((int)f, 32, 64);
+        const uint32_t bits = (uint32_t)(__ballot(f != 0u) & 0xFFFFull);
+        if (lane == 0 && bits) atomicOr(p.i8st_out + kI8StFlags + (n0 >> 5), bits << (n0 & 31));
       }
     }
   };
@@ -1163,6 +1295,7 @@ constexpr int kNW = LLJ_NW;
 constexpr int kD = LLJ_D;
 
 static inline size_t a_image_bytes(int wf, int am, int M, int K, int nw = kNW) {
+  if (am == AM_I8Q) return (size_t)nw * 2 * kQSlotBytes;  // per-wave 2-slot rings
   if (wf == WF_I8) return (((size_t)M * (K + 16)) + 15) & ~(size_t)15;
   if (am == AM_GLOBAL) return 0;
   if (am_stream(am)) return (size_t)nw * 2 * kSSlot * 2;  // per-wave 2-slot rings
@@ -1255,10 +1388,13 @@ constexpr int d_of() {
                 : (EP == EP_SWIGLU ? kD : EP == EP_RESID ? LLJ_DR : LLJ_D1);
 }
 
+#ifndef LLJ_DI8Q
+#define LLJ_DI8Q 4  // AM_I8Q: chunks (2 KiB of int8 weights each) in flight per wave (8 spills)
+#endif
 template <int WF, int AM, int EP, int MB, int NW, int TPW>
 static int launch_t(const GemvParams& p, hipStream_t s) {
   const size_t sm = gemv_smem(WF, AM, p.M, p.K, NW, TPW);
-  auto kern = gemv_kernel<WF, AM, EP, NW, d_of<EP, MB>(), MB, TPW>;
+  auto kern = gemv_kernel<WF, AM, EP, NW, AM == AM_I8Q ? LLJ_DI8Q : d_of<EP, MB>(), MB, TPW>;
   static bool attr_set[16] = {};  // per instantiation and device; set before any graph capture
   if (sm > 64 * 1024) {
     int dev = 0;
@@ -1293,7 +1429,7 @@ static int launch_mb(const GemvParams& p, hipStream_t s) {
 
 template <int WF, int AM, int EP>
 static int launch(const GemvParams& p, hipStream_t s) {
-  if constexpr (am_stream(AM)) {  // batched rows only (M <= 8)
+  if constexpr (am_stream(AM) || AM == AM_I8Q) {  // batched rows only (M <= 8)
     if constexpr (EP == EP_RESID && LLJ_NWR != kNW)
       if (p.K >= LLJ_NWR_KMIN) return launch_mb<WF, AM, EP, 8, LLJ_NWR>(p, s);
     return launch_mb<WF, AM, EP, 8, LLJ_NWM>(p, s);
@@ -1317,6 +1453,7 @@ static int launch(const GemvParams& p, hipStream_t s) {
 // producer's statistics, nstat); otherwise the fused RMSNorm needs the LDS image, and plain rows
 // are staged when they fit.
 static int pick_am(int wf, const GemvParams& p) {
+  if (wf == WF_I8 && p.i8st) return (p.norm_w || p.M > 8) ? -1 : AM_I8Q;  // handed-over row statistics
   if (wf == WF_I8) return (p.norm_w || !p.i8ws || !lds_fits(wf, p.M, p.K)) ? -1 : AM_LDS;
   if (g_stream_a && p.M >= 2 && p.M <= 8) {
     if (!p.norm_w) return AM_STREAM;
@@ -1356,6 +1493,11 @@ static int launch_ep(int ep, const GemvParams& p, hipStream_t s) {
 template <int WF>
 static int launch_fmt(int am, int ep, const GemvParams& p, hipStream_t s) {
   if constexpr (WF == WF_I8) {
+    if (am == AM_I8Q) {  // single-matrix ops only
+      if (ep == EP_RESID) return launch<WF_I8, AM_I8Q, EP_RESID>(p, s);
+      if (ep == EP_STORE) return launch<WF_I8, AM_I8Q, EP_STORE>(p, s);
+      return LLJ_EINVAL;
+    }
     return launch_ep<WF_I8, AM_LDS>(ep, p, s);
   } else {
     if (am == AM_SNORM) return launch_ep<WF, AM_SNORM>(ep, p, s);

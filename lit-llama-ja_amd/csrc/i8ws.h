@@ -58,4 +58,13 @@ __host__ __device__ inline I8Layout i8_layout(const void* ws, int M, int K) {
                   reinterpret_cast<uint8_t*>(b + o.flag), reinterpret_cast<int8_t*>(b + o.aq)};
 }
 
+// LLM.int8() row statistics of a decode activation (M <= 8 rows) handed from the op that produces
+// it to the int8 GEMV that consumes it, instead of a statistics launch in between (attention -> y,
+// SwiGLU -> h): words [0, 8) SCA[m] = max |f16(A[m, k])| over the row's elements below the
+// threshold, as the bits of the non-negative float (atomicMax is order-independent, so the value is
+// the prep pass's exactly); words [kI8StFlags, kI8StFlags + ceil(K / 32)) the outlier columns (any
+// row |f16(A)| >= threshold), bit k % 32 of word k / 32 (atomicOr). Zeroed before the producer runs.
+constexpr int kI8StFlags = 16;
+__host__ __device__ inline int i8st_words(int K) { return kI8StFlags + (K + 31) / 32; }
+
 }  // namespace llj

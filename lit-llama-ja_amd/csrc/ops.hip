@@ -119,9 +119,11 @@ template <int HS, int U, int NTH, int SPECU>
 __global__ __launch_bounds__(NTH) void attention_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                         const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                         const int* __restrict__ pos, int T, int S, int nh,
-                                                        float scale_log2) {
+                                                        float scale_log2, uint32_t* st, float thr, uint32_t* clr,
+                                                        int clr_words) {
   __shared__ float lds[attention_lds_floats<HS, NTH>()];
-  attention_body<HS, U, NTH, false, SPECU>(q, kc, vc, y, pos, T, S, nh, scale_log2, blockIdx.x, blockIdx.y, lds);
+  attention_body<HS, U, NTH, false, SPECU>(q, kc, vc, y, pos, T, S, nh, scale_log2, blockIdx.x, blockIdx.y, lds, 1, 0,
+                                           nullptr, st, thr, clr, clr_words);
 }
 
 // split-K attention over the keys (long contexts): block (head, row, split) -> partial
@@ -464,18 +466,21 @@ int llj_rmsnorm_rows(const void* x, const void* w, float eps, void* y, float* ro
   return 0;
 }
 
-int llj_attention(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
-                  int n_head, int head_size, int S, void* stream) {
+// decode attention, optionally with the LLM.int8 statistics of y (int8 c_proj) and a block to zero
+static int attention_run(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                         int n_head, int head_size, int S, uint32_t* st, float thr, uint32_t* clr, int clr_words,
+                         void* stream) {
   LLJ_REQUIRE(B > 0 && T > 0 && n_head > 0 && S > 0);
   const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
   dim3 grid(n_head, B * T);
   // keys loaded before the position is known at small grids: half a pass (default) or a whole one
   // (option LLJ_OPT_ATT_SPEC_FULL: one memory latency less, more K / V rows read past the position)
   const bool full = opt(LLJ_OPT_ATT_SPEC_FULL) == 1;
-  hipStream_t st = (hipStream_t)stream;
+  hipStream_t st_ = (hipStream_t)stream;
 #define LLJ_ATT_LAUNCH(HS_, SU_)                                                                                   \
-  hipLaunchKernelGGL((attention_kernel<HS_, LLJ_ATT_U, LLJ_ATT_NTH, SU_>), grid, dim3(LLJ_ATT_NTH), 0, st,          \
-                     (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2)
+  hipLaunchKernelGGL((attention_kernel<HS_, LLJ_ATT_U, LLJ_ATT_NTH, SU_>), grid, dim3(LLJ_ATT_NTH), 0, st_,         \
+                     (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2, \
+                     st, thr, clr, clr_words)
   if (head_size == 128) {
     if (full) LLJ_ATT_LAUNCH(128, LLJ_ATT_U); else LLJ_ATT_LAUNCH(128, LLJ_ATT_U / 2);
   } else if (head_size == 64) {
@@ -488,36 +493,60 @@ int llj_attention(const void* q, const void* kcache, const void* vcache, void* y
   return 0;
 }
 
+int llj_attention(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                  int n_head, int head_size, int S, void* stream) {
+  return attention_run(q, kcache, vcache, y, pos, B, T, n_head, head_size, S, nullptr, 0.f, nullptr, 0, stream);
+}
+
 size_t llj_attention_ws_bytes(int rows, int n_head, int head_size, int nsplit) {
   return (size_t)rows * n_head * (nsplit < 1 ? 1 : nsplit) * (head_size + 2) * sizeof(float);
 }
 
-int llj_attention_split(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
-                        int n_head, int head_size, int S, int nsplit, void* part_ws, void* stream) {
-  if (nsplit <= 1) return llj_attention(q, kcache, vcache, y, pos, B, T, n_head, head_size, S, stream);
+static int attention_split_run(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B,
+                               int T, int n_head, int head_size, int S, int nsplit, void* part_ws, uint32_t* st,
+                               float thr, uint32_t* clr, int clr_words, void* stream) {
+  if (nsplit <= 1)
+    return attention_run(q, kcache, vcache, y, pos, B, T, n_head, head_size, S, st, thr, clr, clr_words, stream);
   LLJ_REQUIRE(B > 0 && T > 0 && n_head > 0 && S > 0 && part_ws && nsplit <= 1024);
   const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
   const dim3 grid(n_head, B * T, nsplit), cgrid(n_head, B * T);
-  hipStream_t st = (hipStream_t)stream;
+  hipStream_t s = (hipStream_t)stream;
   if (head_size == 128) {
-    hipLaunchKernelGGL((attention_part_kernel<128, LLJ_ATT_U, LLJ_ATT_NTH>), grid, dim3(LLJ_ATT_NTH), 0, st,
+    hipLaunchKernelGGL((attention_part_kernel<128, LLJ_ATT_U, LLJ_ATT_NTH>), grid, dim3(LLJ_ATT_NTH), 0, s,
                        (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, pos, T, S, n_head, sl2, nsplit,
                        (float*)part_ws);
     LLJ_CHECK_LAUNCH();
-    hipLaunchKernelGGL((attention_combine_kernel<128>), cgrid, dim3(128), 0, st, (const float*)part_ws, (bf16_t*)y,
-                       n_head, nsplit);
+    hipLaunchKernelGGL((attention_combine_kernel<128>), cgrid, dim3(128), 0, s, (const float*)part_ws, (bf16_t*)y,
+                       n_head, nsplit, st, thr, clr, clr_words);
   } else if (head_size == 64) {
-    hipLaunchKernelGGL((attention_part_kernel<64, LLJ_ATT_U, LLJ_ATT_NTH>), grid, dim3(LLJ_ATT_NTH), 0, st,
+    hipLaunchKernelGGL((attention_part_kernel<64, LLJ_ATT_U, LLJ_ATT_NTH>), grid, dim3(LLJ_ATT_NTH), 0, s,
                        (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, pos, T, S, n_head, sl2, nsplit,
                        (float*)part_ws);
     LLJ_CHECK_LAUNCH();
-    hipLaunchKernelGGL((attention_combine_kernel<64>), cgrid, dim3(64), 0, st, (const float*)part_ws, (bf16_t*)y,
-                       n_head, nsplit);
+    hipLaunchKernelGGL((attention_combine_kernel<64>), cgrid, dim3(64), 0, s, (const float*)part_ws, (bf16_t*)y,
+                       n_head, nsplit, st, thr, clr, clr_words);
   } else {
     return LLJ_EINVAL;
   }
   LLJ_CHECK_LAUNCH();
   return 0;
+}
+
+int llj_attention_split(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                        int n_head, int head_size, int S, int nsplit, void* part_ws, void* stream) {
+  return attention_split_run(q, kcache, vcache, y, pos, B, T, n_head, head_size, S, nsplit, part_ws, nullptr, 0.f,
+                             nullptr, 0, stream);
+}
+
+// Decode attention (one-block or split over nsplit key ranges) that also writes the LLM.int8
+// statistics of y for the int8 c_proj (i8ws.h; y_stats zeroed beforehand, B * T <= 8 rows) and zeroes
+// clr_words words at clr (the previous layer's mlp.c_proj statistics block).
+int llj_attention_i8(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
+                     int n_head, int head_size, int S, int nsplit, void* part_ws, void* y_stats, void* clr,
+                     int clr_words, float threshold, void* stream) {
+  LLJ_REQUIRE(y_stats && B * T <= 8 && clr_words >= 0 && (!clr_words || clr));
+  return attention_split_run(q, kcache, vcache, y, pos, B, T, n_head, head_size, S, nsplit, part_ws,
+                             (uint32_t*)y_stats, threshold, (uint32_t*)clr, clr_words, stream);
 }
 
 int llj_sample(const void* logits, int ldl, int M, int V, float temperature, int top_k, const float* u,

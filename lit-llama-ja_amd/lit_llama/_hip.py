@@ -58,6 +58,9 @@ SIGNATURES = {
     "llj_set_tpw_max": [_I],
     "llj_set_stream_a": [_I],
     "llj_set_option": [_I, _I],
+    "llj_attention_i8": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P],
+    "llj_i8_swiglu_stats": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _I, _F, _P],
+    "llj_i8_linear_resid": [_P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P],
     "llj_gemm_linear": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_silu_mul": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
@@ -103,6 +106,8 @@ def lib() -> ctypes.CDLL:
         L.llj_attention_ws_bytes.restype = ctypes.c_size_t
         L.llj_g_i8_ws_bytes.argtypes = [_I, _I]
         L.llj_g_i8_ws_bytes.restype = ctypes.c_size_t
+        L.llj_i8_rowstats_bytes.argtypes = [_I]
+        L.llj_i8_rowstats_bytes.restype = ctypes.c_size_t
         _lib = L
     return _lib
 

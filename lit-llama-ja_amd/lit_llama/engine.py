@@ -11,14 +11,15 @@ with no host round trip (the reference syncs per layer at model.py:221 and per t
 generate.py:86).
 
 Batch B > 1 decodes B equal-length prompts together (each row equals an independent B=1
-run: tests/test_model_gpu.py); the reference's generate() is batch 1 only (generate.py:62).
+run: tests/test_model_gpu.py); the reference's generate() is batch 1 only (generate.py:62). Up to 8
+rows share every fused launch; larger batches take the ops in row slices.
 """
 from __future__ import annotations
 
 import torch
 
 from . import _hip
-from .model import LLaMA, QKV_ROWS, _Work
+from .model import LLaMA, _Work, _enable_i8_handoff
 
 
 class DecodeSession:
@@ -34,8 +35,9 @@ class DecodeSession:
         dev = model.transformer.wte.weight.device
         _hip.require_device(model.transformer.wte.weight, "model")
         self.dev = dev
-        if batch > QKV_ROWS:
-            raise ValueError(f"decode batch {batch} > {QKV_ROWS} rows per fused launch")
+        if batch < 1:
+            raise ValueError(f"decode batch {batch} < 1")
+        # batches past QKV_ROWS (8) run every fused op in row slices of 8 (16 for the plain linears)
         self.cur = torch.zeros(batch, dtype=torch.int32, device=dev)
         self.pos = torch.zeros(1, dtype=torch.int32, device=dev)
         self.tokens = torch.zeros(batch, total_len, dtype=torch.int32, device=dev)
@@ -97,6 +99,7 @@ class DecodeSession:
         else:
             need_i8 = any(s[0] == 2 for layer in self.specs["layers"] for s in layer) or self.specs["head"][0] == 2
             self.work = _Work(m.config, B, self.dev, need_i8, self.S)
+            _enable_i8_handoff(self.work, self.specs)
         self.graph = None  # the caches / operands may have changed
 
     def _step(self):

@@ -149,6 +149,12 @@ I8_GATHER_MAX = 16256
 
 # int8 decode: RMSNorm + LLM.int8() statistics in one launch pair up to this many rows
 I8_NORM_STATS_MAX_M = 16
+# int8 decode rows (M <= I8S_MAX_M): the attention output's and the SwiGLU output's LLM.int8
+# statistics come from the ops that produce them (llj_attention_i8, llj_i8_swiglu_stats) and the
+# int8 c_proj / mlp.c_proj quantize their rows per chunk (llj_i8_linear_resid): no statistics launch
+# for y and h
+I8_HANDOFF = True
+I8S_MAX_M = 8
 
 # weight formats whose kernels remove the nibble offset with the row sums of A (W4P, W8P)
 _ROWSUM_FMTS = (0, 3)
@@ -196,6 +202,11 @@ def _gspec(lin: nn.Module):
     raise NotImplementedError(f"{type(lin).__name__} has no any-shape kernel")
 
 
+def _enable_i8_handoff(w: "_Work", specs) -> None:
+    """The LLM.int8 statistics hand-off (see _Work) when every Linear of every layer is LLM.int8."""
+    w.i8s = w.y_st is not None and all(s[0] == 2 for layer in specs["layers"] for s in layer)
+
+
 class _Work:
     """Per-call scratch for M rows (allocated from torch's caching allocator)."""
 
@@ -240,6 +251,15 @@ class _Work:
             self.i8ws = torch.empty(nb, dtype=torch.uint8, device=device)
         else:
             self.i8ws = None
+        # LLM.int8 decode rows (M <= 8, every Linear int8; enable_i8_handoff): the attention and the
+        # int8 SwiGLU hand their outputs' LLM.int8 statistics to the int8 c_proj / mlp.c_proj (i8ws.h
+        # kI8StFlags blocks, zero at allocation; a step leaves y's zero again)
+        self.i8s = False
+        self.y_st = self.h_st = None
+        if need_i8 and not gemm and M <= I8S_MAX_M and I8_HANDOFF:
+            L = _hip.lib()
+            self.y_st = torch.zeros(L.llj_i8_rowstats_bytes(C) // 4, dtype=torch.int32, device=device)
+            self.h_st = torch.zeros(L.llj_i8_rowstats_bytes(H) // 4, dtype=torch.int32, device=device)
         # split-K attention partials for long caches (llj_attention_split)
         self.nsplit = attn_splits(S)
         self.att_ws = None
@@ -356,6 +376,7 @@ class LLaMA(nn.Module):
             need_i8 = any(s[0] == 2 for layer in specs["layers"] for s in layer) or specs["head"][0] == 2
             w = _Work(cfg, M, dev, need_i8, S, gemm=self._gemm_ok(specs, M))
             w.flash = self._flash_ok(pos, T, S)
+            _enable_i8_handoff(w, specs)
         st = _hip.stream()
         ids = idx.reshape(-1).to(torch.int32)
         if w.generic:
@@ -588,8 +609,15 @@ class LLaMA(nn.Module):
                           w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), B, T, C, nh,
                           S, r0, r, P(w.i8ws), P(rs), P(nst), w.npart, st)
             # 2. attention, 3. c_proj + residual
-            self._attention(w, kc, vc, pos, B, T, S, st)
-            self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst if w.hand else None)
+            if w.i8s and not w.flash:  # y's LLM.int8 statistics from the attention (clears h's block)
+                _hip.call("llj_attention_i8", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), w.y.data_ptr(), pos.data_ptr(),
+                          B, T, nh, C // nh, S, w.nsplit, P(w.att_ws), w.y_st.data_ptr(), w.h_st.data_ptr(),
+                          w.h_st.numel(), Linear8bitLtThreshold, st)
+                _hip.call("llj_i8_linear_resid", w.y.data_ptr(), C, wp.data_ptr(), P(sp), w.x.data_ptr(), C, M, C, C,
+                          w.y_st.data_ptr(), st)
+            else:
+                self._attention(w, kc, vc, pos, B, T, S, st)
+                self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst if w.hand else None)
             # 4. rms_2 + fc1/fc2 + silu*mul
             if f1 != f2:
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")
@@ -607,6 +635,13 @@ class LLaMA(nn.Module):
             else:
                 src, nw, step = w.x, blk.rms_2.scale.data_ptr(), QKV_ROWS
             nst = w.nst if (w.hand and f1 != 2) else None
+            if w.i8s and not w.flash:  # h's LLM.int8 statistics from the SwiGLU (clears y's block)
+                _hip.call("llj_i8_swiglu_stats", src.data_ptr(), w1.data_ptr(), P(s1), w2.data_ptr(), P(s2),
+                          w.h.data_ptr(), M, H, C, P(w.i8ws), 0, w.h_st.data_ptr(), w.y_st.data_ptr(), w.y_st.numel(),
+                          Linear8bitLtThreshold, st)
+                _hip.call("llj_i8_linear_resid", w.h.data_ptr(), H, wd.data_ptr(), P(sd), w.x.data_ptr(), C, M, C, H,
+                          w.h_st.data_ptr(), st)
+                continue
             for r0 in range(0, M, step):
                 r = min(step, M - r0)
                 _hip.call("llj_norm_swiglu", f1, src[r0].data_ptr(), nw, blk.rms_2.eps, w1.data_ptr(), P(s1),

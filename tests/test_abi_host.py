@@ -111,8 +111,8 @@ def test_ctypes_table_matches_header():
         ret, kinds = decls[name]
         assert ret == "int"
         assert [kind[a] for a in argt] == kinds, name
-    assert set(decls) - set(_hip.SIGNATURES) == {"llj_i8_ws_bytes", "llj_attention_ws_bytes", 
-                                                   "llj_g_i8_ws_bytes"}
+    assert set(decls) - set(_hip.SIGNATURES) == {"llj_i8_ws_bytes", "llj_attention_ws_bytes",
+                                                   "llj_g_i8_ws_bytes", "llj_i8_rowstats_bytes"}
 
 
 def test_library_holds_gfx950_code():

@@ -597,8 +597,10 @@ def test_streamed_a_equals_lds_image_forms(hip, wfmt, M):
         a, b = img[name].float().cpu().numpy(), strm[name].float().cpu().numpy()
         if wfmt in (1, W4G_128) or (name == "x" and M >= 5):  # same row-sum route (or none)
             assert np.array_equal(a, b), name
-        else:
-            assert np.mean(a == b) > 0.99, (name, np.mean(a == b))
+        else:  # the offset term (128 + z) * sum_k A cancels most of sum_k A (128 + q): an fp32 ulp of
+            # the row sum moves the bf16 output by one ulp now and then (both routes checked below)
+            assert np.mean(a == b) > 0.9, (name, np.mean(a == b))
+            assert_bf16_close(b, a, name)
     # the streamed forms against the oracle
     xs = strm["x"].float().cpu().numpy()
     assert_bf16_close(xs, x0 + bf16(hin @ Wd_.T), "mlp.c_proj resid")
@@ -799,6 +801,135 @@ def test_attention_split_keys(hip, hs, nh, B, T_, S, p0, nsplit):
          nh, hs, S, nsplit, ws.data_ptr(), st())
     torch.cuda.synchronize()
     assert_bf16_close(y.float().cpu().numpy(), _attn_oracle(q, kc, vc, pos, S, T_, nh, hs), "split attention")
+
+
+def _i8_ws_stats(hip, A, M, K):
+    """(SCA (M,), outlier flags (K,) bool) of llj_i8_stats's workspace for the rows A (M, K)."""
+    from lit_llama import _hip
+
+    ws = torch.empty(hip.llj_i8_ws_bytes(M, K), dtype=torch.uint8, device=dev)
+    call(hip, "llj_i8_stats", A.data_ptr(), A.stride(0), M, K, 6.0, ws.data_ptr(), st())
+    torch.cuda.synchronize()
+    raw = ws.cpu().numpy()
+    # i8ws.h layout: header, part[32][M], cnt[32], list[32][kb], sca[M], flag[K] (16-B aligned)
+    kb = ((K + 31) // 32 + 15) & ~15
+    o_sca = 16 + 4 * 32 * M + 4 * 32 + 4 * 32 * kb
+    o_flag = (o_sca + 4 * M + 15) & ~15
+    return raw[o_sca:o_sca + 4 * M].view(np.float32), raw[o_flag:o_flag + K] != 0
+
+
+def _st_decode(st, M, K):
+    w = st.cpu().numpy().view(np.uint32)
+    flags = np.unpackbits(w[16:16 + (K + 31) // 32].view(np.uint8), bitorder="little")[:K] != 0
+    return w[:M].view(np.float32), flags
+
+
+@pytest.mark.parametrize("M", [1, 5, 8])
+@pytest.mark.parametrize("regime", ["none", "few", "many"])
+def test_int8_statistics_handoff(hip, M, regime):
+    """LLM.int8 decode rows without the statistics launches of y and h: llj_attention_i8 and
+    llj_i8_swiglu_stats write the row statistics of their outputs (SCA and outlier columns by
+    order-independent atomics: bitwise the values llj_i8_stats computes) and zero the other block;
+    llj_i8_linear_resid quantizes its bf16 rows per chunk from them and takes the fp16 side product
+    from the streamed weights -- the same int8 codes as the workspace path (only the side product's
+    fp32 order differs) and the oracle's LLM.int8() result. 7B shapes (C 4096, 32 heads, H 11008)."""
+    from lit_llama import _hip
+
+    rng = np.random.default_rng(1300 + 10 * M + len(regime))
+    C, nh, H, S = 4096, 32, 11008, 64
+    hs = C // nh
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+
+    def wq(N, K):
+        W = bf16(rng.standard_normal((N, K)) * 0.02)
+        Wd = T(W, torch.bfloat16)
+        cb = torch.empty(N, K, dtype=torch.int8, device=dev)
+        scb = torch.empty(N, dtype=torch.float32, device=dev)
+        call(hip, "llj_i8_quant_weight", Wd.data_ptr(), 1, cb.data_ptr(), scb.data_ptr(), N, K, st())
+        cbt = torch.empty_like(cb)
+        call(hip, "llj_i8_repack", cb.data_ptr(), cbt.data_ptr(), N, K, st())
+        torch.cuda.synchronize()
+        return O.int8_quantize_weight(W), cbt, scb
+
+    scale = {"none": 0.5, "few": 1.0, "many": 3.0}[regime]
+    # attention over a cache: y rows; v scaled so that y has (regime) outlier columns
+    kc = T(bf16(rng.standard_normal((M, nh, S, hs))), torch.bfloat16)
+    vv = rng.standard_normal((M, nh, S, hs)).astype(np.float32) * scale
+    if regime == "few":
+        vv[:, 3, :, 7] = 9.0  # one y column >= 6 in every row
+    vc = T(bf16(vv), torch.bfloat16)
+    q = T(bf16(rng.standard_normal((M, C))), torch.bfloat16)
+    pos = T(np.array([40], np.int32))
+    y = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    y_st = torch.full((hip.llj_i8_rowstats_bytes(C) // 4,), 0, dtype=torch.int32, device=dev)
+    h_st = torch.full((hip.llj_i8_rowstats_bytes(H) // 4,), 7, dtype=torch.int32, device=dev)  # to be zeroed
+    call(hip, "llj_attention_i8", q.data_ptr(), kc.data_ptr(), vc.data_ptr(), y.data_ptr(), pos.data_ptr(), M, 1, nh,
+         hs, S, 1, None, y_st.data_ptr(), h_st.data_ptr(), h_st.numel(), 6.0, st())
+    torch.cuda.synchronize()
+    assert not h_st.any()
+    y_ref = torch.empty_like(y)
+    call(hip, "llj_attention", q.data_ptr(), kc.data_ptr(), vc.data_ptr(), y_ref.data_ptr(), pos.data_ptr(), M, 1, nh, hs,
+         S, st())
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+    sca_w, fl_w = _i8_ws_stats(hip, y, M, C)
+    sca_s, fl_s = _st_decode(y_st, M, C)
+    np.testing.assert_array_equal(sca_s, sca_w)
+    np.testing.assert_array_equal(fl_s, fl_w)
+    if regime == "few":
+        assert fl_s.any()
+    # c_proj + residual from y's statistics vs the workspace path and the oracle
+    (cbo, scbo), cbod, scbod = wq(C, C)
+    x0 = T(bf16(rng.standard_normal((M, C))), torch.bfloat16)
+    xa, xb = x0.clone(), x0.clone()
+    call(hip, "llj_i8_linear_resid", y.data_ptr(), C, cbod.data_ptr(), scbod.data_ptr(), xa.data_ptr(), C, M, C, C,
+         y_st.data_ptr(), st())
+    ws = torch.empty(hip.llj_i8_ws_bytes(M, H), dtype=torch.uint8, device=dev)
+    call(hip, "llj_i8_stats", y.data_ptr(), C, M, C, 6.0, ws.data_ptr(), st())
+    call(hip, "llj_linear_resid", 2, y.data_ptr(), C, cbod.data_ptr(), scbod.data_ptr(), xb.data_ptr(), C, M, C, C,
+         ws.data_ptr(), 0, None, st())
+    torch.cuda.synchronize()
+    a, b = xa.float().cpu().numpy(), xb.float().cpu().numpy()
+    assert np.mean(a == b) > 0.98, np.mean(a == b)
+    yh = y.float().cpu().numpy()
+    assert_bf16_close(a, x0.float().cpu().numpy() + bf16(O.int8_linear(yh, cbo, scbo)), f"int8 c_proj M={M}")
+    # SwiGLU over normalized rows -> h and its statistics (and y's block zeroed)
+    xn = rng.standard_normal((M, C)).astype(np.float32) * scale
+    if regime == "few":
+        xn[:, [17, 3001]] *= 8.0
+    xn = bf16(xn)
+    xnd = T(xn, torch.bfloat16)
+    call(hip, "llj_i8_stats", xnd.data_ptr(), C, M, C, 6.0, ws.data_ptr(), st())
+    (cb1, scb1), cb1d, scb1d = wq(H, C)
+    (cb2, scb2), cb2d, scb2d = wq(H, C)
+    # larger fc weights in the "many" regime: h with hundreds of outlier columns (the random weights' own)
+    h = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+    h_ref = torch.empty_like(h)
+    call(hip, "llj_i8_swiglu_stats", xnd.data_ptr(), cb1d.data_ptr(), scb1d.data_ptr(), cb2d.data_ptr(), scb2d.data_ptr(),
+         h.data_ptr(), M, H, C, ws.data_ptr(), 0, h_st.data_ptr(), y_st.data_ptr(), y_st.numel(), 6.0, st())
+    call(hip, "llj_norm_swiglu", 2, xnd.data_ptr(), None, 1e-5, cb1d.data_ptr(), scb1d.data_ptr(), cb2d.data_ptr(),
+         scb2d.data_ptr(), h_ref.data_ptr(), M, H, C, ws.data_ptr(), 0, None, None, 0, st())
+    torch.cuda.synchronize()
+    assert torch.equal(h, h_ref)
+    assert not y_st.any()
+    sca_w, fl_w = _i8_ws_stats(hip, h, M, H)
+    sca_s, fl_s = _st_decode(h_st, M, H)
+    np.testing.assert_array_equal(sca_s, sca_w)
+    np.testing.assert_array_equal(fl_s, fl_w)
+    print(f"[int8 hand-off] M={M} {regime}: y outlier columns {int(_st_decode(y_st, M, C)[1].sum())}, "
+          f"h outlier columns {int(fl_s.sum())}")
+    (cbd_, scbd_), cbdd, scbdd = wq(C, H)
+    xa, xb = x0.clone(), x0.clone()
+    call(hip, "llj_i8_linear_resid", h.data_ptr(), H, cbdd.data_ptr(), scbdd.data_ptr(), xa.data_ptr(), C, M, C, H,
+         h_st.data_ptr(), st())
+    call(hip, "llj_i8_stats", h.data_ptr(), H, M, H, 6.0, ws.data_ptr(), st())
+    call(hip, "llj_linear_resid", 2, h.data_ptr(), H, cbdd.data_ptr(), scbdd.data_ptr(), xb.data_ptr(), C, M, C, H,
+         ws.data_ptr(), 0, None, st())
+    torch.cuda.synchronize()
+    a, b = xa.float().cpu().numpy(), xb.float().cpu().numpy()
+    assert np.mean(a == b) > 0.98, np.mean(a == b)
+    hh = h.float().cpu().numpy()
+    assert_bf16_close(a, x0.float().cpu().numpy() + bf16(O.int8_linear(hh, cbd_, scbd_)), f"int8 mlp.c_proj M={M}")
 
 
 @pytest.mark.parametrize("M", [1, 8])

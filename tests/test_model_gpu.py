@@ -162,6 +162,29 @@ def test_batch8_matches_reference_and_single_rows(golden):
         np.testing.assert_array_equal(out[b], single)
 
 
+def test_batch12_rows_equal_single_runs():
+    """Decode batches past the 8-row fused launches run the ops in row slices (8 rows for the fused
+    norm ops, 16 for the plain linears; rmsnorm_rows instead of the statistics hand-off): every row
+    of a batch of 12 equals its own batch-1 run (margin-guarded against the batch-1 logits)."""
+    import generate as G
+
+    cfg = Cfg(block_size=128, n_layer=2, n_head=4, n_embd=256, vocab_size=2048)
+    m = build(cfg, make_params(cfg, 77))
+    rng = np.random.default_rng(77)
+    prompts = rng.integers(3, 2048, (12, 6)).astype(np.int32)
+    steps = 10
+    out = G.generate_batch(m, torch.from_numpy(prompts).cuda(), steps, max_seq_length=24).cpu().numpy()
+    assert out.shape == (12, 6 + steps)
+    for b in range(12):
+        single = gen(m, prompts[b], steps, max_seq_length=24)
+        if not np.array_equal(out[b], single):
+            s = int(np.nonzero(out[b] != single)[0][0])
+            m.reset_cache()
+            lg = teacher_forced(m, single[None], 6, 24)[0]
+            top = np.sort(lg[s - 6])[::-1]
+            assert top[0] - top[1] < 0.05, (b, s, top[0] - top[1])
+
+
 def test_eos_excludes_token(golden):
     g = golden("eos")
     cfg = Cfg(block_size=64, n_layer=1, n_head=4, n_embd=256, vocab_size=512)
