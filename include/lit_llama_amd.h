@@ -60,9 +60,9 @@ int llj_set_tpw_max(int tiles);
 
 /* Host-side switch (no device work): 1 (default) = batched decode rows (2 <= M <= 8) of the
  * int4 / gptq.int8 / bf16 GEMVs stream their activation rows per K chunk (the fused RMSNorm then
- * takes the residual op's handed-over sums of squares, `nstat`); 0 = the LDS-image forms. Same
- * rounding points either way. Returns the previous value. */
-int llj_set_stream_a(int on);
+ * takes the residual op's handed-over sums of squares, `nstat`); 2 = also single rows; 0 = the
+ * LDS-image forms. Same rounding points either way. Returns the previous value. */
+int llj_set_stream_a(int mode);
 
 /* Host-side A/B options (no device work). Each starts from its environment variable (read once, at
  * first use; -1 = unset = the build default) and can be set per process; launches never read the
@@ -72,7 +72,8 @@ int llj_set_stream_a(int on);
  *   LLJ_OPT_FLASH_PAIR     0..1  flash prefill: (long, short) query-block pairs per workgroup (LLJ_FLASH_PAIR)
  *   LLJ_OPT_GEMM_GLDS      0..1  prefill GEMMs: LDS-DMA (1) or register-staged (0) kernel for every format (LLJ_GEMM_GLDS)
  *   LLJ_OPT_GLDS_COST128   0..   LDS-DMA GEMM: cost of a 256 x 128 tile in % of a 256 x 256 one (LLJ_GLDS_COST128)
- *   LLJ_OPT_GEMV_LDS_A_KB  56..96 decode GEMVs: cap of the staged A image in KiB (LLJ_GEMV_LDS_A_KB) */
+ *   LLJ_OPT_GEMV_LDS_A_KB  56..96 decode GEMVs: cap of the staged A image in KiB (LLJ_GEMV_LDS_A_KB)
+ *   LLJ_OPT_ATT_SPEC_BATCH 0..1  decode attention: the half speculative key pass also past 64 blocks (LLJ_ATT_SPEC_BATCH) */
 enum {
   LLJ_OPT_ATT_SPEC_FULL = 0,
   LLJ_OPT_FLASH_QB = 1,
@@ -80,7 +81,8 @@ enum {
   LLJ_OPT_GEMM_GLDS = 3,
   LLJ_OPT_GLDS_COST128 = 4,
   LLJ_OPT_GEMV_LDS_A_KB = 5,
-  LLJ_OPT_COUNT = 6
+  LLJ_OPT_ATT_SPEC_BATCH = 6,
+  LLJ_OPT_COUNT = 7
 };
 int llj_set_option(int which, int value);
 
@@ -198,9 +200,12 @@ int llj_gemm_i8_qkv_rope(const void* x, const void* CB, const void* SCB, const v
                          const int* pos, int B, int T, int C, int n_head, int S, void* stream);
 /* The outlier columns of an activation (its llj_i8_stats workspace) gathered as f16 rows
  * ao16[M][kpad] and of a weight (CB in I8P, SCB) as f16(CB * SCB / 127) rows w16[N][kpad], zero past
- * the outlier count up to a multiple of 64 (kpad >= K rounded up to 64, kpad % 8 == 0): with both
- * passed to llj_gemm_i8_* (else NULL, NULL, 0) the fp16 outlier side product runs as a dense f16
- * GEMM over them (bitsandbytes' fp16 matmul of the outlier sub-matrices). */
+ * the outlier count up to the next multiple of 64: with both passed to llj_gemm_i8_* (else NULL,
+ * NULL, 0) the fp16 outlier side product runs as a dense f16 GEMM over them (bitsandbytes' fp16
+ * matmul of the outlier sub-matrices). kpad is a capacity in columns: kpad % 64 == 0, kpad >= 64,
+ * (80 + kpad) * 4 <= 64 KiB (the gathers' LDS list); it may be smaller than K. When the activation
+ * has more outlier columns than kpad, the gathers write nothing and the GEMM falls back to its
+ * per-tile side product (same results). */
 int llj_i8_gather_act(const void* A, int lda, int M, int K, const void* i8ws, void* ao16, int kpad, void* stream);
 int llj_i8_gather_weight(const void* CB, const void* SCB, int N, int K, const void* i8ws, void* w16, int kpad,
                          void* stream);
@@ -315,10 +320,11 @@ int llj_g_sample(const float* logits, int ldl, int M, int V, float temperature, 
 /* ---------------------------------------------------------------- LLM.int8() decode statistics hand-off
  * Decode rows (M <= 8) of an llm.int8 model skip the statistics launch of the attention output y and
  * of the SwiGLU output h (Linear8bitLt inputs of attn.c_proj / mlp.c_proj, quantization.py:36-75):
- * the producing op writes the LLM.int8 row statistics into a small block -- words [0, 8) SCA[m] =
- * max |f16(A[m, k])| below the threshold (the bits of the float), words [16, 16 + ceil(K / 32)) the
- * outlier columns (any row |f16(A)| >= threshold) as bits -- with order-independent atomics (max / or:
- * the values of llj_i8_stats exactly), and the int8 GEMV quantizes its bf16 rows per K chunk from it,
+ * the producing op writes the LLM.int8 row statistics into a small block -- words [16 + 8 s + m]
+ * (s < 64 slots) partial SCA[m] = max |f16(A[m, k])| below the threshold (the bits of the float;
+ * SCA[m] = the max over the slots), words [528, 528 + ceil(K / 32)) the outlier columns (any row
+ * |f16(A)| >= threshold) as bits -- with order-independent atomics (max / or: the values of
+ * llj_i8_stats exactly), and the int8 GEMV quantizes its bf16 rows per K chunk from it,
  * taking the fp16 outlier side product from the streamed weights. A block must be zero before its
  * producer runs: llj_attention_i8 zeroes the (previous layer's) h block and llj_i8_swiglu_stats the
  * y block, so a decode step leaves both zero. */

@@ -20,17 +20,17 @@ constexpr int attention_lds_floats() {
   return 2 * NWV + NWV * HS;
 }
 
-// LLM.int8() statistics of attention output rows for the int8 c_proj (i8ws.h kI8StFlags): the
-// calling wave holds 64 consecutive output columns col0 .. col0 + 63 of row m (bf16 bits in ob).
-// Row maximum of |f16(y)| below the threshold (atomicMax on the float bits) and the outlier columns
+// LLM.int8() statistics of attention output rows for the int8 c_proj (i8ws.h): the calling wave
+// holds 64 consecutive output columns col0 .. col0 + 63 of row m (bf16 bits in ob). Row maximum of
+// |f16(y)| below the threshold (atomicMax on the float bits, SCA slot `slot`) and the outlier columns
 // (atomicOr); both order-independent.
-__device__ __forceinline__ void i8_emit_stats64(uint32_t* st, float thr, int m, int col0, uint32_t ob) {
+__device__ __forceinline__ void i8_emit_stats64(uint32_t* st, float thr, int m, int col0, uint32_t ob, int slot) {
   const float a16 = fabsf(f16r(bflo(ob)));
   const bool big = a16 >= thr;
   const float mx = wave_max(big ? 0.f : a16);
   const unsigned long long bal = __ballot(big);
   if ((threadIdx.x & 63) == 0) {
-    atomicMax(st + m, __float_as_uint(mx));
+    atomicMax(st + kI8StSca + 8 * (slot % kI8StSlots) + m, __float_as_uint(mx));
     if ((uint32_t)bal) atomicOr(st + kI8StFlags + (col0 >> 5), (uint32_t)bal);
     if ((uint32_t)(bal >> 32)) atomicOr(st + kI8StFlags + (col0 >> 5) + 1, (uint32_t)(bal >> 32));
   }
@@ -61,7 +61,8 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
                                                int h, int m, float* lds, int nsplit = 1,
                                                int split = 0, float* __restrict__ part = nullptr,
                                                uint32_t* __restrict__ st = nullptr, float thr = 0.f,
-                                               uint32_t* __restrict__ clr = nullptr, int clr_words = 0) {
+                                               uint32_t* __restrict__ clr = nullptr, int clr_words = 0,
+                                               bool spec_ok = false) {
   constexpr int DPL = HS / 16;
   constexpr int NG = NTH / 16;
   constexpr int NWV = NTH / 64;
@@ -102,10 +103,11 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   // loaded before the position is known: the cache rows exist whatever p is, and keys past the
   // valid range are masked below, so the position read and the first K/V reads are one memory
   // latency instead of two; the second half waits for the position and reads only valid rows
-  // (a whole speculative pass read 128 rows at p = 80: 1.6x the K/V bytes the step uses). Only
-  // for small grids (bs = 1: 32 blocks), where the launch is latency-bound; with many blocks the
-  // extra rows past p cost more bandwidth than the latency saved (7B bs=8: 1.79 -> 1.87 ms)
-  const bool spec = !PART && gridDim.x * gridDim.y <= 64;
+  // (a whole speculative pass read 128 rows at p = 80: 1.6x the K/V bytes the step uses). spec_ok
+  // (host): small grids (bs = 1: 32 blocks), where the launch is latency-bound, and -- option
+  // LLJ_OPT_ATT_SPEC_BATCH -- half passes at any grid; a whole pass over many blocks read more rows
+  // past p than the latency saved (7B bs=8: 1.79 -> 1.87 ms)
+  const bool spec = !PART && spec_ok;
   if (spec) load_pass(kg, S, kw, vw, 0, SPECU);
   const int ps = pos[t];
   const int nvalid = ps < S ? ps + 1 : S;
@@ -220,7 +222,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
       const size_t eo = (size_t)m * C + h * HS + d;
       st_out32(y + eo, ob | (pr << 16));
     }
-    if (st) i8_emit_stats64(st, thr, m, h * HS + (d & ~63), ob);  // uniform
+    if (st) i8_emit_stats64(st, thr, m, h * HS + (d & ~63), ob, h);  // uniform; one SCA slot per head
   }
   LLJ_STAMP(5);
 }
@@ -246,7 +248,7 @@ __global__ __launch_bounds__(HS) void attention_combine_kernel(const float* __re
   const uint32_t ob = (uint32_t)f2bf(O / L);
   const uint32_t pr = lane_xor1(ob);
   if (!(d & 1)) *reinterpret_cast<uint32_t*>(y + (size_t)m * nh * HS + h * HS + d) = ob | (pr << 16);
-  if (st) i8_emit_stats64(st, thr, m, h * HS + (d & ~63), ob);
+  if (st) i8_emit_stats64(st, thr, m, h * HS + (d & ~63), ob, h);
   if (clr && h == 0 && m == 0)
     for (int i = d; i < clr_words; i += HS) clr[i] = 0u;
 }

@@ -923,6 +923,8 @@ template <int EP>
 static int gemm_run(int wfmt, GemmParams& p, void* stream) {
   if (p.M < 1 || p.N % kGBN || p.K % kGBK || p.K < kGBK || (p.lda & 7)) return LLJ_EINVAL;
   if (EP != GEP_QKV && (!p.C || (p.ldc & 1))) return LLJ_EINVAL;
+  // the int4 / bf16 kernels assume an even count of 64-deep chunks (gemm_body's __builtin_assume)
+  if ((wfmt == GWF_W4 || wfmt == GWF_BF16) && p.K % 128) return LLJ_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   if (wfmt == GWF_W4) {
     if (!p.sz) return LLJ_EINVAL;

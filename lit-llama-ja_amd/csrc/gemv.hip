@@ -49,11 +49,12 @@ int llj_set_tpw_max(int tiles) {
   return old;
 }
 
-// Streamed-A forms of the batched-row GEMVs (2 <= M <= 8; gemv_impl.h AM_STREAM / AM_SNORM) on
-// (1, default) or off (0: the LDS-image forms); returns the previous setting. Host-side only.
-int llj_set_stream_a(int on) {
+// Streamed-A forms of the GEMVs (gemv_impl.h AM_STREAM / AM_SNORM): 1 (default) for batched rows
+// 2 <= M <= 8, 2 for 1 <= M <= 8, 0 off (the LDS-image forms); returns the previous setting.
+// Host-side only.
+int llj_set_stream_a(int mode) {
   const int old = g_stream_a;
-  g_stream_a = on ? 1 : 0;
+  g_stream_a = mode < 0 ? 0 : mode > 2 ? 2 : mode;
   return old;
 }
 

@@ -927,11 +927,13 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
 #endif
   // AM_SNORM: the producer's partial sums of squares, partials q = lane + 64 i (i < kSnQ) of rows
   // 0..7 (two 16-B loads per partial), issued before the weight stream
-  // AM_I8Q: the producer's SCA of rows 0..7 (bits of non-negative floats), before the weight stream
+  // AM_I8Q: the producer's SCA partials of rows 0..7, slot = lane (bits of non-negative floats),
+  // before the weight stream
   float4 isc[I8Q ? 2 : 1];
   if constexpr (I8Q) {
-    isc[0] = *reinterpret_cast<const float4*>(p.i8st);
-    isc[1] = *reinterpret_cast<const float4*>(p.i8st + 4);
+    static_assert(kI8StSlots == 64, "one SCA slot per lane");
+    isc[0] = *reinterpret_cast<const float4*>(p.i8st + kI8StSca + 8 * lane);
+    isc[1] = *reinterpret_cast<const float4*>(p.i8st + kI8StSca + 8 * lane + 4);
   }
   constexpr int kSnQ = 4;
   float4 snv[SNRM ? kSnQ : 1][2];
@@ -970,7 +972,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     }
   }
   if constexpr (I8Q) {
-    const float sv[8] = {isc[0].x, isc[0].y, isc[0].z, isc[0].w, isc[1].x, isc[1].y, isc[1].z, isc[1].w};
+    const float sv[8] = {wave_max(isc[0].x), wave_max(isc[0].y), wave_max(isc[0].z), wave_max(isc[0].w),
+                         wave_max(isc[1].x), wave_max(isc[1].y), wave_max(isc[1].z), wave_max(isc[1].w)};
     const int r0 = lane >> 4, r1i = (lane >> 4) + 4;
     const int m0c = r0 < M ? r0 : M - 1, m1c = r1i < M ? r1i : M - 1;
 #pragma unroll
@@ -1216,7 +1219,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
             const bool big = m < M && a16 >= p.thr;
             i8col |= big;
             const float mx = row16_max(m < M && !big ? a16 : 0.f);
-            if (row == 0 && m < M) atomicMax(p.i8st_out + m, __float_as_uint(mx));
+            if (row == 0 && m < M) atomicMax(p.i8st_out + kI8StSca + 8 * (ntj[j] % kI8StSlots) + m, __float_as_uint(mx));
           }
         }
       }
@@ -1348,8 +1351,8 @@ static inline int pick_tpw(int ntiles, int M) {
 // multi-tile instantiations: nibble-coded weights with the LDS A image or streamed A
 template <int WF, int AM>
 constexpr bool tpw_ok() { return (WF == WF_W4 || WF == WF_W8) && AM != AM_GLOBAL && LLJ_TPW_MAX > 1; }
-// run-time switch of the streamed-A forms for batched rows (llj_set_stream_a, gemv.hip; A/B and
-// equality tests): 1 = on (default)
+// run-time switch of the streamed-A forms (llj_set_stream_a, gemv.hip; A/B and equality tests):
+// 0 off, 1 = rows 2..8 (default), 2 = rows 1..8
 extern int g_stream_a;
 
 // the LDS A image must leave room for the reduction scratch: <= 96 KiB, M <= 8 rows
@@ -1374,7 +1377,7 @@ constexpr int nw_of() { return AM == AM_GLOBAL ? 2 * kNW : kNW; }
 // batched rows (MB > 1, multi-tile workgroups): chunks in flight per wave (r1[D][TPW] registers
 // scale with the tiles per workgroup) and waves per workgroup, tunable apart from the M == 1 forms
 #ifndef LLJ_DM
-#define LLJ_DM LLJ_D1  // single-matrix ops (QKV, lm_head)
+#define LLJ_DM 2  // single-matrix ops (QKV, lm_head): streamed-A 7B bs=8 2 vs 4: 5,047 -> 5,116 tokens/s (6: 4,913)
 #endif
 #ifndef LLJ_DMS
 #define LLJ_DMS 2  // SwiGLU (two matrices): 2 vs 4 at 7B gptq.int4 bs=8 4,341 -> 4,423 tokens/s (3: 4,362)
@@ -1382,9 +1385,12 @@ constexpr int nw_of() { return AM == AM_GLOBAL ? 2 * kNW : kNW; }
 #ifndef LLJ_NWM
 #define LLJ_NWM LLJ_NW
 #endif
+#ifndef LLJ_DRM
+#define LLJ_DRM 4  // residual ops of batched rows: streamed-A 7B bs=8 4 vs 8: 5,047 -> 5,207 tokens/s
+#endif
 template <int EP, int MB = 1>
 constexpr int d_of() {
-  return MB > 1 ? (EP == EP_SWIGLU ? LLJ_DMS : EP == EP_RESID ? LLJ_DR : LLJ_DM)
+  return MB > 1 ? (EP == EP_SWIGLU ? LLJ_DMS : EP == EP_RESID ? LLJ_DRM : LLJ_DM)
                 : (EP == EP_SWIGLU ? kD : EP == EP_RESID ? LLJ_DR : LLJ_D1);
 }
 
@@ -1455,7 +1461,7 @@ static int launch(const GemvParams& p, hipStream_t s) {
 static int pick_am(int wf, const GemvParams& p) {
   if (wf == WF_I8 && p.i8st) return (p.norm_w || p.M > 8) ? -1 : AM_I8Q;  // handed-over row statistics
   if (wf == WF_I8) return (p.norm_w || !p.i8ws || !lds_fits(wf, p.M, p.K)) ? -1 : AM_LDS;
-  if (g_stream_a && p.M >= 2 && p.M <= 8) {
+  if (g_stream_a && p.M >= (g_stream_a >= 2 ? 1 : 2) && p.M <= 8) {
     if (!p.norm_w) return AM_STREAM;
     if (p.nstat && (reinterpret_cast<uintptr_t>(p.nstat) & 15) == 0) return AM_SNORM;
   }

@@ -60,11 +60,16 @@ __host__ __device__ inline I8Layout i8_layout(const void* ws, int M, int K) {
 
 // LLM.int8() row statistics of a decode activation (M <= 8 rows) handed from the op that produces
 // it to the int8 GEMV that consumes it, instead of a statistics launch in between (attention -> y,
-// SwiGLU -> h): words [0, 8) SCA[m] = max |f16(A[m, k])| over the row's elements below the
-// threshold, as the bits of the non-negative float (atomicMax is order-independent, so the value is
-// the prep pass's exactly); words [kI8StFlags, kI8StFlags + ceil(K / 32)) the outlier columns (any
-// row |f16(A)| >= threshold), bit k % 32 of word k / 32 (atomicOr). Zeroed before the producer runs.
-constexpr int kI8StFlags = 16;
+// SwiGLU -> h). Words [kI8StSca, kI8StSca + 8 kI8StSlots): SCA partials -- slot s, row m at
+// kI8StSca + 8 s + m: the max |f16(A[m, k])| below the threshold over the producer workgroups that
+// map to slot s (as the bits of the non-negative float, atomicMax); SCA[m] = max over the slots.
+// Words [kI8StFlags, kI8StFlags + ceil(K / 32)): the outlier columns (any row |f16(A)| >= threshold),
+// bit k % 32 of word k / 32 (atomicOr). Max and or are order-independent, so the values are the
+// statistics launch's exactly; the slots keep the atomics off a few hot addresses (688 SwiGLU
+// workgroups on 8 words took 47 us). Zeroed before the producer runs.
+constexpr int kI8StSca = 16;
+constexpr int kI8StSlots = 64;
+constexpr int kI8StFlags = kI8StSca + 8 * kI8StSlots;
 __host__ __device__ inline int i8st_words(int K) { return kI8StFlags + (K + 31) / 32; }
 
 }  // namespace llj

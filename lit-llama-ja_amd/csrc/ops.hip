@@ -112,6 +112,9 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__
 #ifndef LLJ_ATT_NTH
 #define LLJ_ATT_NTH 512  // threads per (row, head) block
 #endif
+#ifndef LLJ_ATT_SPEC_BATCH
+#define LLJ_ATT_SPEC_BATCH 0  // half speculative pass at any grid size (A/B: option LLJ_OPT_ATT_SPEC_BATCH)
+#endif
 #ifndef LLJ_ATT_U
 #define LLJ_ATT_U 4  // keys per 16-lane group per pass
 #endif
@@ -120,10 +123,10 @@ __global__ __launch_bounds__(NTH) void attention_kernel(const bf16_t* __restrict
                                                         const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                         const int* __restrict__ pos, int T, int S, int nh,
                                                         float scale_log2, uint32_t* st, float thr, uint32_t* clr,
-                                                        int clr_words) {
+                                                        int clr_words, int spec_ok) {
   __shared__ float lds[attention_lds_floats<HS, NTH>()];
   attention_body<HS, U, NTH, false, SPECU>(q, kc, vc, y, pos, T, S, nh, scale_log2, blockIdx.x, blockIdx.y, lds, 1, 0,
-                                           nullptr, st, thr, clr, clr_words);
+                                           nullptr, st, thr, clr, clr_words, spec_ok != 0);
 }
 
 // split-K attention over the keys (long contexts): block (head, row, split) -> partial
@@ -476,11 +479,13 @@ static int attention_run(const void* q, const void* kcache, const void* vcache, 
   // keys loaded before the position is known at small grids: half a pass (default) or a whole one
   // (option LLJ_OPT_ATT_SPEC_FULL: one memory latency less, more K / V rows read past the position)
   const bool full = opt(LLJ_OPT_ATT_SPEC_FULL) == 1;
+  const int sb = opt(LLJ_OPT_ATT_SPEC_BATCH);
+  const int spec_ok = (int)grid.x * (int)grid.y <= 64 || (!full && (sb < 0 ? LLJ_ATT_SPEC_BATCH : sb) != 0);
   hipStream_t st_ = (hipStream_t)stream;
 #define LLJ_ATT_LAUNCH(HS_, SU_)                                                                                   \
   hipLaunchKernelGGL((attention_kernel<HS_, LLJ_ATT_U, LLJ_ATT_NTH, SU_>), grid, dim3(LLJ_ATT_NTH), 0, st_,         \
                      (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2, \
-                     st, thr, clr, clr_words)
+                     st, thr, clr, clr_words, spec_ok)
   if (head_size == 128) {
     if (full) LLJ_ATT_LAUNCH(128, LLJ_ATT_U); else LLJ_ATT_LAUNCH(128, LLJ_ATT_U / 2);
   } else if (head_size == 64) {

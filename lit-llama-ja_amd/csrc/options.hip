@@ -21,6 +21,7 @@ constexpr OptSpec kOpts[LLJ_OPT_COUNT] = {
     {"LLJ_GEMM_GLDS", 0, 1},         // prefill GEMMs (M >= 256): 1 LDS-DMA kernel, 0 register-staged, for every format
     {"LLJ_GLDS_COST128", 0, 100000}, // LDS-DMA GEMM: cost of a 256 x 128 tile in % of a 256 x 256 one
     {"LLJ_GEMV_LDS_A_KB", 56, 96},   // decode GEMVs: cap of the staged A image (KiB)
+    {"LLJ_ATT_SPEC_BATCH", 0, 1},    // decode attention: the half speculative pass also for large grids
 };
 
 int env_value(int i) {

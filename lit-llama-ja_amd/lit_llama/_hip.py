@@ -85,7 +85,8 @@ class HipError(RuntimeError):
 
 
 # llj_set_option indices (include/lit_llama_amd.h LLJ_OPT_*)
-OPT_ATT_SPEC_FULL, OPT_FLASH_QB, OPT_FLASH_PAIR, OPT_GEMM_GLDS, OPT_GLDS_COST128, OPT_GEMV_LDS_A_KB = range(6)
+(OPT_ATT_SPEC_FULL, OPT_FLASH_QB, OPT_FLASH_PAIR, OPT_GEMM_GLDS, OPT_GLDS_COST128, OPT_GEMV_LDS_A_KB,
+ OPT_ATT_SPEC_BATCH) = range(7)
 
 
 def lib() -> ctypes.CDLL:

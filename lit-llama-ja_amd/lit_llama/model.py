@@ -124,6 +124,7 @@ PRE_NORM_MIN_M = 2  # smallest batch that takes the separate launch (measured be
 # up to 8 rows takes the hand-off
 HAND_NORM = True
 HAND_NORM_MAX_M = 8
+HAND_NORM_MIN_M = 2  # 1: single rows too (with llj_set_stream_a(2); A/B)
 
 
 # prefill / no-cache calls with at least this many rows (B * T) run the MFMA-tiled GEMMs
@@ -241,7 +242,7 @@ class _Work:
         self.xn = torch.empty(M, C, dtype=bf, device=device) if (need_i8 or self.pre or gemm) else None
         self.rs = torch.empty(M, dtype=torch.float32, device=device) if self.pre else None
         # norm statistics hand-off (HAND_NORM): partials [C / 16 tiles][16 rows]
-        self.hand = (HAND_NORM and not need_i8 and not gemm and 2 <= M <= HAND_NORM_MAX_M
+        self.hand = (HAND_NORM and not need_i8 and not gemm and HAND_NORM_MIN_M <= M <= HAND_NORM_MAX_M
                      and C % 16 == 0 and C // 16 <= 512)
         self.npart = C // 16
         self.nst = torch.empty(self.npart * 16, dtype=torch.float32, device=device) if self.hand else None

@@ -6,10 +6,11 @@ bench.build_model's synthetic weights, 16-token prompts, max_seq_length 144. The
 single rows), through size-independent properties:
 
 * a captured-graph decode gives bitwise the ids and logits of the same steps launched eagerly;
-* every row of a batch-8 decode is the batch-1 decode of its own prompt (reference generate.py:18-89
-  runs one sequence; a batch is B independent runs): ids equal until the first step whose batch-1
-  top-1 / top-2 logit margin is within the bf16 noise of the two paths, and the logits of the equal
-  steps close;
+* every row of a batch-8 gptq.int4 decode is the batch-1 decode of its own prompt (reference
+  generate.py:18-89 runs one sequence; a batch is B independent runs): ids equal until the first step
+  whose batch-1 top-1 / top-2 logit margin is within the bf16 noise of the two paths, and the logits
+  of the equal steps close (LLM.int8 has batch-wide outlier columns: there the hand-off is checked
+  against the statistics launches instead);
 * logits are finite.
 """
 import numpy as np
@@ -98,15 +99,43 @@ def test_13b_int4_full_depth_graph_equals_eager():
     torch.cuda.empty_cache()
 
 
-def test_7b_llm_int8_full_depth_batch_rows():
+def test_7b_llm_int8_full_depth_handoff_equals_statistics_launches():
+    """C3 (7B llm.int8, batch 8). LLM.int8's outlier columns are those of the whole batch (any row's
+    |f16(A)| >= 6.0: bitsandbytes' rule), so a batch row is NOT its own batch-1 run -- the property
+    here is the hand-off's: decode with the attention / SwiGLU handing y's and h's statistics to the
+    int8 residual GEMVs (model.I8_HANDOFF) gives the same int8 codes as the statistics launches, so
+    the ids equal theirs until a step whose top-2 margin is within the side product's fp32-order
+    noise, with close logits; graph replay equals eager launches bitwise."""
     import bench
+    from lit_llama import model as MD
 
     model = bench.build_model("7B", "llm.int8")
     V = model.config.vocab_size
     p8 = _prompts(8, V, 13)
-    ids8, log8 = _graph_equals_eager(model, p8)
-    # LLM.int8's activation codes flip with the rows' fp32 sums (the int8 path's noise floor is ~2x
-    # the int4 one's)
-    _rows_equal_single(model, p8, ids8, log8, margin_tol=0.1, rel_tol=5e-2)
+    ids_h, log_h = _graph_equals_eager(model, p8)
+    # the hand-off's own logits against the statistics launches': summary for the record
+    old = MD.I8_HANDOFF
+    MD.I8_HANDOFF = False
+    try:
+        ids_w, log_w = _decode(model, p8, use_graph=True)
+    finally:
+        MD.I8_HANDOFF = old
+    assert np.isfinite(log_w).all()
+    rels = [float(np.linalg.norm(log_h[s] - log_w[s]) / np.linalg.norm(log_w[s])) for s in range(STEPS + 1)]
+    print(f"[full depth int8] hand-off vs statistics launches, rel per step: {[round(r, 4) for r in rels]}")
+    for b in range(8):
+        for s in range(STEPS + 1):
+            lh, lw = log_h[s, b], log_w[s, b]
+            rel = np.linalg.norm(lh - lw) / np.linalg.norm(lw)
+            # a one-ulp difference of a bf16 output (the side product's fp32 order) moves an int8
+            # code downstream by a whole quantization step: over 32 layers two valid LLM.int8
+            # evaluations differ by several percent (the 2-layer noise floor is 2.5e-2, DESIGN.md section 4)
+            assert rel < 0.15, (b, s, rel)
+            t = T_PROMPT + s
+            if ids_h[b, t] != ids_w[b, t]:
+                top = np.sort(lw)[::-1]
+                dmax = float(np.abs(lh - lw).max())
+                assert top[0] - top[1] <= max(0.05, 2 * dmax), (b, s, top[0] - top[1], dmax)
+                break
     del model
     torch.cuda.empty_cache()

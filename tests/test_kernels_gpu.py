@@ -325,11 +325,14 @@ def _attn_oracle(q, kc, vc, pos, S, T_, nh, hs):
 @pytest.mark.parametrize("hs,nh,B,T_,S,p0", [(128, 4, 1, 1, 144, 80), (128, 3, 8, 1, 144, 143), (64, 4, 2, 5, 16, 0),
                                             (128, 2, 1, 1, 10, 37), (128, 2, 2, 1, 2048, 2000), (128, 32, 1, 1, 256, 90),
                                             (128, 8, 1, 1, 256, 40)])
-@pytest.mark.parametrize("spec", ["half", "full"])
+@pytest.mark.parametrize("spec", ["half", "full", "batch"])
 def test_attention(hip, hs, nh, B, T_, S, p0, spec):
+    """Decode attention against the oracle; keys loaded before the position is known: a half or a
+    whole pass at small grids, or (batch) the half pass at every grid size."""
     from lit_llama import _hip
 
-    with option(hip, _hip.OPT_ATT_SPEC_FULL, 1 if spec == "full" else 0):  # keys loaded before the position (bs = 1)
+    with option(hip, _hip.OPT_ATT_SPEC_FULL, 1 if spec == "full" else 0), \
+            option(hip, _hip.OPT_ATT_SPEC_BATCH, 1 if spec == "batch" else 0):
         _attention_case(hip, hs, nh, B, T_, S, p0)
 
 
@@ -819,9 +822,12 @@ def _i8_ws_stats(hip, A, M, K):
 
 
 def _st_decode(st, M, K):
+    """(SCA (M,), outlier flags (K,)) of a hand-off statistics block (i8ws.h: 64 SCA slots of 8 rows
+    from word 16, the flag bits from word 16 + 512)."""
     w = st.cpu().numpy().view(np.uint32)
-    flags = np.unpackbits(w[16:16 + (K + 31) // 32].view(np.uint8), bitorder="little")[:K] != 0
-    return w[:M].view(np.float32), flags
+    sca = w[16:16 + 512].view(np.float32).reshape(64, 8).max(0)[:M]
+    flags = np.unpackbits(w[528:528 + (K + 31) // 32].view(np.uint8), bitorder="little")[:K] != 0
+    return sca, flags
 
 
 @pytest.mark.parametrize("M", [1, 5, 8])

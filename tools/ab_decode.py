@@ -6,6 +6,7 @@ weights, so box-to-box and clock drift cancel. Prints one JSON line per (variant
   python tools/ab_decode.py --variants base:ATTN_RESID=0 fused:ATTN_RESID=1 --batch 1 8
 A variant may also name another build of the library (same ABI, e.g. other -D macros):
   python tools/ab_decode.py --variants base d8:LIB=scratch/d8.so
+and the host-side knobs TPW (llj_set_tpw_max) and STREAM (llj_set_stream_a).
 """
 from __future__ import annotations
 
@@ -50,7 +51,7 @@ def main():
     from lit_llama import _hip
 
     default_lib = _hip.LIB_PATH
-    defaults = {k: getattr(MD, k) for _, f in variants for k in f if k not in ("LIB", "TPW")}
+    defaults = {k: getattr(MD, k) for _, f in variants for k in f if k not in ("LIB", "TPW", "STREAM", "SPECB")}
     res = {(n, b): [] for n, _ in variants for b in args.batch}
     for r in range(args.rounds):
         for b in args.batch:
@@ -63,8 +64,10 @@ def main():
                 if _hip.LIB_PATH != lib:  # experiment variant of the library (same ABI)
                     _hip.LIB_PATH, _hip._lib = lib, None
                 _hip.lib().llj_set_tpw_max(int(flags.get("TPW", 4)))
+                _hip.lib().llj_set_stream_a(int(flags.get("STREAM", 1)))
+                _hip.lib().llj_set_option(_hip.OPT_ATT_SPEC_BATCH, int(flags.get("SPECB", -1)))
                 for k, v in flags.items():
-                    if k not in ("LIB", "TPW"):
+                    if k not in ("LIB", "TPW", "STREAM", "SPECB"):
                         setattr(MD, k, v)
                 t = bench.time_decode(model, b, 16, args.max_seq_length, 5, args.steps, 1)
                 ms = t["gpu_seconds"] / args.steps * 1e3

@@ -1,0 +1,86 @@
+// Minimal repro of the rocprofv3 --pmc crash (rc 139 inside hipLaunchKernel) on the batched-row
+// GEMV launches: one GEMV entry point of _lljamd.so called directly (no Python), so the crash can be
+// bisected by argv under `rocprofv3 --pmc FETCH_SIZE -- ./pmc_repro <op> <M> <N> <K>`.
+//   op: i8 (llj_linear, LLM.int8, workspace from llj_i8_stats), i8q (llj_i8_linear_resid),
+//       w4 (llj_linear, int4 W4P), i8swiglu (llj_norm_swiglu wfmt 2)
+// Build: hipcc --offload-arch=gfx950 -O2 pmc_repro.cpp -I../../include -L../../lit-llama-ja_amd/lit_llama
+//        -l:_lljamd.so -Wl,-rpath,'$ORIGIN/../../lit-llama-ja_amd/lit_llama' -o pmc_repro
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "lit_llama_amd.h"
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e = (x);                                                    \
+    if (e != hipSuccess) {                                                 \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      return 2;                                                            \
+    }                                                                      \
+  } while (0)
+
+static void* dev_rand(size_t bytes, unsigned seed, int kind) {
+  std::vector<unsigned char> h(bytes);
+  srand(seed);
+  if (kind == 0) {  // bf16 values around N(0, 1): random sign/mantissa, exponent near 127
+    for (size_t i = 0; i + 1 < bytes; i += 2) {
+      const unsigned short v = (unsigned short)(((rand() & 1) << 15) | ((126 + rand() % 3) << 7) | (rand() & 127));
+      memcpy(&h[i], &v, 2);
+    }
+  } else if (kind == 1) {  // fp32 scales
+    for (size_t i = 0; i + 3 < bytes; i += 4) {
+      const float v = 0.5f + (rand() % 1000) * 1e-3f;
+      memcpy(&h[i], &v, 4);
+    }
+  } else {
+    for (auto& b : h) b = (unsigned char)rand();
+  }
+  void* d = nullptr;
+  if (hipMalloc(&d, bytes) != hipSuccess) return nullptr;
+  hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice);
+  return d;
+}
+
+int main(int argc, char** argv) {
+  const char* op = argc > 1 ? argv[1] : "i8";
+  const int M = argc > 2 ? atoi(argv[2]) : 8, N = argc > 3 ? atoi(argv[3]) : 4096, K = argc > 4 ? atoi(argv[4]) : 4096;
+  const int reps = argc > 5 ? atoi(argv[5]) : 3;
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  void* A = dev_rand((size_t)M * K * 2, 1, 0);
+  void* W = dev_rand((size_t)N * K, 2, 2);
+  void* W2 = dev_rand((size_t)N * K, 3, 2);
+  void* sz = dev_rand((size_t)N * 8, 4, 1);
+  void* x = dev_rand((size_t)M * N * 2, 5, 0);
+  void* C = dev_rand((size_t)M * N * 2, 6, 0);
+  void* ws = nullptr;
+  CK(hipMalloc(&ws, llj_i8_ws_bytes(M, K > N ? K : N)));
+  void* st = nullptr;
+  CK(hipMalloc(&st, llj_i8_rowstats_bytes(K)));
+  CK(hipMemset(st, 0, llj_i8_rowstats_bytes(K)));
+  int rc = 0;
+  for (int r = 0; r < reps && rc == 0; ++r) {
+    if (!strcmp(op, "i8")) {
+      rc = llj_i8_stats(A, K, M, K, 6.f, ws, s);
+      if (!rc) rc = llj_linear(2, A, K, W, sz, nullptr, C, N, M, N, K, ws, 0, nullptr, s);
+    } else if (!strcmp(op, "i8q")) {
+      rc = llj_i8_linear_resid(A, K, W, sz, x, N, M, N, K, st, s);
+    } else if (!strcmp(op, "i8swiglu")) {
+      rc = llj_i8_stats(A, K, M, K, 6.f, ws, s);
+      if (!rc) rc = llj_norm_swiglu(2, A, nullptr, 1e-5f, W, sz, W2, sz, C, M, N, K, ws, 0, nullptr, nullptr, 0, s);
+    } else if (!strcmp(op, "w4")) {
+      rc = llj_linear(0, A, K, W, sz, nullptr, C, N, M, N, K, nullptr, 0, nullptr, s);
+    } else {
+      fprintf(stderr, "unknown op %s\n", op);
+      return 2;
+    }
+    fprintf(stderr, "[pmc_repro] %s M=%d N=%d K=%d rep %d rc %d\n", op, M, N, K, r, rc);
+  }
+  CK(hipStreamSynchronize(s));
+  printf("pmc_repro %s M=%d N=%d K=%d done rc=%d\n", op, M, N, K, rc);
+  return rc;
+}
