@@ -333,11 +333,18 @@ size_t llj_i8_rowstats_bytes(int K);
 int llj_attention_i8(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
                      int n_head, int head_size, int S, int nsplit, void* part_ws, void* y_stats, void* clr,
                      int clr_words, float threshold, void* stream);
-/* llj_norm_swiglu for wfmt 2 (x = the normalized rows of llj_i8_norm_stats, i8ws its workspace) + h's
- * statistics into h_stats; zeroes clr_words words at clr. */
+/* llj_norm_swiglu for wfmt 2 on decode rows x (M <= 8) with x's statistics in exactly one of i8ws
+ * (llj_i8_norm_stats) and x_stats (a hand-off block, llj_i8_norm_rowstats) + h's statistics into
+ * h_stats; zeroes clr_words words at clr. */
 int llj_i8_swiglu_stats(const void* x, const void* CB1, const void* SCB1, const void* CB2, const void* SCB2, void* h,
-                        int M, int H, int K, const void* i8ws, int i8_row0, void* h_stats, void* clr, int clr_words,
-                        float threshold, void* stream);
+                        int M, int H, int K, const void* i8ws, const void* x_stats, void* h_stats, void* clr,
+                        int clr_words, float threshold, void* stream);
+/* llj_i8_norm_stats for M <= 8 rows (norm_w NULL: llj_i8_stats of x) that also writes x's (or the
+ * normalized rows') hand-off block st; any GEMV entry point takes it in place of i8ws with wfmt
+ * 2 | LLJ_WF_I8_ROWSTATS (the rows then quantized per chunk inside the GEMV). */
+#define LLJ_WF_I8_ROWSTATS 0x10000
+int llj_i8_norm_rowstats(const void* x, const void* norm_w, float eps, void* xn, int M, int K, float threshold, void* ws,
+                         void* st, void* stream);
 /* x[M, N] += LLM.int8(A)[M, K] . CB^T (CB in I8P, SCB) with A's statistics `stats` (M <= 8). */
 int llj_i8_linear_resid(const void* A, int lda, const void* CB, const void* SCB, void* x, int ldx, int M, int N, int K,
                         const void* stats, void* stream);

@@ -23,7 +23,12 @@ template <int EP>
 static int run(int wfmt, GemvParams& p, void* stream) {
   // wfmt: weight format in bits [0, 8); WF_W4G carries its group size (in 128-deep chunks) above
   const int wf = wfmt & 0xff;
-  p.gch = wfmt >> 8;
+  p.gch = (wfmt >> 8) & 0xff;
+  if (wf == WF_I8 && (wfmt & LLJ_WF_I8_ROWSTATS)) {  // i8ws is a decode hand-off block (AM_I8Q)
+    if (!p.i8ws) return LLJ_EINVAL;
+    p.i8st = (const uint32_t*)p.i8ws;
+    p.i8ws = nullptr;
+  }
   if (int e = check_shape(wf, p)) return e;
   // norm statistics hand-off: partial sums of squares [npart][16] (row slot = row of the call),
   // written by a residual op, read by the next norm-fused op; at most 16 rows, 2 partials per thread
@@ -142,17 +147,19 @@ int llj_i8_linear_resid(const void* A, int lda, const void* CB, const void* SCB,
   return run<EP_RESID>(WF_I8, p, stream);
 }
 
-// h = silu(xn . CB1^T) * (xn . CB2^T) for LLM.int8 (llj_norm_swiglu, wfmt 2, i8ws from
-// llj_i8_norm_stats) that also writes the LLM.int8 statistics of h (h_stats, zeroed beforehand) and
-// zeroes clr_words words at clr (the attention output's statistics block of the next layer).
+// h = silu(xn . CB1^T) * (xn . CB2^T) for LLM.int8 decode rows -- xn's statistics either in i8ws
+// (llj_i8_norm_stats) or as a hand-off block x_stats (llj_i8_norm_rowstats: rows quantized per chunk,
+// AM_I8Q) -- that also writes the LLM.int8 statistics of h (h_stats, zeroed beforehand) and zeroes
+// clr_words words at clr (the attention output's statistics block of the next layer).
 int llj_i8_swiglu_stats(const void* x, const void* CB1, const void* SCB1, const void* CB2, const void* SCB2, void* h,
-                        int M, int H, int K, const void* i8ws, int i8_row0, void* h_stats, void* clr, int clr_words,
-                        float threshold, void* stream) {
-  if (!h_stats || M > 8 || clr_words < 0 || (clr_words && !clr)) return LLJ_EINVAL;
+                        int M, int H, int K, const void* i8ws, const void* x_stats, void* h_stats, void* clr,
+                        int clr_words, float threshold, void* stream) {
+  if (!i8ws == !x_stats || !h_stats || M > 8 || clr_words < 0 || (clr_words && !clr)) return LLJ_EINVAL;
   GemvParams p{};
   p.A = (const bf16_t*)x; p.lda = K; p.M = M; p.N = H; p.K = K;
   p.W = CB1; p.W2 = CB2; p.sz = (const float2*)SCB1; p.sz2 = (const float2*)SCB2; p.C = (bf16_t*)h; p.ldc = H;
-  p.i8ws = i8ws; p.m0 = i8_row0;
+  p.i8ws = i8ws;  // the statistics launch's workspace (the LDS image of the quantized rows), or
+  p.i8st = (const uint32_t*)x_stats;  // x's hand-off block (rows quantized per chunk)
   p.i8st_out = (uint32_t*)h_stats; p.clr = (uint32_t*)clr; p.clr_words = clr_words; p.thr = threshold;
   return run<EP_SWIGLU>(WF_I8, p, stream);
 }

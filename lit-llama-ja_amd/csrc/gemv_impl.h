@@ -446,7 +446,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   constexpr bool SNRM = (AM == AM_SNORM);
   static_assert(!STRM || (MB == 8 && !I8), "streamed A: batched rows, non-int8 formats");
   constexpr bool I8Q = (AM == AM_I8Q);  // int8 rows quantized per chunk from handed-over statistics
-  static_assert(!I8Q || (I8 && MB == 8 && !DUAL && TPW == 1), "AM_I8Q: int8 single-matrix ops, batched rows");
+  static_assert(!I8Q || (I8 && MB == 8 && TPW == 1), "AM_I8Q: int8, batched rows, one tile per workgroup");
   constexpr bool ASTR = STRM || I8Q;  // bf16 A rows streamed per chunk
   constexpr bool ALDS = (I8 && !I8Q) || (AM != AM_GLOBAL && !STRM && !I8Q);
   // row sums of A for the nibble offset: an extra MFMA against a ones fragment for the global-A
@@ -542,10 +542,13 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   // segment (AM_SNORM); rn0 / rn1 = the RMSNorm rstd of those two rows
   u32x4 sa[ASTR ? D : 1][2], sg[SNRM ? D : 1];
   u32x4 sfl[I8Q ? D : 1];  // AM_I8Q: the chunk's 128 outlier-column bits (the same in every lane)
-  float qi0 = 0.f, qi1 = 0.f, i8scb = 0.f;  // AM_I8Q: 127 / SCA of the lane's two rows; SCB[n] / 127
-  float sd[I8Q ? 8 : 1];  // AM_I8Q: this lane's fp16 side-product partials of rows 0..7 (its column, its k group)
+  float qi0 = 0.f, qi1 = 0.f, i8scb = 0.f, i8scb2 = 0.f;  // AM_I8Q: 127 / SCA of the lane's two rows; SCB[n] / 127
+  // AM_I8Q: this lane's fp16 side-product partials of rows 0..7 (its column, its k group; sd2: c_fc2)
+  float sd[I8Q ? 8 : 1], sd2[I8Q && DUAL ? 8 : 1];
 #pragma unroll
   for (int m = 0; m < (I8Q ? 8 : 1); ++m) sd[m] = 0.f;
+#pragma unroll
+  for (int m = 0; m < (I8Q && DUAL ? 8 : 1); ++m) sd2[m] = 0.f;
   const bf16_t* aptr[2];
   const bf16_t* gptr = p.norm_w + 8 * (lane & 15);
   float rn0 = 1.f, rn1 = 1.f;
@@ -628,16 +631,27 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         any |= (uint32_t)__shfl_xor((int)any, 32, 64);
         any = (uint32_t)uniform((int)any);
         const u32x4 c0 = r1[d][0][0], c1 = r1[d][0][1];
+        auto cbyte = [](const u32x4 cv, int j) {  // int8 code j & 15 of a 16-byte lane block, as float
+          const int wi = (j & 15) >> 2;
+          const uint32_t wd = wi == 0 ? cv[0] : wi == 1 ? cv[1] : wi == 2 ? cv[2] : cv[3];
+          return (float)(int)(int8_t)((wd >> (8 * (j & 3))) & 0xFFu);
+        };
         for (uint32_t rem = any; rem; rem &= rem - 1u) {
           const int j = __builtin_ctz(rem);
           if ((m32 >> j) & 1u) {
-            const int kk = 64 * (j >> 4) + 16 * grp + (j & 15), wi = (j & 15) >> 2;
-            const u32x4 cv = (j >> 4) ? c1 : c0;
-            const uint32_t wd = wi == 0 ? cv[0] : wi == 1 ? cv[1] : wi == 2 ? cv[2] : cv[3];
-            const float cbv = (float)(int)(int8_t)((wd >> (8 * (j & 3))) & 0xFFu);
-            const float w = f16r(cbv * i8scb);
+            const int kk = 64 * (j >> 4) + 16 * grp + (j & 15);
+            const float w = f16r(cbyte((j >> 4) ? c1 : c0, j) * i8scb);
+            float a16[8];
 #pragma unroll
-            for (int m = 0; m < 8; ++m) sd[m] += f16r(bf2f(bslot[m * kSRow + kk])) * w;
+            for (int m = 0; m < 8; ++m) {
+              a16[m] = f16r(bf2f(bslot[m * kSRow + kk]));
+              sd[m] += a16[m] * w;
+            }
+            if constexpr (DUAL) {
+              const float w2 = f16r(cbyte((j >> 4) ? r2[d][0][1] : r2[d][0][0], j) * i8scb2);
+#pragma unroll
+              for (int m = 0; m < 8; ++m) sd2[m] += a16[m] * w2;
+            }
           }
         }
       }
@@ -987,6 +1001,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     for (int m = 1; m < 8; ++m) mine = tid == m ? sv[m] : mine;
     if (tid < 8) sca[tid] = mine;
     i8scb = e_a[0].x / 127.f;
+    if constexpr (DUAL) i8scb2 = e_b[0].x / 127.f;
   }
   // int8: the per-k-block outlier counts the side product starts from, loaded now (one memory
   // latency less in the tail; needed once the stream is done)
@@ -1078,6 +1093,12 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
         if (lane < 16) side[(wave * 8 + m) * 16 + lane] = v;
+        if constexpr (DUAL) {
+          float v2 = sd2[m];
+          v2 += __shfl_xor(v2, 16, 64);
+          v2 += __shfl_xor(v2, 32, 64);
+          if (lane < 16) side[NW * 8 * 16 + (wave * 8 + m) * 16 + lane] = v2;
+        }
       }
     } else if constexpr (I8) {
       i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W), reinterpret_cast<const float*>(p.sz), ntj[0] * 16,
@@ -1400,7 +1421,7 @@ constexpr int d_of() {
 template <int WF, int AM, int EP, int MB, int NW, int TPW>
 static int launch_t(const GemvParams& p, hipStream_t s) {
   const size_t sm = gemv_smem(WF, AM, p.M, p.K, NW, TPW);
-  auto kern = gemv_kernel<WF, AM, EP, NW, AM == AM_I8Q ? LLJ_DI8Q : d_of<EP, MB>(), MB, TPW>;
+  auto kern = gemv_kernel<WF, AM, EP, NW, AM == AM_I8Q ? (EP == EP_SWIGLU ? LLJ_DMS : LLJ_DI8Q) : d_of<EP, MB>(), MB, TPW>;
   static bool attr_set[16] = {};  // per instantiation and device; set before any graph capture
   if (sm > 64 * 1024) {
     int dev = 0;
@@ -1499,11 +1520,7 @@ static int launch_ep(int ep, const GemvParams& p, hipStream_t s) {
 template <int WF>
 static int launch_fmt(int am, int ep, const GemvParams& p, hipStream_t s) {
   if constexpr (WF == WF_I8) {
-    if (am == AM_I8Q) {  // single-matrix ops only
-      if (ep == EP_RESID) return launch<WF_I8, AM_I8Q, EP_RESID>(p, s);
-      if (ep == EP_STORE) return launch<WF_I8, AM_I8Q, EP_STORE>(p, s);
-      return LLJ_EINVAL;
-    }
+    if (am == AM_I8Q) return launch_ep<WF_I8, AM_I8Q>(ep, p, s);
     return launch_ep<WF_I8, AM_LDS>(ep, p, s);
   } else {
     if (am == AM_SNORM) return launch_ep<WF, AM_SNORM>(ep, p, s);

@@ -21,7 +21,9 @@ struct I8WsHeader {
   int mtot, K, nsb, kb;
 };
 
-__host__ __device__ inline int i8_kb(int K) { return ((K + kNSB - 1) / kNSB + 15) & ~15; }
+// k-block width: a multiple of 32, so a block's outlier flags are whole 32-bit words of the
+// hand-off block below
+__host__ __device__ inline int i8_kb(int K) { return ((K + kNSB - 1) / kNSB + 31) & ~31; }
 
 __host__ __device__ inline size_t i8_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 

@@ -224,7 +224,8 @@ template <bool NORM, int VPT>
 __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restrict__ x, int lda,
                                                            const bf16_t* __restrict__ w, float eps,
                                                            bf16_t* __restrict__ xn, int M, int K, float thr,
-                                                           char* __restrict__ ws, int kb) {
+                                                           char* __restrict__ ws, int kb,
+                                                           uint32_t* __restrict__ st = nullptr) {
   constexpr int MR = 8;
   __shared__ int flag[1024];
   __shared__ float red[MR][4];
@@ -335,6 +336,22 @@ __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restr
   }
   if (tid < M) L.part[(size_t)b * M + tid] = __int_as_float(pmax[tid]);
   if (b == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb};
+  if (st) {  // uniform: the decode hand-off block (i8ws.h) for the streamed int8 GEMVs (AM_I8Q)
+    if (b == 0 && tid < 8 * kI8StSlots) {  // SCA in slot 0, the other slots 0
+      const int m = tid;
+      float sca = 0.f;
+      if (m < M) {
+        const int g = m & 3, r = m >> 2;
+        sca = fmaxf(fmaxf(mred[4 * g][r], mred[4 * g + 1][r]), fmaxf(mred[4 * g + 2][r], mred[4 * g + 3][r]));
+      }
+      st[kI8StSca + tid] = __float_as_uint(sca);
+    }
+    for (int wd = tid; 32 * wd < k1 - k0; wd += 1024) {  // this k-block's flag words (kb % 32 == 0)
+      uint32_t bits = 0;
+      for (int j = 0; j < 32 && 32 * wd + j < k1 - k0; ++j) bits |= (uint32_t)(flag[32 * wd + j] != 0) << j;
+      st[kI8StFlags + (k0 >> 5) + wd] = bits;
+    }
+  }
   if (tid < 64) {  // compact the flags into the list, 64 columns per ballot
     int c = 0;
     for (int i0 = 0; i0 < k1 - k0; i0 += 64) {
@@ -521,12 +538,12 @@ __global__ __launch_bounds__(256) void i8_gather_weight_kernel(const int8_t* __r
 // i8_prep_one_kernel for M <= 8, K <= 6 * 2048 (with the norm 4 * 2048), M * (k-block width / 8) <= 1024: returns 0 after the
 // launch (or -hipError), 1 when the shape is outside that envelope (nothing launched)
 static int i8_prep_one(bool norm, const bf16_t* x, int lda, const bf16_t* w, float eps, bf16_t* xn, int M, int K,
-                       float thr, void* ws, void* stream) {
+                       float thr, void* ws, void* stream, uint32_t* st = nullptr) {
   const int kb = i8_kb(K), vpt = (K / 8 + 255) / 256;
   if (M > 8 || vpt > (norm ? 4 : 6) || M * (kb / 8) > 1024 || lda % 8) return 1;
   hipStream_t s = (hipStream_t)stream;
 #define LLJ_P1(N, V) \
-  hipLaunchKernelGGL((i8_prep_one_kernel<N, V>), dim3(kNSB), dim3(1024), 0, s, x, lda, w, eps, xn, M, K, thr, (char*)ws, kb)
+  hipLaunchKernelGGL((i8_prep_one_kernel<N, V>), dim3(kNSB), dim3(1024), 0, s, x, lda, w, eps, xn, M, K, thr, (char*)ws, kb, st)
   if (norm) {
     if (vpt <= 2) LLJ_P1(true, 2); else LLJ_P1(true, 4);
   } else {
@@ -594,6 +611,17 @@ int llj_i8_norm_stats(const void* x, const void* norm_w, float eps, void* xn, in
   hipLaunchKernelGGL(i8_quant_act_kernel, dim3(M), dim3(256), 0, s, (const bf16_t*)xn, K, M, K, (char*)ws);
   LLJ_CHECK_LAUNCH();
   return 0;
+}
+
+// llj_i8_norm_stats for decode rows (M <= 8, one launch) that also writes the decode hand-off block
+// `st` (i8ws.h: SCA in slot 0, the outlier bits) read by the streamed int8 GEMVs (wfmt 2 |
+// LLJ_WF_I8_ROWSTATS). norm_w NULL: statistics of x itself (no norm, xn unused).
+int llj_i8_norm_rowstats(const void* x, const void* norm_w, float eps, void* xn, int M, int K, float threshold, void* ws,
+                         void* st, void* stream) {
+  LLJ_REQUIRE(st && M > 0 && M <= 8 && K > 0 && K % 16 == 0 && i8_kb(K) <= 1024 && (!norm_w || xn));
+  const int e = i8_prep_one(norm_w != nullptr, (const bf16_t*)x, K, (const bf16_t*)norm_w, eps, (bf16_t*)xn, M, K,
+                            threshold, ws, stream, (uint32_t*)st);
+  return e > 0 ? LLJ_EINVAL : -e;  // > 0: outside the one-launch envelope
 }
 
 int llj_i8_gather_act(const void* A, int lda, int M, int K, const void* ws, void* ao16, int kpad, void* stream) {

@@ -59,7 +59,8 @@ SIGNATURES = {
     "llj_set_stream_a": [_I],
     "llj_set_option": [_I, _I],
     "llj_attention_i8": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P],
-    "llj_i8_swiglu_stats": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _I, _F, _P],
+    "llj_i8_swiglu_stats": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _F, _P],
+    "llj_i8_norm_rowstats": [_P, _P, _F, _P, _I, _I, _F, _P, _P, _P],
     "llj_i8_linear_resid": [_P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P],
     "llj_gemm_linear": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
@@ -85,6 +86,7 @@ class HipError(RuntimeError):
 
 
 # llj_set_option indices (include/lit_llama_amd.h LLJ_OPT_*)
+WF_I8_ROWSTATS = 0x10000  # wfmt flag: i8ws is a decode hand-off block (include/lit_llama_amd.h)
 (OPT_ATT_SPEC_FULL, OPT_FLASH_QB, OPT_FLASH_PAIR, OPT_GEMM_GLDS, OPT_GLDS_COST128, OPT_GEMV_LDS_A_KB,
  OPT_ATT_SPEC_BATCH) = range(7)
 

@@ -156,6 +156,11 @@ I8_NORM_STATS_MAX_M = 16
 # for y and h
 I8_HANDOFF = True
 I8S_MAX_M = 8
+# ... and the norm outputs (rms_1 / rms_2 / ln_f rows) quantized per chunk inside the int8 GEMVs from a
+# hand-off block written by their statistics launch (llj_i8_norm_rowstats), instead of the launch's
+# quantized rows staged in LDS: measured slower (7B llm.int8 bs=8: QKV 14.8 -> 19.1 us, C3 2,671 ->
+# 2,436 tokens/s; the 768 / 688 workgroups re-quantize the same rows), so off
+I8_NORM_ROWSTATS = False
 
 # weight formats whose kernels remove the nibble offset with the row sums of A (W4P, W8P)
 _ROWSUM_FMTS = (0, 3)
@@ -256,11 +261,13 @@ class _Work:
         # int8 SwiGLU hand their outputs' LLM.int8 statistics to the int8 c_proj / mlp.c_proj (i8ws.h
         # kI8StFlags blocks, zero at allocation; a step leaves y's zero again)
         self.i8s = False
-        self.y_st = self.h_st = None
+        self.y_st = self.h_st = self.n_st = None
         if need_i8 and not gemm and M <= I8S_MAX_M and I8_HANDOFF:
             L = _hip.lib()
             self.y_st = torch.zeros(L.llj_i8_rowstats_bytes(C) // 4, dtype=torch.int32, device=device)
             self.h_st = torch.zeros(L.llj_i8_rowstats_bytes(H) // 4, dtype=torch.int32, device=device)
+            # the norm outputs' block (rms_1 / rms_2 / ln_f), rewritten whole by llj_i8_norm_rowstats
+            self.n_st = torch.zeros(L.llj_i8_rowstats_bytes(C) // 4, dtype=torch.int32, device=device)
         # split-K attention partials for long caches (llj_attention_split)
         self.nsplit = attn_splits(S)
         self.att_ws = None
@@ -591,7 +598,14 @@ class LLaMA(nn.Module):
             kc, vc = kv[i]
             # 1. rms_1 + c_attn + rope + kv write
             rs = None
-            if fa == 2:
+            if fa == 2 and w.i8s and I8_NORM_ROWSTATS:  # the norm + xn's hand-off block, rows quantized in the GEMV
+                _hip.call("llj_i8_norm_rowstats", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
+                          w.xn.data_ptr(), M, C, Linear8bitLtThreshold, w.i8ws.data_ptr(), w.n_st.data_ptr(), st)
+                _hip.call("llj_norm_qkv_rope", fa | _hip.WF_I8_ROWSTATS, w.xn.data_ptr(), None, blk.rms_1.eps,
+                          wa.data_ptr(), P(sa), w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(),
+                          pos.data_ptr(), B, T, C, nh, S, 0, M, w.n_st.data_ptr(), None, None, 0, st)
+                src = None
+            elif fa == 2:
                 self._i8_norm_prep(w.x, blk.rms_1, w.xn, M, C, w, st)
                 src, nw = w.xn, None
             elif w.hand and i > 0:  # the previous mlp.c_proj handed over the sums of squares
@@ -604,7 +618,7 @@ class LLaMA(nn.Module):
             else:
                 src, nw = w.x, blk.rms_1.scale.data_ptr()
             nst = w.nst if (w.hand and i > 0 and fa != 2) else None
-            for r0 in range(0, M, QKV_ROWS):
+            for r0 in range(0, M if src is not None else 0, QKV_ROWS):
                 r = min(QKV_ROWS, M - r0)
                 _hip.call("llj_norm_qkv_rope", fa, src.data_ptr(), nw, blk.rms_1.eps, wa.data_ptr(), P(sa),
                           w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), B, T, C, nh,
@@ -623,7 +637,11 @@ class LLaMA(nn.Module):
             if f1 != f2:
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")
             rs = None
-            if f1 == 2:
+            if f1 == 2 and w.i8s and I8_NORM_ROWSTATS:
+                _hip.call("llj_i8_norm_rowstats", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
+                          w.xn.data_ptr(), M, C, Linear8bitLtThreshold, w.i8ws.data_ptr(), w.n_st.data_ptr(), st)
+                src, nw, step = w.xn, None, I8_ROWS
+            elif f1 == 2:
                 self._i8_norm_prep(w.x, blk.rms_2, w.xn, M, C, w, st)
                 src, nw, step = w.xn, None, I8_ROWS
             elif w.hand:  # c_proj handed over the sums of squares
@@ -637,9 +655,10 @@ class LLaMA(nn.Module):
                 src, nw, step = w.x, blk.rms_2.scale.data_ptr(), QKV_ROWS
             nst = w.nst if (w.hand and f1 != 2) else None
             if w.i8s and not w.flash:  # h's LLM.int8 statistics from the SwiGLU (clears y's block)
+                ns = I8_NORM_ROWSTATS
                 _hip.call("llj_i8_swiglu_stats", src.data_ptr(), w1.data_ptr(), P(s1), w2.data_ptr(), P(s2),
-                          w.h.data_ptr(), M, H, C, P(w.i8ws), 0, w.h_st.data_ptr(), w.y_st.data_ptr(), w.y_st.numel(),
-                          Linear8bitLtThreshold, st)
+                          w.h.data_ptr(), M, H, C, None if ns else w.i8ws.data_ptr(), w.n_st.data_ptr() if ns else None,
+                          w.h_st.data_ptr(), w.y_st.data_ptr(), w.y_st.numel(), Linear8bitLtThreshold, st)
                 _hip.call("llj_i8_linear_resid", w.h.data_ptr(), H, wd.data_ptr(), P(sd), w.x.data_ptr(), C, M, C, H,
                           w.h_st.data_ptr(), st)
                 continue
@@ -676,6 +695,13 @@ class LLaMA(nn.Module):
             return
         f, W, sz = specs["head"]
         rs = nst = None
+        if f == 2 and w.i8s and I8_NORM_ROWSTATS and x is w.x:  # ln_f + xn's hand-off block
+            xn = w.xn
+            _hip.call("llj_i8_norm_rowstats", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), M, C,
+                      Linear8bitLtThreshold, w.i8ws.data_ptr(), w.n_st.data_ptr(), st)
+            _hip.call("llj_norm_linear", f | _hip.WF_I8_ROWSTATS, xn.data_ptr(), None, ln.eps, W.data_ptr(),
+                      _hip.ptr(sz), out.data_ptr(), out.stride(0), M, V, C, w.n_st.data_ptr(), 0, None, None, 0, st)
+            return
         if f == 2:
             xn = torch.empty_like(x)
             self._i8_norm_prep(x, ln, xn, M, C, w, st)

@@ -737,7 +737,7 @@ def _check_i8_ws(ws, a, M, K, thr=6.0):
     ascending per k-block; SCA = row max of the other elements; aq = round(A16 * 127 / SCA),
     outlier columns 0; part = the per-(k-block, row) maxima."""
     nsb = 32
-    kb = ((K + nsb - 1) // nsb + 15) & ~15
+    kb = ((K + nsb - 1) // nsb + 31) & ~31
     a16 = np.abs(a.astype(np.float16).astype(np.float32))
     out = a16 >= thr
     flag = out.any(0)
@@ -815,7 +815,7 @@ def _i8_ws_stats(hip, A, M, K):
     torch.cuda.synchronize()
     raw = ws.cpu().numpy()
     # i8ws.h layout: header, part[32][M], cnt[32], list[32][kb], sca[M], flag[K] (16-B aligned)
-    kb = ((K + 31) // 32 + 15) & ~15
+    kb = ((K + 31) // 32 + 31) & ~31
     o_sca = 16 + 4 * 32 * M + 4 * 32 + 4 * 32 * kb
     o_flag = (o_sca + 4 * M + 15) & ~15
     return raw[o_sca:o_sca + 4 * M].view(np.float32), raw[o_flag:o_flag + K] != 0
@@ -905,20 +905,37 @@ def test_int8_statistics_handoff(hip, M, regime):
         xn[:, [17, 3001]] *= 8.0
     xn = bf16(xn)
     xnd = T(xn, torch.bfloat16)
+    n_st = torch.full((hip.llj_i8_rowstats_bytes(C) // 4,), 3, dtype=torch.int32, device=dev)  # rewritten whole
+    call(hip, "llj_i8_norm_rowstats", xnd.data_ptr(), None, 1e-5, None, M, C, 6.0, ws.data_ptr(), n_st.data_ptr(), st())
+    torch.cuda.synchronize()
+    sca_w, fl_w = _i8_ws_stats(hip, xnd, M, C)  # (re-runs llj_i8_stats into ws for the workspace path below)
+    sca_s, fl_s = _st_decode(n_st, M, C)
+    np.testing.assert_array_equal(sca_s, sca_w)
+    np.testing.assert_array_equal(fl_s, fl_w)
     call(hip, "llj_i8_stats", xnd.data_ptr(), C, M, C, 6.0, ws.data_ptr(), st())
     (cb1, scb1), cb1d, scb1d = wq(H, C)
     (cb2, scb2), cb2d, scb2d = wq(H, C)
     # larger fc weights in the "many" regime: h with hundreds of outlier columns (the random weights' own)
     h = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
     h_ref = torch.empty_like(h)
+    h_ws = torch.empty_like(h)  # the same with xn's statistics launch workspace (the model's default)
+    h_st2 = torch.zeros_like(h_st)
     call(hip, "llj_i8_swiglu_stats", xnd.data_ptr(), cb1d.data_ptr(), scb1d.data_ptr(), cb2d.data_ptr(), scb2d.data_ptr(),
-         h.data_ptr(), M, H, C, ws.data_ptr(), 0, h_st.data_ptr(), y_st.data_ptr(), y_st.numel(), 6.0, st())
+         h_ws.data_ptr(), M, H, C, ws.data_ptr(), None, h_st2.data_ptr(), None, 0, 6.0, st())
+    call(hip, "llj_i8_swiglu_stats", xnd.data_ptr(), cb1d.data_ptr(), scb1d.data_ptr(), cb2d.data_ptr(), scb2d.data_ptr(),
+         h.data_ptr(), M, H, C, None, n_st.data_ptr(), h_st.data_ptr(), y_st.data_ptr(), y_st.numel(), 6.0, st())
     call(hip, "llj_norm_swiglu", 2, xnd.data_ptr(), None, 1e-5, cb1d.data_ptr(), scb1d.data_ptr(), cb2d.data_ptr(),
          scb2d.data_ptr(), h_ref.data_ptr(), M, H, C, ws.data_ptr(), 0, None, None, 0, st())
     torch.cuda.synchronize()
-    assert torch.equal(h, h_ref)
+    # same int8 codes; the fp16 side product's fp32 order differs (in-stream vs after the stream)
+    assert np.mean(h.float().cpu().numpy() == h_ref.float().cpu().numpy()) > 0.98
+    assert torch.equal(h_ws, h_ref)  # the workspace form is the LDS-image SwiGLU with statistics added
+    for got, want in zip(_st_decode(h_st2, M, H), _i8_ws_stats(hip, h_ws, M, H)):
+        np.testing.assert_array_equal(got, want)
+    hexp = bf16(bf16(O.silu(bf16(O.int8_linear(xn, cb1, scb1)))) * bf16(O.int8_linear(xn, cb2, scb2)))
+    assert_bf16_close(h.float().cpu().numpy(), hexp, f"int8 swiglu (streamed) M={M}", rel=3e-2)
     assert not y_st.any()
-    sca_w, fl_w = _i8_ws_stats(hip, h, M, H)
+    sca_w, fl_w = _i8_ws_stats(hip, h, M, H)  # h's statistics from the streamed SwiGLU's own output
     sca_s, fl_s = _st_decode(h_st, M, H)
     np.testing.assert_array_equal(sca_s, sca_w)
     np.testing.assert_array_equal(fl_s, fl_w)
@@ -936,6 +953,25 @@ def test_int8_statistics_handoff(hip, M, regime):
     assert np.mean(a == b) > 0.98, np.mean(a == b)
     hh = h.float().cpu().numpy()
     assert_bf16_close(a, x0.float().cpu().numpy() + bf16(O.int8_linear(hh, cbd_, scbd_)), f"int8 mlp.c_proj M={M}")
+    # QKV + RoPE + KV write and lm_head-style store on the norm rows' hand-off block (wfmt 2 | ROWSTATS)
+    (cbq, scbq), cbqd, scbqd = wq(3 * C, C)
+    rope = O.build_rope_cache(128, hs)
+    roped = T(rope)
+    qo = torch.zeros(M, C, dtype=torch.bfloat16, device=dev)
+    kq = torch.zeros(M, nh, S, hs, dtype=torch.bfloat16, device=dev)
+    vq = torch.zeros_like(kq)
+    call(hip, "llj_norm_qkv_rope", 2 | _hip.WF_I8_ROWSTATS, xnd.data_ptr(), None, 1e-5, cbqd.data_ptr(), scbqd.data_ptr(),
+         qo.data_ptr(), kq.data_ptr(), vq.data_ptr(), roped.data_ptr(), pos.data_ptr(), M, 1, C, nh, S, 0, M,
+         n_st.data_ptr(), None, None, 0, st())
+    lo = torch.empty(M, 3 * C, dtype=torch.bfloat16, device=dev)
+    call(hip, "llj_norm_linear", 2 | _hip.WF_I8_ROWSTATS, xnd.data_ptr(), None, 1e-5, cbqd.data_ptr(), scbqd.data_ptr(),
+         lo.data_ptr(), 3 * C, M, 3 * C, C, n_st.data_ptr(), 0, None, None, 0, st())
+    torch.cuda.synchronize()
+    qkv = bf16(O.int8_linear(xn, cbq, scbq))
+    assert_bf16_close(lo.float().cpu().numpy(), qkv, f"int8 linear (streamed) M={M}")
+    qe = O.apply_rope(qkv[:, :C].reshape(M, 1, nh, hs), rope[[40]]).reshape(M, C)
+    assert_bf16_close(qo.float().cpu().numpy(), qe, f"int8 q (streamed) M={M}")
+    assert_bf16_close(vq.float().cpu().numpy()[:, :, 40].reshape(M, C), qkv[:, 2 * C:], f"int8 v (streamed) M={M}")
 
 
 @pytest.mark.parametrize("M", [1, 8])
