@@ -2,7 +2,8 @@
 // GEMV launches: one GEMV entry point of _lljamd.so called directly (no Python), so the crash can be
 // bisected by argv under `rocprofv3 --pmc FETCH_SIZE -- ./pmc_repro <op> <M> <N> <K>`.
 //   op: i8 (llj_linear, LLM.int8, workspace from llj_i8_stats), i8q (llj_i8_linear_resid),
-//       w4 (llj_linear, int4 W4P), i8swiglu (llj_norm_swiglu wfmt 2)
+//       w4 (llj_linear, int4 W4P), i8swiglu (llj_norm_swiglu wfmt 2), prep (llj_i8_norm_stats),
+//       qw (llj_i8_quant_weight of an M x K bf16 matrix), gemm_i8 (llj_i8_stats + llj_gemm_i8_linear)
 // Build: hipcc --offload-arch=gfx950 -O2 pmc_repro.cpp -I../../include -L../../lit-llama-ja_amd/lit_llama
 //        -l:_lljamd.so -Wl,-rpath,'$ORIGIN/../../lit-llama-ja_amd/lit_llama' -o pmc_repro
 #include <hip/hip_runtime.h>
@@ -72,6 +73,13 @@ int main(int argc, char** argv) {
     } else if (!strcmp(op, "i8swiglu")) {
       rc = llj_i8_stats(A, K, M, K, 6.f, ws, s);
       if (!rc) rc = llj_norm_swiglu(2, A, nullptr, 1e-5f, W, sz, W2, sz, C, M, N, K, ws, 0, nullptr, nullptr, 0, s);
+    } else if (!strcmp(op, "prep")) {  // RMSNorm + LLM.int8 statistics, one launch (the rms_1 / rms_2 prep)
+      rc = llj_i8_norm_stats(A, x, 1e-5f, C, M, K, 6.f, ws, s);
+    } else if (!strcmp(op, "qw")) {  // weight quantization (model build)
+      rc = llj_i8_quant_weight(A, 1, W, sz, M, K, s);
+    } else if (!strcmp(op, "gemm_i8")) {  // prefill: statistics of M rows + the LLM.int8 GEMM
+      rc = llj_i8_stats(A, K, M, K, 6.f, ws, s);
+      if (!rc) rc = llj_gemm_i8_linear(A, K, W, sz, ws, nullptr, nullptr, 0, C, N, M, N, K, s);
     } else if (!strcmp(op, "w4")) {
       rc = llj_linear(0, A, K, W, sz, nullptr, C, N, M, N, K, nullptr, 0, nullptr, s);
     } else {

@@ -10,7 +10,9 @@ mkdir -p $D $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 PASSES=${PMC_PASSES:-"bs8 c3"}
 run() {  # tag counters bench-args
-  timeout -s KILL 150 rocprofv3 --pmc $2 --output-format csv -d $D -o $1 -- python3 $R/bench.py $3 > $D/$1.log 2>&1
+  local filt=""
+  [ -n "$PMC_REGEX" ] && filt="--kernel-include-regex $PMC_REGEX"  # counters of the matching kernels only
+  timeout -s KILL 150 rocprofv3 --pmc $2 $filt --output-format csv -d $D -o $1 -- python3 $R/bench.py $3 > $D/$1.log 2>&1
   rc=$?
   echo "$1 rc=$rc" | tee -a $R/gpurun_out/${OUT}_status.log
   tail -3 $D/$1.log >> $R/gpurun_out/${OUT}_status.log
