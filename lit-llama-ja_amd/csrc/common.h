@@ -96,7 +96,15 @@ int opt(int which);
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Cross-lane moves inside a DPP row (16 lanes) as one VALU op each, instead of __shfl_xor's
+// A zero in a VGPR that the compiler cannot see through. Added to the index of a load from a
+// wave-uniform address it keeps the value in VGPRs: the compiler moves a uniform value to SGPRs
+// with a readfirstlane right after its load -- a vmcnt wait for that load, and for every load
+// issued before it, at the point of issue (a prefetch that waits for itself).
+__device__ __forceinline__ int vzero() {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}// Cross-lane moves inside a DPP row (16 lanes) as one VALU op each, instead of __shfl_xor's
 // ds_bpermute (an LDS round trip plus a wait).
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {

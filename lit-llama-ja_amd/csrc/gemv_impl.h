@@ -66,10 +66,10 @@ enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2, AM_STREAM = 3, AM_SNORM = 4
 constexpr int kSRow = 136;
 constexpr int kSSlot = 8 * kSRow;
 __host__ __device__ constexpr bool am_stream(int am) { return am == AM_STREAM || am == AM_SNORM; }
-// AM_I8Q per-wave ring slot: the quantized rows (8 x 144 B) then the bf16 rows (8 x kSRow elements,
-// read only for chunks with outlier columns)
+// AM_I8Q per-wave ring slot: the quantized rows (8 x 144 B) then, for chunks with outlier columns,
+// those columns' f16(A) of the 8 rows, column-major (128 x 16 B; only outlier columns written / read)
 constexpr int kQRow = 144;
-constexpr int kQSlotBytes = 8 * kQRow + kSSlot * 2;
+constexpr int kQSlotBytes = 8 * kQRow + 128 * 16;
 enum : int { EP_STORE = 0, EP_RESID = 1, EP_QKV = 2, EP_SWIGLU = 3 };
 
 // int8 activation workspace written by llj_i8_stats (int8.hip): i8ws.h
@@ -422,7 +422,19 @@ struct APre {
 #define LLJ_ABAR 0
 #endif
 #ifndef LLJ_ABL
-#define LLJ_ABL 0  // ablation switches for profiling only (1 no A prologue, 2 no compute, 4 no epilogue)
+#define LLJ_ABL 0  // ablation switches for profiling only (1 no A prologue, 2 no compute, 4 no epilogue, 8 no AM_I8Q side loop)
+#endif
+#ifndef LLJ_I8_SIS
+#define LLJ_I8_SIS 1  // int8 A image: in-stream fp16 side product from the prep's aval table (0: after the stream)
+#endif
+#ifndef LLJ_I8_SIS_E
+#define LLJ_I8_SIS_E 2  // outlier entries per chunk loaded with its weights (a k-block with more: side product after the stream)
+#endif
+#ifndef LLJ_LOADFENCE
+#define LLJ_LOADFENCE 0  // 1: the weight refills stay where the loop issues them (see the main loop)
+#endif
+#ifndef LLJ_ROT
+#define LLJ_ROT 0  // 1: each workgroup starts its chunk walk at a rotation (A/B of HBM access spread)
 #endif
 
 // LDS tail (floats) behind the A image / reduction scratch: [0, 8) per-row RMSNorm rstd (int8:
@@ -544,11 +556,20 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   u32x4 sfl[I8Q ? D : 1];  // AM_I8Q: the chunk's 128 outlier-column bits (the same in every lane)
   float qi0 = 0.f, qi1 = 0.f, i8scb = 0.f, i8scb2 = 0.f;  // AM_I8Q: 127 / SCA of the lane's two rows; SCB[n] / 127
   // AM_I8Q: this lane's fp16 side-product partials of rows 0..7 (its column, its k group; sd2: c_fc2)
-  float sd[I8Q ? 8 : 1], sd2[I8Q && DUAL ? 8 : 1];
+  float sd[I8 ? 8 : 1], sd2[I8 && DUAL ? 8 : 1];
 #pragma unroll
-  for (int m = 0; m < (I8Q ? 8 : 1); ++m) sd[m] = 0.f;
+  for (int m = 0; m < (I8 ? 8 : 1); ++m) sd[m] = 0.f;
 #pragma unroll
-  for (int m = 0; m < (I8Q && DUAL ? 8 : 1); ++m) sd2[m] = 0.f;
+  for (int m = 0; m < (I8 && DUAL ? 8 : 1); ++m) sd2[m] = 0.f;
+  // int8 A image (SIS): the chunk's outlier count and its first LLJ_I8_SIS_E (column, f16(A) rows)
+  // entries of the prep's list / aval table, loaded with the chunk's weights (the workspace layout
+  // from this launch's M and K: valid addresses whatever the header says; used only when `sis`)
+  constexpr bool SIS = I8 && !I8Q && LLJ_I8_SIS && D <= 4;  // (the depth-8 forms: registers)
+  constexpr int SE = SIS ? LLJ_I8_SIS_E : 1;
+  int scn[SIS ? D : 1], sk[SIS ? D : 1][SE];
+  u32x4 sav[SIS ? D : 1][SE];
+  bool sis = false;  // uniform: the workspace carries aval and its k-blocks are the chunks
+  const I8Layout Lp = i8_layout(p.i8ws, SIS ? p.M : 1, SIS ? p.K : 128);
   const bf16_t* aptr[2];
   const bf16_t* gptr = p.norm_w + 8 * (lane & 15);
   float rn0 = 1.f, rn1 = 1.f;
@@ -559,14 +580,31 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       aptr[h] = p.A + (size_t)(rr < M ? rr : M - 1) * p.lda + 8 * (lane & 15);
     }
   }
+  // chunk of the wave's i-th step: its chunks wave, wave + NW, ... in order, or (LLJ_ROT) started at a
+  // per-workgroup rotation so that the workgroups do not all stream the same chunk offsets together
+  const int rot = LLJ_ROT && nmy > 0 ? uniform((int)(blockIdx.x % (unsigned)nmy)) : 0;
+  auto chunk_of = [&](int i) {
+    int ii = i < nmy ? i : nmy - 1;
+    if (LLJ_ROT) ii = ii + rot >= nmy ? ii + rot - nmy : ii + rot;
+    return wave + NW * ii;
+  };
+  const int vz = (I8Q || SIS) ? vzero() : 0;  // uniform side data stays in VGPRs (common.h vzero)
   auto load = [&](int d, int i) {
-    int c = wave + NW * (i < nmy ? i : nmy - 1);
+    int c = chunk_of(i);
     c = c < 0 ? 0 : (c >= KC ? KC - 1 : c);  // always a valid chunk (loads past the end are unused)
     if constexpr (ASTR) {  // the chunk's activation rows first: they arrive before its weights
 #pragma unroll
       for (int h = 0; h < 2; ++h) sa[d][h] = *reinterpret_cast<const u32x4*>(aptr[h] + 128 * c);
       if constexpr (SNRM) sg[d] = *reinterpret_cast<const u32x4*>(gptr + 128 * c);
-      if constexpr (I8Q) sfl[d] = *reinterpret_cast<const u32x4*>(p.i8st + kI8StFlags + 4 * c);
+      if constexpr (I8Q) sfl[d] = *reinterpret_cast<const u32x4*>(p.i8st + kI8StFlags + 4 * c + vz);
+    }
+    if constexpr (SIS) {
+      scn[d] = Lp.cnt[(c < kNSB ? c : kNSB - 1) + vz];
+#pragma unroll
+      for (int e = 0; e < SE; ++e) {
+        sk[d][e] = Lp.list[128 * c + e + vz];
+        sav[d][e] = __builtin_bit_cast(u32x4, Lp.aval[128 * c + e + vz]);
+      }
     }
     if constexpr (GRP) {
       const size_t go = (size_t)(c / p.gch) * p.N + row;
@@ -590,7 +628,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     }
   };
   auto compute = [&](int d, int i) {
-    const int c = wave + NW * i;
+    const int c = chunk_of(i);
     if constexpr ((LLJ_ABL & 2) != 0) {  // ablation: loads only
 #pragma unroll
       for (int j = 0; j < TPW; ++j) {
@@ -617,43 +655,116 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       const uint32_t fb = (pick(seg >> 2) >> (8 * (seg & 3))) & 0xFFu;
       *reinterpret_cast<uint2*>(qslot + (lane >> 4) * kQRow + 8 * seg) = quant8f(sa[d][0], fb, qi0);
       *reinterpret_cast<uint2*>(qslot + ((lane >> 4) + 4) * kQRow + 8 * seg) = quant8f(sa[d][1], fb, qi1);
+      bool continue_side = true;  // (LLJ_ABL & 8: timing ablation without the side loop)
       if ((fw[0] | fw[1] | fw[2] | fw[3]) != 0u) {  // uniform: the chunk has outlier columns
         // fp16 side product from the weight registers: lane (column n, k group g) holds CB[n, k] of
-        // k = 64 t + 16 g + j (t = 0, 1; j < 16) of the chunk; f16(A) of all rows from the bf16 slot
-        bf16_t* bslot = reinterpret_cast<bf16_t*>(qslot + 8 * kQRow);
-        *reinterpret_cast<u32x4*>(bslot + (lane >> 4) * kSRow + 8 * seg) = sa[d][0];
-        *reinterpret_cast<u32x4*>(bslot + ((lane >> 4) + 4) * kSRow + 8 * seg) = sa[d][1];
+        // k = 64 t + 16 g + j (t = 0, 1; j < 16) of the chunk. The outlier columns' f16(A) of all 8
+        // rows go to a column-major table in the slot (16 B per column: one read per column), each
+        // lane writing the outlier columns of its own two row segments
+        _Float16* ocol = reinterpret_cast<_Float16*>(qslot + 8 * kQRow);
+        // Registers a loop reads are pinned first (an empty asm that "writes" them): a loop reading
+        // a register its load is still filling gets a vmcnt(0) inside it -- which also waits for
+        // the weight prefetch of the next chunks (measured: the down projection's side product
+        // cost 7 us of 24 with it)
+        u32x4 p0 = sa[d][0], p1 = sa[d][1];
+        asm volatile("" : "+v"(p0), "+v"(p1));
+        for (uint32_t rb = fb; rb; rb &= rb - 1u) {  // divergent, usually no or one column
+          const int e = __builtin_ctz(rb), kc = 8 * seg + e;
+          const uint32_t w0 = p0[e >> 1], w1 = p1[e >> 1];
+          ocol[8 * kc + (lane >> 4)] = (_Float16)((e & 1) ? bfhi(w0) : bflo(w0));
+          ocol[8 * kc + (lane >> 4) + 4] = (_Float16)((e & 1) ? bfhi(w1) : bflo(w1));
+        }
         const uint32_t m32 = ((pick(grp >> 1) >> (16 * (grp & 1))) & 0xFFFFu) |
                              (((pick(2 + (grp >> 1)) >> (16 * (grp & 1))) & 0xFFFFu) << 16);
-        // columns j of any k group's range, in a uniform (not unrolled) loop over the set bits
-        uint32_t any = m32;
-        any |= (uint32_t)__shfl_xor((int)any, 16, 64);
-        any |= (uint32_t)__shfl_xor((int)any, 32, 64);
-        any = (uint32_t)uniform((int)any);
-        const u32x4 c0 = r1[d][0][0], c1 = r1[d][0][1];
-        auto cbyte = [](const u32x4 cv, int j) {  // int8 code j & 15 of a 16-byte lane block, as float
-          const int wi = (j & 15) >> 2;
-          const uint32_t wd = wi == 0 ? cv[0] : wi == 1 ? cv[1] : wi == 2 ? cv[2] : cv[3];
+        if constexpr ((LLJ_ABL & 8) != 0) continue_side = false;
+        // each k group walks its own outlier columns (ascending j: the per-lane order of a walk over
+        // the union); trip count = the most any group holds in this chunk (uniform, from the words),
+        // two columns per trip so that their table reads share one LDS latency
+        auto pc16 = [](uint32_t v, int h) { return __builtin_popcount((v >> (16 * h)) & 0xFFFFu); };
+        const int niter = continue_side ? uniform(max(max(pc16(fw[0], 0) + pc16(fw[2], 0), pc16(fw[0], 1) + pc16(fw[2], 1)),
+                                                      max(pc16(fw[1], 0) + pc16(fw[3], 0), pc16(fw[1], 1) + pc16(fw[3], 1))))
+                                        : 0;
+        u32x4 c0 = r1[d][0][0], c1 = r1[d][0][1];
+        u32x4 e0 = DUAL ? r2[d][0][0] : c0, e1 = DUAL ? r2[d][0][1] : c1;
+        asm volatile("" : "+v"(c0), "+v"(c1));  // pinned before the loop (see above)
+        if constexpr (DUAL) asm volatile("" : "+v"(e0), "+v"(e1));
+        auto cbyte = [](const u32x4 lo, const u32x4 hi, int j) {  // int8 code j (0..31, per lane) as float
+          const int wi = j >> 2;
+          uint32_t wd = lo[0];
+          wd = wi == 1 ? lo[1] : wd;
+          wd = wi == 2 ? lo[2] : wd;
+          wd = wi == 3 ? lo[3] : wd;
+          wd = wi == 4 ? hi[0] : wd;
+          wd = wi == 5 ? hi[1] : wd;
+          wd = wi == 6 ? hi[2] : wd;
+          wd = wi == 7 ? hi[3] : wd;
           return (float)(int)(int8_t)((wd >> (8 * (j & 3))) & 0xFFu);
         };
-        for (uint32_t rem = any; rem; rem &= rem - 1u) {
-          const int j = __builtin_ctz(rem);
-          if ((m32 >> j) & 1u) {
-            const int kk = 64 * (j >> 4) + 16 * grp + (j & 15);
-            const float w = f16r(cbyte((j >> 4) ? c1 : c0, j) * i8scb);
+        auto kk_of = [&](int jb) { return 64 * (jb >> 4) + 16 * grp + (jb & 15); };
+        uint32_t rem = m32;
+        for (int it = 0; it < niter; it += 2) {
+          const bool v0 = rem != 0u;
+          const int j0 = v0 ? __builtin_ctz(rem) : 0;
+          rem &= rem - 1u;
+          const bool v1 = rem != 0u;
+          const int j1 = v1 ? __builtin_ctz(rem) : 0;
+          rem &= rem - 1u;
+          // f16(A) of rows 0..7 of both columns (a lane without a column reads a valid slot, unused)
+          const u32x4 ov0 = *reinterpret_cast<const u32x4*>(ocol + 8 * kk_of(j0));
+          const u32x4 ov1 = *reinterpret_cast<const u32x4*>(ocol + 8 * kk_of(j1));
+          auto acc_col = [&](int jb, const u32x4 ov) {
+            const float w = f16r(cbyte(c0, c1, jb) * i8scb);
             float a16[8];
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
-              a16[m] = f16r(bf2f(bslot[m * kSRow + kk]));
+              a16[m] = (float)__builtin_bit_cast(_Float16, (uint16_t)((ov[m >> 1] >> (16 * (m & 1))) & 0xFFFFu));
               sd[m] += a16[m] * w;
             }
             if constexpr (DUAL) {
-              const float w2 = f16r(cbyte((j >> 4) ? r2[d][0][1] : r2[d][0][0], j) * i8scb2);
+              const float w2 = f16r(cbyte(e0, e1, jb) * i8scb2);
+#pragma unroll
+              for (int m = 0; m < 8; ++m) sd2[m] += a16[m] * w2;
+            }
+          };
+          if (v0) acc_col(j0, ov0);
+          if (v1) acc_col(j1, ov1);
+        }
+      }
+    }
+    if constexpr (SIS) {
+      if (sis) {  // uniform
+        const int n = uniform(scn[d]);
+        u32x4 c0 = r1[d][0][0], c1 = r1[d][0][1];
+        u32x4 e0 = DUAL ? r2[d][0][0] : c0, e1 = DUAL ? r2[d][0][1] : c1;
+        if (n > 0) {  // pinned before the loops (see the AM_I8Q side product)
+          asm volatile("" : "+v"(c0), "+v"(c1));
+          if constexpr (DUAL) asm volatile("" : "+v"(e0), "+v"(e1));
+        }
+        auto side_col = [&](int k, const u32x4 ov) {  // one outlier column k of this chunk (uniform)
+          const int kk = k - 128 * c, t = kk >> 6;
+          if (((kk >> 4) & 3) == grp) {  // the lanes holding CB[n, k]
+            const int jj = kk & 15, wi = jj >> 2;
+            const u32x4 cv = t ? c1 : c0;
+            const uint32_t wd = wi == 0 ? cv[0] : wi == 1 ? cv[1] : wi == 2 ? cv[2] : cv[3];
+            const float w = f16r((float)(int)(int8_t)((wd >> (8 * (jj & 3))) & 0xFFu) * i8scb);
+            float a16[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+              a16[m] = (float)__builtin_bit_cast(_Float16, (uint16_t)((ov[m >> 1] >> (16 * (m & 1))) & 0xFFFFu));
+              sd[m] += a16[m] * w;
+            }
+            if constexpr (DUAL) {
+              const u32x4 cv2 = t ? e1 : e0;
+              const uint32_t wd2 = wi == 0 ? cv2[0] : wi == 1 ? cv2[1] : wi == 2 ? cv2[2] : cv2[3];
+              const float w2 = f16r((float)(int)(int8_t)((wd2 >> (8 * (jj & 3))) & 0xFFu) * i8scb2);
 #pragma unroll
               for (int m = 0; m < 8; ++m) sd2[m] += a16[m] * w2;
             }
           }
-        }
+        };
+#pragma unroll
+        for (int e = 0; e < SE; ++e)  // every chunk has at most SE (the prologue's condition for sis)
+          if (e < n) side_col(uniform(sk[d][e]), sav[d][e]);
       }
     }
     if constexpr (STRM) {
@@ -679,6 +790,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
           acc[j] = mfma_bf16(a, dequant_w4(r1[d][j][0][t], msk, mag), acc[j]);
           if (DUAL) acc2[j] = mfma_bf16(a, dequant_w4(r2[d][j][0][t], msk, mag), acc2[j]);
         }
+        // (a uniform branch per step; the unconditional form with a zero fragment measured slower:
+        // without the block boundaries the compiler sank the refills to the loop end, 5,243 -> 4,821
+        // tokens/s at bs=8, profiles/r05_ab_bs8.jsonl)
         if (SACC && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);  // else: row sums from the prologue / caller
       } else if constexpr (GRP) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
@@ -1010,6 +1124,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
     const I8Layout L8 = i8_layout(p.i8ws, h.mtot, h.K);
     i8cnt = L8.cnt[lane < kNSB ? lane : 0];
+    if constexpr (SIS) {
+      // in-stream only when every chunk's outlier columns are among its prefetched entries (no
+      // load inside a loop in the stream: that would wait for the weight prefetch); else after it
+      const float most = wave_max((float)(lane < h.nsb ? i8cnt : 0));
+      sis = h.kb == 128 && h.mtot == M && h.K == p.K && p.m0 == 0 && M <= 8 && L8.avh[0] == 1 && most <= (float)SE;
+      i8scb = e_a[0].x / 127.f;
+      if constexpr (DUAL) i8scb2 = e_b[0].x / 127.f;
+    }
     constexpr int SPC = kSpE<NW> * NT / kNSB;
 #pragma unroll
     for (int e = 0; e < kSpE<NW>; ++e) {
@@ -1061,18 +1183,23 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   // chunk i lives in buffer i % D; after computing it the buffer is refilled with chunk i + D.
   // The steady loop runs while every refill is a real chunk; the peeled tail (< 2D chunks)
   // issues no loads past the last chunk, so nothing is in flight when the epilogue waits.
+  // LLJ_LOADFENCE: an empty asm with a memory clobber after each refill keeps the compiler from
+  // sinking the refills to the end of the unrolled loop body (it did, for register pressure: then
+  // every D-chunk round started with a full memory latency exposed)
   int i0 = 0;
   for (; i0 + 2 * D <= nmy; i0 += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       compute(d, i0 + d);
       load(d, i0 + d + D);
+      if constexpr (LLJ_LOADFENCE != 0) asm volatile("" ::: "memory");
     }
   }
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     if (i0 + d < nmy) compute(d, i0 + d);
     if (i0 + d + D < nmy) load(d, i0 + d + D);
+    if constexpr (LLJ_LOADFENCE != 0) asm volatile("" ::: "memory");
   }
 #pragma unroll
   for (int d = 0; d < D; ++d)
@@ -1086,7 +1213,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   float* side = reinterpret_cast<float*>(smem + kRedBytes);
   if (NW > 1) {
     if (ALDS || ASTR) __syncthreads();  // every wave is done reading the A image / ring it aliases
-    if constexpr (I8Q) {  // the in-stream side partials: sum the 4 k groups, one partial per (wave, row, column)
+    auto side_partials = [&]() {  // the in-stream side partials: sum the 4 k groups, one per (wave, row, column)
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         float v = sd[m];
@@ -1100,12 +1227,19 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
           if (lane < 16) side[NW * 8 * 16 + (wave * 8 + m) * 16 + lane] = v2;
         }
       }
+    };
+    if constexpr (I8Q) {
+      side_partials();
     } else if constexpr (I8) {
-      i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W), reinterpret_cast<const float*>(p.sz), ntj[0] * 16,
-                       side, smem, i8cnt, i8spk);
-      if (DUAL)
-        i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W2), reinterpret_cast<const float*>(p.sz2),
-                         ntj[0] * 16, side + NW * 8 * 16, smem, i8cnt, i8spk);
+      if (sis) {  // uniform (SIS)
+        side_partials();
+      } else {
+        i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W), reinterpret_cast<const float*>(p.sz), ntj[0] * 16,
+                         side, smem, i8cnt, i8spk);
+        if (DUAL)
+          i8_side_tile<NW>(p, reinterpret_cast<const int8_t*>(p.W2), reinterpret_cast<const float*>(p.sz2),
+                           ntj[0] * 16, side + NW * 8 * 16, smem, i8cnt, i8spk);
+      }
     }
     if constexpr (I8) {
       int* mine = reinterpret_cast<int*>(red) + (size_t)(wave * 64 + lane) * NV;
@@ -1406,6 +1540,9 @@ constexpr int nw_of() { return AM == AM_GLOBAL ? 2 * kNW : kNW; }
 #ifndef LLJ_NWM
 #define LLJ_NWM LLJ_NW
 #endif
+#ifndef LLJ_NWS
+#define LLJ_NWS LLJ_NWM  // waves per workgroup of the batched-row SwiGLU (A/B)
+#endif
 #ifndef LLJ_DRM
 #define LLJ_DRM 4  // residual ops of batched rows: streamed-A 7B bs=8 4 vs 8: 5,047 -> 5,207 tokens/s
 #endif
@@ -1459,6 +1596,7 @@ static int launch(const GemvParams& p, hipStream_t s) {
   if constexpr (am_stream(AM) || AM == AM_I8Q) {  // batched rows only (M <= 8)
     if constexpr (EP == EP_RESID && LLJ_NWR != kNW)
       if (p.K >= LLJ_NWR_KMIN) return launch_mb<WF, AM, EP, 8, LLJ_NWR>(p, s);
+    if constexpr (EP == EP_SWIGLU && LLJ_NWS != LLJ_NWM) return launch_mb<WF, AM, EP, 8, LLJ_NWS>(p, s);
     return launch_mb<WF, AM, EP, 8, LLJ_NWM>(p, s);
   } else {
   // the register-staged prologue has an M == 1 class (bs = 1 decode) and an M <= 8 class

@@ -7,6 +7,9 @@
 //   sca[M]         SCA[m] = max over the k-blocks of part
 //   flag[K]        1 for an outlier column
 //   aq[M][K]       the activation quantized once: round(A16 * 127 / SCA), outlier columns 0
+//   avh[4]         avh[0] = 1 when aval below is valid (the one-launch decode prep, M <= 8), else 0
+//   aval[nsb][kb]  f16(A) of rows 0..7 of each listed outlier column (16 B, list order; rows >= M 0):
+//                  the int8 GEMV's in-stream fp16 side product reads them with the chunk's weights
 // Quantizing once here (instead of in every GEMV workgroup) is what keeps the batched int8
 // GEMV weight-streaming.
 #pragma once
@@ -29,7 +32,7 @@ __host__ __device__ inline size_t i8_align16(size_t x) { return (x + 15) & ~(siz
 
 // byte offsets of the arrays (the layout above)
 struct I8Offsets {
-  size_t part, cnt, list, sca, flag, aq, total;
+  size_t part, cnt, list, sca, flag, aq, avh, aval, total;
 };
 __host__ __device__ inline I8Offsets i8_offsets(int M, int K) {
   I8Offsets o;
@@ -39,7 +42,9 @@ __host__ __device__ inline I8Offsets i8_offsets(int M, int K) {
   o.sca = o.list + sizeof(int) * (size_t)kNSB * i8_kb(K);
   o.flag = i8_align16(o.sca + sizeof(float) * (size_t)M);
   o.aq = i8_align16(o.flag + (size_t)K);
-  o.total = o.aq + (size_t)M * K;
+  o.avh = i8_align16(o.aq + (size_t)M * K);
+  o.aval = o.avh + 16;
+  o.total = o.aval + (size_t)16 * kNSB * i8_kb(K);
   return o;
 }
 
@@ -50,6 +55,8 @@ struct I8Layout {
   float* sca;
   uint8_t* flag;  // flag[k] = 1 for an outlier column
   int8_t* aq;
+  int* avh;
+  uint4* aval;
 };
 
 __host__ __device__ inline I8Layout i8_layout(const void* ws, int M, int K) {
@@ -57,7 +64,8 @@ __host__ __device__ inline I8Layout i8_layout(const void* ws, int M, int K) {
   const I8Offsets o = i8_offsets(M, K);
   return I8Layout{reinterpret_cast<float*>(b + o.part), reinterpret_cast<int*>(b + o.cnt),
                   reinterpret_cast<int*>(b + o.list), reinterpret_cast<float*>(b + o.sca),
-                  reinterpret_cast<uint8_t*>(b + o.flag), reinterpret_cast<int8_t*>(b + o.aq)};
+                  reinterpret_cast<uint8_t*>(b + o.flag), reinterpret_cast<int8_t*>(b + o.aq),
+                  reinterpret_cast<int*>(b + o.avh), reinterpret_cast<uint4*>(b + o.aval)};
 }
 
 // LLM.int8() row statistics of a decode activation (M <= 8 rows) handed from the op that produces

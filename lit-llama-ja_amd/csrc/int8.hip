@@ -22,7 +22,7 @@ __global__ __launch_bounds__(256) void i8_stats_kernel(const bf16_t* __restrict_
   __shared__ int flag[1024];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const I8Layout L = i8_layout(ws, M, K);
-  if (b == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb};
+  if (b == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb}, L.avh[0] = 0;  // no aval
   const int k0 = b * kb;
   const int k1 = min(K, k0 + kb);
   for (int i = tid; i < kb; i += 256) flag[i] = 0;
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void i8_stats_rows_kernel(const bf16_t* __rest
                                                             float thr, char* __restrict__ ws, int kb) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const I8Layout L = i8_layout(ws, M, K);
-  if (b == 0 && blockIdx.y == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb};
+  if (b == 0 && blockIdx.y == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb}, L.avh[0] = 0;  // no aval
   const int k0 = b * kb, k1 = min(K, k0 + kb);
   const int nv = k1 > k0 ? (k1 - k0) >> 3 : 0;
   const bool act = lane < nv;
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void i8_norm_stats_kernel(const bf16_t* __rest
   __shared__ int rmax[MR];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const I8Layout L = i8_layout(ws, M, K);
-  if (b == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb};
+  if (b == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb}, L.avh[0] = 0;  // no aval
   const int k0 = b * kb;
   const int k1 = min(K, k0 + kb);
   const int nvec = K >> 3;
@@ -220,6 +220,9 @@ __device__ __forceinline__ uint2 quant8(uint4 x, uint2 fl, float inv) {
 // elements below the threshold itself (redundant across blocks, no grid-wide dependency); then it
 // finishes its own k-block: outlier flags, the list, part, the normalized rows (xn) and the
 // quantized rows (aq). Block 0 writes the header and SCA.
+#ifndef LLJ_PREP_ABL
+#define LLJ_PREP_ABL 0  // timing ablations only (results wrong): 1 no sums of squares, 2 no row maxima, 4 no row loads, 8 no list
+#endif
 template <bool NORM, int VPT>
 __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restrict__ x, int lda,
                                                            const bf16_t* __restrict__ w, float eps,
@@ -232,6 +235,7 @@ __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restr
   __shared__ float rr[MR];
   __shared__ float mred[16][MR];
   __shared__ int pmax[MR];
+  __shared__ uint4 vals[MR][1024 / 8];  // the own k-block's (normalized) rows, for aval
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int grp = tid >> 8, lt = tid & 255, gw = lt >> 6;  // row group, thread / wave within it
   const I8Layout L = i8_layout(ws, M, K);
@@ -244,14 +248,16 @@ __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restr
   const uint4 oa = reinterpret_cast<const uint4*>(x + (size_t)om * lda)[ov];
   uint4 og = oa;
   if (NORM) og = reinterpret_cast<const uint4*>(w)[ov];
-  // rows grp and grp + 4, vectors lt + 256 j
+  // rows grp and grp + 4, vectors lt + 256 j (past the row: zeros, which add nothing to either pass)
   uint4 xa[2][VPT], ga[VPT];
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
-      const int m = grp + 4 * r < M ? grp + 4 * r : M - 1, v = lt + 256 * j < nvec ? lt + 256 * j : nvec - 1;
-      xa[r][j] = reinterpret_cast<const uint4*>(x + (size_t)m * lda)[v];
+      const bool ok = lt + 256 * j < nvec;
+      const int m = grp + 4 * r < M ? grp + 4 * r : M - 1, v = ok ? lt + 256 * j : nvec - 1;
+      const uint4 t = (LLJ_PREP_ABL & 4) ? oa : reinterpret_cast<const uint4*>(x + (size_t)m * lda)[v];
+      xa[r][j] = ok ? t : make_uint4(0u, 0u, 0u, 0u);
     }
   if (NORM) {
 #pragma unroll
@@ -259,16 +265,17 @@ __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restr
   }
   for (int i = tid; i < kb; i += 1024) flag[i] = 0;
   if (tid < MR) pmax[tid] = 0;
-  if (NORM) {
+  if (NORM && !(LLJ_PREP_ABL & 1)) {
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       float a = 0.f;
 #pragma unroll
       for (int j = 0; j < VPT; ++j) {
-        if (lt + 256 * j < nvec) {
-          const uint32_t aw[4] = {xa[r][j].x, xa[r][j].y, xa[r][j].z, xa[r][j].w};
+        const uint32_t aw[4] = {xa[r][j].x, xa[r][j].y, xa[r][j].z, xa[r][j].w};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) a += round_bf(bflo(aw[i]) * bflo(aw[i])) + round_bf(bfhi(aw[i]) * bfhi(aw[i]));
+        for (int i = 0; i < 4; ++i) {  // a += bf16(lo * lo) + bf16(hi * hi), llj_rmsnorm's order
+          const f32x2 q = unpk(cvt_pk(unpk(aw[i]) * unpk(aw[i])));
+          a += q.x + q.y;
         }
       }
       a = wave_sum(a);
@@ -278,27 +285,31 @@ __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restr
     if (tid < MR) rr[tid] = round_bf(rsqrtf(round_bf(round_bf((red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3]) / (float)K) + eps)));
     __syncthreads();
   }
-  // each row's maximum of the (normalized) elements below the threshold
+  if ((LLJ_PREP_ABL & 1) && tid < MR) rr[tid] = 1.f;
+  if (LLJ_PREP_ABL & 1) __syncthreads();
+  // each row's maximum of the (normalized) elements below the threshold. The elements are bf16
+  // values, exact in fp16 wherever |v| >= 2^-14, and fp16 rounding is monotonic: for a threshold
+  // >= 2^-14, max f16(|v|) over f16(|v|) < thr is f16(max |v| over |v| < thr) -- no per-element
+  // conversion (the i8_stats_kernel rule, bit for bit)
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
+  for (int r = 0; r < ((LLJ_PREP_ABL & 2) ? 0 : 2); ++r) {
     const float rn = NORM ? rr[grp + 4 * r < M ? grp + 4 * r : M - 1] : 1.f;
+    const f32x2 rn2 = {rn, rn};
     float mx = 0.f;
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
-      if (lt + 256 * j < nvec) {
-        uint32_t aw[4] = {xa[r][j].x, xa[r][j].y, xa[r][j].z, xa[r][j].w};
-        if (NORM) {
-          aw[0] = norm_pair(aw[0], ga[j].x, rn); aw[1] = norm_pair(aw[1], ga[j].y, rn);
-          aw[2] = norm_pair(aw[2], ga[j].z, rn); aw[3] = norm_pair(aw[3], ga[j].w, rn);
-        }
+      const uint32_t aw[4] = {xa[r][j].x, xa[r][j].y, xa[r][j].z, xa[r][j].w};
+      const uint32_t gw4[4] = {ga[j].x, ga[j].y, ga[j].z, ga[j].w};
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float av = fabsf(to_f16f((i & 1) ? bfhi(aw[i >> 1]) : bflo(aw[i >> 1])));
-          mx = av < thr ? fmaxf(mx, av) : mx;
-        }
+      for (int i = 0; i < 4; ++i) {
+        f32x2 v = unpk(aw[i]);
+        if (NORM) v = unpk(cvt_pk(unpk(gw4[i]) * unpk(cvt_pk(v * rn2))));  // g * bf16(x * r), rounded
+        const float a0 = fabsf(v.x), a1 = fabsf(v.y);
+        mx = fmaxf(mx, a0 < thr ? a0 : 0.f);
+        mx = fmaxf(mx, a1 < thr ? a1 : 0.f);
       }
     }
-    mx = wave_max(mx);
+    mx = to_f16f(wave_max(mx));
     if (lane == 0) mred[tid >> 6][r] = mx;  // wave (grp, gw): slot r <-> row grp + 4 r
   }
   if (!NORM) __syncthreads();  // flag / pmax zeroed before any thread sets them (NORM: synced above)
@@ -311,6 +322,7 @@ __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restr
   }
   if (own) {
     if (NORM) reinterpret_cast<uint4*>(xn + (size_t)om * K)[ov] = on;
+    vals[om][ov - (k0 >> 3)] = on;
     const uint32_t ow[4] = {on.x, on.y, on.z, on.w};
     float mx = 0.f;
 #pragma unroll
@@ -335,7 +347,7 @@ __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restr
     if (b == 0 && ov == (k0 >> 3)) L.sca[om] = sca;
   }
   if (tid < M) L.part[(size_t)b * M + tid] = __int_as_float(pmax[tid]);
-  if (b == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb};
+  if (b == 0 && tid == 0) *reinterpret_cast<I8WsHeader*>(ws) = I8WsHeader{M, K, kNSB, kb}, L.avh[0] = 1;  // aval written
   if (st) {  // uniform: the decode hand-off block (i8ws.h) for the streamed int8 GEMVs (AM_I8Q)
     if (b == 0 && tid < 8 * kI8StSlots) {  // SCA in slot 0, the other slots 0
       const int m = tid;
@@ -352,12 +364,26 @@ __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restr
       st[kI8StFlags + (k0 >> 5) + wd] = bits;
     }
   }
-  if (tid < 64) {  // compact the flags into the list, 64 columns per ballot
+  if (tid < 64 && !(LLJ_PREP_ABL & 8)) {  // compact the flags into the list, 64 columns per ballot
     int c = 0;
     for (int i0 = 0; i0 < k1 - k0; i0 += 64) {
       const bool f = i0 + lane < k1 - k0 && flag[i0 + lane];
       const unsigned long long bal = __ballot(f);
-      if (f) L.list[b * kb + c + __popcll(bal & ((1ull << lane) - 1ull))] = k0 + i0 + lane;
+      if (f) {
+        const int e = b * kb + c + __popcll(bal & ((1ull << lane) - 1ull)), kc = i0 + lane;
+        L.list[e] = k0 + kc;
+        uint32_t h[4] = {0u, 0u, 0u, 0u};  // f16(A) of rows 0..7 (rows >= M: 0)
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          if (m < M) {
+            const uint4 v = vals[m][kc >> 3];
+            const uint32_t wv = (kc & 7) < 4 ? ((kc & 7) < 2 ? v.x : v.y) : ((kc & 7) < 6 ? v.z : v.w);
+            const float a = (kc & 1) ? bfhi(wv) : bflo(wv);
+            h[m >> 1] |= (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) << (16 * (m & 1));
+          }
+        }
+        L.aval[e] = make_uint4(h[0], h[1], h[2], h[3]);
+      }
       c += __popcll(bal);
     }
     if (lane == 0) L.cnt[b] = c;

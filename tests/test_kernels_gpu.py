@@ -238,14 +238,16 @@ def test_bf16_linear(hip, M, N, K):
     assert_bf16_close(got, x @ W.T + bias, f"bf16 M={M}")
 
 
-@pytest.mark.parametrize("outliers", [0, 3, 300, 700])
+@pytest.mark.parametrize("outliers", [0, 3, 120, 300, 700])
 @pytest.mark.parametrize("M", [1, 8])
 def test_int8_linear_vs_restatement(hip, M, outliers):
-    """LLM.int8() against the oracle's restatement (bitsandbytes absent: parity unpinned). 300
-    outlier columns (about what the synthetic 7B down projection sees at bs=8) run the side
-    product from the LDS stash of CB bytes; 700 (> kStashCols = 512) also the global-read tail."""
+    """LLM.int8() against the oracle's restatement (bitsandbytes absent: parity unpinned). At K 4096
+    the side product runs inside the weight stream from the prep's aval table (3 columns: within
+    the entries prefetched per chunk; 120: past them, ~4 per chunk); 300 outlier columns (about what
+    the synthetic 7B down projection sees at bs=8, K 11008) run it after the stream from the LDS
+    stash of CB bytes; 700 (> kStashCols = 512) also the global-read tail."""
     rng = np.random.default_rng(M + 100 * outliers)
-    N, K = (256, 4096) if outliers <= 3 else (256, 11008)
+    N, K = (256, 4096) if outliers <= 120 else (256, 11008)
     W = bf16(rng.standard_normal((N, K)) * 0.02)
     x = rng.standard_normal((M, K)).astype(np.float32)
     if outliers:

@@ -1,0 +1,37 @@
+#!/bin/bash
+# Round-5 batch N: uniform side data loaded into VGPRs (no readfirstlane at the load), the row-sum
+# MFMA without a per-step branch; A/B of the load fence (bs=8 int4, bs=1, C3) and of SIS; tests.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r05n
+mkdir -p $O
+cd $R
+export TMPDIR=/tmp
+chk() {
+  echo "$1 rc=$2" >> $O/status.log
+  case $2 in 0) ;; *) echo "stopping after $1" >> $O/status.log; exit $2;; esac
+}
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > $O/t_kern.log 2>&1
+chk "kernel tests" $?
+timeout -k 10 400 python -u -m pytest tests/test_model_7b_gpu.py tests/test_model_gpu.py -x -q --timeout 200 --timeout-method thread > $O/t_model.log 2>&1
+chk "model tests" $?
+timeout -k 10 300 python -u -m pytest tests/test_fulldepth_gpu.py -x -v -s --timeout 250 --timeout-method thread > $O/t_full.log 2>&1
+chk "full depth" $?
+timeout -k 10 300 python -u tools/ab_decode.py --batch 8 --rounds 3 --steps 50 --quantize llm.int8 --variants \
+  new fence:LIB=scratch/fence.so nosis:LIB=scratch/nosis.so > $O/ab_c3.jsonl 2> $O/ab_c3.err
+chk "ab c3" $?
+timeout -k 10 300 python -u tools/ab_decode.py --batch 8 --rounds 3 --steps 50 --variants new fence:LIB=scratch/fence.so \
+  > $O/ab_bs8.jsonl 2> $O/ab_bs8.err
+chk "ab bs8" $?
+timeout -k 10 300 python -u tools/ab_decode.py --batch 1 --rounds 3 --steps 60 --variants new fence:LIB=scratch/fence.so \
+  > $O/ab_bs1.jsonl 2> $O/ab_bs1.err
+chk "ab bs1" $?
+timeout -k 10 300 python -u tools/config_suite.py --only C3,C3-o0,C3-o6x20 --steps 50 > $O/configs.log 2>&1
+chk "configs" $?
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/profc3 -o run -- \
+  python -u bench.py --decode-only --batch 8 --steps 20 --quantize llm.int8 > $O/profc3.log 2>&1
+chk "trace c3" $?
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof8 -o run -- \
+  python -u bench.py --decode-only --batch 8 --steps 20 > $O/prof8.log 2>&1
+chk "trace bs8" $?
+exit 0

@@ -6,7 +6,8 @@ of the library, never the product .so). Each GEMV workgroup stamps s_memrealtime
 sync after every GEMV launch and its stamps are read back; prints, per op of one layer, the
 median / p90 of each phase relative to the launch's first workgroup start.
 
-  python tools/phase_trace.py [--build] [--layer 5] [--batch 1]
+  python tools/phase_trace.py [--build] [--layer 5] [--batch 1] [--quantize llm.int8] [--lib scratch/x.so]
+  (--build [--defines LLJ_ABL=8 ...] --lib <out>: a trace build with extra macros)
 """
 from __future__ import annotations
 
@@ -25,7 +26,7 @@ sys.path.insert(0, str(REPO / "lit-llama-ja_amd"))
 TRACE_SO = REPO / "scratch" / "lljamd_trace.so"
 
 GEMV_CALLS = {"llj_norm_qkv_rope": "qkv", "llj_linear_resid": "resid", "llj_norm_swiglu": "swiglu",
-              "llj_norm_linear": "head"}
+              "llj_norm_linear": "head", "llj_i8_linear_resid": "resid", "llj_i8_swiglu_stats": "swiglu"}
 
 
 def main():
@@ -33,20 +34,25 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--layer", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--quantize", default="gptq.int4")
+    ap.add_argument("--lib", default=None)
+    ap.add_argument("--defines", nargs="*", default=[])
     a = ap.parse_args()
+    lib_path = REPO / a.lib if a.lib else TRACE_SO
     from lit_llama import _build, _hip
 
     if a.build:
-        TRACE_SO.parent.mkdir(exist_ok=True)
-        _build.build(force=True, out=TRACE_SO, defines=["LLJ_TRACE=1"])
+        lib_path.parent.mkdir(exist_ok=True)
+        _build.build(force=True, out=lib_path, defines=["LLJ_TRACE=1"] + a.defines)
         return
-    _hip.LIB_PATH, _hip._lib = TRACE_SO, None
+    _hip.LIB_PATH, _hip._lib = lib_path, None
     L = _hip.lib()
-    L.llj_trace_copy_w4.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    copy = L.llj_trace_copy_i8 if a.quantize == "llm.int8" else L.llj_trace_copy_w4
+    copy.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     import bench
     from lit_llama.engine import DecodeSession
 
-    model = bench.build_model("7B", "gptq.int4")
+    model = bench.build_model("7B", a.quantize)
     sess = DecodeSession(model, a.batch, 144, 120, use_graph=False)
     prompts = torch.randint(3, 32000, (a.batch, 16), generator=torch.Generator().manual_seed(0)).cuda()
     sess.prefill(prompts)
@@ -61,7 +67,7 @@ def main():
         orig(name, *args)
         if name in GEMV_CALLS:
             torch.cuda.synchronize()
-            L.llj_trace_copy_w4(buf.ctypes.data, buf.nbytes)
+            copy(buf.ctypes.data, buf.nbytes)
             count[name] = count.get(name, 0) + 1
             records.append((name, count[name], buf.reshape(8192, 8).copy()))
             buf[:] = 0
@@ -70,12 +76,13 @@ def main():
     torch.cuda.synchronize()
     _hip.call = orig
     out = {}
-    per_layer = {"llj_norm_qkv_rope": 1, "llj_linear_resid": 2, "llj_norm_swiglu": 1, "llj_norm_linear": 1}
+    per_layer = {"llj_norm_qkv_rope": 1, "llj_linear_resid": 2, "llj_norm_swiglu": 1, "llj_norm_linear": 1,
+                 "llj_i8_linear_resid": 2, "llj_i8_swiglu_stats": 1}
     for name, k, tr in records:
         layer = (k - 1) // per_layer[name]
         if name != "llj_norm_linear" and layer != a.layer:
             continue
-        tag = GEMV_CALLS[name] + ("" if name != "llj_linear_resid" else ("_cproj" if (k - 1) % 2 == 0 else "_down"))
+        tag = GEMV_CALLS[name] + ("" if GEMV_CALLS[name] != "resid" else ("_cproj" if (k - 1) % 2 == 0 else "_down"))
         nwg = {"qkv": 768, "swiglu": 688, "head": 2000}.get(GEMV_CALLS[name], 256) // max(1, 1)
         st = tr[:nwg, :6].astype(np.int64)
         valid = (st[:, 0] > 0) & (st[:, 5] >= st[:, 0])
@@ -88,7 +95,8 @@ def main():
         out[tag] = res
         print(tag, json.dumps(res), flush=True)
     (REPO / "gpurun_out").mkdir(exist_ok=True)
-    (REPO / "gpurun_out" / f"phase_trace_bs{a.batch}.json").write_text(json.dumps(out, indent=1))
+    tag = f"{a.quantize}_bs{a.batch}" + (f"_{Path(a.lib).stem}" if a.lib else "")
+    (REPO / "gpurun_out" / f"phase_trace_{tag}.json").write_text(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
