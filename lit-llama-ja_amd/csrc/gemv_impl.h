@@ -68,6 +68,9 @@ constexpr int kSSlot = 8 * kSRow;
 __host__ __device__ constexpr bool am_stream(int am) { return am == AM_STREAM || am == AM_SNORM; }
 // AM_I8Q per-wave ring slot: the quantized rows (8 x 144 B) then, for chunks with outlier columns,
 // those columns' f16(A) of the 8 rows, column-major (128 x 16 B; only outlier columns written / read)
+#ifndef LLJ_I8Q_FAST
+#define LLJ_I8Q_FAST 0  // AM_I8Q: 1 quant8_fast for rows with SCA >= 1/64 (2: its scalar form), 0 quant8f always
+#endif
 constexpr int kQRow = 144;
 constexpr int kQSlotBytes = 8 * kQRow + 128 * 16;
 enum : int { EP_STORE = 0, EP_RESID = 1, EP_QKV = 2, EP_SWIGLU = 3 };
@@ -396,6 +399,34 @@ __device__ __forceinline__ uint2 quant8f(const u32x4 x, uint32_t fb, float inv) 
   return make_uint2(o[0], o[1]);
 }
 
+// quant8f without the per-element fp16 round trip, clamp and convert, for rows with SCA >= 1/64:
+// bf16 values are exact in fp16 above 2^-14 (below it, |a| * 127 / SCA < 0.5 either way: code 0),
+// |f16(a)| <= SCA bounds |a * inv| by 127, and rint comes from adding 1.5 * 2^23 (round to nearest
+// even, the code in the low byte, two's complement). Bitwise quant8f's codes for finite rows.
+__device__ __forceinline__ uint2 quant8_fast(const u32x4 x, uint32_t fb, float inv) {
+#pragma clang fp contract(off)
+  const f32x2 inv2 = {inv, inv}, mg = {12582912.f, 12582912.f};
+  uint32_t b[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (LLJ_I8Q_FAST == 2) {  // scalar form (A/B of the packed one)
+      b[2 * i] = __builtin_bit_cast(uint32_t, __fadd_rn(__fmul_rn(bflo(x[i]), inv), 12582912.f));
+      b[2 * i + 1] = __builtin_bit_cast(uint32_t, __fadd_rn(__fmul_rn(bfhi(x[i]), inv), 12582912.f));
+    } else {
+      const f32x2 q = unpk(x[i]) * inv2 + mg;  // two roundings (no fma): fl(fl(a * inv) + 1.5 * 2^23)
+      b[2 * i] = __builtin_bit_cast(uint32_t, q.x);
+      b[2 * i + 1] = __builtin_bit_cast(uint32_t, q.y);
+    }
+  }
+  auto pack4 = [](uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t nib) {
+    const uint32_t w = (b0 & 0xFFu) | ((b1 & 0xFFu) << 8) | ((b2 & 0xFFu) << 16) | (b3 << 24);  // low bytes
+    const uint32_t m1 = (nib * 0x00204081u) & 0x01010101u;  // bit e of nib -> byte e = 1
+    const uint32_t m = (m1 << 8) - m1;                       // ... = 0xFF (borrow-free), the outlier bytes
+    return w & ~m;
+  };
+  return make_uint2(pack4(b[0], b[1], b[2], b[3], fb & 0xFu), pack4(b[4], b[5], b[6], b[7], (fb >> 4) & 0xFu));
+}
+
 template <int V>
 struct IC {
   static constexpr int value = V;
@@ -422,7 +453,7 @@ struct APre {
 #define LLJ_ABAR 0
 #endif
 #ifndef LLJ_ABL
-#define LLJ_ABL 0  // ablation switches for profiling only (1 no A prologue, 2 no compute, 4 no epilogue, 8 no AM_I8Q side loop)
+#define LLJ_ABL 0  // ablation switches for profiling only (1 no A prologue, 2 no compute, 4 no epilogue, 8 no AM_I8Q side loop, 16 no streamed-A loads)
 #endif
 #ifndef LLJ_I8_SIS
 #define LLJ_I8_SIS 1  // int8 A image: in-stream fp16 side product from the prep's aval table (0: after the stream)
@@ -555,6 +586,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   u32x4 sa[ASTR ? D : 1][2], sg[SNRM ? D : 1];
   u32x4 sfl[I8Q ? D : 1];  // AM_I8Q: the chunk's 128 outlier-column bits (the same in every lane)
   float qi0 = 0.f, qi1 = 0.f, i8scb = 0.f, i8scb2 = 0.f;  // AM_I8Q: 127 / SCA of the lane's two rows; SCB[n] / 127
+  bool qfast = false;  // AM_I8Q: every row's SCA >= 1/64 (quant8_fast's exactness condition)
   // AM_I8Q: this lane's fp16 side-product partials of rows 0..7 (its column, its k group; sd2: c_fc2)
   float sd[I8 ? 8 : 1], sd2[I8 && DUAL ? 8 : 1];
 #pragma unroll
@@ -594,7 +626,12 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     c = c < 0 ? 0 : (c >= KC ? KC - 1 : c);  // always a valid chunk (loads past the end are unused)
     if constexpr (ASTR) {  // the chunk's activation rows first: they arrive before its weights
 #pragma unroll
-      for (int h = 0; h < 2; ++h) sa[d][h] = *reinterpret_cast<const u32x4*>(aptr[h] + 128 * c);
+      for (int h = 0; h < 2; ++h) {
+        if constexpr ((LLJ_ABL & 16) != 0)  // ablation: no activation traffic (constant rows)
+          sa[d][h] = u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+        else
+          sa[d][h] = *reinterpret_cast<const u32x4*>(aptr[h] + 128 * c);
+      }
       if constexpr (SNRM) sg[d] = *reinterpret_cast<const u32x4*>(gptr + 128 * c);
       if constexpr (I8Q) sfl[d] = *reinterpret_cast<const u32x4*>(p.i8st + kI8StFlags + 4 * c + vz);
     }
@@ -653,8 +690,13 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         return i == 0 ? fw[0] : i == 1 ? fw[1] : i == 2 ? fw[2] : fw[3];
       };
       const uint32_t fb = (pick(seg >> 2) >> (8 * (seg & 3))) & 0xFFu;
-      *reinterpret_cast<uint2*>(qslot + (lane >> 4) * kQRow + 8 * seg) = quant8f(sa[d][0], fb, qi0);
-      *reinterpret_cast<uint2*>(qslot + ((lane >> 4) + 4) * kQRow + 8 * seg) = quant8f(sa[d][1], fb, qi1);
+      if (qfast) {  // uniform: every row's SCA >= 1/64 (the prologue)
+        *reinterpret_cast<uint2*>(qslot + (lane >> 4) * kQRow + 8 * seg) = quant8_fast(sa[d][0], fb, qi0);
+        *reinterpret_cast<uint2*>(qslot + ((lane >> 4) + 4) * kQRow + 8 * seg) = quant8_fast(sa[d][1], fb, qi1);
+      } else {
+        *reinterpret_cast<uint2*>(qslot + (lane >> 4) * kQRow + 8 * seg) = quant8f(sa[d][0], fb, qi0);
+        *reinterpret_cast<uint2*>(qslot + ((lane >> 4) + 4) * kQRow + 8 * seg) = quant8f(sa[d][1], fb, qi1);
+      }
       bool continue_side = true;  // (LLJ_ABL & 8: timing ablation without the side loop)
       if ((fw[0] | fw[1] | fw[2] | fw[3]) != 0u) {  // uniform: the chunk has outlier columns
         // fp16 side product from the weight registers: lane (column n, k group g) holds CB[n, k] of
@@ -1110,6 +1152,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       if (m == m0c) qi0 = inv;
       if (m == m1c) qi1 = inv;
     }
+    qfast = LLJ_I8Q_FAST != 0;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) qfast = qfast && (m >= M || sv[m] >= 0.015625f);
     float mine = sv[0];  // the epilogue's SCA (tail; rows >= M unused); selects, not a dynamic index
 #pragma unroll
     for (int m = 1; m < 8; ++m) mine = tid == m ? sv[m] : mine;

@@ -899,6 +899,8 @@ def test_int8_statistics_handoff(hip, M, regime):
     torch.cuda.synchronize()
     a, b = xa.float().cpu().numpy(), xb.float().cpu().numpy()
     assert np.mean(a == b) > 0.98, np.mean(a == b)
+    if not fl_s.any():  # no outlier columns: identical int8 codes and exact int32 sums -> bitwise equal
+        assert np.array_equal(a, b)  # (the per-chunk quantization, quant8_fast, is the statistics launch's)
     yh = y.float().cpu().numpy()
     assert_bf16_close(a, x0.float().cpu().numpy() + bf16(O.int8_linear(yh, cbo, scbo)), f"int8 c_proj M={M}")
     # SwiGLU over normalized rows -> h and its statistics (and y's block zeroed)
