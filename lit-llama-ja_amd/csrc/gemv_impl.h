@@ -69,7 +69,7 @@ __host__ __device__ constexpr bool am_stream(int am) { return am == AM_STREAM ||
 // AM_I8Q per-wave ring slot: the quantized rows (8 x 144 B) then, for chunks with outlier columns,
 // those columns' f16(A) of the 8 rows, column-major (128 x 16 B; only outlier columns written / read)
 #ifndef LLJ_I8Q_FAST
-#define LLJ_I8Q_FAST 0  // AM_I8Q: 1 quant8_fast for rows with SCA >= 1/64 (2: its scalar form), 0 quant8f always
+#define LLJ_I8Q_FAST 1  // AM_I8Q: 1 quant8_fast for rows with SCA >= 1/64, 0 quant8f always
 #endif
 constexpr int kQRow = 144;
 constexpr int kQSlotBytes = 8 * kQRow + 128 * 16;
@@ -404,19 +404,15 @@ __device__ __forceinline__ uint2 quant8f(const u32x4 x, uint32_t fb, float inv) 
 // |f16(a)| <= SCA bounds |a * inv| by 127, and rint comes from adding 1.5 * 2^23 (round to nearest
 // even, the code in the low byte, two's complement). Bitwise quant8f's codes for finite rows.
 __device__ __forceinline__ uint2 quant8_fast(const u32x4 x, uint32_t fb, float inv) {
-#pragma clang fp contract(off)
-  const f32x2 inv2 = {inv, inv}, mg = {12582912.f, 12582912.f};
   uint32_t b[8];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if constexpr (LLJ_I8Q_FAST == 2) {  // scalar form (A/B of the packed one)
-      b[2 * i] = __builtin_bit_cast(uint32_t, __fadd_rn(__fmul_rn(bflo(x[i]), inv), 12582912.f));
-      b[2 * i + 1] = __builtin_bit_cast(uint32_t, __fadd_rn(__fmul_rn(bfhi(x[i]), inv), 12582912.f));
-    } else {
-      const f32x2 q = unpk(x[i]) * inv2 + mg;  // two roundings (no fma): fl(fl(a * inv) + 1.5 * 2^23)
-      b[2 * i] = __builtin_bit_cast(uint32_t, q.x);
-      b[2 * i + 1] = __builtin_bit_cast(uint32_t, q.y);
-    }
+  for (int e = 0; e < 8; ++e) {
+    // fl(fl(a * inv) + 1.5 * 2^23): the product is pinned (empty asm) so that it is not contracted
+    // into one fma (a single rounding would differ at ties); scalar: the packed-vector form of this
+    // loop was miscompiled (ROCm 7.2: the odd elements dropped)
+    float p = ((e & 1) ? bfhi(x[e >> 1]) : bflo(x[e >> 1])) * inv;
+    asm volatile("" : "+v"(p));
+    b[e] = __builtin_bit_cast(uint32_t, p + 12582912.f);
   }
   auto pack4 = [](uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t nib) {
     const uint32_t w = (b0 & 0xFFu) | ((b1 & 0xFFu) << 8) | ((b2 & 0xFFu) << 16) | (b3 << 24);  // low bytes
