@@ -83,7 +83,11 @@ def main():
         if name != "llj_norm_linear" and layer != a.layer:
             continue
         tag = GEMV_CALLS[name] + ("" if GEMV_CALLS[name] != "resid" else ("_cproj" if (k - 1) % 2 == 0 else "_down"))
-        nwg = {"qkv": 768, "swiglu": 688, "head": 2000}.get(GEMV_CALLS[name], 256) // max(1, 1)
+        ntiles = {"qkv": 768, "swiglu": 688, "head": 2000}.get(GEMV_CALLS[name], 256)
+        tpw = 1
+        if a.batch > 1 and a.quantize == "gptq.int4":  # multi-tile workgroups (pick_tpw: 256 CUs, <= 4; residual <= 2)
+            tpw = min(4 if GEMV_CALLS[name] != "resid" else 2, -(-ntiles // 256))
+        nwg = -(-ntiles // tpw)
         st = tr[:nwg, :6].astype(np.int64)
         valid = (st[:, 0] > 0) & (st[:, 5] >= st[:, 0])
         t0 = st[valid, 0].min()
