@@ -61,7 +61,10 @@ enum : int { WF_W4 = 0, WF_BF16 = 1, WF_I8 = 2, WF_W8 = 3, WF_W4G = 4 };
 // quantized per chunk with the row statistics its producer handed over (i8st: SCA per row, outlier
 // column bits), and the fp16 outlier side product is taken from the chunk's weight registers as the
 // chunk streams -- no statistics launch, no int8 A image, no side-product pass after the stream.
-enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2, AM_STREAM = 3, AM_SNORM = 4, AM_I8Q = 5 };
+// AM_I8S (LLM.int8, batched decode rows with a statistics workspace): the rows quantized once by the
+// statistics launch (ws aq) are streamed per chunk into the same per-wave ring as AM_I8Q's -- no
+// workgroup-wide int8 A image, no prologue barrier.
+enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2, AM_STREAM = 3, AM_SNORM = 4, AM_I8Q = 5, AM_I8S = 6 };
 // streamed A: elements per staged row (128 + 8 pad: rows land on distinct bank groups) and per slot
 constexpr int kSRow = 136;
 constexpr int kSSlot = 8 * kSRow;
@@ -457,6 +460,9 @@ struct APre {
 #ifndef LLJ_I8_SIS_E
 #define LLJ_I8_SIS_E 2  // outlier entries per chunk loaded with its weights (a k-block with more: side product after the stream)
 #endif
+#ifndef LLJ_I8S
+#define LLJ_I8S 1  // int8 GEMVs with a statistics workspace: stream its quantized rows (AM_I8S) for 2..8 rows
+#endif
 #ifndef LLJ_LOADFENCE
 #define LLJ_LOADFENCE 0  // 1: the weight refills stay where the loop issues them (see the main loop)
 #endif
@@ -486,8 +492,11 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   static_assert(!STRM || (MB == 8 && !I8), "streamed A: batched rows, non-int8 formats");
   constexpr bool I8Q = (AM == AM_I8Q);  // int8 rows quantized per chunk from handed-over statistics
   static_assert(!I8Q || (I8 && MB == 8 && TPW == 1), "AM_I8Q: int8, batched rows, one tile per workgroup");
+  constexpr bool I8S = (AM == AM_I8S);  // int8 rows of the statistics workspace streamed per chunk
+  static_assert(!I8S || (I8 && MB == 8 && TPW == 1), "AM_I8S: int8, batched rows, one tile per workgroup");
   constexpr bool ASTR = STRM || I8Q;  // bf16 A rows streamed per chunk
-  constexpr bool ALDS = (I8 && !I8Q) || (AM != AM_GLOBAL && !STRM && !I8Q);
+  constexpr bool QRING = I8Q || I8S;  // int8 rows through the per-wave ring (kQSlotBytes slots)
+  constexpr bool ALDS = (I8 && !QRING) || (AM != AM_GLOBAL && !STRM && !QRING);
   // row sums of A for the nibble offset: an extra MFMA against a ones fragment for the global-A
   // form and for batched norm-fused rows (LLJ_SACC_NORM; the VALU sums + 8 wave reductions of the
   // prologue sit on its critical path), else summed while the LDS image is written
@@ -512,7 +521,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   // scratch] [tail: 128 words for staging scratch / int8 SCA]
   const int a_stride = I8 ? K + 16 : K + 8;  // elements (bytes for int8)
   const size_t a_bytes = ALDS ? (((size_t)M * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15)
-                              : STRM ? (size_t)NW * 2 * kSSlot * 2 : I8Q ? (size_t)NW * 2 * kQSlotBytes : 0;
+                              : STRM ? (size_t)NW * 2 * kSSlot * 2 : QRING ? (size_t)NW * 2 * kQSlotBytes : 0;
   constexpr int NV = 8 * TPW + 4;  // reduction words per lane: acc, acc2 of every tile, sacc
   constexpr size_t kRedBytes = (size_t)NW * 64 * NV * 4;
   constexpr size_t kScratch = kRedBytes + (I8 ? (size_t)2 * NW * 8 * 16 * 4 : 0);  // + int8 side partials
@@ -598,6 +607,12 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   u32x4 sav[SIS ? D : 1][SE];
   bool sis = false;  // uniform: the workspace carries aval and its k-blocks are the chunks
   const I8Layout Lp = i8_layout(p.i8ws, SIS ? p.M : 1, SIS ? p.K : 128);
+  // AM_I8S: lane l carries 16-B segment (l & 7) of quantized row (l >> 3) of each of its chunks (rows
+  // past M: clamped copies of row M - 1, never stored); the workspace holds exactly these M rows
+  u32x4 s8[I8S ? D : 1];
+  const int8_t* s8ptr = I8S ? reinterpret_cast<const int8_t*>(p.i8ws) + i8_offsets(1, p.K).aq +
+                                  (size_t)(p.m0 + ((lane >> 3) < M ? (lane >> 3) : M - 1)) * p.K + 16 * (lane & 7)
+                            : nullptr;  // (aq first in the workspace: row r at a fixed offset, i8ws.h)
   const bf16_t* aptr[2];
   const bf16_t* gptr = p.norm_w + 8 * (lane & 15);
   float rn0 = 1.f, rn1 = 1.f;
@@ -631,6 +646,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       if constexpr (SNRM) sg[d] = *reinterpret_cast<const u32x4*>(gptr + 128 * c);
       if constexpr (I8Q) sfl[d] = *reinterpret_cast<const u32x4*>(p.i8st + kI8StFlags + 4 * c + vz);
     }
+    if constexpr (I8S) s8[d] = *reinterpret_cast<const u32x4*>(s8ptr + 128 * c);
     if constexpr (SIS) {
       scn[d] = Lp.cnt[(c < kNSB ? c : kNSB - 1) + vz];
 #pragma unroll
@@ -678,6 +694,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     // LDS keeps a wave's accesses in order, no barrier)
     bf16_t* slot = reinterpret_cast<bf16_t*>(smem) + (size_t)(wave * 2 + (d & 1)) * kSSlot;
     unsigned char* qslot = smem + (size_t)(wave * 2 + (d & 1)) * kQSlotBytes;
+    if constexpr (I8S) *reinterpret_cast<u32x4*>(qslot + (lane >> 3) * kQRow + 16 * (lane & 7)) = s8[d];
     if constexpr (I8Q) {
       // quantize the lane's two row segments (LLM.int8 rows with the producer's SCA and outlier bits)
       const u32x4 fw = sfl[d];
@@ -819,7 +836,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       // LDS lanes of rows >= M read row 0 (abase clamped): their output rows are never stored, and
       // an unconditional read keeps the hot loop free of divergent LDS accesses
       const u32x4 av = STRM ? *reinterpret_cast<const u32x4*>(slot + (row & 7) * kSRow + kofs<WF>(t, grp))
-                       : I8Q ? *reinterpret_cast<const u32x4*>(qslot + (row & 7) * kQRow + kofs<WF>(t, grp))
+                       : QRING ? *reinterpret_cast<const u32x4*>(qslot + (row & 7) * kQRow + kofs<WF>(t, grp))
                        : ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
       if constexpr (WF == WF_W4) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
@@ -1195,6 +1212,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   }
   if constexpr ((LLJ_ABL & 1) != 0) {  // ablation: no A prologue (garbage A)
   } else if constexpr (I8Q) {
+  } else if constexpr (I8S) {  // the epilogue's SCA only (read after the reduction barrier)
+    const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
+    if (tid < M) sca[tid] = i8_layout(p.i8ws, h.mtot, h.K).sca[p.m0 + tid];
   } else if constexpr (I8) {
     stage_i8<NW>(p, reinterpret_cast<int8_t*>(smem), a_stride, sca);
     __syncthreads();
@@ -1253,7 +1273,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   // int8 side products in the LDS beyond the reduction scratch (the A image is no longer read)
   float* side = reinterpret_cast<float*>(smem + kRedBytes);
   if (NW > 1) {
-    if (ALDS || ASTR) __syncthreads();  // every wave is done reading the A image / ring it aliases
+    if (ALDS || ASTR || QRING) __syncthreads();  // every wave is done reading the A image / ring it aliases
     auto side_partials = [&]() {  // the in-stream side partials: sum the 4 k groups, one per (wave, row, column)
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
@@ -1494,7 +1514,7 @@ constexpr int kNW = LLJ_NW;
 constexpr int kD = LLJ_D;
 
 static inline size_t a_image_bytes(int wf, int am, int M, int K, int nw = kNW) {
-  if (am == AM_I8Q) return (size_t)nw * 2 * kQSlotBytes;  // per-wave 2-slot rings
+  if (am == AM_I8Q || am == AM_I8S) return (size_t)nw * 2 * kQSlotBytes;  // per-wave 2-slot rings
   if (wf == WF_I8) return (((size_t)M * (K + 16)) + 15) & ~(size_t)15;
   if (am == AM_GLOBAL) return 0;
   if (am_stream(am)) return (size_t)nw * 2 * kSSlot * 2;  // per-wave 2-slot rings
@@ -1634,7 +1654,7 @@ static int launch_mb(const GemvParams& p, hipStream_t s) {
 
 template <int WF, int AM, int EP>
 static int launch(const GemvParams& p, hipStream_t s) {
-  if constexpr (am_stream(AM) || AM == AM_I8Q) {  // batched rows only (M <= 8)
+  if constexpr (am_stream(AM) || AM == AM_I8Q || AM == AM_I8S) {  // batched rows only (M <= 8)
     if constexpr (EP == EP_RESID && LLJ_NWR != kNW)
       if (p.K >= LLJ_NWR_KMIN) return launch_mb<WF, AM, EP, 8, LLJ_NWR>(p, s);
     if constexpr (EP == EP_SWIGLU && LLJ_NWS != LLJ_NWM) return launch_mb<WF, AM, EP, 8, LLJ_NWS>(p, s);
@@ -1660,7 +1680,11 @@ static int launch(const GemvParams& p, hipStream_t s) {
 // are staged when they fit.
 static int pick_am(int wf, const GemvParams& p) {
   if (wf == WF_I8 && p.i8st) return (p.norm_w || p.M > 8) ? -1 : AM_I8Q;  // handed-over row statistics
-  if (wf == WF_I8) return (p.norm_w || !p.i8ws || !lds_fits(wf, p.M, p.K)) ? -1 : AM_LDS;
+  if (wf == WF_I8) {
+    if (p.norm_w || !p.i8ws) return -1;
+    if (LLJ_I8S && g_stream_a && p.M >= 2 && p.M <= 8) return AM_I8S;
+    return lds_fits(wf, p.M, p.K) ? AM_LDS : -1;
+  }
   if (g_stream_a && p.M >= (g_stream_a >= 2 ? 1 : 2) && p.M <= 8) {
     if (!p.norm_w) return AM_STREAM;
     if (p.nstat && (reinterpret_cast<uintptr_t>(p.nstat) & 15) == 0) return AM_SNORM;
@@ -1700,6 +1724,7 @@ template <int WF>
 static int launch_fmt(int am, int ep, const GemvParams& p, hipStream_t s) {
   if constexpr (WF == WF_I8) {
     if (am == AM_I8Q) return launch_ep<WF_I8, AM_I8Q>(ep, p, s);
+    if (am == AM_I8S) return launch_ep<WF_I8, AM_I8S>(ep, p, s);
     return launch_ep<WF_I8, AM_LDS>(ep, p, s);
   } else {
     if (am == AM_SNORM) return launch_ep<WF, AM_SNORM>(ep, p, s);

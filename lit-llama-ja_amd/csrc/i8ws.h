@@ -1,12 +1,14 @@
 // LLM.int8() activation workspace (filled by llj_i8_stats, read by the int8 GEMV).
 //
 //   [0, 16)        header {mtot, K, nsb, kb}
+//   aq[M][K]       the activation quantized once: round(A16 * 127 / SCA), outlier columns 0 -- first,
+//                  so that row r is at 16 + r * K whatever M is (the streamed int8 GEMV, AM_I8S,
+//                  addresses its rows before it has read the header)
 //   part[nsb][M]   fp32 per-(k-block, row) absmax of the non-outlier elements
 //   cnt[nsb]       outlier columns found in each k-block
 //   list[nsb][kb]  their column indices (ascending within a block)
 //   sca[M]         SCA[m] = max over the k-blocks of part
 //   flag[K]        1 for an outlier column
-//   aq[M][K]       the activation quantized once: round(A16 * 127 / SCA), outlier columns 0
 //   avh[4]         avh[0] = 1 when aval below is valid (the one-launch decode prep, M <= 8), else 0
 //   aval[nsb][kb]  f16(A) of rows 0..7 of each listed outlier column (16 B, list order; rows >= M 0):
 //                  the int8 GEMV's in-stream fp16 side product reads them with the chunk's weights
@@ -36,13 +38,13 @@ struct I8Offsets {
 };
 __host__ __device__ inline I8Offsets i8_offsets(int M, int K) {
   I8Offsets o;
-  o.part = 16;
+  o.aq = 16;
+  o.part = i8_align16(o.aq + (size_t)M * K);
   o.cnt = o.part + sizeof(float) * (size_t)kNSB * M;
   o.list = o.cnt + sizeof(int) * kNSB;
   o.sca = o.list + sizeof(int) * (size_t)kNSB * i8_kb(K);
   o.flag = i8_align16(o.sca + sizeof(float) * (size_t)M);
-  o.aq = i8_align16(o.flag + (size_t)K);
-  o.avh = i8_align16(o.aq + (size_t)M * K);
+  o.avh = i8_align16(o.flag + (size_t)K);
   o.aval = o.avh + 16;
   o.total = o.aval + (size_t)16 * kNSB * i8_kb(K);
   return o;

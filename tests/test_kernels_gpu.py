@@ -745,12 +745,12 @@ def _check_i8_ws(ws, a, M, K, thr=6.0):
     flag = out.any(0)
     small = np.where(out, 0.0, a16)
     al = lambda x: (x + 15) & ~15  # noqa: E731
-    o_part = 16
+    o_aq = 16  # the quantized rows first (csrc/i8ws.h), then the statistics
+    o_part = al(o_aq + M * K)
     o_cnt = o_part + 4 * nsb * M
     o_list = o_cnt + 4 * nsb
     o_sca = o_list + 4 * nsb * kb
     o_flag = al(o_sca + 4 * M)
-    o_aq = al(o_flag + K)
     hdr = ws[:16].view(np.int32)
     assert list(hdr) == [M, K, nsb, kb]
     part = ws[o_part:o_cnt].view(np.float32).reshape(nsb, M)
@@ -816,9 +816,10 @@ def _i8_ws_stats(hip, A, M, K):
     call(hip, "llj_i8_stats", A.data_ptr(), A.stride(0), M, K, 6.0, ws.data_ptr(), st())
     torch.cuda.synchronize()
     raw = ws.cpu().numpy()
-    # i8ws.h layout: header, part[32][M], cnt[32], list[32][kb], sca[M], flag[K] (16-B aligned)
+    # i8ws.h layout: header, aq[M][K], part[32][M], cnt[32], list[32][kb], sca[M], flag[K] (16-B aligned)
     kb = ((K + 31) // 32 + 31) & ~31
-    o_sca = 16 + 4 * 32 * M + 4 * 32 + 4 * 32 * kb
+    o_part = (16 + M * K + 15) & ~15
+    o_sca = o_part + 4 * 32 * M + 4 * 32 + 4 * 32 * kb
     o_flag = (o_sca + 4 * M + 15) & ~15
     return raw[o_sca:o_sca + 4 * M].view(np.float32), raw[o_flag:o_flag + K] != 0
 

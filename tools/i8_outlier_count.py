@@ -33,7 +33,8 @@ def main():
 
     def count(ws_ptr, M, K):
         torch.cuda.synchronize()
-        off_cnt = 16 + 4 * 32 * M  # i8ws.h: header, per-(k-block, row) absmax, then the 32 per-block counts
+        # i8ws.h: header, the quantized rows, per-(k-block, row) absmax, then the 32 per-block counts
+        off_cnt = ((16 + M * K + 15) & ~15) + 4 * 32 * M
         host = (ctypes.c_int * 32)()
         hip_memcpy(host, ctypes.c_void_p(ws_ptr + off_cnt), ctypes.c_size_t(128), 3)
         stats[(M, K)].append(sum(host))
