@@ -75,7 +75,8 @@ __host__ __device__ constexpr bool am_stream(int am) { return am == AM_STREAM ||
 #define LLJ_I8Q_FAST 1  // AM_I8Q: 1 quant8_fast for rows with SCA >= 1/64, 0 quant8f always
 #endif
 constexpr int kQRow = 144;
-constexpr int kQSlotBytes = 8 * kQRow + 128 * 16;
+constexpr int kQSlotBytes = 8 * kQRow + 128 * 32;  // AM_I8Q: + the outlier columns' f16(A) as fp32 (32 B per column)
+constexpr int kQSlotBytesS = 8 * kQRow;            // AM_I8S: the int8 rows only
 enum : int { EP_STORE = 0, EP_RESID = 1, EP_QKV = 2, EP_SWIGLU = 3 };
 
 // int8 activation workspace written by llj_i8_stats (int8.hip): i8ws.h
@@ -495,7 +496,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   constexpr bool I8S = (AM == AM_I8S);  // int8 rows of the statistics workspace streamed per chunk
   static_assert(!I8S || (I8 && MB == 8 && TPW == 1), "AM_I8S: int8, batched rows, one tile per workgroup");
   constexpr bool ASTR = STRM || I8Q;  // bf16 A rows streamed per chunk
-  constexpr bool QRING = I8Q || I8S;  // int8 rows through the per-wave ring (kQSlotBytes slots)
+  constexpr bool QRING = I8Q || I8S;  // int8 rows through the per-wave ring
+  constexpr int QSB = I8Q ? kQSlotBytes : kQSlotBytesS;  // its slot bytes
   constexpr bool ALDS = (I8 && !QRING) || (AM != AM_GLOBAL && !STRM && !QRING);
   // row sums of A for the nibble offset: an extra MFMA against a ones fragment for the global-A
   // form and for batched norm-fused rows (LLJ_SACC_NORM; the VALU sums + 8 wave reductions of the
@@ -521,7 +523,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   // scratch] [tail: 128 words for staging scratch / int8 SCA]
   const int a_stride = I8 ? K + 16 : K + 8;  // elements (bytes for int8)
   const size_t a_bytes = ALDS ? (((size_t)M * a_stride * (I8 ? 1 : 2) + 15) & ~(size_t)15)
-                              : STRM ? (size_t)NW * 2 * kSSlot * 2 : QRING ? (size_t)NW * 2 * kQSlotBytes : 0;
+                              : STRM ? (size_t)NW * 2 * kSSlot * 2 : QRING ? (size_t)NW * 2 * QSB : 0;
   constexpr int NV = 8 * TPW + 4;  // reduction words per lane: acc, acc2 of every tile, sacc
   constexpr size_t kRedBytes = (size_t)NW * 64 * NV * 4;
   constexpr size_t kScratch = kRedBytes + (I8 ? (size_t)2 * NW * 8 * 16 * 4 : 0);  // + int8 side partials
@@ -693,7 +695,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     // wave's ring slot d % 2, read back as MFMA fragments (one wave writes and reads its own slot:
     // LDS keeps a wave's accesses in order, no barrier)
     bf16_t* slot = reinterpret_cast<bf16_t*>(smem) + (size_t)(wave * 2 + (d & 1)) * kSSlot;
-    unsigned char* qslot = smem + (size_t)(wave * 2 + (d & 1)) * kQSlotBytes;
+    unsigned char* qslot = smem + (size_t)(wave * 2 + (d & 1)) * QSB;
     if constexpr (I8S) *reinterpret_cast<u32x4*>(qslot + (lane >> 3) * kQRow + 16 * (lane & 7)) = s8[d];
     if constexpr (I8Q) {
       // quantize the lane's two row segments (LLM.int8 rows with the producer's SCA and outlier bits)
@@ -716,7 +718,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         // k = 64 t + 16 g + j (t = 0, 1; j < 16) of the chunk. The outlier columns' f16(A) of all 8
         // rows go to a column-major table in the slot (16 B per column: one read per column), each
         // lane writing the outlier columns of its own two row segments
-        _Float16* ocol = reinterpret_cast<_Float16*>(qslot + 8 * kQRow);
+        float* ocol = reinterpret_cast<float*>(qslot + 8 * kQRow);  // f16(A) values held as fp32: no convert per read
         // Registers a loop reads are pinned first (an empty asm that "writes" them): a loop reading
         // a register its load is still filling gets a vmcnt(0) inside it -- which also waits for
         // the weight prefetch of the next chunks (measured: the down projection's side product
@@ -726,8 +728,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         for (uint32_t rb = fb; rb; rb &= rb - 1u) {  // divergent, usually no or one column
           const int e = __builtin_ctz(rb), kc = 8 * seg + e;
           const uint32_t w0 = p0[e >> 1], w1 = p1[e >> 1];
-          ocol[8 * kc + (lane >> 4)] = (_Float16)((e & 1) ? bfhi(w0) : bflo(w0));
-          ocol[8 * kc + (lane >> 4) + 4] = (_Float16)((e & 1) ? bfhi(w1) : bflo(w1));
+          ocol[8 * kc + (lane >> 4)] = f16r((e & 1) ? bfhi(w0) : bflo(w0));
+          ocol[8 * kc + (lane >> 4) + 4] = f16r((e & 1) ? bfhi(w1) : bflo(w1));
         }
         const uint32_t m32 = ((pick(grp >> 1) >> (16 * (grp & 1))) & 0xFFFFu) |
                              (((pick(2 + (grp >> 1)) >> (16 * (grp & 1))) & 0xFFFFu) << 16);
@@ -765,24 +767,23 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
           const int j1 = v1 ? __builtin_ctz(rem) : 0;
           rem &= rem - 1u;
           // f16(A) of rows 0..7 of both columns (a lane without a column reads a valid slot, unused)
-          const u32x4 ov0 = *reinterpret_cast<const u32x4*>(ocol + 8 * kk_of(j0));
-          const u32x4 ov1 = *reinterpret_cast<const u32x4*>(ocol + 8 * kk_of(j1));
-          auto acc_col = [&](int jb, const u32x4 ov) {
+          const float4 oa0 = *reinterpret_cast<const float4*>(ocol + 8 * kk_of(j0));
+          const float4 ob0 = *reinterpret_cast<const float4*>(ocol + 8 * kk_of(j0) + 4);
+          const float4 oa1 = *reinterpret_cast<const float4*>(ocol + 8 * kk_of(j1));
+          const float4 ob1 = *reinterpret_cast<const float4*>(ocol + 8 * kk_of(j1) + 4);
+          auto acc_col = [&](int jb, const float4 oa, const float4 ob) {
             const float w = f16r(cbyte(c0, c1, jb) * i8scb);
-            float a16[8];
+            const float a16[8] = {oa.x, oa.y, oa.z, oa.w, ob.x, ob.y, ob.z, ob.w};
 #pragma unroll
-            for (int m = 0; m < 8; ++m) {
-              a16[m] = (float)__builtin_bit_cast(_Float16, (uint16_t)((ov[m >> 1] >> (16 * (m & 1))) & 0xFFFFu));
-              sd[m] += a16[m] * w;
-            }
+            for (int m = 0; m < 8; ++m) sd[m] += a16[m] * w;
             if constexpr (DUAL) {
               const float w2 = f16r(cbyte(e0, e1, jb) * i8scb2);
 #pragma unroll
               for (int m = 0; m < 8; ++m) sd2[m] += a16[m] * w2;
             }
           };
-          if (v0) acc_col(j0, ov0);
-          if (v1) acc_col(j1, ov1);
+          if (v0) acc_col(j0, oa0, ob0);
+          if (v1) acc_col(j1, oa1, ob1);
         }
       }
     }
@@ -1514,7 +1515,8 @@ constexpr int kNW = LLJ_NW;
 constexpr int kD = LLJ_D;
 
 static inline size_t a_image_bytes(int wf, int am, int M, int K, int nw = kNW) {
-  if (am == AM_I8Q || am == AM_I8S) return (size_t)nw * 2 * kQSlotBytes;  // per-wave 2-slot rings
+  if (am == AM_I8Q) return (size_t)nw * 2 * kQSlotBytes;  // per-wave 2-slot rings
+  if (am == AM_I8S) return (size_t)nw * 2 * kQSlotBytesS;
   if (wf == WF_I8) return (((size_t)M * (K + 16)) + 15) & ~(size_t)15;
   if (am == AM_GLOBAL) return 0;
   if (am_stream(am)) return (size_t)nw * 2 * kSSlot * 2;  // per-wave 2-slot rings
