@@ -735,31 +735,22 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
                              (((pick(2 + (grp >> 1)) >> (16 * (grp & 1))) & 0xFFFFu) << 16);
         if constexpr ((LLJ_ABL & 8) != 0) continue_side = false;
         // each k group walks its own outlier columns (ascending j: the per-lane order of a walk over
-        // the union); trip count = the most any group holds in this chunk (uniform, from the words),
-        // two columns per trip so that their table reads share one LDS latency
-        auto pc16 = [](uint32_t v, int h) { return __builtin_popcount((v >> (16 * h)) & 0xFFFFu); };
-        const int niter = continue_side ? uniform(max(max(pc16(fw[0], 0) + pc16(fw[2], 0), pc16(fw[0], 1) + pc16(fw[2], 1)),
-                                                      max(pc16(fw[1], 0) + pc16(fw[3], 0), pc16(fw[1], 1) + pc16(fw[3], 1))))
-                                        : 0;
+        // the union), two columns per trip so that their table reads share one LDS latency; the walk
+        // ends when no lane has a column left (a ballot per trip, no per-chunk trip count)
         u32x4 c0 = r1[d][0][0], c1 = r1[d][0][1];
         u32x4 e0 = DUAL ? r2[d][0][0] : c0, e1 = DUAL ? r2[d][0][1] : c1;
         asm volatile("" : "+v"(c0), "+v"(c1));  // pinned before the loop (see above)
         if constexpr (DUAL) asm volatile("" : "+v"(e0), "+v"(e1));
         auto cbyte = [](const u32x4 lo, const u32x4 hi, int j) {  // int8 code j (0..31, per lane) as float
-          const int wi = j >> 2;
-          uint32_t wd = lo[0];
-          wd = wi == 1 ? lo[1] : wd;
-          wd = wi == 2 ? lo[2] : wd;
-          wd = wi == 3 ? lo[3] : wd;
-          wd = wi == 4 ? hi[0] : wd;
-          wd = wi == 5 ? hi[1] : wd;
-          wd = wi == 6 ? hi[2] : wd;
-          wd = wi == 7 ? hi[3] : wd;
+          const bool h = (j & 16) != 0;  // the 16-byte half, then the word in it (selects, no indexing)
+          const int wi = (j >> 2) & 3;
+          const uint32_t a = h ? hi[0] : lo[0], b = h ? hi[1] : lo[1], c = h ? hi[2] : lo[2], e = h ? hi[3] : lo[3];
+          const uint32_t wd = wi == 0 ? a : wi == 1 ? b : wi == 2 ? c : e;
           return (float)(int)(int8_t)((wd >> (8 * (j & 3))) & 0xFFu);
         };
         auto kk_of = [&](int jb) { return 64 * (jb >> 4) + 16 * grp + (jb & 15); };
-        uint32_t rem = m32;
-        for (int it = 0; it < niter; it += 2) {
+        uint32_t rem = continue_side ? m32 : 0u;
+        while (__ballot(rem != 0u) != 0ull) {
           const bool v0 = rem != 0u;
           const int j0 = v0 ? __builtin_ctz(rem) : 0;
           rem &= rem - 1u;
