@@ -24,7 +24,7 @@ summarize() {
 }
 B8="--batch 8 --steps 4 --warmup 1 --decode-only --eager"
 C3="--batch 8 --steps 4 --warmup 1 --decode-only --eager --quantize llm.int8"
-SQ="SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_VALU_MFMA_BUSY_CYCLES,SQ_WAIT_ANY,GRBM_GUI_ACTIVE"
+SQ="SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_VALU_MFMA_BUSY_CYCLES,SQ_WAIT_ANY,SQ_INSTS_VALU,SQ_ACTIVE_INST_VALU,GRBM_GUI_ACTIVE"
 for p in $PASSES; do
   a=$B8; [ $p = c3 ] && a=$C3; [ $p = bs1 ] && a="--batch 1 --steps 4 --warmup 1 --decode-only --eager"
   run ${p}_fetch "FETCH_SIZE" "$a"
