@@ -62,7 +62,19 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&ws, llj_i8_ws_bytes(M, K > N ? K : N)));
   void* st = nullptr;
   CK(hipMalloc(&st, llj_i8_rowstats_bytes(K)));
-  CK(hipMemset(st, 0, llj_i8_rowstats_bytes(K)));
+  {  // a realistic hand-off block: SCA 4.0 for rows 0..7 in slot 0, ~K/40 outlier columns (i8ws.h layout)
+    std::vector<uint32_t> w(llj_i8_rowstats_bytes(K) / 4, 0u);
+    const float sca = 4.f;
+    uint32_t sbits;
+    memcpy(&sbits, &sca, 4);
+    for (int m = 0; m < 8; ++m) w[16 + m] = sbits;
+    srand(7);
+    for (int i = 0; i < K / 40; ++i) {
+      const int k = rand() % K;
+      w[16 + 8 * 64 + k / 32] |= 1u << (k % 32);
+    }
+    CK(hipMemcpy(st, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+  }
   int rc = 0;
   for (int r = 0; r < reps && rc == 0; ++r) {
     if (!strcmp(op, "i8")) {

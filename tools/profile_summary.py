@@ -96,8 +96,13 @@ def main():
         out["passes"][tag] = sorted(names)
     for key, cs in groups.items():
         tag, n, grid = key.split("|")
-        prefix = tag.split("_")[0]  # bs1 / bs8 / c1 / c3 / c3b8 (int8 bs=8 decode in 4-row slices)
-        k = out["kernels"].setdefault(f"{n} grid {grid}", {"op": op_of(n, int(grid), multi=prefix in ("bs8", "c3b8", "c3"))})
+        prefix = tag.split("_")[0]  # bs1 / bs8 / c1 / c3 / c3b8 (int8 bs=8 decode in 4-row slices) / c3h
+        op = op_of(n, int(grid), multi=prefix in ("bs8", "c3b8", "c3", "c3h"))
+        if prefix == "c3h" and op:  # the C++ harness at one C3 shape per run: the op is in the tag
+            op = {"qkv": "qkv", "head": "lm_head", "swiglu": "swiglu", "cproj": "attn.c_proj",
+                  "down": "mlp.c_proj"}.get(tag.split("_")[1], op)
+            prefix = "c3h_" + tag.split("_")[1]
+        k = out["kernels"].setdefault(f"{n} grid {grid}" + (f" ({prefix})" if prefix.startswith("c3h") else ""), {"op": op})
         ent = k.setdefault(prefix, {})
         ent["dispatches"] = max(ent.get("dispatches", 0), max(len(v) for v in cs.values()))
         for c, v in cs.items():
@@ -112,7 +117,7 @@ def main():
                 if prefix in ("bs1", "bs8") and k["op"]:
                     ent["algorithmic_bytes"] = algo_bytes_int4(k["op"], 8 if prefix == "bs8" else 1)
                     ent["traffic_over_algorithmic"] = round(ent["hbm_bytes"] / ent["algorithmic_bytes"], 3)
-                elif prefix in ("c3", "c3b8") and k["op"] and name.startswith("llj::gemv_kernel<2,"):
+                elif (prefix in ("c3", "c3b8") or prefix.startswith("c3h")) and k["op"] and name.startswith("llj::gemv_kernel<2,"):
                     ent["algorithmic_bytes"] = algo_bytes_int8(k["op"], 4 if prefix == "c3b8" else 8)
                     ent["traffic_over_algorithmic"] = round(ent["hbm_bytes"] / ent["algorithmic_bytes"], 3)
             if "SQ_VALU_MFMA_BUSY_CYCLES" in ent and ent.get("GRBM_GUI_ACTIVE"):
