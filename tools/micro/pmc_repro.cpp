@@ -3,7 +3,8 @@
 // bisected by argv under `rocprofv3 --pmc FETCH_SIZE -- ./pmc_repro <op> <M> <N> <K>`.
 //   op: i8 (llj_linear, LLM.int8, workspace from llj_i8_stats), i8q (llj_i8_linear_resid),
 //       w4 (llj_linear, int4 W4P), i8swiglu (llj_norm_swiglu wfmt 2), prep (llj_i8_norm_stats),
-//       qw (llj_i8_quant_weight of an M x K bf16 matrix), gemm_i8 (llj_i8_stats + llj_gemm_i8_linear)
+//       qw (llj_i8_quant_weight of an M x K bf16 matrix), gemm_i8 (llj_i8_stats + llj_gemm_i8_linear),
+//       atti8 (llj_attention_i8: M rows, N = n_embd, a K-slot cache)
 // Build: hipcc --offload-arch=gfx950 -O2 pmc_repro.cpp -I../../include -L../../lit-llama-ja_amd/lit_llama
 //        -l:_lljamd.so -Wl,-rpath,'$ORIGIN/../../lit-llama-ja_amd/lit_llama' -o pmc_repro
 #include <hip/hip_runtime.h>
@@ -92,6 +93,23 @@ int main(int argc, char** argv) {
     } else if (!strcmp(op, "gemm_i8")) {  // prefill: statistics of M rows + the LLM.int8 GEMM
       rc = llj_i8_stats(A, K, M, K, 6.f, ws, s);
       if (!rc) rc = llj_gemm_i8_linear(A, K, W, sz, ws, nullptr, nullptr, 0, C, N, M, N, K, s);
+    } else if (!strcmp(op, "atti8")) {  // decode attention of M rows over a K-slot cache, LLM.int8 statistics of y
+      // (N = n_embd, 128-dim heads; the cache holds positions 0..K-1, the rows attend at position K/2)
+      // (its own q (M x N), y statistics block for N columns and caches: the shared buffers are sized by K)
+      static void *kc = nullptr, *vc = nullptr, *pos = nullptr, *q = nullptr, *yst = nullptr;
+      const int nh = N / 128, S = K;
+      if (!kc) {
+        q = dev_rand((size_t)M * N * 2, 10, 0);
+        CK(hipMalloc(&yst, llj_i8_rowstats_bytes(N)));
+        CK(hipMemset(yst, 0, llj_i8_rowstats_bytes(N)));
+        kc = dev_rand((size_t)M * nh * S * 128 * 2, 8, 0);
+        vc = dev_rand((size_t)M * nh * S * 128 * 2, 9, 0);
+        std::vector<int> hp(M, S / 2);
+        CK(hipMalloc(&pos, M * sizeof(int)));
+        CK(hipMemcpy(pos, hp.data(), M * sizeof(int), hipMemcpyHostToDevice));
+      }
+      if (N % 128 || M > 8) { fprintf(stderr, "atti8: N %% 128 == 0, M <= 8\n"); return 2; }
+      rc = llj_attention_i8(q, kc, vc, C, (const int*)pos, M, 1, nh, 128, S, 1, nullptr, yst, nullptr, 0, 6.f, s);
     } else if (!strcmp(op, "w4")) {
       rc = llj_linear(0, A, K, W, sz, nullptr, C, N, M, N, K, nullptr, 0, nullptr, s);
     } else {

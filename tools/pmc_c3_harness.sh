@@ -16,7 +16,7 @@ summarize() {
 }
 # op tag -> harness args (M N K): QKV / lm_head shapes on the workspace GEMV (AM_I8S, store epilogue),
 # SwiGLU, attn.c_proj / mlp.c_proj on the hand-off GEMV (AM_I8Q), the norm + statistics launch
-CASES="qkv:i8:8:12288:4096 head:i8:8:32000:4096 swiglu:i8swiglu:8:11008:4096 cproj:i8q:8:4096:4096 down:i8q:8:4096:11008 prep:prep:8:4096:4096"
+CASES=${C3H_CASES:-"qkv:i8:8:12288:4096 head:i8:8:32000:4096 swiglu:i8swiglu:8:11008:4096 cproj:i8q:8:4096:4096 down:i8q:8:4096:11008 prep:prep:8:4096:4096 attn:atti8:8:4096:144"}
 for cc in $CASES; do
   IFS=: read tag op m n k <<< "$cc"
   for pass in fetch write sq; do
