@@ -24,7 +24,11 @@ Also reported, on the same JSON line:
   cpu_baseline  the numpy port of the reference's CPU path (oracle/, dequantize-every-call
                 like ColBlockQuantizedLinear's fallback, quantization.py:420-421) timed on a
                 bounded sample (one decode token through a few layers, scaled to 32);
-  bs8           the same workload at batch 8 (aggregate tokens/s and its step roofline).
+  bs8           the same workload at batch 8 (aggregate tokens/s and its step roofline);
+  c4_13b        BASELINE configs[4]: LLaMA-13B gptq.int4 bs=1 on every replica;
+  c1_bf16       BASELINE configs[1]: LLaMA-7B bf16 (unquantized) bs=1;
+  c3_int8       BASELINE configs[3]: LLaMA-7B llm.int8 bs=8 (random weights' outlier columns; `regimes`
+                adds SURVEY §8d's 6 columns x20).
 """
 from __future__ import annotations
 
@@ -478,6 +482,26 @@ def c4_leg(args, ws):
     return out
 
 
+def config_leg(args, ws, name: str, mode, B: int, outliers=None, workload: str = ""):
+    """One more BASELINE.json config on the same replicas and timing as the headline: C1 (LLaMA-7B
+    bf16, bs=1; reference generate.py:121 bf16-true) and C3 (LLaMA-7B llm.int8, bs=8, reference
+    quantization.py:36-75) in the outlier regimes of build_model. The model is built, timed and freed
+    here, so the legs never hold two 7B models at once."""
+    import gc
+
+    m = build_model(name, mode, outliers=outliers)
+    r = time_decode(m, B, args.prompt_len, args.max_seq_length, args.warmup, args.steps, ws)
+    t, tok = aggregate(r["seconds"], r["tokens"], ws)
+    sb = step_bytes(m, B, r["pos_mean"])
+    out = {"workload": workload, "value": round(tok / t, 2), "unit": "tokens/s", "n_replicas": ws, "batch": B,
+           "ms_per_step": round(t / args.steps * 1e3, 4),
+           "step_roofline_frac": round(sb / (r["seconds"] / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}
+    del r["session"], m
+    gc.collect()
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -491,6 +515,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bs8", action="store_true")
     ap.add_argument("--no-c4", action="store_true", help="skip the LLaMA-13B replica leg (C4)")
+    ap.add_argument("--no-configs", action="store_true", help="skip the C1 (7B bf16 bs=1) and C3 (7B llm.int8 bs=8) legs")
     ap.add_argument("--only-dominant", action="store_true",
                     help="profiling aid: only the dominant-kernel loop (for the PMC traffic passes)")
     ap.add_argument("--decode-only", action="store_true",
@@ -571,11 +596,25 @@ def main():
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and mode == "gptq.int4":
         cpu = cpu_baseline(model)
 
-    c4 = None
-    if not args.no_c4 and args.model == "7B" and mode == "gptq.int4":
+    c4 = c1 = c3 = None
+    legs = args.model == "7B" and mode == "gptq.int4"
+    r.pop("session", None)  # the headline's numbers stay in r; its graph and cache are freed
+    if legs:
         del model
+        import gc
+
+        gc.collect()
         torch.cuda.empty_cache()
+    if not args.no_c4 and legs:
         c4 = c4_leg(args, ws)
+    if not args.no_configs and legs:
+        c1 = config_leg(args, ws, "7B", None, 1,
+                        workload="LLaMA-7B bf16 (unquantized) greedy decode, batch 1 per replica (BASELINE configs[1])")
+        c3 = config_leg(args, ws, "7B", "llm.int8", 8,
+                        workload="LLaMA-7B --quantize llm.int8 greedy decode, batch 8 per replica (BASELINE configs[3]); "
+                                 "outlier columns: the random weights' own")
+        c3["regimes"] = {"6x20": config_leg(args, ws, "7B", "llm.int8", 8, outliers="6x20",
+                                            workload="C3 with SURVEY 8d's regime: 6 columns of every Linear input x20")}
 
     if rank == 0:
         name = {"gptq.int4": "gptq.int4", "llm.int8": "llm.int8", "none": "bf16"}[args.quantize]
@@ -621,6 +660,8 @@ def main():
             "cpu_baseline": cpu,
             "bs8": bs8,
             "c4_13b": c4,
+            "c1_bf16": c1,
+            "c3_int8": c3,
         }
         print(json.dumps(line), flush=True)
     if ws > 1:

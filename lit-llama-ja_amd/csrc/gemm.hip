@@ -459,9 +459,10 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
     int* s_k = s_pre + 64;                      // [kSideK] this round's columns
     _Float16* sa16 = reinterpret_cast<_Float16*>(smem + 512);          // [128 rows][kSideP]
     _Float16* sb16 = sa16 + BM * kSideP;                               // [128 columns][kSideP]
-    const I8WsHeader h8 = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
+    I8WsHeader h8 = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
+    h8.nsb = i8_nsb_clamp(h8.nsb);
     if (tid < 64) {
-      const int cn = tid < h8.nsb ? L8.cnt[tid] : 0;
+      const int cn = tid < h8.nsb ? i8_cnt_clamp(L8.cnt[tid], h8.kb) : 0;
       int x = cn;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
@@ -526,7 +527,7 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
         if (fi < total) {
           int b = 0;
           while (b + 1 < h8.nsb && s_pre[b + 1] <= fi) ++b;
-          k = L8.list[b * h8.kb + (fi - s_pre[b])];
+          k = i8_col_clamp(L8.list[b * h8.kb + (fi - s_pre[b])], p.K);
         }
         s_k[tid] = k;
       }

@@ -262,15 +262,16 @@ __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float*
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nl = tid & 15, g = tid >> 4;
   constexpr int NG = NW * 4, NT = NW * 64;
-  const I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
+  I8WsHeader h = *reinterpret_cast<const I8WsHeader*>(p.i8ws);
   const I8Layout L = i8_layout(p.i8ws, h.mtot, h.K);
+  h.nsb = i8_nsb_clamp(h.nsb);  // counts and list entries bounded by what they index (i8ws.h)
   int* s_pre = reinterpret_cast<int*>(stage);           // [kNSB + 1] prefix of the block counts
   int* s_k = s_pre + 64;                                // [kSideChunk] column indices
   float* s_a = reinterpret_cast<float*>(s_k + kSideChunk);  // [8][kSideChunk] f16(A) values
   const int n = n0 + nl, M = p.M;
   const float scb = SCB[n] / 127.f;
   if (tid < 64) {  // prefix sum of the per-block outlier counts (kNSB <= 64; cnt_lane = cnt[lane], loaded early)
-    int c = tid < h.nsb ? cnt_lane : 0;
+    int c = tid < h.nsb ? i8_cnt_clamp(cnt_lane, h.kb) : 0;
     int x = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -298,7 +299,7 @@ __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float*
       const int q = tid + NT * e, b = q / SPC, j = q % SPC;
       const bool mine = b < h.nsb && j < s_pre[b + 1] - s_pre[b];
       ie[e] = mine ? s_pre[b] + j : -1;
-      const int k = mine ? spk[e] : 0, kk = k & 127;  // (k = 0: a valid address, never stored)
+      const int k = mine ? i8_col_clamp(spk[e], p.K) : 0, kk = k & 127;  // (k = 0: a valid address, never stored)
 #pragma unroll
       for (int m = 0; m < 8; ++m) av[e][m] = bf2f(p.A[(size_t)(m < M ? m : 0) * p.lda + k]);
       const int8_t* cbp = CB + (((size_t)(n0 >> 4) * (p.K >> 7) + (k >> 7)) * 2 + (kk >> 6)) * 1024 +
@@ -335,7 +336,7 @@ __device__ void i8_side_tile(const GemvParams& p, const int8_t* CB, const float*
       const int fi = c0 + i;
       int b = 0;
       while (b + 1 < h.nsb && s_pre[b + 1] <= fi) ++b;  // blocks are few (kNSB)
-      const int k = L.list[b * h.kb + (fi - s_pre[b])];
+      const int k = i8_col_clamp(L.list[b * h.kb + (fi - s_pre[b])], p.K);
       s_k[i] = k;
 #pragma unroll
       for (int m = 0; m < 8; ++m)

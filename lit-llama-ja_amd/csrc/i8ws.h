@@ -32,6 +32,14 @@ __host__ __device__ inline int i8_kb(int K) { return ((K + kNSB - 1) / kNSB + 31
 
 __host__ __device__ inline size_t i8_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// A count or a list entry read back from a workspace is bounded by what it indexes before use: a
+// stale or corrupt workspace (a count past kb, a column outside [0, K)) then gives wrong numbers,
+// never an out-of-bounds read (the r05i fault: a prep variant that skipped the list compaction left
+// the counts stale and the side product walked past the list)
+__host__ __device__ inline int i8_cnt_clamp(int c, int kb) { return c < 0 ? 0 : (c > kb ? kb : c); }
+__host__ __device__ inline int i8_col_clamp(int k, int K) { return k < 0 ? 0 : (k >= K ? K - 1 : k); }
+__host__ __device__ inline int i8_nsb_clamp(int nsb) { return nsb < 0 ? 0 : (nsb > kNSB ? kNSB : nsb); }
+
 // byte offsets of the arrays (the layout above)
 struct I8Offsets {
   size_t part, cnt, list, sca, flag, aq, avh, aval, total;

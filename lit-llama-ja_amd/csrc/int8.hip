@@ -364,6 +364,7 @@ __global__ __launch_bounds__(1024) void i8_prep_one_kernel(const bf16_t* __restr
       st[kI8StFlags + (k0 >> 5) + wd] = bits;
     }
   }
+  if ((LLJ_PREP_ABL & 8) && tid == 0) L.cnt[b] = 0;  // the ablation skips the list, never the count a consumer reads
   if (tid < 64 && !(LLJ_PREP_ABL & 8)) {  // compact the flags into the list, 64 columns per ballot
     int c = 0;
     for (int i0 = 0; i0 < k1 - k0; i0 += 64) {
@@ -491,8 +492,9 @@ __global__ __launch_bounds__(256) void i8_quant_weight_kernel(const void* __rest
 // when the count exceeds it nothing is gathered and the GEMM runs its per-tile side product.
 __device__ __forceinline__ int i8_flat_list(const I8Layout& L, const I8WsHeader& h, int* s_pre, int* s_list, int cap) {
   const int tid = threadIdx.x, lane = tid & 63;
+  const int nsb = i8_nsb_clamp(h.nsb);
   if (tid < 64) {
-    const int c = tid < h.nsb ? L.cnt[tid] : 0;
+    const int c = tid < nsb ? i8_cnt_clamp(L.cnt[tid], h.kb) : 0;
     int x = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -503,11 +505,12 @@ __device__ __forceinline__ int i8_flat_list(const I8Layout& L, const I8WsHeader&
     if (tid == 0) s_pre[0] = 0;
   }
   __syncthreads();
-  if (s_pre[h.nsb] > cap) return s_pre[h.nsb];  // over capacity: the caller gathers nothing
-  for (int b = 0; b < h.nsb; ++b)
-    for (int j = tid; j < s_pre[b + 1] - s_pre[b]; j += blockDim.x) s_list[s_pre[b] + j] = L.list[b * h.kb + j];
+  if (s_pre[nsb] > cap) return s_pre[nsb];  // over capacity: the caller gathers nothing
+  for (int b = 0; b < nsb; ++b)
+    for (int j = tid; j < s_pre[b + 1] - s_pre[b]; j += blockDim.x)
+      s_list[s_pre[b] + j] = i8_col_clamp(L.list[b * h.kb + j], h.K);
   __syncthreads();
-  return s_pre[h.nsb];
+  return s_pre[nsb];
 }
 
 __global__ __launch_bounds__(256) void i8_gather_act_kernel(const bf16_t* __restrict__ A, int lda, const char* __restrict__ ws,
@@ -550,7 +553,7 @@ __global__ __launch_bounds__(256) void i8_gather_weight_kernel(const int8_t* __r
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int j = j0 + 16 * u;
-      const int k = j < total ? s_list[j] : 0, kk = k & 127;
+      const int k = j < total ? i8_col_clamp(s_list[j], K) : 0, kk = k & 127;
       q[u] = CB[(((size_t)nt * (K >> 7) + (k >> 7)) * 2 + (kk >> 6)) * 1024 + (16 * ((kk >> 4) & 3) + r) * 16 + (kk & 15)];
     }
 #pragma unroll
@@ -567,6 +570,9 @@ static int i8_prep_one(bool norm, const bf16_t* x, int lda, const bf16_t* w, flo
                        float thr, void* ws, void* stream, uint32_t* st = nullptr) {
   const int kb = i8_kb(K), vpt = (K / 8 + 255) / 256;
   if (M > 8 || vpt > (norm ? 4 : 6) || M * (kb / 8) > 1024 || lda % 8) return 1;
+  // its row maximum compares bf16 values with thr and rounds the maximum to fp16 once, which is the
+  // per-element fp16 rule only for 2^-14 <= thr <= 65504 (fp16's normal range): else the two passes
+  if (!(thr >= 0x1p-14f && thr <= 65504.f)) return 1;
   hipStream_t s = (hipStream_t)stream;
 #define LLJ_P1(N, V) \
   hipLaunchKernelGGL((i8_prep_one_kernel<N, V>), dim3(kNSB), dim3(1024), 0, s, x, lda, w, eps, xn, M, K, thr, (char*)ws, kb, st)

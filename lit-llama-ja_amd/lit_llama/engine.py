@@ -102,7 +102,22 @@ class DecodeSession:
             _enable_i8_handoff(self.work, self.specs)
         self.graph = None  # the caches / operands may have changed
 
+    def _reset_handoff(self):
+        """The LLM.int8 hand-off blocks (_Work.y_st / h_st) must be zero when a step starts; a
+        completed step leaves them so, a step that raised part-way may not: zero them again."""
+        w = self.work
+        if w is not None and getattr(w, "y_st", None) is not None:
+            w.y_st.zero_()
+            w.h_st.zero_()
+
     def _step(self):
+        try:
+            self._step_launches()
+        except BaseException:
+            self._reset_handoff()
+            raise
+
+    def _step_launches(self):
         m, w, B = self.model, self.work, self.B
         cfg = m.config
         st = _hip.stream()

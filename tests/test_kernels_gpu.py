@@ -1467,3 +1467,85 @@ def test_gemm_grouped_dequant_equals_get_weight_bf16(hip, scale_kind):
     torch.cuda.synchronize()
     wref = O.colblock_get_weight(qw, sc, z, 4, tile_cols=g, bf16=True)
     np.testing.assert_array_equal(out.float().cpu().numpy().T, wref)
+
+
+def _i8_ws_offsets(M, K):
+    """Byte offsets of (cnt, list) in the statistics workspace (csrc/i8ws.h i8_offsets)."""
+    a16 = lambda v: (v + 15) & ~15
+    kb = ((K + 31) // 32 + 31) & ~31
+    part = a16(16 + M * K)
+    cnt = part + 4 * 32 * M
+    return cnt, cnt + 4 * 32, kb
+
+
+@pytest.mark.parametrize("M,K,outliers", [(8, 4096, 3), (8, 11008, 300), (64, 4096, 6)])
+def test_int8_consumers_bound_stale_outlier_counts(hip, M, K, outliers):
+    """Robustness (the r05i fault): a workspace whose per-k-block outlier counts exceed the list width
+    kb and whose list holds columns outside [0, K) must not make the int8 consumers read out of bounds.
+    The GEMV (decode rows: in-stream side product, the after-stream fast and general paths) and, for
+    prompt rows, the gathers + the LLM.int8 GEMM take the counts clamped to kb and the columns clamped
+    to [0, K): the call returns 0, the device reports no fault and the outputs are finite (their
+    values are those of the clamped list, i.e. wrong by design, and are not checked)."""
+    rng = np.random.default_rng(M + K + outliers)
+    N = 256
+    W = bf16(rng.standard_normal((N, K)) * 0.02)
+    cbt, scb, _, _ = _i8_operands(hip, W)
+    xd = T(_i8_act(rng, M, K, outliers), torch.bfloat16)
+    ws = torch.empty(hip.llj_i8_ws_bytes(M, K), dtype=torch.uint8, device=dev)
+    call(hip, "llj_i8_stats", xd.data_ptr(), K, M, K, 6.0, ws.data_ptr(), st())
+    torch.cuda.synchronize()
+    cnt_off, list_off, kb = _i8_ws_offsets(M, K)
+    ws[cnt_off:cnt_off + 4 * 32].view(torch.int32).fill_(1 << 20)  # every block "full" past kb
+    lst = ws[list_off:list_off + 4 * 32 * kb].view(torch.int32)
+    lst.copy_(torch.randint(-(1 << 30), 1 << 30, lst.shape, dtype=torch.int32, device=dev))
+    out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=dev)
+    if M <= 8:
+        call(hip, "llj_linear", 2, xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), None, out.data_ptr(), N, M, N, K,
+             ws.data_ptr(), 0, None, st())
+    else:
+        ao, (g1,), kp, keep = _i8_gather(hip, xd, M, K, ws, [(cbt, scb, N)], True)
+        call(hip, "llj_gemm_i8_linear", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), ao, g1, kp,
+             out.data_ptr(), N, M, N, K, st())
+        out2 = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=dev)
+        call(hip, "llj_gemm_i8_linear", xd.data_ptr(), K, cbt.data_ptr(), scb.data_ptr(), ws.data_ptr(), None, None, 0,
+             out2.data_ptr(), N, M, N, K, st())  # the per-tile side product (no gathers)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out2.float()).all()
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all()
+
+
+@pytest.mark.parametrize("M,regime", [(1, "few"), (8, "few"), (8, "none")])
+def test_int8_statistics_handoff_split_attention(hip, M, regime):
+    """llj_attention_i8 over a long cache (nsplit > 1: key ranges per block, the statistics of y
+    written by attention_combine_kernel, which also zeroes h's block): y equals llj_attention_split's
+    output bitwise, y's SCA and outlier columns equal llj_i8_stats' bitwise, and h's block comes back
+    zero. 7B head shape (32 heads x 128), S = 2048, p = 2000, 16 splits."""
+    rng = np.random.default_rng(2100 + M + len(regime))
+    C, nh, H, S, p0, nsplit = 4096, 32, 11008, 2048, 2000, 16
+    hs = C // nh
+    kc = T(bf16(rng.standard_normal((M, nh, S, hs))), torch.bfloat16)
+    vv = rng.standard_normal((M, nh, S, hs)).astype(np.float32) * (0.5 if regime == "none" else 1.0)
+    if regime == "few":
+        vv[:, 5, :, 9] = 9.0  # one y column >= 6 in every row
+    vc = T(bf16(vv), torch.bfloat16)
+    q = T(bf16(rng.standard_normal((M, C))), torch.bfloat16)
+    pos = T(np.array([p0], np.int32))
+    ws = torch.empty(hip.llj_attention_ws_bytes(M, nh, hs, nsplit), dtype=torch.uint8, device=dev)
+    y = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    y_st = torch.zeros(hip.llj_i8_rowstats_bytes(C) // 4, dtype=torch.int32, device=dev)
+    h_st = torch.full((hip.llj_i8_rowstats_bytes(H) // 4,), 7, dtype=torch.int32, device=dev)  # to be zeroed
+    call(hip, "llj_attention_i8", q.data_ptr(), kc.data_ptr(), vc.data_ptr(), y.data_ptr(), pos.data_ptr(), M, 1, nh,
+         hs, S, nsplit, ws.data_ptr(), y_st.data_ptr(), h_st.data_ptr(), h_st.numel(), 6.0, st())
+    torch.cuda.synchronize()
+    assert not h_st.any()
+    y_ref = torch.empty_like(y)
+    call(hip, "llj_attention_split", q.data_ptr(), kc.data_ptr(), vc.data_ptr(), y_ref.data_ptr(), pos.data_ptr(), M, 1,
+         nh, hs, S, nsplit, ws.data_ptr(), st())
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+    sca_w, fl_w = _i8_ws_stats(hip, y, M, C)
+    sca_s, fl_s = _st_decode(y_st, M, C)
+    np.testing.assert_array_equal(sca_s, sca_w)
+    np.testing.assert_array_equal(fl_s, fl_w)
+    assert fl_s.any() == (regime == "few")
