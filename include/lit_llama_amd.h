@@ -238,6 +238,11 @@ int llj_i8_quant_weight(const void* W, int dtype, void* CB, void* SCB, int N, in
  * trailing update W[:, i2:] -= Err1 · Hinv[i1:i2, i2:] is a plain GEMM left to the caller. */
 int llj_gptq_block(const float* hinv, int K, int i1, float* wt, int N, const float* scale, const float* zero,
                    int bits, float* qt, float* err, float* loss, void* stream);
+/* llj_gptq_block for GPTQQuantizer(blocksize=b) (quantization.py:437, 557-596): the column loop over
+ * the b-column block [i1, i1 + b), b in {16, 32, 64, 128}; err (b, N). Requires i1 % b == 0,
+ * i1 + b <= K. llj_gptq_block is this with b = 128. */
+int llj_gptq_block_bs(const float* hinv, int K, int i1, int blocksize, float* wt, int N, const float* scale,
+                      const float* zero, int bits, float* qt, float* err, float* loss, void* stream);
 /* ColBlockQuantizedLinear.pack_weight (quantization.py:374-388) from reconstructions qt (K, N)
  * fp32: code = uint8(clamp(q / scale + zero, 0, 2^bits - 1)) (truncating), entries_per_byte =
  * 8/bits codes per byte; qw is quant_weight in its column-major storage: byte (n, j) at j*N + n. */

@@ -4,12 +4,14 @@
 // the device, host side); what is specific to GPTQ is the sequential column loop inside a
 // 128-column block (quantization.py:568-596) and the ColBlock packing (pack_weight, 374-388).
 //
-// llj_gptq_block: 8 or 4 lanes per weight row (rows are independent inside a block: the update of
+// llj_gptq_block(_bs): 8 or 4 lanes per weight row (rows are independent inside a block: the update of
 // row r uses only its own error and the shared Hinv1 rows). The block's 128 columns of each row
 // and Hinv1^T sit in LDS (32 or 64 rows per workgroup: 20 + 66 KiB); 16 columns at a time are quantized
 // in registers, then the rest of the block takes their 16 updates per column in one LDS round
 // trip, the columns split over the row's lanes. Weights are passed
 // transposed (Wt: K x N, element (k, n) at k * N + n) so column i of 128 rows is one coalesced load.
+// The block is the reference's `blocksize` (557; 16 / 32 / 64 / 128: whole 16-column register
+// groups, at most the 128 columns the LDS holds).
 // Every arithmetic step is the reference's fp32 op in the reference's order, rounded on its own
 // (this file is built with -ffp-contract=off, lit_llama/_build.py), so a block reproduces the torch CPU
 // loop bitwise given the same W1 and Hinv1.
@@ -35,6 +37,7 @@ constexpr int kHs = kGptqBlock + 1;   // LDS row stride of Hinv1^T (odd: conflic
 // (N / 64) workgroups fill the chip (N / 128 single-lane workgroups used 32-96 CUs at 7B shapes).
 template <int kGptqRows, int kGptqLanes, int kWs>
 __global__ __launch_bounds__(kGptqRows * kGptqLanes) void gptq_block_kernel(const float* __restrict__ hinv, int K, int i1,
+                                                                  int blk,
                                                                   float* __restrict__ wt, int N,
                                                                   const float* __restrict__ scale,
                                                                   const float* __restrict__ zero, float maxq,
@@ -45,18 +48,18 @@ __global__ __launch_bounds__(kGptqRows * kGptqLanes) void gptq_block_kernel(cons
   constexpr int kGptqThreads = kGptqRows * kGptqLanes;
   const int tid = threadIdx.x;
   const int t = tid / kGptqLanes, l = tid % kGptqLanes;
-  for (int v = tid; v < kGptqBlock * kGptqBlock; v += kGptqThreads) {
-    const int i = v / kGptqBlock, j = v % kGptqBlock;
+  for (int v = tid; v < blk * blk; v += kGptqThreads) {
+    const int i = v / blk, j = v % blk;
     hsT[j * kHs + i] = hinv[(size_t)(i1 + i) * K + i1 + j];
   }
   const int n = blockIdx.x * kGptqRows + t;
   const int nn = n < N ? n : N - 1;  // clamped: loads stay in bounds, stores are guarded
   const float s = scale[nn], z = zero[nn];
-  for (int j = l; j < kGptqBlock; j += kGptqLanes) ws[j * kWs + t] = wt[(size_t)(i1 + j) * N + nn];
+  for (int j = l; j < blk; j += kGptqLanes) ws[j * kWs + t] = wt[(size_t)(i1 + j) * N + nn];
   __syncthreads();
   const bool writer = l == 0 && n < N;
   float lsum = 0.f;
-  for (int b = 0; b < kGptqBlock; b += kGptqSub) {
+  for (int b = 0; b < blk; b += kGptqSub) {
     float r[kGptqSub], e[kGptqSub];
 #pragma unroll
     for (int u = 0; u < kGptqSub; ++u) r[u] = ws[(b + u) * kWs + t];
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(kGptqRows * kGptqLanes) void gptq_block_kernel(cons
     __syncthreads();  // every lane has read the group's columns before any lane rewrites ws
     // the rest of the block, column by column: the group's updates in increasing i, as the
     // reference applies them one column i at a time
-    for (int j = b + kGptqSub + l; j < kGptqBlock; j += kGptqLanes) {
+    for (int j = b + kGptqSub + l; j < blk; j += kGptqLanes) {
       float acc = ws[j * kWs + t];
       const float* hc = hsT + j * kHs + b;  // Hinv1[b .. b+15][j]
 #pragma unroll
@@ -123,20 +126,26 @@ using namespace llj;
 
 extern "C" {
 
-int llj_gptq_block(const float* hinv, int K, int i1, float* wt, int N, const float* scale, const float* zero,
-                   int bits, float* qt, float* err, float* loss, void* stream) {
-  LLJ_REQUIRE(K > 0 && N > 0 && i1 >= 0 && i1 % kGptqBlock == 0 && i1 + kGptqBlock <= K);
+int llj_gptq_block_bs(const float* hinv, int K, int i1, int blocksize, float* wt, int N, const float* scale,
+                      const float* zero, int bits, float* qt, float* err, float* loss, void* stream) {
+  LLJ_REQUIRE(blocksize >= kGptqSub && blocksize <= kGptqBlock && blocksize % kGptqSub == 0);
+  LLJ_REQUIRE(K > 0 && N > 0 && i1 >= 0 && i1 % blocksize == 0 && i1 + blocksize <= K);
   LLJ_REQUIRE(bits == 2 || bits == 4 || bits == 8);
   LLJ_REQUIRE(hinv && wt && scale && zero && qt && err && loss);
   const float maxq = (float)((1 << bits) - 1);
   if (N > 8192)
     hipLaunchKernelGGL((gptq_block_kernel<64, 4, 80>), dim3((N + 63) / 64), dim3(256), 0, (hipStream_t)stream, hinv,
-                       K, i1, wt, N, scale, zero, maxq, qt, err, loss);
+                       K, i1, blocksize, wt, N, scale, zero, maxq, qt, err, loss);
   else
     hipLaunchKernelGGL((gptq_block_kernel<32, 8, 40>), dim3((N + 31) / 32), dim3(256), 0, (hipStream_t)stream, hinv,
-                       K, i1, wt, N, scale, zero, maxq, qt, err, loss);
+                       K, i1, blocksize, wt, N, scale, zero, maxq, qt, err, loss);
   LLJ_CHECK_LAUNCH();
   return 0;
+}
+
+int llj_gptq_block(const float* hinv, int K, int i1, float* wt, int N, const float* scale, const float* zero,
+                   int bits, float* qt, float* err, float* loss, void* stream) {
+  return llj_gptq_block_bs(hinv, K, i1, kGptqBlock, wt, N, scale, zero, bits, qt, err, loss, stream);
 }
 
 int llj_colblock_pack(const float* qt, int K, int N, const float* scale, const float* zero, int bits,

@@ -41,6 +41,7 @@ SIGNATURES = {
     "llj_i8_gather_act": [_P, _I, _I, _I, _P, _P, _I, _P],
     "llj_i8_gather_weight": [_P, _P, _I, _I, _P, _P, _I, _P],
     "llj_gptq_block": [_P, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P],
+    "llj_gptq_block_bs": [_P, _I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P],
     "llj_colblock_pack": [_P, _I, _I, _P, _P, _I, _P, _P],
     "llj_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_attention_prefill": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],

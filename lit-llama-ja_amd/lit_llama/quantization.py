@@ -404,10 +404,11 @@ class GPTQQuantizer:
     error)`. The calibration Hessian, the Cholesky factors and the trailing block update are
     library work on the device (torch GEMM / rocSOLVER); the sequential 128-column loop and the
     ColBlock packing are the HIP kernels `llj_gptq_block` / `llj_colblock_pack` (csrc/gptq.hip).
-    Supported: per-channel, asymmetric, blocksize 128 (the configuration quantize/gptq.py uses),
-    groupsize -1 or a multiple of 128 (grouped scales: each group's (scale, zero) is found when the
-    column loop reaches its first column, from the weights as updated so far (reference 571-577);
-    with groupsize % 128 == 0 that is the start of a 128-column block), in_features % 128 == 0.
+    Supported: perchannel True / False and sym False / True (find_params_weight, reference 475-514),
+    blocksize 16 / 32 / 64 / 128 (557; quantize/gptq.py uses the defaults: per-channel, asymmetric,
+    128), groupsize -1 or a multiple of 128 (grouped scales: each group's (scale, zero) is found when
+    the column loop reaches its first column, from the weights as updated so far (reference 571-577);
+    with groupsize % 128 == 0 that is the start of a block), in_features % 128 == 0.
     fp32 weights reproduce the reference's op order;
     other weight dtypes are quantized from their fp32 value (the reference would round the
     packing step in that dtype). No CPU path."""
@@ -415,10 +416,9 @@ class GPTQQuantizer:
     def __init__(self, linear_module, *, bits, perchannel=True, sym=False, blocksize=128, percdamp=0.01,
                  groupsize=-1, actorder=False):
         assert isinstance(linear_module, torch.nn.Linear)
-        if not perchannel or sym or blocksize != 128 or (groupsize != -1 and (groupsize <= 0 or groupsize % 128)):
-            raise NotImplementedError("GPTQQuantizer HIP path: perchannel=True, sym=False, blocksize=128, "
-                                      "groupsize -1 or a multiple of 128 (the gptq.int4 / gptq.int8 producer "
-                                      "configuration)")
+        if blocksize not in (16, 32, 64, 128) or (groupsize != -1 and (groupsize <= 0 or groupsize % 128)):
+            raise NotImplementedError("GPTQQuantizer HIP path: blocksize 16 / 32 / 64 / 128, groupsize -1 or a "
+                                      "multiple of 128")
         assert not (actorder and groupsize != -1), "The permutation trick does not work for grouped quantization"
         self.linear_module = linear_module
         self.dev = linear_module.weight.device
@@ -437,17 +437,28 @@ class GPTQQuantizer:
         self.zeros = torch.zeros_like(self.scales)
 
     def find_params_weight(self, x):
-        """reference 475-514 (per-channel, asymmetric). The row min / max reduce on the device
-        (exact); the N-element divisions run on the host, because torch's device division by a
-        scalar multiplies by its reciprocal (not the reference's correctly rounded quotient)."""
+        """reference 475-514. The row min / max reduce on the device (exact); the N-element divisions
+        run on the host, because torch's device division by a scalar multiplies by its reciprocal
+        (not the reference's correctly rounded quotient). perchannel=False: one (scale, zero) over
+        the whole matrix, repeated per row (481-482, 503-506); sym: the range symmetric about 0 and
+        zero = (maxq + 1) / 2 (488-492, 498-499)."""
+        rows = x.shape[0]
+        if not self.perchannel:
+            x = x.flatten().unsqueeze(0)
         tmp = torch.zeros(x.shape[0], device=x.device)
         xmin = torch.minimum(x.min(1)[0], tmp).cpu()
         xmax = torch.maximum(x.max(1)[0], tmp).cpu()
+        if self.sym:
+            xmax = torch.maximum(torch.abs(xmin), xmax)
+            neg = xmin < 0
+            xmin[neg] = -xmax[neg]
         both0 = (xmin == 0) & (xmax == 0)
         xmin[both0] = -1
         xmax[both0] = +1
         scale = (xmax - xmin) / self.maxq
-        zero = torch.round(-xmin / scale)
+        zero = torch.full_like(scale, (self.maxq + 1) / 2) if self.sym else torch.round(-xmin / scale)
+        if not self.perchannel:
+            scale, zero = scale.repeat(rows), zero.repeat(rows)
         return scale.reshape(-1, 1).to(x.device), zero.reshape(-1, 1).to(x.device)
 
     def collect_input_stats(self, _1, inp, _2):
@@ -512,7 +523,7 @@ class GPTQQuantizer:
                 self.zeros[:, gi] = gz.reshape(-1)
                 scg[gi] = self.scales[:, gi].float().contiguous()
                 zrg[gi] = self.zeros[:, gi].float().contiguous()
-            _hip.call("llj_gptq_block", Hinv.data_ptr(), K, i1, Wt.data_ptr(), N, scg[gi].data_ptr(),
+            _hip.call("llj_gptq_block_bs", Hinv.data_ptr(), K, i1, B, Wt.data_ptr(), N, scg[gi].data_ptr(),
                       zrg[gi].data_ptr(), self.bits, Qt.data_ptr(), Err.data_ptr(), loss.data_ptr(), s)
             if i2 < K:  # W[:, i2:] -= Err1 @ Hinv[i1:i2, i2:] (596), transposed
                 Wt[i2:] -= Hinv[i1:i2, i2:].t().matmul(Err)

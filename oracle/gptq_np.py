@@ -22,17 +22,29 @@ import scipy.linalg
 F32 = np.float32
 
 
-def find_params_weight(W: np.ndarray, bits: int):
-    """quantization.py:475-514 (perchannel=True, sym=False): per-row (scale, zero)."""
+def find_params_weight(W: np.ndarray, bits: int, perchannel: bool = True, sym: bool = False):
+    """quantization.py:475-514: per-row (scale, zero) (perchannel), or one pair for the whole matrix
+    repeated per row (perchannel=False, 481-482 / 503-506); sym: the range symmetric about 0
+    (488-492) and zero = (maxq + 1) / 2 (498-499)."""
     maxq = F32(2 ** bits - 1)
     x = W.astype(F32)
+    if not perchannel:
+        x = x.reshape(1, -1)
     xmin = np.minimum(x.min(1), F32(0))
     xmax = np.maximum(x.max(1), F32(0))
+    if sym:
+        xmax = np.maximum(np.abs(xmin), xmax).astype(F32)
+        xmin = np.where(xmin < 0, -xmax, xmin).astype(F32)
     both0 = (xmin == 0) & (xmax == 0)
     xmin = np.where(both0, F32(-1), xmin).astype(F32)
     xmax = np.where(both0, F32(1), xmax).astype(F32)
     scale = ((xmax - xmin) / maxq).astype(F32)
-    zero = np.round(-xmin / scale).astype(F32)  # np.round is half-to-even like torch.round
+    if sym:
+        zero = np.full_like(scale, (maxq + 1) / 2).astype(F32)
+    else:
+        zero = np.round(-xmin / scale).astype(F32)  # np.round is half-to-even like torch.round
+    if not perchannel:
+        scale, zero = np.repeat(scale, W.shape[0]), np.repeat(zero, W.shape[0])
     return scale, zero
 
 
@@ -96,13 +108,13 @@ def gptq_block(W1: np.ndarray, Hinv1: np.ndarray, scale, zero, bits: int):
 
 
 def gptq_quantize(W: np.ndarray, H: np.ndarray, bits: int, blocksize: int = 128, actorder: bool = True,
-                  percdamp: float = 0.01, groupsize: int = -1):
+                  percdamp: float = 0.01, groupsize: int = -1, perchannel: bool = True, sym: bool = False):
     """GPTQQuantizer.quantize (quantization.py:532-614). W (N, K) fp32, H (K, K). Returns
     (Q reconstructions (N, K), scale, zero, error) with scale / zero (N,) for groupsize -1, else
     (N, ceil(K / groupsize)) (see the module header: grouped parity unpinned)."""
     assert not (actorder and groupsize != -1)  # 465-467
     W = W.astype(F32).copy()
-    scale, zero = find_params_weight(W, bits)
+    scale, zero = find_params_weight(W, bits, perchannel, sym)
     K0 = W.shape[1]
     if groupsize != -1:
         G = (K0 + groupsize - 1) // groupsize
@@ -124,7 +136,7 @@ def gptq_quantize(W: np.ndarray, H: np.ndarray, bits: int, blocksize: int = 128,
             for i in range(i2 - i1):
                 c = i1 + i
                 if c % groupsize == 0:
-                    cur = find_params_weight(W[:, c:c + groupsize], bits)
+                    cur = find_params_weight(W[:, c:c + groupsize], bits, perchannel, sym)
                     scales[:, c // groupsize], zeros[:, c // groupsize] = cur
                 bs[:, i], bz[:, i] = cur
         Q1, Err1, L1 = gptq_block(W[:, i1:i2], Hinv[i1:i2, i1:i2], bs, bz, bits)

@@ -267,6 +267,41 @@ def gen_gptq():
     save("gptq", **out)
 
 
+def gen_gptq_opts():
+    """GPTQQuantizer (quantization.py:424-614) with the constructor options quantize/gptq.py leaves at
+    their defaults: sym=True (find_params_weight 488-501: symmetric range, zero (maxq + 1) / 2),
+    perchannel=False (479-482, 503-506: one (scale, zero) for the whole matrix, repeated per row) and
+    blocksizes 64 / 32 (557: the lazy-batch block of the column loop). Same record as gen_gptq plus
+    the options."""
+    out = {}
+    cases = {"sym": (96, 256, 4, 128, True, True, True, 31), "pt": (64, 256, 4, 128, False, False, True, 32),
+             "b64": (80, 384, 4, 64, True, False, True, 33), "b32": (64, 256, 8, 32, True, True, False, 34),
+             "b16": (48, 128, 4, 16, False, True, False, 35)}
+    for tag, (N, K, bits, bs, perch, sym, act, seed) in cases.items():
+        rng = np.random.default_rng(seed)
+        W = (rng.standard_normal((N, K)) * 0.05).astype(np.float32)
+        W[:, :8] *= 4.0
+        W[:16] += 0.02  # rows with a one-signed range (the symmetric rule's xmin >= 0 branch)
+        W[:4] = np.abs(W[:4])
+        X = rng.standard_normal((4, 32, K)).astype(np.float32) * rng.uniform(0.2, 2.0, K).astype(np.float32)
+        lin = torch.nn.Linear(K, N, bias=False)
+        lin.weight.data = torch.from_numpy(W.copy())
+        gq = rq.GPTQQuantizer(lin, bits=bits, perchannel=perch, sym=sym, blocksize=bs, groupsize=-1, actorder=act)
+        h = lin.register_forward_hook(gq.collect_input_stats)
+        with torch.no_grad():
+            for j in range(X.shape[0]):
+                lin(torch.from_numpy(X[j:j + 1]))
+        h.remove()
+        H = gq.H.clone().numpy()
+        qm, err = gq.quantize()
+        out.update({f"{tag}_W": W, f"{tag}_X": X, f"{tag}_H": H, f"{tag}_bits": np.int64(bits),
+                    f"{tag}_opts": np.array([bs, int(perch), int(sym), int(act)], np.int64),
+                    f"{tag}_quant_weight": qm.quant_weight.contiguous().numpy(),
+                    f"{tag}_scales": qm.scales.numpy().reshape(-1), f"{tag}_zeros": qm.zeros.numpy().reshape(-1),
+                    f"{tag}_error": np.float64(err)})
+    save("gptq_opts", **out)
+
+
 def gen_gptq_grouped():
     """Grouped ColBlockQuantizedLinear (tile_cols = g; pack_weight / get_weight / forward =
     get_weight + F.linear, quantization.py:374-421) with per-group (scale, zero) from the
@@ -638,6 +673,6 @@ def gen_ref_ckpt():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ops", "colblock", "tiny", "int4_gptq", "kv_roll", "batch", "eos", "gptq", "hf_convert",
-                             "meta_convert", "bf16_init", "sampled", "sampled_fp32", "ppl", "gptq_grouped", "ref_ckpt"]
+                             "meta_convert", "bf16_init", "sampled", "sampled_fp32", "ppl", "gptq_grouped", "ref_ckpt", "gptq_opts"]
     for w in which:
         globals()[f"gen_{w}"]()

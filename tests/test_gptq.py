@@ -47,6 +47,37 @@ def test_oracle_matches_reference_gptq(t):
     assert e == pytest.approx(err, rel=1e-4)
 
 
+OPTS = np.load(Path(__file__).parent / "golden" / "gptq_opts.npz")
+OPT_CASES = ["sym", "pt", "b64", "b32", "b16"]
+
+
+def opt_case(t):
+    bs, perch, sym, act = (int(v) for v in OPTS[f"{t}_opts"])
+    return (OPTS[f"{t}_W"], OPTS[f"{t}_X"], OPTS[f"{t}_H"], int(OPTS[f"{t}_bits"]), OPTS[f"{t}_quant_weight"],
+            OPTS[f"{t}_scales"], OPTS[f"{t}_zeros"], float(OPTS[f"{t}_error"]), bs, bool(perch), bool(sym), bool(act))
+
+
+@pytest.mark.parametrize("t", OPT_CASES)
+def test_oracle_matches_reference_gptq_options(t):
+    """sym=True, perchannel=False and blocksizes 64 / 32 / 16 (reference 475-514, 557): the oracle's
+    Hessian, scales, zeros and packed bytes against the reference's own GPTQQuantizer run
+    (tests/golden/gptq_opts.npz, make_golden.py gen_gptq_opts)."""
+    W, X, H, bits, qw, sc, zr, err, bs, perch, sym, act = opt_case(t)
+    Hh, n = np.zeros((W.shape[1],) * 2, np.float32), 0
+    for j in range(X.shape[0]):
+        Hh, n = G.collect_input_stats(Hh, n, X[j:j + 1])
+    np.testing.assert_array_equal(Hh, H)
+    Q, s, z, e = G.gptq_quantize(W, H, bits, blocksize=bs, actorder=act, perchannel=perch, sym=sym)
+    np.testing.assert_array_equal(s, sc)
+    np.testing.assert_array_equal(z, zr)
+    np.testing.assert_array_equal(G.pack_weight(Q, s, z, bits), qw)
+    assert e == pytest.approx(err, rel=1e-4)
+    if sym:
+        assert (zr == 2 ** (bits - 1)).all()
+    if not perch:
+        assert len(np.unique(sc)) == 1
+
+
 def test_fixture_has_dead_column_and_actorder_case():
     W, X, H, *_ = case("a")
     assert np.diag(H)[5] == 0  # quantization.py:544-546 path
@@ -166,6 +197,56 @@ def test_gptq_quantizer_matches_reference(hip, t):
     assert np.abs(got - ref).max() <= 1
     assert (got != ref).mean() <= 5e-3
     assert e == pytest.approx(err, rel=1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t", OPT_CASES)
+def test_gptq_quantizer_options_match_reference(hip, t):
+    """GPTQQuantizer(sym=..., perchannel=..., blocksize=...) on the device against the reference's own
+    run with those options (gptq_opts.npz): scales / zeros identical, every code within 1 of the
+    reference's and at most 0.5 % different (device GEMM / rocSOLVER vs CPU LAPACK); and the column
+    loop kernel at that block size bitwise against the oracle's on the oracle's running weights."""
+    from lit_llama import _hip
+    from lit_llama.quantization import GPTQQuantizer
+    W, X, H, bits, qw, sc, zr, err, bs, perch, sym, act = opt_case(t)
+    N, K = W.shape
+    lin = torch.nn.Linear(K, N, bias=False).to(dev)
+    lin.weight.data = torch.from_numpy(W).to(dev)
+    gq = GPTQQuantizer(lin, bits=bits, perchannel=perch, sym=sym, blocksize=bs, groupsize=-1, actorder=act)
+    h = lin.register_forward_hook(gq.collect_input_stats)
+    with torch.no_grad():
+        for j in range(X.shape[0]):
+            lin(torch.from_numpy(X[j:j + 1]).to(dev))
+    h.remove()
+    qm, e = gq.quantize()
+    np.testing.assert_array_equal(qm.scales.cpu().numpy().reshape(-1), sc)
+    np.testing.assert_array_equal(qm.zeros.cpu().numpy().reshape(-1), zr)
+    got, ref = codes_of(qm.quant_weight.cpu().numpy(), bits), codes_of(qw, bits)
+    assert np.abs(got - ref).max() <= 1
+    assert (got != ref).mean() <= 5e-3
+    assert e == pytest.approx(err, rel=1e-2)
+    # the kernel alone, block by block on the oracle's running weights
+    scale, zero = G.find_params_weight(W, bits, perch, sym)
+    Hinv, perm, dead = G.hinv_upper(H, act)
+    Wr = W.astype(np.float32).copy()
+    Wr[:, dead] = 0
+    if perm is not None:
+        Wr = Wr[:, perm]
+    hd = torch.from_numpy(Hinv).to(dev)
+    sd, zd = torch.from_numpy(scale).to(dev), torch.from_numpy(zero).to(dev)
+    for i1 in range(0, K, bs):
+        i2 = i1 + bs
+        Q1, E1, L1 = G.gptq_block(Wr[:, i1:i2], Hinv[i1:i2, i1:i2], scale, zero, bits)
+        wt = torch.from_numpy(np.ascontiguousarray(Wr.T)).to(dev)
+        qt = torch.full((K, N), np.nan, dtype=torch.float32, device=dev)
+        errb = torch.empty(bs, N, dtype=torch.float32, device=dev)
+        loss = torch.zeros(N, dtype=torch.float32, device=dev)
+        _hip.call("llj_gptq_block_bs", hd.data_ptr(), K, i1, bs, wt.data_ptr(), N, sd.data_ptr(), zd.data_ptr(), bits,
+                  qt.data_ptr(), errb.data_ptr(), loss.data_ptr(), _st())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(qt[i1:i2].cpu().numpy().T, Q1)
+        np.testing.assert_array_equal(errb.cpu().numpy().T, E1)
+        Wr[:, i2:] = (Wr[:, i2:] - (E1 @ Hinv[i1:i2, i2:]).astype(np.float32)).astype(np.float32)
 
 
 @pytest.mark.gpu
