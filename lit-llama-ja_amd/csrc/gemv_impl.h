@@ -468,6 +468,9 @@ struct APre {
 #ifndef LLJ_LOADFENCE
 #define LLJ_LOADFENCE 0  // 1: the weight refills stay where the loop issues them (see the main loop)
 #endif
+#ifndef LLJ_AFRAG
+#define LLJ_AFRAG 1  // 1: a chunk's NSTEP A fragments read together before its MFMAs (0: one read per step)
+#endif
 #ifndef LLJ_ROT
 #define LLJ_ROT 0  // 1: each workgroup starts its chunk walk at a rotation (A/B of HBM access spread)
 #endif
@@ -824,13 +827,21 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       *reinterpret_cast<u32x4*>(slot + (lane >> 4) * kSRow + 8 * (lane & 15)) = x0;
       *reinterpret_cast<u32x4*>(slot + ((lane >> 4) + 4) * kSRow + 8 * (lane & 15)) = x1;
     }
+    // the chunk's A fragments, all read before the first MFMA: one LDS latency per chunk (LLJ_AFRAG;
+    // read per step, a uniform branch between the steps kept every step's read behind a full
+    // lgkmcnt(0) wait -- exposed at one wave per SIMD, the batched forms)
+    u32x4 avs[NSTEP];
 #pragma unroll
     for (int t = 0; t < NSTEP; ++t) {
       // LDS lanes of rows >= M read row 0 (abase clamped): their output rows are never stored, and
       // an unconditional read keeps the hot loop free of divergent LDS accesses
-      const u32x4 av = STRM ? *reinterpret_cast<const u32x4*>(slot + (row & 7) * kSRow + kofs<WF>(t, grp))
-                       : QRING ? *reinterpret_cast<const u32x4*>(qslot + (row & 7) * kQRow + kofs<WF>(t, grp))
-                       : ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
+      avs[t] = STRM ? *reinterpret_cast<const u32x4*>(slot + (row & 7) * kSRow + kofs<WF>(t, grp))
+               : QRING ? *reinterpret_cast<const u32x4*>(qslot + (row & 7) * kQRow + kofs<WF>(t, grp))
+               : ALDS ? *reinterpret_cast<const u32x4*>(abase + EB * (128 * c + kofs<WF>(t, grp))) : ra[d][t];
+    }
+#pragma unroll
+    for (int t = 0; t < NSTEP; ++t) {
+      const u32x4 av = avs[t];
       if constexpr (WF == WF_W4) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
@@ -838,10 +849,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
           acc[j] = mfma_bf16(a, dequant_w4(r1[d][j][0][t], msk, mag), acc[j]);
           if (DUAL) acc2[j] = mfma_bf16(a, dequant_w4(r2[d][j][0][t], msk, mag), acc2[j]);
         }
-        // (a uniform branch per step; the unconditional form with a zero fragment measured slower:
-        // without the block boundaries the compiler sank the refills to the loop end, 5,243 -> 4,821
-        // tokens/s at bs=8, profiles/r05_ab_bs8.jsonl)
-        if (SACC && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);  // else: row sums from the prologue / caller
+        // (a uniform branch; the unconditional form with a zero fragment measured slower: without
+        // the block boundaries the compiler sank the refills to the loop end, 5,243 -> 4,821
+        // tokens/s at bs=8, profiles/r05_ab_bs8.jsonl). LLJ_AFRAG: one branch per chunk, after the steps
+        if (!LLJ_AFRAG && SACC && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);  // else: row sums from the prologue / caller
       } else if constexpr (GRP) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
@@ -861,7 +872,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
             acc2[j] = mfma_bf16(a, dequant_w4(r2[d][j][1][t], msk, mag_hi), acc2[j]);
           }
         }
-        if (SACC && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);
+        if (!LLJ_AFRAG && SACC && !p.rowsum) sacc = mfma_bf16(a, ones, sacc);
       } else if constexpr (WF == WF_BF16) {
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
@@ -873,6 +884,12 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         const i32x4 a = __builtin_bit_cast(i32x4, av);
         iacc = mfma_i8(a, __builtin_bit_cast(i32x4, r1[d][0][t]), iacc);
         if (DUAL) iacc2 = mfma_i8(a, __builtin_bit_cast(i32x4, r2[d][0][t]), iacc2);
+      }
+    }
+    if constexpr (LLJ_AFRAG && W4L && SACC) {  // the chunk's A row sums (nibble offset), one uniform branch
+      if (!p.rowsum) {
+#pragma unroll
+        for (int t = 0; t < NSTEP; ++t) sacc = mfma_bf16(__builtin_bit_cast(bf16x8, avs[t]), ones, sacc);
       }
     }
     if constexpr (GRP) {  // s_g * (sum_c A (128 + q) - (128 + z_g) * sum_c A)
