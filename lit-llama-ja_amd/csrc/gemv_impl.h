@@ -454,7 +454,7 @@ struct APre {
 #define LLJ_ABAR 0
 #endif
 #ifndef LLJ_ABL
-#define LLJ_ABL 0  // ablation switches for profiling only (1 no A prologue, 2 no compute, 4 no epilogue, 8 no AM_I8Q side loop, 16 no streamed-A loads)
+#define LLJ_ABL 0  // ablation switches for profiling only (1 no A prologue, 2 no compute, 4 no epilogue, 8 no AM_I8Q side loop, 16 no streamed-A loads, 32 no epilogue stores)
 #endif
 #ifndef LLJ_I8_SIS
 #define LLJ_I8_SIS 1  // int8 A image: in-stream fp16 side product from the prep's aval table (0: after the stream)
@@ -470,6 +470,9 @@ struct APre {
 #endif
 #ifndef LLJ_AFRAG
 #define LLJ_AFRAG 1  // 1: a chunk's NSTEP A fragments read together before its MFMAs (0: one read per step)
+#endif
+#ifndef LLJ_FLAT_EPI
+#define LLJ_FLAT_EPI 1  // 1: batched-row epilogues spread over every thread of the workgroup (0: per owner lane)
 #endif
 #ifndef LLJ_ROT
 #define LLJ_ROT 0  // 1: each workgroup starts its chunk walk at a rotation (A/B of HBM access spread)
@@ -916,7 +919,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   constexpr int RR = MB == 1 ? 1 : 4;
   int e_ps[4] = {0, 0, 0, 0};
   auto issue_pos = [&]() {
-    if constexpr (EP == EP_QKV) {
+    if constexpr (EP == EP_QKV && !(MB > 1 && LLJ_FLAT_EPI != 0)) {
 #pragma unroll
       for (int r = 0; r < RR; ++r) {
         const int mm = 4 * grp + r < M ? 4 * grp + r : M - 1;
@@ -925,11 +928,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     }
   };
   float2 e_a[TPW], e_b[TPW];
-  bf16_t e_braw[TPW];
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
     e_a[j] = e_b[j] = make_float2(1.f, 0.f);
-    e_braw[j] = 0;
   }
   float e_rs[4] = {0.f, 0.f, 0.f, 0.f};  // caller's row sums (p.rowsum) of rows 4*grp + r
   auto issue_const = [&]() {  // weights-side epilogue operands (never written in a launch)
@@ -943,18 +944,54 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         e_a[j].x = reinterpret_cast<const float*>(p.sz)[n];
         if (DUAL) e_b[j].x = reinterpret_cast<const float*>(p.sz2)[n];
       }
-      if (p.bias) e_braw[j] = p.bias[n];
     }
     // an epilogue load under divergent control flow would put a vmcnt(0) between the
     // row stores (stores count in vmcnt): read the row sums here (the branch is uniform)
-    if (W4L && p.rowsum) {
+    if (W4L && p.rowsum && !(MB > 1 && LLJ_FLAT_EPI != 0)) {
 #pragma unroll
       for (int r = 0; r < RR; ++r) e_rs[r] = p.rowsum[4 * grp + r < M ? 4 * grp + r : M - 1];
     }
   };
+  // flat epilogue (batched rows, LLJ_FLAT_EPI): after the reduction every thread of the workgroup
+  // finishes whole output elements -- element e = tid + NT q of the (tile slot j, row m, column c)
+  // space, c fastest, so c = tid & 15 = this lane's column `row` in every slot (e_a / e_b
+  // apply as loaded) and (j, m) follow from rm = (tid >> 4) + 4 NW q. The per-lane form runs 4 rows
+  // per lane on the TPW owner waves and idles the lanes of MFMA rows >= M (half of them at M = 8)
+  constexpr bool FLAT = MB > 1 && LLJ_FLAT_EPI != 0;
+  constexpr int FQ = FLAT ? (TPW * 16 * 16 + NW * 64 - 1) / (NW * 64) : 1;  // passes for M <= 16
+  int f_j[FQ], f_m[FQ], f_ps[FQ];
+  bool f_v[FQ];
+  float f_rs[FQ];
+  bf16_t f_xr[FQ];
+  float2 f_cs[FQ];
+#pragma unroll
+  for (int q = 0; q < FQ; ++q) {
+    f_j[q] = f_m[q] = f_ps[q] = 0;
+    f_v[q] = false;
+    f_rs[q] = 0.f;
+    f_xr[q] = 0;
+    f_cs[q] = make_float2(1.f, 0.f);
+  }
+  auto issue_flat = [&]() {  // the flat elements' row operands (branch-free, clamped addresses)
+    if constexpr (FLAT) {
+#pragma unroll
+      for (int q = 0; q < FQ; ++q) {
+        const int rm = (int)(threadIdx.x >> 4) + 4 * NW * q;
+        const int jj = rm / M, mm = rm - jj * M;
+        const bool v = jj < TPW && nt0 + jj < ntiles;
+        f_v[q] = v;
+        f_j[q] = v ? jj : 0;
+        f_m[q] = v ? mm : 0;
+        const int nt = nt0 + f_j[q] < ntiles ? nt0 + f_j[q] : ntiles - 1;
+        if constexpr (EP == EP_QKV) f_ps[q] = p.pos[p.T == 1 ? 0 : (p.m0 + f_m[q]) % p.T];  // (T rows per sequence)
+        if constexpr (EP == EP_RESID) f_xr[q] = p.C[(size_t)f_m[q] * p.ldc + nt * 16 + row];
+        if (W4L && p.rowsum) f_rs[q] = p.rowsum[f_m[q]];
+      }
+    }
+  };
   bf16_t e_xr[TPW][4];
   auto issue_xr = [&]() {  // residual stream values this workgroup updates
-    if constexpr (EP == EP_RESID) {
+    if constexpr (EP == EP_RESID && !FLAT) {
 #pragma unroll
       for (int j = 0; j < TPW; ++j)
 #pragma unroll
@@ -1114,6 +1151,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   issue_pos();
   issue_const();
   issue_xr();
+  issue_flat();
   a_issue_any();
 #if LLJ_ABAR
   __builtin_amdgcn_s_barrier();  // experiment: every wave's A loads ahead of any weight load
@@ -1209,7 +1247,16 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   }
   LLJ_STAMP(1);
   float2 e_cs[TPW][4];
-  if constexpr (EP == EP_QKV) {  // RoPE rows of the rows' positions (needs e_ps: waits for it only)
+  if constexpr (EP == EP_QKV && FLAT) {  // the flat elements' RoPE (cos, sin) (needs f_ps: waits for it only)
+    const int Cd = p.n_head * p.head_size;
+#pragma unroll
+    for (int q = 0; q < FQ; ++q) {
+      const int nt = nt0 + f_j[q] < ntiles ? nt0 + f_j[q] : ntiles - 1;
+      const int n0 = nt * 16, region = n0 >= 2 * Cd ? 2 : (n0 >= Cd ? 1 : 0);
+      const int dd = (n0 + row - region * Cd) & (p.head_size - 1);
+      f_cs[q] = *reinterpret_cast<const float2*>(p.rope + ((size_t)f_ps[q] * (p.head_size >> 1) + (dd >> 1)) * 2);
+    }
+  } else if constexpr (EP == EP_QKV) {  // RoPE rows of the rows' positions (needs e_ps: waits for it only)
     const int Cd = p.n_head * p.head_size;
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
@@ -1332,162 +1379,206 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
       for (int r = 0; r < 4; ++r) mine[8 * TPW + r] = sacc[r];
     }
     __syncthreads();
-    if (wave >= TPW) return;  // owns no tile slot
+    if (!FLAT && wave >= TPW) return;  // owns no tile slot (the flat epilogue uses every wave)
   }
   LLJ_STAMP(4);
 
-  // ---- epilogue of tile slot j (its owner wave): lane holds C[m = 4*grp + r][n = nj[j]]
-  auto epilogue = [&](const int j, const f32x4 ya, const f32x4 yb, const f32x4 ys, const i32x4 yi,
-                      const i32x4 yi2) {
-    const int n = nj[j], n0 = ntj[j] * 16;
-    if constexpr ((LLJ_ABL & 4) != 0) {  // ablation: minimal epilogue
-      if (ya[0] == 1234.5f && row < M) p.C[n] = f2bf(ya[1] + yb[2]);
-      return;
-    }
-    const float s1 = e_a[j].x, o1 = e_a[j].y, s2 = e_b[j].x, o2 = e_b[j].y;
-    bool i8col = false;  // EP_SWIGLU int8 statistics: this lane's column has an outlier
-    const float bias = p.bias ? bf2f(e_braw[j]) : 0.f;
+  // ---- epilogue: output element (tile slot j, local row m, this lane's column `row`) from its reduced
+  // accumulators. Every lane of a 16-lane column group calls it together (the RoPE partner and the
+  // 16-column row sums / maxima are DPP exchanges inside the group); act: the element exists (the
+  // row is < M and the tile slot is a real tile). Returns the int8 SwiGLU statistics' outlier flag.
+  // (LLJ_ABL & 32: timing ablation, every output computed, no store issued -- ldc is never negative)
+  auto epi_store = [&](void* dst, uint32_t v) {
+    if ((LLJ_ABL & 32) == 0 || p.ldc < 0) st_out32(dst, v);
+  };
+  auto sel = [](auto const& arr, int j) {  // arr[j] for a runtime j < TPW (selects, no dynamic register index)
+    auto v = arr[0];
 #pragma unroll
-    for (int r = 0; r < RR; ++r) {
-      if (r >= M) break;  // m = 4 grp + r >= r: no lane of the wave has a row left (uniform)
-      const int m = 4 * grp + r;
-      float y, y2 = 0.f;
-      if (W4L) {
-        float sa = ys[r];
-        if (p.rowsum) {
-          sa = e_rs[r];  // rows >= M hold a clamped copy; their outputs are not stored
-        } else if constexpr (ALDS && !SACC) {
-          sa = 0.f;
-          if (m < M) {
+    for (int i = 1; i < TPW; ++i) v = j == i ? arr[i] : v;
+    return v;
+  };
+  auto elem = [&](const int j, const int m, const bool act, const float ya, const float yb, const float ys,
+                  const int yi, const int yi2, const int ps, const float2 cs, const float rsv,
+                  const bf16_t xr) -> bool {
+    const int nt = nt0 + j < ntiles ? nt0 + j : ntiles - 1;
+    const int n = nt * 16 + row, n0 = nt * 16;
+    const float2 ea = sel(e_a, j), eb = sel(e_b, j);
+    const float s1 = ea.x, o1 = ea.y, s2 = eb.x, o2 = eb.y;
+    // (no Linear of the LLaMA path has a bias: the read stays in the epilogue, behind a uniform branch)
+    const float bias = p.bias ? bf2f(p.bias[n]) : 0.f;
+    float y, y2 = 0.f;
+    if (W4L) {
+      float sa = ys;
+      if (p.rowsum) {
+        sa = rsv;  // rows >= M hold a clamped copy; their outputs are not stored
+      } else if constexpr (ALDS && !SACC) {
+        sa = 0.f;
+        if (act) {
 #pragma unroll
-            for (int w = 0; w < NW; ++w) sa += tail[TL_RS + w * 8 + m];
-          }
-        }
-        y = s1 * (ya[r] - o1 * sa);
-        if (DUAL) y2 = s2 * (yb[r] - o2 * sa);
-      } else if (WF == WF_BF16 || GRP) {
-        y = ya[r];
-        y2 = yb[r];
-      } else {
-        // mm_dequant (fp16 out) + fp16 outlier product, then cast back (bnb MatMul8bitLt)
-        const float sa = m < M ? sca[m] : 0.f;
-        const float kq = 1.f / (127.f * 127.f);
-        y = (float)yi[r] * (sa * s1 * kq);
-        if (DUAL) y2 = (float)yi2[r] * (sa * s2 * kq);
-        if (m < M) {
-          float sd = 0.f, sd2 = 0.f;
-#pragma unroll
-          for (int w = 0; w < NW; ++w) {
-            sd += side[(w * 8 + m) * 16 + row];
-            if (DUAL) sd2 += side[NW * 128 + (w * 8 + m) * 16 + row];
-          }
-          y = (float)(_Float16)((float)(_Float16)y + sd);
-          if (DUAL) y2 = (float)(_Float16)((float)(_Float16)y2 + sd2);
+          for (int w = 0; w < NW; ++w) sa += tail[TL_RS + w * 8 + m];
         }
       }
-      y += bias;
-      if (EP == EP_QKV) {
-        // c_attn output rounded to bf16 (model.py:204), then RoPE in fp32 (model.py:318-329)
-        const float v = round_bf(y);
-        const float partner = lane_xor1(v);
-        if (m < M) {
-          // head_size is a power of two (64 / 128, checked on the host): shifts, no divisions
-          const int Cd = p.n_head * p.head_size;
-          const int hs_sh = uniform(31 - __builtin_clz(p.head_size));
-          const int region = uniform(n0 / Cd);  // 0 q, 1 k, 2 v (uniform per tile)
-          const int nc = n - region * Cd;
-          const int h = nc >> hs_sh, dd = nc & (p.head_size - 1);
-          const int mg = p.m0 + m;
-          const int b = p.T == 1 ? mg : mg / p.T;
-          const int ps = e_ps[r];
-          float out = v;
-          if (region < 2) {
-            const float c = e_cs[j][r].x, sn = e_cs[j][r].y;
-            out = (dd & 1) ? (v * c + partner * sn) : (v * c - partner * sn);
-          }
-          const uint32_t ob = (uint32_t)f2bf(out);
-          const uint32_t pr = lane_xor1(ob);  // columns (dd, dd + 1) leave as one 4-byte store
-          if (!(dd & 1)) {
-            bf16_t* dst;
-            size_t ei;
-            if (region == 0) {
-              dst = p.q_out;
-              ei = (size_t)mg * Cd + nc;
-            } else {
-              int slot = ps;
-              if (slot >= p.S) slot %= p.S;  // ring wrap only (no division on the common path)
-              dst = region == 1 ? p.kcache : p.vcache;
-              ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
-            }
-            st_out32(dst + ei, ob | (pr << 16));
-          }
+      y = s1 * (ya - o1 * sa);
+      if (DUAL) y2 = s2 * (yb - o2 * sa);
+    } else if (WF == WF_BF16 || GRP) {
+      y = ya;
+      y2 = yb;
+    } else {
+      // mm_dequant (fp16 out) + fp16 outlier product, then cast back (bnb MatMul8bitLt)
+      const float sa = act ? sca[m] : 0.f;
+      const float kq = 1.f / (127.f * 127.f);
+      y = (float)yi * (sa * s1 * kq);
+      if (DUAL) y2 = (float)yi2 * (sa * s2 * kq);
+      if (act) {
+        float sd = 0.f, sd2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          sd += side[(w * 8 + m) * 16 + row];
+          if (DUAL) sd2 += side[NW * 128 + (w * 8 + m) * 16 + row];
         }
-      } else if (EP == EP_RESID) {
-        // x = x + h in bf16 (model.py:172-173)
-        const float xn = round_bf(bf2f(e_xr[j][r]) + round_bf(y));
-        const uint32_t xb = (uint32_t)f2bf(xn);
-        const uint32_t pr = lane_xor1(xb);
-        if (m < M && !(row & 1)) st_out32(p.C + (size_t)m * p.ldc + n, xb | (pr << 16));
-        if (p.nstat_out) {  // uniform: the next RMSNorm's sum of squares over this tile's 16 columns
-          const float sq = row16_sum(m < M ? round_bf(xn * xn) : 0.f);
-          if (row == 0 && m < M) st_out32(p.nstat_out + (size_t)ntj[j] * kNstRows + m, __builtin_bit_cast(uint32_t, sq));
-        }
-      } else {
-        const uint32_t ob = (uint32_t)f2bf(out_value<EP>(y, y2));
-        const uint32_t pr = lane_xor1(ob);
-        if (m < M && !(row & 1)) {
-          const size_t ei = (size_t)m * p.ldc + n;
-          st_out32(p.C + ei, ob | (pr << 16));
-        }
-        if constexpr (EP == EP_SWIGLU && I8) {
-          if (p.i8st_out) {  // uniform: LLM.int8 statistics of h for the int8 mlp.c_proj (AM_I8Q)
-            const float a16 = fabsf(f16r(bflo(ob)));
-            const bool big = m < M && a16 >= p.thr;
-            i8col |= big;
-            const float mx = row16_max(m < M && !big ? a16 : 0.f);
-            if (row == 0 && m < M) atomicMax(p.i8st_out + kI8StSca + 8 * (ntj[j] % kI8StSlots) + m, __float_as_uint(mx));
+        y = (float)(_Float16)((float)(_Float16)y + sd);
+        if (DUAL) y2 = (float)(_Float16)((float)(_Float16)y2 + sd2);
+      }
+    }
+    y += bias;
+    bool big = false;
+    if (EP == EP_QKV) {
+      // c_attn output rounded to bf16 (model.py:204), then RoPE in fp32 (model.py:318-329)
+      const float v = round_bf(y);
+      const float partner = lane_xor1(v);
+      if (act) {
+        // head_size is a power of two (64 / 128, checked on the host): shifts, no divisions
+        const int Cd = p.n_head * p.head_size;
+        const int hs_sh = uniform(31 - __builtin_clz(p.head_size));
+        const int region = n0 >= 2 * Cd ? 2 : (n0 >= Cd ? 1 : 0);  // 0 q, 1 k, 2 v (per tile)
+        const int nc = n - region * Cd;
+        const int h = nc >> hs_sh, dd = nc & (p.head_size - 1);
+        const int mg = p.m0 + m;
+        const int b = p.T == 1 ? mg : mg / p.T;
+        float out = v;
+        if (region < 2) out = (dd & 1) ? (v * cs.x + partner * cs.y) : (v * cs.x - partner * cs.y);
+        const uint32_t ob = (uint32_t)f2bf(out);
+        const uint32_t pr = lane_xor1(ob);  // columns (dd, dd + 1) leave as one 4-byte store
+        if (!(dd & 1)) {
+          bf16_t* dst;
+          size_t ei;
+          if (region == 0) {
+            dst = p.q_out;
+            ei = (size_t)mg * Cd + nc;
+          } else {
+            int slot = ps;
+            if (slot >= p.S) slot %= p.S;  // ring wrap only (no division on the common path)
+            dst = region == 1 ? p.kcache : p.vcache;
+            ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
           }
+          epi_store(dst + ei, ob | (pr << 16));
+        }
+      }
+    } else if (EP == EP_RESID) {
+      // x = x + h in bf16 (model.py:172-173)
+      const float xn = round_bf(bf2f(xr) + round_bf(y));
+      const uint32_t xb = (uint32_t)f2bf(xn);
+      const uint32_t pr = lane_xor1(xb);
+      if (act && !(row & 1)) epi_store(p.C + (size_t)m * p.ldc + n, xb | (pr << 16));
+      if (p.nstat_out) {  // uniform: the next RMSNorm's sum of squares over this tile's 16 columns
+        const float sq = row16_sum(act ? round_bf(xn * xn) : 0.f);
+        if (row == 0 && act) epi_store(p.nstat_out + (size_t)nt * kNstRows + m, __builtin_bit_cast(uint32_t, sq));
+      }
+    } else {
+      const uint32_t ob = (uint32_t)f2bf(out_value<EP>(y, y2));
+      const uint32_t pr = lane_xor1(ob);
+      if (act && !(row & 1)) epi_store(p.C + (size_t)m * p.ldc + n, ob | (pr << 16));
+      if constexpr (EP == EP_SWIGLU && I8) {
+        if (p.i8st_out) {  // uniform: LLM.int8 statistics of h for the int8 mlp.c_proj (AM_I8Q)
+          const float a16 = fabsf(f16r(bflo(ob)));
+          big = act && a16 >= p.thr;
+          const float mx = row16_max(act && !big ? a16 : 0.f);
+          if (row == 0 && act) atomicMax(p.i8st_out + kI8StSca + 8 * (nt % kI8StSlots) + m, __float_as_uint(mx));
         }
       }
     }
-    if constexpr (EP == EP_SWIGLU && I8) {
-      if (p.i8st_out) {  // the tile's outlier columns (any row), 16 bits of one flag word
-        uint32_t f = i8col ? 1u : 0u;
-        f |= (uint32_t)__shfl_xor((int)f, 16, 64);
-        f |= (uint32_t)__shfl_xor((int)f, 32, 64);
-        const uint32_t bits = (uint32_t)(__ballot(f != 0u) & 0xFFFFull);
-        if (lane == 0 && bits) atomicOr(p.i8st_out + kI8StFlags + (n0 >> 5), bits << (n0 & 31));
-      }
-    }
+    return big;
   };
 
+  if constexpr ((LLJ_ABL & 4) != 0) {  // ablation: minimal epilogue
+    if (wave == 0 && acc[0][0] == 1234.5f && row < M) p.C[nj[0]] = f2bf(acc[0][1] + acc2[0][2]);
+  } else if constexpr (FLAT) {
+    // every thread finishes the elements e = tid + NT q of the (tile slot, row, column) space (f_j /
+    // f_m / f_v from the prologue); the element's NW wave partials are summed in wave order, as below
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) {
-    if (j % NW != wave || !tvalid[j]) continue;  // uniform
-    f32x4 ya = acc[j], yb = acc2[j], ys = sacc;
-    i32x4 yi = iacc, yi2 = iacc2;
-    if (NW > 1) {
+    for (int q = 0; q < FQ; ++q) {
+      const int j = f_j[q], m = f_m[q];
+      const int src = ((m >> 2) << 4) | row, r = m & 3;  // the lane holding (m, row) in the MFMA layout
+      float ya = 0.f, yb = 0.f, ys = 0.f;
+      int yi = 0, yi2 = 0;
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
+        const float* o = red + (size_t)(w * 64 + src) * NV;
         if constexpr (I8) {
-          const int* o = reinterpret_cast<const int*>(red) + (size_t)(w * 64 + lane) * NV;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            yi[r] = w == 0 ? o[r] : yi[r] + o[r];
-            yi2[r] = w == 0 ? o[4 + r] : yi2[r] + o[4 + r];
-          }
+          const int* oi = reinterpret_cast<const int*>(o);
+          yi = w == 0 ? oi[r] : yi + oi[r];
+          yi2 = w == 0 ? oi[4 + r] : yi2 + oi[4 + r];
         } else {
-          const float* o = red + (size_t)(w * 64 + lane) * NV;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            ya[r] = w == 0 ? o[8 * j + r] : ya[r] + o[8 * j + r];
-            yb[r] = w == 0 ? o[8 * j + 4 + r] : yb[r] + o[8 * j + 4 + r];
-            ys[r] = w == 0 ? o[8 * TPW + r] : ys[r] + o[8 * TPW + r];
-          }
+          ya = w == 0 ? o[8 * j + r] : ya + o[8 * j + r];
+          if (DUAL) yb = w == 0 ? o[8 * j + 4 + r] : yb + o[8 * j + 4 + r];
+          if (SACC) ys = w == 0 ? o[8 * TPW + r] : ys + o[8 * TPW + r];
+        }
+      }
+      const bool big = elem(j, m, f_v[q], ya, yb, ys, yi, yi2, f_ps[q], f_cs[q], f_rs[q], f_xr[q]);
+      if constexpr (EP == EP_SWIGLU && I8) {
+        if (p.i8st_out) {  // each 16-lane group's outlier columns: 16 bits of its tile's flag word
+          const unsigned long long bal = __ballot(big);
+          const uint32_t bits = (uint32_t)(bal >> (lane & 48)) & 0xFFFFu;
+          const int nt = nt0 + j < ntiles ? nt0 + j : ntiles - 1;
+          if (row == 0 && bits) atomicOr(p.i8st_out + kI8StFlags + (nt >> 1), bits << (16 * (nt & 1)));
         }
       }
     }
-    epilogue(j, ya, yb, ys, yi, yi2);
+  } else {
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      if (j % NW != wave || !tvalid[j]) continue;  // uniform
+      f32x4 ya = acc[j], yb = acc2[j], ys = sacc;
+      i32x4 yi = iacc, yi2 = iacc2;
+      if (NW > 1) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          if constexpr (I8) {
+            const int* o = reinterpret_cast<const int*>(red) + (size_t)(w * 64 + lane) * NV;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              yi[r] = w == 0 ? o[r] : yi[r] + o[r];
+              yi2[r] = w == 0 ? o[4 + r] : yi2[r] + o[4 + r];
+            }
+          } else {
+            const float* o = red + (size_t)(w * 64 + lane) * NV;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              ya[r] = w == 0 ? o[8 * j + r] : ya[r] + o[8 * j + r];
+              yb[r] = w == 0 ? o[8 * j + 4 + r] : yb[r] + o[8 * j + 4 + r];
+              ys[r] = w == 0 ? o[8 * TPW + r] : ys[r] + o[8 * TPW + r];
+            }
+          }
+        }
+      }
+      bool i8col = false;  // EP_SWIGLU int8 statistics: this lane's column has an outlier
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        if (r >= M) break;  // m = 4 grp + r >= r: no lane of the wave has a row left (uniform)
+        const int m = 4 * grp + r;
+        i8col |= elem(j, m, m < M, ya[r], yb[r], ys[r], yi[r], yi2[r], e_ps[r], e_cs[j][r], e_rs[r], e_xr[j][r]);
+      }
+      if constexpr (EP == EP_SWIGLU && I8) {
+        if (p.i8st_out) {  // the tile's outlier columns (any row), 16 bits of one flag word
+          const int n0 = ntj[j] * 16;
+          uint32_t f = i8col ? 1u : 0u;
+          f |= (uint32_t)__shfl_xor((int)f, 16, 64);
+          f |= (uint32_t)__shfl_xor((int)f, 32, 64);
+          const uint32_t bits = (uint32_t)(__ballot(f != 0u) & 0xFFFFull);
+          if (lane == 0 && bits) atomicOr(p.i8st_out + kI8StFlags + (n0 >> 5), bits << (n0 & 31));
+        }
+      }
+    }
   }
   LLJ_STAMP(5);
 }
