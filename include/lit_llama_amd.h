@@ -145,6 +145,11 @@ int llj_attention_prefill(const void* q, const void* kcache, const void* vcache,
  * part_ws (llj_attention_ws_bytes(B*T, n_head, head_size, nsplit) bytes), merged in split order
  * by a second launch. nsplit <= 1 is llj_attention itself. Same softmax up to summation order. */
 size_t llj_attention_ws_bytes(int rows, int n_head, int head_size, int nsplit);
+/* Decode attention (model.py:237) as nsplit <= 4 interleaved key splits per (row, head) whose
+ * unnormalized partials (outputs, max, sum; llj_attention_ws_bytes layout) go to part_ws with no
+ * combine launch: llj_linear_resid_attn merges them in attn.c_proj's prologue (one row). */
+int llj_attention_part(const void* q, const void* kcache, const void* vcache, const int* pos, int B, int T,
+                       int n_head, int head_size, int S, int nsplit, void* part_ws, void* stream);
 int llj_attention_split(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
                         int n_head, int head_size, int S, int nsplit, void* part_ws, void* stream);
 
@@ -154,6 +159,11 @@ int llj_attention_split(const void* q, const void* kcache, const void* vcache, v
  * statistics of the next RMSNorm (model.py:281), handed to the norm-fused op that follows. */
 int llj_linear_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M,
                      int N, int K, const void* i8ws, int i8_row0, float* nstat_out, void* stream);
+/* llj_linear_resid for one row whose A is the attention output merged from llj_attention_part's
+ * partials in the prologue (attn.c_proj + model.py:172-173 without the combine launch); wfmt 0 / 1 / 3,
+ * K = n_head * head_size < 8192. */
+int llj_linear_resid_attn(int wfmt, const void* part, int nsplit, int n_head, const void* W, const void* sz, void* x,
+                          int ldx, int N, int K, float* nstat_out, void* stream);
 /* h[M, H] = silu(rms_2(x) . W1^T) * (rms_2(x) . W2^T)  (model.py:173, 258). M <= 8. */
 int llj_norm_swiglu(int wfmt, const void* x, const void* norm_w, float eps, const void* W1, const void* sz1,
                     const void* W2, const void* sz2, void* h, int M, int H, int K, const void* i8ws, int i8_row0,

@@ -53,8 +53,15 @@ __device__ __forceinline__ void softmax_merge(float& mx, float& l, float* o, con
 
 // PART: split-K over the keys (long contexts): this block takes key range `split` of `nsplit`
 // equal ranges (>= one pass of NG * U keys each) of the valid keys and writes its unnormalized partial (outputs, running max,
-// sum) to part[((m * nh + h) * nsplit + split) * (HS + 2)]; attention_combine_kernel merges.
-template <int HS, int U, int NTH, bool PART = false, int SPECU = U / 2>
+// sum) to part[((m * nh + h) * nsplit + split) * kAttPart<HS>]; attention_combine_kernel merges.
+// ILV (with PART): interleaved splits for short caches -- block `split` takes the key groups
+// j = split * NG + kg + NG * nsplit * i (a fixed set whatever the position, so its first pass can be
+// loaded before the position is known); the partials are merged in the consumer's prologue (the
+// attn.c_proj GEMV, gemv_impl.h apart) instead of a combine launch.
+template <int HS>
+constexpr int kAttPart = HS + 4;  // floats per partial record: HS outputs, max, sum, 2 pad (16-byte records)
+
+template <int HS, int U, int NTH, bool PART = false, int SPECU = U / 2, bool ILV = false>
 __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                const int* __restrict__ pos, int T, int S, int nh, float scale_log2,
@@ -78,12 +85,13 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   const size_t base = ((size_t)(b * nh + h) * S) * HS + sub * DPL;  // elements
   // K/V rows of one pass (U keys of this group): every load first, rows clamped into the cache
   // keys u in [u0, u1) of a pass; past jlim: row 0 (an L2 hit after the first pass, never used)
+  const int KS = ILV ? NG * nsplit : NG;  // key stride between a group's keys of one pass
   auto load_pass = [&](int j0, int jlim, uint32_t (&kw)[U][DPL / 2], uint32_t (&vw)[U][DPL / 2], int u0 = 0,
                        int u1 = U) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (u < u0 || u >= u1) continue;
-      const int j = j0 + NG * u < jlim ? j0 + NG * u : 0;
+      const int j = j0 + KS * u < jlim ? j0 + KS * u : 0;
       const size_t eo = base + (size_t)j * HS;
       if constexpr (DPL == 8) {
         const uint4 a = *reinterpret_cast<const uint4*>(kc + eo);
@@ -107,13 +115,15 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   // (host): small grids (bs = 1: 32 blocks), where the launch is latency-bound, and -- option
   // LLJ_OPT_ATT_SPEC_BATCH -- half passes at any grid; a whole pass over many blocks read more rows
   // past p than the latency saved (7B bs=8: 1.79 -> 1.87 ms)
-  const bool spec = !PART && spec_ok;
-  if (spec) load_pass(kg, S, kw, vw, 0, SPECU);
+  const bool spec = (!PART || ILV) && spec_ok;
+  if (spec) load_pass((ILV ? split * NG : 0) + kg, S, kw, vw, 0, SPECU);
   const int ps = pos[t];
   const int nvalid = ps < S ? ps + 1 : S;
   // key range of this block (the whole valid range unless split)
   int jbeg = 0, jend = nvalid;
-  if constexpr (PART) {  // ranges of at least one full pass (NG * U keys); the rest stay empty
+  if constexpr (ILV) {
+    jbeg = split * NG;
+  } else if constexpr (PART) {  // ranges of at least one full pass (NG * U keys); the rest stay empty
     const int chunk = max((nvalid + nsplit - 1) / nsplit, NG * U);
     jbeg = split * chunk;
     jend = min(nvalid, jbeg + chunk);
@@ -143,7 +153,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
   for (int i = 0; i < DPL; ++i) o[i] = 0.f;
 
   bool first = spec;
-  for (int j0 = jbeg + kg; j0 < jend; j0 += NG * U) {
+  for (int j0 = jbeg + kg; j0 < jend; j0 += KS * U) {
     if (!first) load_pass(j0, jend, kw, vw);
     else if (SPECU < U) load_pass(j0, jend, kw, vw, SPECU, U);  // the speculative pass's second half
     first = false;
@@ -153,7 +163,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
 #pragma unroll
       for (int i = 0; i < DPL / 2; ++i) s += qf[2 * i] * bflo(kw[u][i]) + qf[2 * i + 1] * bfhi(kw[u][i]);
       s = row16_sum(s);  // the 16 lanes of this key
-      if (j0 + NG * u >= jend) continue;
+      if (j0 + KS * u >= jend) continue;
       const float mn = fmaxf(mx, s);
       const float corr = exp2f(mx - mn);
       const float pj = exp2f(s - mn);
@@ -207,7 +217,7 @@ __device__ __forceinline__ void attention_body(const bf16_t* __restrict__ q, con
       O += s_o[w * HS + d] * f;
     }
     if constexpr (PART) {  // unnormalized partial: outputs, then (max, sum)
-      float* dst = part + ((size_t)(m * nh + h) * nsplit + split) * (HS + 2);
+      float* dst = part + ((size_t)(m * nh + h) * nsplit + split) * kAttPart<HS>;
       dst[d] = O;
       if (d == 0) {
         dst[HS] = M;
@@ -235,12 +245,12 @@ __global__ __launch_bounds__(HS) void attention_combine_kernel(const float* __re
                                                                float thr = 0.f, uint32_t* __restrict__ clr = nullptr,
                                                                int clr_words = 0) {
   const int h = blockIdx.x, m = blockIdx.y, d = threadIdx.x;
-  const float* src = part + (size_t)(m * nh + h) * nsplit * (HS + 2);
+  const float* src = part + (size_t)(m * nh + h) * nsplit * kAttPart<HS>;
   float M = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, src[(size_t)s * (HS + 2) + HS]);
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, src[(size_t)s * kAttPart<HS> + HS]);
   float L = 0.f, O = 0.f;
   for (int s = 0; s < nsplit; ++s) {
-    const float* ps = src + (size_t)s * (HS + 2);
+    const float* ps = src + (size_t)s * kAttPart<HS>;
     const float f = ps[HS] == -INFINITY ? 0.f : exp2f(ps[HS] - M);
     L += ps[HS + 1] * f;
     O += ps[d] * f;

@@ -147,6 +147,21 @@ int llj_i8_linear_resid(const void* A, int lda, const void* CB, const void* SCB,
   return run<EP_RESID>(WF_I8, p, stream);
 }
 
+// x[1,N] += y . W^T with y the decode attention output of one row, merged in the prologue from the
+// nsplit interleaved key-split partials of llj_attention_part (no combine launch): attn.c_proj +
+// model.py:172. Bitwise llj_linear_resid of attention_combine_kernel's y over the same partials.
+int llj_linear_resid_attn(int wfmt, const void* part, int nsplit, int n_head, const void* W, const void* sz, void* x,
+                          int ldx, int N, int K, float* nstat_out, void* stream) {
+  if (!part || nsplit < 1 || nsplit > kMergeMax || n_head < 1 || K % n_head) return LLJ_EINVAL;
+  GemvParams p{};
+  p.nstat_out = nstat_out;
+  p.apart = (const float*)part; p.asplit = nsplit; p.n_head = n_head; p.head_size = K / n_head;
+  if (p.head_size < 8 || (p.head_size & (p.head_size - 1))) return LLJ_EINVAL;
+  p.A = nullptr; p.lda = K; p.M = 1; p.N = N; p.K = K;
+  p.W = W; p.sz = (const float2*)sz; p.C = (bf16_t*)x; p.ldc = ldx;
+  return run<EP_RESID>(wfmt, p, stream);
+}
+
 // h = silu(xn . CB1^T) * (xn . CB2^T) for LLM.int8 decode rows -- xn's statistics either in i8ws
 // (llj_i8_norm_stats) or as a hand-off block x_stats (llj_i8_norm_rowstats: rows quantized per chunk,
 // AM_I8Q) -- that also writes the LLM.int8 statistics of h (h_stats, zeroed beforehand) and zeroes

@@ -64,7 +64,11 @@ enum : int { WF_W4 = 0, WF_BF16 = 1, WF_I8 = 2, WF_W8 = 3, WF_W4G = 4 };
 // AM_I8S (LLM.int8, batched decode rows with a statistics workspace): the rows quantized once by the
 // statistics launch (ws aq) are streamed per chunk into the same per-wave ring as AM_I8Q's -- no
 // workgroup-wide int8 A image, no prologue barrier.
-enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2, AM_STREAM = 3, AM_SNORM = 4, AM_I8Q = 5, AM_I8S = 6 };
+// AM_MERGE (one row, the attn.c_proj residual op): the LDS image of AM_LDS built from the decode
+// attention's unnormalized per-split partials (apart: llj_attention_part) -- the split merge of
+// attention_combine_kernel, in its order, in the prologue instead of a combine launch
+enum : int { AM_GLOBAL = 0, AM_LDS = 1, AM_NORM = 2, AM_STREAM = 3, AM_SNORM = 4, AM_I8Q = 5, AM_I8S = 6, AM_MERGE = 7 };
+constexpr int kMergeMax = 4;  // AM_MERGE: at most this many key splits per head
 // streamed A: elements per staged row (128 + 8 pad: rows land on distinct bank groups) and per slot
 constexpr int kSRow = 136;
 constexpr int kSSlot = 8 * kSRow;
@@ -121,6 +125,9 @@ struct GemvParams {
   uint32_t* clr;
   int clr_words;
   float thr;
+  // AM_MERGE: attention partials [(n_head)][asplit][head_size + 4] floats (attention.h kAttPart) of row 0
+  const float* apart;
+  int asplit;
 };
 constexpr int kNstRows = 16;
 #ifndef LLJ_SACC_NORM
@@ -1025,10 +1032,33 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   // rows held in registers: MB == 1 -> 1; else the smallest of 2 / 4 / 8 covering M (rows past M
   // are clamped duplicates of row M-1: loaded, never used)
   const int mr = MB == 1 ? 1 : uniform(M <= 2 ? 2 : M <= 4 ? 4 : 8);
+  // AM_MERGE: per A vector (8 dims of one head) and split, the partial's 8 outputs and (max, sum)
+  constexpr bool MERGE = (AM == AM_MERGE);
+  u32x4 mo[MERGE ? APre<MB, NORM>::XR : 1][MERGE ? kMergeMax : 1][2];
+  float2 mml[MERGE ? APre<MB, NORM>::XR : 1][MERGE ? kMergeMax : 1];
   auto a_issue = [&](auto rsc, auto mrc) {
     constexpr int RS = decltype(rsc)::value;
     constexpr int MR = decltype(mrc)::value;
     static_assert(MR * RS <= AP::XR, "A registers");
+    if constexpr (MERGE && RS > 4) {  // (K < 8192 on this path: never more than 4 vectors per thread)
+      return;
+    } else if constexpr (MERGE) {  // one row: the partials of this thread's vectors (clamped: always valid)
+      const int hs = p.head_size, hsh = 31 - __builtin_clz(hs);
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const int v = tid + NT * j, vv = v < nvec ? v : nvec - 1;
+        const int hh = (8 * vv) >> hsh, d0 = (8 * vv) & (hs - 1);
+#pragma unroll
+        for (int sp = 0; sp < kMergeMax; ++sp) {
+          const int sc = sp < p.asplit ? sp : p.asplit - 1;
+          const float* rec = p.apart + ((size_t)hh * p.asplit + sc) * (hs + 4);
+          mo[j][sp][0] = *reinterpret_cast<const u32x4*>(rec + d0);
+          mo[j][sp][1] = *reinterpret_cast<const u32x4*>(rec + d0 + 4);
+          mml[j][sp] = *reinterpret_cast<const float2*>(rec + hs);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int m = 0; m < MR; ++m)
 #pragma unroll
@@ -1061,6 +1091,28 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   auto a_finish = [&](auto rsc, auto mrc) {
     constexpr int RS = decltype(rsc)::value;
     constexpr int MR = decltype(mrc)::value;
+    if constexpr (MERGE && RS <= 4) {  // y = sum_s O_s f_s / sum_s L_s f_s, f_s = exp2(M_s - max M): attention_combine_kernel's order
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        float Mx = -INFINITY;
+#pragma unroll
+        for (int sp = 0; sp < kMergeMax; ++sp)
+          if (sp < p.asplit) Mx = fmaxf(Mx, mml[j][sp].x);
+        float L = 0.f, O[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int sp = 0; sp < kMergeMax; ++sp) {
+          if (sp >= p.asplit) break;
+          const float f = mml[j][sp].x == -INFINITY ? 0.f : exp2f(mml[j][sp].x - Mx);
+          L += mml[j][sp].y * f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) O[i] += __builtin_bit_cast(float, mo[j][sp][i >> 2][i & 3]) * f;
+        }
+        u32x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (uint32_t)f2bf(O[2 * i] / L) | ((uint32_t)f2bf(O[2 * i + 1] / L) << 16);
+        ap.x[j] = o;
+      }
+    }
     if (NORM) {
       float* redf = tail + 8;  // [wave][8] fp32
       {
@@ -1781,6 +1833,7 @@ static int launch(const GemvParams& p, hipStream_t s) {
 // producer's statistics, nstat); otherwise the fused RMSNorm needs the LDS image, and plain rows
 // are staged when they fit.
 static int pick_am(int wf, const GemvParams& p) {
+  if (p.apart) return (p.M == 1 && !p.norm_w && lds_fits(wf, 1, p.K)) ? AM_MERGE : -1;
   if (wf == WF_I8 && p.i8st) return (p.norm_w || p.M > 8) ? -1 : AM_I8Q;  // handed-over row statistics
   if (wf == WF_I8) {
     if (p.norm_w || !p.i8ws) return -1;
@@ -1824,6 +1877,12 @@ static int launch_ep(int ep, const GemvParams& p, hipStream_t s) {
 }
 template <int WF>
 static int launch_fmt(int am, int ep, const GemvParams& p, hipStream_t s) {
+  if (am == AM_MERGE) {  // the attn.c_proj residual op of one row (llj_linear_resid_attn)
+    if constexpr (WF == WF_W4 || WF == WF_BF16 || WF == WF_W8) {
+      if (ep == EP_RESID && p.M == 1 && p.K < LLJ_NWR_KMIN) return launch_mb<WF, AM_MERGE, EP_RESID, 1>(p, s);
+    }
+    return LLJ_EINVAL;
+  }
   if constexpr (WF == WF_I8) {
     if (am == AM_I8Q) return launch_ep<WF_I8, AM_I8Q>(ep, p, s);
     if (am == AM_I8S) return launch_ep<WF_I8, AM_I8S>(ep, p, s);

@@ -140,6 +140,18 @@ __global__ __launch_bounds__(NTH) void attention_part_kernel(const bf16_t* __res
                                    blockIdx.z, part);
 }
 
+// interleaved key splits of a short cache (attention.h ILV), partials merged by the consumer
+template <int HS, int U, int NTH, int SPECU>
+__global__ __launch_bounds__(NTH) void attention_ilv_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+                                                            const bf16_t* __restrict__ vc, const int* __restrict__ pos,
+                                                            int T, int S, int nh, float scale_log2, int nsplit,
+                                                            float* __restrict__ part, int spec_ok) {
+  __shared__ float lds[attention_lds_floats<HS, NTH>()];
+  attention_body<HS, U, NTH, true, SPECU, true>(q, kc, vc, nullptr, pos, T, S, nh, scale_log2, blockIdx.x, blockIdx.y,
+                                                lds, nsplit, blockIdx.z, part, nullptr, 0.f, nullptr, 0,
+                                                spec_ok != 0);
+}
+
 // ---- greedy next token: argmax over bf16 logits (lowest index on ties). Reference
 // generate.py:66-74 with top_k = 1 (multinomial over the kept maximum).
 __global__ __launch_bounds__(1024) void argmax_kernel(const bf16_t* __restrict__ logits, int ldl, int V,
@@ -504,7 +516,7 @@ int llj_attention(const void* q, const void* kcache, const void* vcache, void* y
 }
 
 size_t llj_attention_ws_bytes(int rows, int n_head, int head_size, int nsplit) {
-  return (size_t)rows * n_head * (nsplit < 1 ? 1 : nsplit) * (head_size + 2) * sizeof(float);
+  return (size_t)rows * n_head * (nsplit < 1 ? 1 : nsplit) * (head_size + 4) * sizeof(float);  // kAttPart
 }
 
 static int attention_split_run(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B,
@@ -546,6 +558,30 @@ int llj_attention_split(const void* q, const void* kcache, const void* vcache, v
 // Decode attention (one-block or split over nsplit key ranges) that also writes the LLM.int8
 // statistics of y for the int8 c_proj (i8ws.h; y_stats zeroed beforehand, B * T <= 8 rows) and zeroes
 // clr_words words at clr (the previous layer's mlp.c_proj statistics block).
+// Decode attention as nsplit interleaved key splits per (row, head) (block s takes the key groups
+// s * NG + NG * nsplit * i: a fixed set, loaded before the position is known at small grids), each writing
+// its unnormalized partial to part_ws; no combine launch -- llj_linear_resid_attn merges them in its prologue.
+int llj_attention_part(const void* q, const void* kcache, const void* vcache, const int* pos, int B, int T,
+                       int n_head, int head_size, int S, int nsplit, void* part_ws, void* stream) {
+  LLJ_REQUIRE(B > 0 && T > 0 && n_head > 0 && S > 0 && part_ws && nsplit >= 1 && nsplit <= 64);
+  const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
+  const dim3 grid(n_head, B * T, nsplit);
+  const int spec_ok = (int)(grid.x * grid.y * grid.z) <= 256;
+  hipStream_t s = (hipStream_t)stream;
+  if (head_size == 128)
+    hipLaunchKernelGGL((attention_ilv_kernel<128, LLJ_ATT_U, LLJ_ATT_NTH, LLJ_ATT_U / 2>), grid, dim3(LLJ_ATT_NTH), 0, s,
+                       (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, pos, T, S, n_head, sl2, nsplit,
+                       (float*)part_ws, spec_ok);
+  else if (head_size == 64)
+    hipLaunchKernelGGL((attention_ilv_kernel<64, LLJ_ATT_U, LLJ_ATT_NTH, LLJ_ATT_U / 2>), grid, dim3(LLJ_ATT_NTH), 0, s,
+                       (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, pos, T, S, n_head, sl2, nsplit,
+                       (float*)part_ws, spec_ok);
+  else
+    return LLJ_EINVAL;
+  LLJ_CHECK_LAUNCH();
+  return 0;
+}
+
 int llj_attention_i8(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
                      int n_head, int head_size, int S, int nsplit, void* part_ws, void* y_stats, void* clr,
                      int clr_words, float threshold, void* stream) {

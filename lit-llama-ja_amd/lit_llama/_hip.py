@@ -46,6 +46,8 @@ SIGNATURES = {
     "llj_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_attention_prefill": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_linear_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P],
+    "llj_linear_resid_attn": [_I, _P, _I, _I, _P, _P, _P, _I, _I, _I, _P, _P],
+    "llj_attention_part": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
     "llj_norm_swiglu": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _I, _P],
     "llj_norm_linear": [_I, _P, _P, _F, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P],
     "llj_i8_stats": [_P, _I, _I, _I, _F, _P, _P],

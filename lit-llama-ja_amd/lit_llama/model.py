@@ -106,6 +106,11 @@ ATTN_SPLIT_KEYS = 256  # 7B bs=1 at p = 2000 (S = 2048): 33.1 us one block, 14.4
 FLASH_MIN_T = 32
 
 
+# decode attention of ONE row as ATT_MERGE interleaved key splits per head (llj_attention_part) merged in
+# attn.c_proj's prologue (llj_linear_resid_attn) instead of one block per head; 0 = off (A/B, verdict r5 #4)
+ATT_MERGE = 0
+
+
 def attn_splits(S: int) -> int:
     """key ranges per (row, head) for a cache of S slots (1 = the one-block attention)."""
     if S < ATTN_SPLIT_MIN_S:
@@ -274,6 +279,12 @@ class _Work:
         if self.nsplit > 1:
             nb = _hip.lib().llj_attention_ws_bytes(M, cfg.n_head, C // cfg.n_head, self.nsplit)
             self.att_ws = torch.empty(nb, dtype=torch.uint8, device=device)
+        # one decode row, short cache: interleaved split partials merged in attn.c_proj (ATT_MERGE)
+        self.att_merge = ATT_MERGE if (ATT_MERGE > 1 and M == 1 and self.nsplit <= 1 and not need_i8) else 0
+        self.att_part = None
+        if self.att_merge:
+            nb = _hip.lib().llj_attention_ws_bytes(1, cfg.n_head, C // cfg.n_head, self.att_merge)
+            self.att_part = torch.empty(nb, dtype=torch.uint8, device=device)
 
 
 class LLaMA(nn.Module):
@@ -630,6 +641,11 @@ class LLaMA(nn.Module):
                           w.h_st.numel(), Linear8bitLtThreshold, st)
                 _hip.call("llj_i8_linear_resid", w.y.data_ptr(), C, wp.data_ptr(), P(sp), w.x.data_ptr(), C, M, C, C,
                           w.y_st.data_ptr(), st)
+            elif w.att_merge and not w.flash and fp in (0, 1, 3):  # split partials, merged by c_proj (A/B)
+                _hip.call("llj_attention_part", w.q.data_ptr(), kc.data_ptr(), vc.data_ptr(), pos.data_ptr(), B, T, nh,
+                          C // nh, S, w.att_merge, w.att_part.data_ptr(), st)
+                _hip.call("llj_linear_resid_attn", fp, w.att_part.data_ptr(), w.att_merge, nh, wp.data_ptr(), P(sp),
+                          w.x.data_ptr(), C, C, C, P(w.nst) if w.hand else None, st)
             else:
                 self._attention(w, kc, vc, pos, B, T, S, st)
                 self._resid(fp, w.y, wp, sp, w.x, M, C, C, w, st, w.nst if w.hand else None)

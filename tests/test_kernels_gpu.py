@@ -1549,3 +1549,45 @@ def test_int8_statistics_handoff_split_attention(hip, M, regime):
     np.testing.assert_array_equal(sca_s, sca_w)
     np.testing.assert_array_equal(fl_s, fl_w)
     assert fl_s.any() == (regime == "few")
+
+
+@pytest.mark.parametrize("nsplit,p0,S", [(2, 80, 144), (4, 80, 144), (4, 143, 144), (3, 300, 256), (4, 5, 144)])
+def test_attention_part_merged_in_cproj(hip, nsplit, p0, S):
+    """Decode attention of one row as nsplit interleaved key splits (llj_attention_part: block s takes
+    the key groups s * 32 + 32 nsplit i) whose partials attn.c_proj merges in its prologue
+    (llj_linear_resid_attn, wfmt 0 int4): x0 + bf16(y) . W^T against the oracle's attention + Linear, and
+    against the one-block attention + llj_linear_resid within the bf16 bound (the splits sum the keys
+    in another fp32 order). p0 >= S: the rolled ring; p0 = 5: most splits empty."""
+    rng = np.random.default_rng(nsplit * 1000 + p0 + S)
+    nh, hs = 32, 128
+    C = nh * hs
+    kc = bf16(rng.standard_normal((1, nh, S, hs)))
+    vc = bf16(rng.standard_normal((1, nh, S, hs)))
+    q = bf16(rng.standard_normal((1, C)) * 2)
+    pos = np.array([p0], np.int32)
+    qd, kd, vd, pd = T(q, torch.bfloat16), T(kc, torch.bfloat16), T(vc, torch.bfloat16), T(pos)
+    part = torch.full((hip.llj_attention_ws_bytes(1, nh, hs, nsplit),), 0xFF, dtype=torch.uint8, device=dev)
+    call(hip, "llj_attention_part", qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), pd.data_ptr(), 1, 1, nh, hs, S, nsplit,
+         part.data_ptr(), st())
+    Wref, Wd, szd = quant_operands(hip, rng, 0, C, C)
+    x0 = bf16(rng.standard_normal((1, C)))
+    xa = T(x0, torch.bfloat16)
+    call(hip, "llj_linear_resid_attn", 0, part.data_ptr(), nsplit, nh, Wd.data_ptr(), szd.data_ptr(), xa.data_ptr(), C,
+         C, C, None, st())
+    y = torch.empty(1, C, dtype=torch.bfloat16, device=dev)
+    call(hip, "llj_attention", qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), y.data_ptr(), pd.data_ptr(), 1, 1, nh, hs, S,
+         st())
+    xb = T(x0, torch.bfloat16)
+    call(hip, "llj_linear_resid", 0, y.data_ptr(), C, Wd.data_ptr(), szd.data_ptr(), xb.data_ptr(), C, 1, C, C, None, 0,
+         None, st())
+    torch.cuda.synchronize()
+    yo = bf16(_attn_oracle(q, kc, vc, pos, S, 1, nh, hs))
+    ref = x0 + bf16(yo.astype(np.float64) @ Wref.T.astype(np.float64))
+    assert_bf16_close(xa.float().cpu().numpy(), ref, f"merged attn.c_proj nsplit={nsplit} p={p0}", rel=2e-2)
+    assert_bf16_close(xa.float().cpu().numpy(), xb.float().cpu().numpy(), "merged vs one-block + resid", rel=2e-2)
+    # the partials themselves: the combine formula on the host gives the attention output
+    pr = part.cpu().numpy().view(np.float32).reshape(nh, nsplit, hs + 4)
+    Mx = pr[:, :, hs].max(1, keepdims=True)
+    f = np.where(pr[:, :, hs] == -np.inf, 0.0, np.exp2(pr[:, :, hs] - Mx))
+    ym = (pr[:, :, :hs] * f[..., None]).sum(1) / (pr[:, :, hs + 1] * f).sum(1, keepdims=True)
+    assert_bf16_close(ym.reshape(1, C), yo, f"merged partials nsplit={nsplit} p={p0}", rel=2e-2)
