@@ -1034,7 +1034,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
   const int mr = MB == 1 ? 1 : uniform(M <= 2 ? 2 : M <= 4 ? 4 : 8);
   // AM_MERGE: per A vector (8 dims of one head) and split, the partial's 8 outputs and (max, sum)
   constexpr bool MERGE = (AM == AM_MERGE);
-  u32x4 mo[MERGE ? APre<MB, NORM>::XR : 1][MERGE ? kMergeMax : 1][2];
+  // (plain floats: a u32x4 element read with a computed index returned element 0 for every index, §8)
+  float mo[MERGE ? APre<MB, NORM>::XR : 1][MERGE ? kMergeMax : 1][8];
   float2 mml[MERGE ? APre<MB, NORM>::XR : 1][MERGE ? kMergeMax : 1];
   auto a_issue = [&](auto rsc, auto mrc) {
     constexpr int RS = decltype(rsc)::value;
@@ -1052,8 +1053,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         for (int sp = 0; sp < kMergeMax; ++sp) {
           const int sc = sp < p.asplit ? sp : p.asplit - 1;
           const float* rec = p.apart + ((size_t)hh * p.asplit + sc) * (hs + 4);
-          mo[j][sp][0] = *reinterpret_cast<const u32x4*>(rec + d0);
-          mo[j][sp][1] = *reinterpret_cast<const u32x4*>(rec + d0 + 4);
+          const float4 o0 = *reinterpret_cast<const float4*>(rec + d0);
+          const float4 o1 = *reinterpret_cast<const float4*>(rec + d0 + 4);
+          mo[j][sp][0] = o0.x; mo[j][sp][1] = o0.y; mo[j][sp][2] = o0.z; mo[j][sp][3] = o0.w;
+          mo[j][sp][4] = o1.x; mo[j][sp][5] = o1.y; mo[j][sp][6] = o1.z; mo[j][sp][7] = o1.w;
           mml[j][sp] = *reinterpret_cast<const float2*>(rec + hs);
         }
       }
@@ -1105,7 +1108,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
           const float f = mml[j][sp].x == -INFINITY ? 0.f : exp2f(mml[j][sp].x - Mx);
           L += mml[j][sp].y * f;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) O[i] += __builtin_bit_cast(float, mo[j][sp][i >> 2][i & 3]) * f;
+          for (int i = 0; i < 8; ++i) O[i] += mo[j][sp][i] * f;
         }
         u32x4 o;
 #pragma unroll
