@@ -123,6 +123,11 @@ def test_7b_llm_int8_full_depth_handoff_equals_statistics_launches():
     assert np.isfinite(log_w).all()
     rels = [float(np.linalg.norm(log_h[s] - log_w[s]) / np.linalg.norm(log_w[s])) for s in range(STEPS + 1)]
     print(f"[full depth int8] hand-off vs statistics launches, rel per step: {[round(r, 4) for r in rels]}")
+    # step 0 (the prompt's last row: no hand-off involved) is the same computation: bitwise equal; step 1
+    # (the first decode step, every row on the same inputs in both runs): the whole batch within 0.1
+    # (measured 0.0748 on MI355X, round 6: the side product's fp32 order through 32 layers)
+    assert rels[0] == 0.0, rels[0]
+    assert rels[1] < 0.1, rels[1]
     for b in range(8):
         for s in range(STEPS + 1):
             lh, lw = log_h[s, b], log_w[s, b]
