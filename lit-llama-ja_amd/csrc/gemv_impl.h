@@ -478,6 +478,9 @@ struct APre {
 #ifndef LLJ_AFRAG
 #define LLJ_AFRAG 1  // 1: a chunk's NSTEP A fragments read together before its MFMAs (0: one read per step)
 #endif
+#ifndef LLJ_PF
+#define LLJ_PF 0  // L2 prefetch distance of the weight stream in chunks (0 off; A/B)
+#endif
 #ifndef LLJ_FLAT_EPI
 #define LLJ_FLAT_EPI 1  // 1: batched-row epilogues spread over every thread of the workgroup (0: per owner lane)
 #endif
@@ -648,6 +651,18 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
     return wave + NW * ii;
   };
   const int vz = (I8Q || SIS) ? vzero() : 0;  // uniform side data stays in VGPRs (common.h vzero)
+  // L2 prefetch (LLJ_PF > 0): with chunk i's loads, one dword per lane of chunk i + LLJ_PF's weight
+  // blocks (a wave's 64 lanes touch the whole 1 KiB block, so its lines are in L2 when the real
+  // 16-byte loads come): in-flight bytes past the register ring at 1 VGPR per block. The dword is
+  // "used" (an empty asm) when its slot is reloaded, so the compiler counts it in its waits.
+  constexpr int PF = LLJ_PF;
+  uint32_t pfv[PF > 0 ? D : 1][TPW][WV][2];
+#pragma unroll
+  for (int d = 0; d < (PF > 0 ? D : 1); ++d)
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+#pragma unroll
+      for (int v = 0; v < WV; ++v) pfv[d][j][v][0] = pfv[d][j][v][1] = 0u;
   auto load = [&](int d, int i) {
     int c = chunk_of(i);
     c = c < 0 ? 0 : (c >= KC ? KC - 1 : c);  // always a valid chunk (loads past the end are unused)
@@ -686,6 +701,19 @@ __device__ __forceinline__ void gemv_body(const GemvParams& p, const int nt0, un
         r1[d][j][v] = __builtin_nontemporal_load(w1[j] + (size_t)c * wstep + vstride * v);
         if (DUAL) r2[d][j][v] = __builtin_nontemporal_load(w2[j] + (size_t)c * wstep + vstride * v);
       }
+    if constexpr (PF > 0) {
+      int cp = i + PF < nmy ? chunk_of(i + PF) : -1;
+      const bool pf_on = cp >= 0;  // (past the wave's last chunk: a re-read of chunk c, an L2 hit)
+      cp = pf_on ? cp : c;
+#pragma unroll
+      for (int j = 0; j < TPW; ++j)
+#pragma unroll
+        for (int v = 0; v < WV; ++v) {
+          asm volatile("" ::"v"(pfv[d][j][v][0]), "v"(pfv[d][j][v][1]));  // the slot's previous prefetch
+          pfv[d][j][v][0] = *reinterpret_cast<const uint32_t*>(w1[j] + (size_t)cp * wstep + vstride * v);
+          if (DUAL) pfv[d][j][v][1] = *reinterpret_cast<const uint32_t*>(w2[j] + (size_t)cp * wstep + vstride * v);
+        }
+    }
     if (!ALDS) {
 #pragma unroll
       for (int t = 0; t < NSTEP; ++t)
