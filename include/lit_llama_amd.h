@@ -73,7 +73,8 @@ int llj_set_stream_a(int mode);
  *   LLJ_OPT_GEMM_GLDS      0..1  prefill GEMMs: LDS-DMA (1) or register-staged (0) kernel for every format (LLJ_GEMM_GLDS)
  *   LLJ_OPT_GLDS_COST128   0..   LDS-DMA GEMM: cost of a 256 x 128 tile in % of a 256 x 256 one (LLJ_GLDS_COST128)
  *   LLJ_OPT_GEMV_LDS_A_KB  56..96 decode GEMVs: cap of the staged A image in KiB (LLJ_GEMV_LDS_A_KB)
- *   LLJ_OPT_ATT_SPEC_BATCH 0..1  decode attention: the half speculative key pass also past 64 blocks (LLJ_ATT_SPEC_BATCH) */
+ *   LLJ_OPT_ATT_SPEC_BATCH 0..1  decode attention: the half speculative key pass also past 64 blocks (LLJ_ATT_SPEC_BATCH)
+ *   LLJ_OPT_GEMM_W4Z       0..1  prefill int4 GEMMs with LLJ_WF_ZINT: convert-once LDS-DMA kernel (1) or the int4 default (0) (LLJ_GEMM_W4Z) */
 enum {
   LLJ_OPT_ATT_SPEC_FULL = 0,
   LLJ_OPT_FLASH_QB = 1,
@@ -82,7 +83,8 @@ enum {
   LLJ_OPT_GLDS_COST128 = 4,
   LLJ_OPT_GEMV_LDS_A_KB = 5,
   LLJ_OPT_ATT_SPEC_BATCH = 6,
-  LLJ_OPT_COUNT = 7
+  LLJ_OPT_GEMM_W4Z = 7,
+  LLJ_OPT_COUNT = 8
 };
 int llj_set_option(int which, int value);
 
@@ -180,7 +182,12 @@ int llj_norm_linear(int wfmt, const void* x, const void* norm_w, float eps, cons
  * through LDS (csrc/gemm.hip). wfmt 0 (int4 W4P, sz = (scale, 128 + zero)), 1 (bf16 (N, K)),
  * 3 (gptq.int8 W8P, sz = (scale, 2176 + zero)) or 4 | (g / 128) << 8 (grouped int4, sz per
  * (group, column) as for llj_linear; B fragments dequantized to bf16((q - z) * s)).
- * N % 128 == 0, K % 128 == 0, lda % 8 == 0; any M >= 1. Same epilogue semantics as the GEMVs. */
+ * N % 128 == 0, K % 128 == 0, lda % 8 == 0; any M >= 1. Same epilogue semantics as the GEMVs.
+ * wfmt 0 | LLJ_WF_ZINT: int4 whose zeros are all integers (GPTQ's round(-min / scale); the caller
+ * checks): for M >= 256 each chunk's codes are converted once per workgroup into an exact bf16
+ * (q - z) tile and the scale is applied in the epilogue, y = s * sum_k A (q - z) -- the reference
+ * kernel's ((q - zero) * scale) . A (quantization.py:263-267) with the scale factored out. */
+#define LLJ_WF_ZINT 0x20000
 int llj_gemm_linear(int wfmt, const void* A, int lda, const void* W, const void* sz, void* C, int ldc, int M, int N,
                     int K, void* stream);
 /* x[M, N] += A . W^T (bf16 residual add, model.py:172-173). */

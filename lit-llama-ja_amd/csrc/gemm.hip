@@ -48,7 +48,8 @@
 
 namespace llj {
 
-enum : int { GWF_W4 = 0, GWF_BF16 = 1, GWF_I8 = 2, GWF_W8 = 3, GWF_W4G = 4 };
+// GWF_W4Z: int4 W4P with integral zeros (LLJ_WF_ZINT) in the convert-once LDS-DMA GEMM (internal)
+enum : int { GWF_W4 = 0, GWF_BF16 = 1, GWF_I8 = 2, GWF_W8 = 3, GWF_W4G = 4, GWF_W4Z = 5 };
 enum : int { GEP_STORE = 0, GEP_RESID = 1, GEP_QKV = 2, GEP_SILU_MUL = 3 };
 
 struct GemmParams {
@@ -662,16 +663,22 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 
 template <int WF, int BN>
 struct GldsGeo {
-  // waves along N: 4 at BN 256; at BN 128, 2 for bf16 (64 x 64 per wave: fewer A fragment reads) and
-  // LLJ_GLDS_W4_WN for int4 (4: 128 x 32 per wave, each B fragment dequantized by 2 waves instead of 4)
+  // waves along N: 4 at BN 256; at BN 128, 2 for bf16 and the convert-once int4 (64 x 64 per wave:
+  // fewer A fragment reads) and LLJ_GLDS_W4_WN for the per-fragment int4 (4: 128 x 32 per wave, each B
+  // fragment dequantized by 2 waves instead of 4)
+  static constexpr bool CVT = WF == GWF_W4Z;
   static constexpr int WN = BN == 256 ? 4 : WF == GWF_W4 ? LLJ_GLDS_W4_WN : 2, WM = 8 / WN;
   static constexpr int MI = 256 / WM / 16, NJ = BN / WN / 16;
   static constexpr size_t SA = 256 * 128;
-  static constexpr size_t SB = WF == GWF_W4 ? 8192 : (size_t)BN * 128;  // W4 at BN 128: waves 4-7 stage a copy
+  // int4 (both forms) at BN 128: the chunk's 4 KiB of W4P codes, waves 4-7 staging a copy (equal DMA
+  // counts per wave)
+  static constexpr size_t SB = (WF == GWF_W4 || CVT) ? 8192 : (size_t)BN * 128;
   static constexpr size_t STAGE = SA + SB;
-  static constexpr int NST = 3 * STAGE + 1024 <= 160 * 1024 ? 3 : 2;
-  static constexpr size_t LDS = NST * STAGE + 1024;  // + the row sums (W4)
-  static constexpr int NG = 4 + (WF == GWF_W4 ? 1 : BN / 64);  // glds per thread per chunk
+  // convert-once int4: two bf16 (q - z) B tiles (BN rows x 128 B, the bf16 image) after the stages
+  static constexpr size_t BF = CVT ? 2 * (size_t)BN * 128 : 0;
+  static constexpr int NST = 3 * STAGE + BF + 1024 <= 160 * 1024 ? 3 : 2;
+  static constexpr size_t LDS = NST * STAGE + BF + 1024;  // + the row sums (per-fragment int4)
+  static constexpr int NG = 4 + ((WF == GWF_W4 || CVT) ? 1 : BN / 64);  // glds per thread per chunk
 };
 
 template <int N>
@@ -681,10 +688,12 @@ __device__ __forceinline__ void wait_vm() {
 
 template <int WF, int EP, int BN>
 __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
-  static_assert(WF == GWF_BF16 || WF == GWF_W4, "LDS-DMA GEMM: bf16 and int4 W4P");
+  static_assert(WF == GWF_BF16 || WF == GWF_W4 || WF == GWF_W4Z, "LDS-DMA GEMM: bf16 and int4 W4P");
+  static_assert(WF != GWF_W4Z || BN == 128, "convert-once int4: 256 x 128 tiles");
   using G = GldsGeo<WF, BN>;
   constexpr int MI = G::MI, NJ = G::NJ, WN = G::WN, NST = G::NST;
-  constexpr bool NIB = WF == GWF_W4;
+  constexpr bool NIB = WF == GWF_W4;  // per-fragment dequant (bf16 128 + q) + row sums
+  constexpr bool CVT = G::CVT;        // W4P codes converted once per chunk into a bf16 (q - z) tile
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w / WN, wc = w % WN;
@@ -710,18 +719,27 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     asrc[q] = p.A + (size_t)(m < M ? m : M - 1) * p.lda + 8 * dseg;
   }
   const char* bsrc;
-  if constexpr (NIB) {  // W4P: wave w stages tiles 2 w, 2 w + 1 (BN 128: waves 4-7 a copy of 0-3's)
+  if constexpr (NIB || CVT) {  // W4P: wave w stages tiles 2 w, 2 w + 1 (BN 128: waves 4-7 a copy of 0-3's)
     const int tl = (2 * w + (lane >> 5)) % (BN / 16);
     bsrc = reinterpret_cast<const char*>(p.W) + (size_t)(n0 / 16 + tl) * KC128 * 1024 + 16 * (lane & 31);
   } else {
     bsrc = reinterpret_cast<const char*>(reinterpret_cast<const bf16_t*>(p.W) + (size_t)(n0 + drow) * K + 8 * dseg);
   }
+  // convert-once int4: the codes run one chunk ahead of A (DMA group c = A(c) + the codes of chunk
+  // c + 1, into the stage buffer of chunk c + 1), so a chunk's codes have landed one iteration before
+  // its MFMAs and are converted into its bf16 tile in between
+  auto stage_codes = [&](int buf, int c) {
+    __builtin_amdgcn_global_load_lds(bsrc + (size_t)(c >> 1) * 1024 + 512 * (c & 1),
+                                     (lds_void_t*)(smem + (size_t)buf * G::STAGE + G::SA + 1024 * w), 16, 0, 0);
+  };
   auto stage = [&](int buf, int c) {
     unsigned char* base = smem + (size_t)buf * G::STAGE;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       __builtin_amdgcn_global_load_lds(asrc[q] + (size_t)c * 64, (lds_void_t*)(base + (64 * q + 8 * w) * 128), 16, 0, 0);
-    if constexpr (NIB) {
+    if constexpr (CVT) {
+      stage_codes(buf + 1 == NST ? 0 : buf + 1, c + 1 < KC ? c + 1 : KC - 1);
+    } else if constexpr (NIB) {
       __builtin_amdgcn_global_load_lds(bsrc + (size_t)(c >> 1) * 1024 + 512 * (c & 1),
                                        (lds_void_t*)(base + G::SA + 1024 * w), 16, 0, 0);
     } else {
@@ -787,9 +805,40 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
       for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
-  auto compute = [&](int buf) {
+  // convert-once int4: wave w converts tile w's codes of a chunk (lane: word pair gp of W4P lane L =
+  // 16 s + column) into 16-B segments 4 s + 2 gp, 4 s + 2 gp + 1 of B row 16 w + column, in the bf16
+  // image's swizzle: bf16(128 + q) - (128 + z) in fp32 is q - z exactly (integral zeros), so the tile
+  // holds exact integers and the scale is applied in the epilogue
+  const unsigned char* bf_lds = smem + NST * G::STAGE;
+  float zoff = 0.f;  // 128 + zero of this lane's column
+  if constexpr (CVT) zoff = p.sz[n0 + 16 * w + ((lane >> 1) & 15)].y;
+  auto convert = [&](int buf, int slot) {
+    const int L = lane >> 1, gp = lane & 1, col = L & 15, s = L >> 4, cr = 16 * w + col;
+    // the read in asm, with its own wait: read as a plain LDS load, hipcc waits vmcnt(0) for every
+    // LDS-DMA in flight first (the next chunks' too), de-pipelining the loop
+    const uint32_t ra = (uint32_t)(uintptr_t)(lds_void_t*)(smem + (size_t)buf * G::STAGE + G::SA + 512 * w + 16 * L + 8 * gp);
+    uint2 wv2;
+    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(wv2) : "v"(ra) : "memory");
+    const uint32_t da = (uint32_t)(uintptr_t)(lds_void_t*)(bf_lds + (size_t)slot * BN * 128 + cr * 128);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t wv = h ? wv2.y : wv2.x;
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t d = and_or(wv >> (4 * e), msk, mag);  // bf16 pair (128 + q_lo, 128 + q_hi)
+        const float lo = __uint_as_float(d << 16) - zoff, hi = __uint_as_float(d & 0xFFFF0000u) - zoff;
+        o[e] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xFFFF0000u);  // exact: small integers
+      }
+      // (asm too: hipcc also waits vmcnt(0) before a plain LDS store while LDS-DMAs are in flight; the
+      // loop's lgkmcnt(0) before its barrier retires it)
+      const u32x4 ov = {o[0], o[1], o[2], o[3]};
+      asm volatile("ds_write_b128 %0, %1" ::"v"(da + (((4 * s + 2 * gp + h) ^ ((col >> 1) & 7)) * 16)), "v"(ov) : "memory");
+    }
+  };
+  auto compute = [&](int buf, int slot) {
     const unsigned char* Ab = smem + (size_t)buf * G::STAGE;
-    const unsigned char* Bb = Ab + G::SA;
+    const unsigned char* Bb = CVT ? bf_lds + (size_t)slot * BN * 128 : Ab + G::SA;
     if constexpr (LLJ_GLDS_PRE && BN == 128) {  // both MFMA steps' fragments read before either's MFMAs
       bf16x8 af0[MI], bf0[NJ], af1[MI], bf1[NJ];
       frags(Ab, Bb, 0, af0, bf0);
@@ -807,9 +856,18 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   };
 
   // ---- K loop: NST - 1 chunks staged ahead
+  if constexpr (CVT) {  // chunk 0's codes first, converted before the loop
+    static_assert(NST == 3, "convert-once int4: three stages");
+    stage_codes(0, 0);
+  }
 #pragma unroll
   for (int c = 0; c < NST - 1; ++c)
     if (c < KC) stage(c, c);
+  if constexpr (CVT) {
+    wait_vm<2 * G::NG>();  // chunk 0's codes (KC >= 2: both groups were issued)
+    __builtin_amdgcn_s_barrier();
+    convert(0, 0);
+  }
   int cb = 0;  // buffer of chunk t
   for (int tc = 0; tc < KC; ++tc) {
     if constexpr (NST == 3) {
@@ -817,10 +875,13 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     } else {
       wait_vm<0>();
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of chunk t - 1 are done
-    __builtin_amdgcn_s_barrier();  // chunk t landed for every wave; chunk t - 1's buffer is free
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads (and tile writes) of chunk t - 1 are done
+    __builtin_amdgcn_s_barrier();  // chunk t landed for every wave (CVT: and chunk t + 1's codes); t - 1's buffers are free
     if (tc + NST - 1 < KC) stage(cb == 0 ? NST - 1 : cb - 1, tc + NST - 1);
-    compute(cb);
+    if constexpr (CVT) {
+      if (tc + 1 < KC) convert(cb + 1 == NST ? 0 : cb + 1, (tc + 1) & 1);
+    }
+    compute(cb, tc & 1);
     cb = cb + 1 == NST ? 0 : cb + 1;
   }
 
@@ -842,7 +903,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     const int nblk = n0 + wc * 16 * NJ + 16 * j;
     const int n = nblk + row;
     float2 szn = make_float2(1.f, 0.f);
-    if constexpr (NIB) szn = p.sz[n];
+    if constexpr (NIB || CVT) szn = p.sz[n];
     constexpr int GI = (MI > 4 && EP == GEP_QKV) ? 1 : 4;  // row blocks whose operands are in flight together
 #pragma unroll
     for (int i0 = 0; i0 < MI; i0 += GI) {
@@ -864,6 +925,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
           const int m = m0 + ml;
           float y = acc[i0 + i][j][r];
           if constexpr (NIB) y = szn.x * (y - szn.y * rs_lds[ml]);
+          if constexpr (CVT) y = szn.x * y;
           gemm_store_elem<EP>(p, y, m, n, nblk, m < M, row, Cd, opv[i][r], bps[i][r]);
         }
       }
@@ -920,8 +982,21 @@ static int gemm_glds_run(const GemmParams& p, hipStream_t s) {
   return gemm_glds_launch<WF, EP, 128>(p, s);
 }
 
+// option LLJ_OPT_GEMM_W4Z (LLJ_GEMM_W4Z) 1 / 0: int4 with integral zeros (LLJ_WF_ZINT) in the
+// convert-once LDS-DMA kernel / in the int4 default kernel
+#ifndef LLJ_GEMM_W4Z
+#define LLJ_GEMM_W4Z 1
+#endif
+static bool w4z_enabled() {
+  const int o = opt(LLJ_OPT_GEMM_W4Z);
+  return o >= 0 ? o != 0 : LLJ_GEMM_W4Z != 0;
+}
+
 template <int EP>
 static int gemm_run(int wfmt, GemmParams& p, void* stream) {
+  const bool zint = (wfmt & LLJ_WF_ZINT) != 0;  // int4 only: every zero is an integer
+  wfmt &= ~LLJ_WF_ZINT;
+  if (zint && wfmt != GWF_W4) return LLJ_EINVAL;
   if (p.M < 1 || p.N % kGBN || p.K % kGBK || p.K < kGBK || (p.lda & 7)) return LLJ_EINVAL;
   if (EP != GEP_QKV && (!p.C || (p.ldc & 1))) return LLJ_EINVAL;
   // the int4 / bf16 kernels assume an even count of 64-deep chunks (gemm_body's __builtin_assume)
@@ -929,6 +1004,7 @@ static int gemm_run(int wfmt, GemmParams& p, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (wfmt == GWF_W4) {
     if (!p.sz) return LLJ_EINVAL;
+    if (zint && p.M >= 256 && w4z_enabled()) return gemm_glds_launch<GWF_W4Z, EP, 128>(p, s);
     if (p.M >= 256 && p.K % 128 == 0 && glds_enabled(GWF_W4)) return gemm_glds_run<GWF_W4, EP>(p, s);
     if (LLJ_GEMM_BM256_W4 && p.M >= 256) return gemm_launch<GWF_W4, EP, 256>(p, s);
     return gemm_launch<GWF_W4, EP>(p, s);

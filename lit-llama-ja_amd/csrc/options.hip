@@ -22,6 +22,7 @@ constexpr OptSpec kOpts[LLJ_OPT_COUNT] = {
     {"LLJ_GLDS_COST128", 0, 100000}, // LDS-DMA GEMM: cost of a 256 x 128 tile in % of a 256 x 256 one
     {"LLJ_GEMV_LDS_A_KB", 56, 96},   // decode GEMVs: cap of the staged A image (KiB)
     {"LLJ_ATT_SPEC_BATCH", 0, 1},    // decode attention: the half speculative pass also for large grids
+    {"LLJ_GEMM_W4Z", 0, 1},          // prefill int4 GEMMs with integral zeros: the convert-once LDS-DMA kernel
 };
 
 int env_value(int i) {

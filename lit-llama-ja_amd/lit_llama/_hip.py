@@ -90,8 +90,9 @@ class HipError(RuntimeError):
 
 # llj_set_option indices (include/lit_llama_amd.h LLJ_OPT_*)
 WF_I8_ROWSTATS = 0x10000  # wfmt flag: i8ws is a decode hand-off block (include/lit_llama_amd.h)
+WF_ZINT = 0x20000  # prefill GEMM wfmt flag: int4 whose zeros are all integers (include/lit_llama_amd.h)
 (OPT_ATT_SPEC_FULL, OPT_FLASH_QB, OPT_FLASH_PAIR, OPT_GEMM_GLDS, OPT_GLDS_COST128, OPT_GEMV_LDS_A_KB,
- OPT_ATT_SPEC_BATCH) = range(7)
+ OPT_ATT_SPEC_BATCH, OPT_GEMM_W4Z) = range(8)
 
 
 def lib() -> ctypes.CDLL:

@@ -143,6 +143,19 @@ _GEMM_FMTS = (0, 1, 2, 3, 4)  # weight formats (low byte of wfmt; 4 = grouped in
 def _gemm_fmt(wfmt: int) -> bool:
     return (wfmt & 0xFF) in _GEMM_FMTS
 
+
+# int4 prompt GEMMs of Linears whose zeros are all integers (GPTQ's round(-min / scale)): each chunk's
+# codes converted once per workgroup into an exact bf16 (q - z) tile, the scale in the epilogue
+# (LLJ_WF_ZINT; csrc/gemm.hip, the convert-once LDS-DMA kernel at M >= 256)
+GEMM_ZINT = True
+
+
+def _gz(wfmt: int, lin: nn.Module) -> int:
+    """wfmt of a prompt-GEMM call on `lin`: int4 with LLJ_WF_ZINT when its zeros are integers."""
+    if GEMM_ZINT and wfmt == 0 and hasattr(lin, "zeros_integral") and lin.zeros_integral():
+        return wfmt | _hip.WF_ZINT
+    return wfmt
+
 # LLM.int8 prompt rows: the outlier columns of each GEMM's activation and weight pre-gathered as f16
 # rows (llj_i8_gather_act / _weight), so the fp16 side product runs as a dense f16 GEMM over them
 I8_GATHER = True
@@ -520,10 +533,10 @@ class LLaMA(nn.Module):
             else:
                 _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_1.scale.data_ptr(), blk.rms_1.eps,
                           w.xn.data_ptr(), None, M, C, st)
-                _hip.call("llj_gemm_qkv_rope", fa, w.xn.data_ptr(), wa.data_ptr(), P(sa), w.q.data_ptr(),
+                _hip.call("llj_gemm_qkv_rope", _gz(fa, blk.attn.c_attn), w.xn.data_ptr(), wa.data_ptr(), P(sa), w.q.data_ptr(),
                           kc.data_ptr(), vc.data_ptr(), self.rope_cache.data_ptr(), pos.data_ptr(), B, T, C, nh, S, st)
             self._attention(w, kc, vc, pos, B, T, S, st)
-            self._gemm_resid(fp, w.y, wp, sp, w.x, M, C, C, w, st)
+            self._gemm_resid(_gz(fp, blk.attn.c_proj), w.y, wp, sp, w.x, M, C, C, w, st)
             if f1 != f2:
                 raise TypeError("c_fc1 and c_fc2 must share a weight format")
             if f1 == 2:
@@ -536,11 +549,11 @@ class LLaMA(nn.Module):
             else:
                 _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
                           w.xn.data_ptr(), None, M, C, st)
-                _hip.call("llj_gemm_linear", f1, w.xn.data_ptr(), C, w1.data_ptr(), P(s1), w.h.data_ptr(), H, M, H, C,
-                          st)
-                _hip.call("llj_gemm_silu_mul", f2, w.xn.data_ptr(), C, w2.data_ptr(), P(s2), w.h.data_ptr(), H, M, H,
-                          C, st)
-            self._gemm_resid(fd, w.h, wd, sd, w.x, M, C, H, w, st)
+                _hip.call("llj_gemm_linear", _gz(f1, blk.mlp.c_fc1), w.xn.data_ptr(), C, w1.data_ptr(), P(s1),
+                          w.h.data_ptr(), H, M, H, C, st)
+                _hip.call("llj_gemm_silu_mul", _gz(f2, blk.mlp.c_fc2), w.xn.data_ptr(), C, w2.data_ptr(), P(s2),
+                          w.h.data_ptr(), H, M, H, C, st)
+            self._gemm_resid(_gz(fd, blk.mlp.c_proj), w.h, wd, sd, w.x, M, C, H, w, st)
 
     def _gemm_resid(self, f, A, W, sz, x, M, N, K, w, st):
         """x += A . W^T for many rows (LLM.int8: the statistics of A first)."""
@@ -730,8 +743,8 @@ class LLaMA(nn.Module):
         elif M >= GEMM_MIN_ROWS and _gemm_fmt(f) and C % 128 == 0 and V % 128 == 0:  # many rows: GEMM
             xn = torch.empty_like(x)
             _hip.call("llj_rmsnorm_rows", x.data_ptr(), ln.scale.data_ptr(), ln.eps, xn.data_ptr(), None, M, C, st)
-            _hip.call("llj_gemm_linear", f, xn.data_ptr(), C, W.data_ptr(), _hip.ptr(sz), out.data_ptr(), out.stride(0),
-                      M, V, C, st)
+            _hip.call("llj_gemm_linear", _gz(f, self.lm_head), xn.data_ptr(), C, W.data_ptr(), _hip.ptr(sz),
+                      out.data_ptr(), out.stride(0), M, V, C, st)
             return
         elif x is w.x and w.hand and f != 2 and len(self.transformer.h) > 0:  # the last mlp.c_proj's partials
             nst = w.nst

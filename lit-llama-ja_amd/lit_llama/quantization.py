@@ -78,6 +78,7 @@ class ColBlockQuantizedLinear(torch.nn.Module):
         self._qkey = None   # (data_ptr, version) of quant_weight right after its in-place repack
         self._szkey = None  # (scales, zeros) identity the _sz pairs were built from
         self._g = None      # any-shape path: (key, fp32 scales, fp32 zeros)
+        self._zint = None   # (_szkey, every zero an integer) -- zeros_integral()
 
     # ---- reference buffer utilities (quantization.py:374-409) -------------------------
     def pack_weight(self, weight):
@@ -182,7 +183,21 @@ class ColBlockQuantizedLinear(torch.nn.Module):
             self._qkey = None
         self._szkey = None
         self._g = None
+        self._zint = None
         return super()._apply(fn, *args, **kwargs)
+
+    def zeros_integral(self) -> bool:
+        """Every zero an integer of magnitude <= 240 (GPTQ's round(-min / scale), clamped to the code
+        range): the prompt GEMMs then convert the codes into an exact bf16 (q - z) tile
+        (LLJ_WF_ZINT, csrc/gemm.hip). One device sync per scales / zeros version; False while a
+        graph is being captured (the default int4 kernel then runs)."""
+        self._prepare()
+        if self._zint is None or self._zint[0] != self._szkey:
+            if torch.cuda.is_current_stream_capturing():
+                return False
+            zr = self.zeros.float()
+            self._zint = (self._szkey, bool(torch.equal(zr, torch.round(zr))) and float(zr.abs().max()) <= 240.0)
+        return self._zint[1]
 
     def _wspec(self):
         """(wfmt, weight operand, sz operand) for the fused model kernels."""
@@ -365,6 +380,19 @@ class Linear8bitLt(torch.nn.Module):
                 self.weight.copy_(cb)
             self._ikey = None
         return super()._apply(fn, *args, **kwargs)
+
+    def zeros_integral(self) -> bool:
+        """Every zero an integer of magnitude <= 240 (GPTQ's round(-min / scale), clamped to the code
+        range): the prompt GEMMs then convert the codes into an exact bf16 (q - z) tile
+        (LLJ_WF_ZINT, csrc/gemm.hip). One device sync per scales / zeros version; False while a
+        graph is being captured (the default int4 kernel then runs)."""
+        self._prepare()
+        if self._zint is None or self._zint[0] != self._szkey:
+            if torch.cuda.is_current_stream_capturing():
+                return False
+            zr = self.zeros.float()
+            self._zint = (self._szkey, bool(torch.equal(zr, torch.round(zr))) and float(zr.abs().max()) <= 240.0)
+        return self._zint[1]
 
     def _wspec(self):
         self._prepare()

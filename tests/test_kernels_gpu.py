@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 import torch
 
+from lit_llama import _hip
 from oracle import llama_np as O
 from tests.helpers import assert_bf16_close, bf16, w4p_pack_np, w8p_pack_np
 
@@ -109,7 +110,7 @@ def quant_operands(hip, rng, wfmt, N, K):
         g = 128 * (wfmt >> 8)
         qw, sc, z = rand_w4g(rng, N, K, g)
         return O.colblock_get_weight(qw, sc, z, 4, tile_cols=g), repack(hip, qw), sz_grouped(hip, sc, z)
-    if wfmt == 0:
+    if wfmt & ~_hip.WF_ZINT == 0:  # int4 W4P (integral zeros: LLJ_WF_ZINT may be set)
         qw, sc, z = rand_w4(rng, N, K)
         return O.colblock_get_weight(qw, sc, z, 4), repack(hip, qw), sz_of(hip, sc, z)
     if wfmt == 3:
@@ -1188,8 +1189,64 @@ def test_gemm_glds_tiles(hip, glds_tile, wfmt, M, N, K):
     assert_bf16_close(xr.float().cpu().numpy(), x0 + bf16(y), f"gemm resid {glds_tile} wfmt={wfmt}")
 
 
+ZINT4 = _hip.WF_ZINT  # int4 with integral zeros: the convert-once LDS-DMA kernel at M >= 256
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 512, 256), (300, 4096, 4096), (520, 11008, 4096), (257, 4096, 11008),
+                                   (2048, 12288, 4096), (100, 384, 1024)])
+def test_gemm_w4z_convert_once(hip, M, N, K):
+    """int4 prompt GEMM with LLJ_WF_ZINT (each chunk's codes converted once per workgroup into a bf16
+    (q - z) tile, the scale in the epilogue; M < 256 takes the default int4 kernel) against the
+    oracle, store and residual epilogues, ragged M; and the same call with the option off (the
+    default int4 kernel) within bf16 rounding of it."""
+    rng = np.random.default_rng(M + N + K + 5)
+    Wref, Wd, szd = quant_operands(hip, rng, ZINT4, N, K)
+    x = bf16(rng.standard_normal((M, K)).astype(np.float32))
+    xd = T(x, torch.bfloat16)
+    outs = []
+    for w4z in (1, 0):
+        old = hip.llj_set_option(_hip.OPT_GEMM_W4Z, w4z)
+        out = torch.full((M + 1, N), 7.0, dtype=torch.bfloat16, device=dev)  # row M: canary
+        call(hip, "llj_gemm_linear", ZINT4, xd.data_ptr(), K, Wd.data_ptr(), szd.data_ptr(), out.data_ptr(), N, M, N,
+             K, st())
+        hip.llj_set_option(_hip.OPT_GEMM_W4Z, old)
+        torch.cuda.synchronize()
+        outs.append(out.float().cpu().numpy())
+    y = x @ Wref.T
+    o = outs[0]
+    assert_bf16_close(o[:M], y, f"gemm w4z M={M} N={N} K={K}")
+    assert (o[M] == 7.0).all(), "wrote past row M"
+    assert_bf16_close(outs[1][:M], o[:M], f"gemm w4z vs default int4 M={M}")
+    x0 = bf16(rng.standard_normal((M, N)).astype(np.float32))
+    xr = T(x0, torch.bfloat16)
+    call(hip, "llj_gemm_resid", ZINT4, xd.data_ptr(), K, Wd.data_ptr(), szd.data_ptr(), xr.data_ptr(), N, M, N, K,
+         st())
+    torch.cuda.synchronize()
+    assert_bf16_close(xr.float().cpu().numpy(), x0 + bf16(y), f"gemm w4z resid M={M}")
+
+
+def test_gemm_w4z_exact_on_integer_rows(hip):
+    """The convert-once tile is exact: with small-integer activations every product and fp32 partial
+    sum is an integer below 2^24, so the GEMM is bitwise bf16(s * sum_k a (q - z))."""
+    rng = np.random.default_rng(606)
+    M, N, K = 512, 1024, 4096
+    qw, sc, z = rand_w4(rng, N, K)
+    Wd, szd = repack(hip, qw), sz_of(hip, sc, z)
+    a = rng.integers(-4, 5, size=(M, K)).astype(np.float32)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    call(hip, "llj_gemm_linear", ZINT4, T(a, torch.bfloat16).data_ptr(), K, Wd.data_ptr(), szd.data_ptr(),
+         out.data_ptr(), N, M, N, K, st())
+    torch.cuda.synchronize()
+    codes = np.empty((N, K), dtype=np.int64)
+    codes[:, 0::2] = qw & 15
+    codes[:, 1::2] = qw >> 4
+    acc = a.astype(np.int64) @ (codes - z.astype(np.int64)).T  # exact integers
+    want = bf16(sc.reshape(1, N).astype(np.float32) * acc.astype(np.float32))
+    np.testing.assert_array_equal(out.float().cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("glds_tile", ["256x256", "256x128"], indirect=True)
-@pytest.mark.parametrize("wfmt", [0, 1])
+@pytest.mark.parametrize("wfmt", [0, 1, ZINT4])
 def test_gemm_glds_qkv_swiglu(hip, glds_tile, wfmt):
     """The LDS-DMA GEMM's QKV + RoPE + KV-write and silu * mul epilogues in both tile shapes
     (M = 2 x 150 prompt rows, 8 heads of 128; SwiGLU hidden 2816 = 11 x 256)."""

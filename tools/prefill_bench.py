@@ -32,7 +32,11 @@ def main():
     ap.add_argument("--modes", nargs="+", default=["gptq.int4", "none"])
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--model", default="7B")
+    ap.add_argument("--ab-w4z", type=int, default=0,
+                    help="rounds of an interleaved A/B of the convert-once int4 GEMM (LLJ_OPT_GEMM_W4Z 1 vs 0)")
     a = ap.parse_args()
+    if a.ab_w4z:
+        return ab_w4z(a)
     for mode in a.modes:
         model = bench.build_model(a.model, None if mode == "none" else mode)
         cfg = model.config
@@ -56,6 +60,42 @@ def main():
                               "linear_mfma_frac_of_2.5PF": round(flops / s / 2.5e15, 4)}), flush=True)
         del model
         torch.cuda.empty_cache()
+
+
+
+def ab_w4z(a):
+    """Interleaved A/B in one process: the int4 window with the convert-once GEMM (option 1) and with
+    the default int4 kernel (0), a.ab_w4z rounds of a.iters windows each; one JSON line per arm."""
+    sys.path.insert(0, str(REPO / "lit-llama-ja_amd"))
+    from lit_llama import _hip
+    L = _hip.lib()
+    model = bench.build_model(a.model, "gptq.int4")
+    cfg = model.config
+    for T in a.T:
+        idx = torch.randint(3, cfg.vocab_size, (1, T), generator=torch.Generator().manual_seed(T)).cuda()
+        res = {1: [], 0: []}
+        with torch.no_grad():
+            for arm in (1, 0):
+                L.llj_set_option(_hip.OPT_GEMM_W4Z, arm)
+                model(idx)  # warm-up per arm
+            for _ in range(a.ab_w4z):
+                for arm in (1, 0):
+                    L.llj_set_option(_hip.OPT_GEMM_W4Z, arm)
+                    torch.cuda.synchronize()
+                    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    ev0.record()
+                    for _ in range(a.iters):
+                        model(idx)
+                    ev1.record()
+                    torch.cuda.synchronize()
+                    res[arm].append(ev0.elapsed_time(ev1) / a.iters)
+        L.llj_set_option(_hip.OPT_GEMM_W4Z, -1)
+        for arm in (1, 0):
+            v = sorted(res[arm])
+            print(json.dumps({"mode": "gptq.int4", "model": a.model, "T": T,
+                              "arm": "convert-once (q - z) tile" if arm else "default int4 kernel",
+                              "ms_per_window_median": round(v[len(v) // 2], 3), "ms_min": round(v[0], 3),
+                              "rounds": a.ab_w4z}), flush=True)
 
 
 if __name__ == "__main__":
