@@ -83,20 +83,39 @@ struct GemmParams {
 // element is computed and stored (gemm_store_elem) -- one load latency per block instead of a
 // load -> store dependence per element (7B 2048-token window: the QKV and silu * mul GEMMs ran
 // 20-26 % slower than the plain store GEMM of the same shape with per-element loads).
-// QKV rows: sequence b and position ps of (clamped) row m, computed once per row.
-__device__ __forceinline__ int2 qkv_row(const GemmParams& p, int m) {
+// QKV rows: sequence b, position ps and KV-cache ring slot of (clamped) row m, computed once per row
+// and tile (the divisions by T and S stay out of the per-element path)
+struct QkvRow {
+  int ps;    // position (RoPE row)
+  int kvrow; // element offset of (sequence b, head 0, ring slot) in the K / V caches
+};
+__device__ __forceinline__ QkvRow qkv_row(const GemmParams& p, int m) {
   const int mm = m < p.M ? m : p.M - 1;
-  return make_int2(mm / p.T, p.pos[mm % p.T]);
+  const int ps = p.pos[mm % p.T];
+  const int slot = ps < p.S ? ps : ps % p.S;
+  return QkvRow{ps, ((mm / p.T) * p.n_head * p.S + slot) * p.head_size};
+}
+// QKV columns: region (0 q, 1 k, 2 v; uniform per 16-column block), column within the region, head
+// offset in the caches and dimension, computed once per 16-column block and lane
+struct QkvCol {
+  int region, nc, hoff, dd;
+};
+__device__ __forceinline__ QkvCol qkv_col(const GemmParams& p, int nblk, int n, int Cd) {
+  QkvCol c;
+  c.region = nblk / Cd;
+  c.nc = n - c.region * Cd;
+  const int h = c.nc / p.head_size;
+  c.dd = c.nc - h * p.head_size;
+  c.hoff = h * p.S * p.head_size;
+  return c;
 }
 template <int EP>
-__device__ __forceinline__ float2 gemm_operand(const GemmParams& p, int m, int n, int ps, int Cd) {
+__device__ __forceinline__ float2 gemm_operand(const GemmParams& p, int m, int n, const QkvRow& qr, const QkvCol& qc) {
   if constexpr (EP == GEP_RESID || EP == GEP_SILU_MUL) {
     const int mm = m < p.M ? m : p.M - 1;  // rows past M: a clamped copy, never stored
     return make_float2(bf2f(p.C[(size_t)mm * p.ldc + n]), 0.f);
   } else if constexpr (EP == GEP_QKV) {
-    const int region = n / Cd;  // 0 q, 1 k, 2 v (uniform per 16-column block)
-    const int dd = (n - region * Cd) % p.head_size;
-    if (region < 2) return *reinterpret_cast<const float2*>(p.rope + ((size_t)ps * (p.head_size >> 1) + (dd >> 1)) * 2);
+    if (qc.region < 2) return *reinterpret_cast<const float2*>(p.rope + ((size_t)qr.ps * (p.head_size >> 1) + (qc.dd >> 1)) * 2);
     return make_float2(1.f, 0.f);
   } else {
     return make_float2(0.f, 0.f);
@@ -104,35 +123,31 @@ __device__ __forceinline__ float2 gemm_operand(const GemmParams& p, int m, int n
 }
 
 // One output element of a tile epilogue: y (the dequantized accumulator, fp32) at row m (live: m < M;
-// rows past M are computed on a clamped copy and never stored), column n of the 16-column block nblk;
-// row = lane & 15 (the column within the block); op = gemm_operand's value, (b, ps) = qkv_row's. Every
-// lane of the wave calls it (lane_xor1 pairs neighbouring columns into one 4-byte store).
+// rows past M are computed on a clamped copy and never stored), column n; row = lane & 15 (the column
+// within the block); op = gemm_operand's value, qr / qc = qkv_row's / qkv_col's. Every lane of the
+// wave calls it (lane_xor1 pairs neighbouring columns into one 4-byte store).
 template <int EP>
-__device__ __forceinline__ void gemm_store_elem(const GemmParams& p, float y, int m, int n, int nblk, bool live, int row,
-                                                int Cd, float2 op, int2 bps) {
+__device__ __forceinline__ void gemm_store_elem(const GemmParams& p, float y, int m, int n, bool live, int row,
+                                                int Cd, float2 op, const QkvRow& qr, const QkvCol& qc) {
   const int M = p.M;
   if constexpr (EP == GEP_QKV) {
     const float v = round_bf(y);  // c_attn output in bf16 (model.py:204), RoPE in fp32
     const float partner = lane_xor1(v);
-    const int region = nblk / Cd;  // 0 q, 1 k, 2 v: uniform per 16-column block
-    const int nc = n - region * Cd;
-    const int h = nc / p.head_size, dd = nc % p.head_size;
+    const int dd = qc.dd;
     const int mm = live ? m : M - 1;
-    const int b = bps.x, ps = bps.y;
     float out = v;
-    if (region < 2) out = (dd & 1) ? (v * op.x + partner * op.y) : (v * op.x - partner * op.y);
+    if (qc.region < 2) out = (dd & 1) ? (v * op.x + partner * op.y) : (v * op.x - partner * op.y);
     const uint32_t ob = (uint32_t)f2bf(out);
     const uint32_t pr = lane_xor1(ob);
     if (live && !(dd & 1)) {
       bf16_t* dst;
       size_t ei;
-      if (region == 0) {
+      if (qc.region == 0) {
         dst = p.q_out;
-        ei = (size_t)mm * Cd + nc;
+        ei = (size_t)mm * Cd + qc.nc;
       } else {
-        const int slot = ps < p.S ? ps : ps % p.S;
-        dst = region == 1 ? p.kcache : p.vcache;
-        ei = (((size_t)b * p.n_head + h) * p.S + slot) * p.head_size + dd;
+        dst = qc.region == 1 ? p.kcache : p.vcache;
+        ei = (size_t)qr.kvrow + qc.hoff + dd;
       }
       *reinterpret_cast<uint32_t*>(dst + ei) = ob | (pr << 16);
     }
@@ -571,6 +586,13 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
 
   // ---- epilogue: lane holds rows m0 + wr*64 + 16i + 4g + r, column n0 + wc*64 + 16j + row
   const int Cd = p.n_head * p.head_size;
+  QkvRow qrow[EP == GEP_QKV ? MI : 1][4] = {};  // QKV: per row, once per tile
+  if constexpr (EP == GEP_QKV) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) qrow[i][r] = qkv_row(p, m0 + wr * 16 * MI + 16 * i + 4 * g + r);
+  }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int n = n0 + wc * 16 * NJ + 16 * j + row;
@@ -578,18 +600,17 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
     if constexpr (NIB) szn = p.sz[n];
     if constexpr (I8) szn.x = reinterpret_cast<const float*>(p.sz)[n];  // SCB
     const int nblk = n0 + wc * 16 * NJ + 16 * j;  // first column of this 16-column block
+    const QkvCol qc = EP == GEP_QKV ? qkv_col(p, nblk, n, Cd) : QkvCol{};
     constexpr int GI = I8 ? (EP == GEP_QKV ? 1 : 2) : 4;  // row blocks whose operands are in flight together (LLM.int8: 3 accumulator sets live)
 #pragma unroll
     for (int i0 = 0; i0 < MI; i0 += GI) {
-      int2 bps[GI][4];  // QKV: (sequence, position) per row
       float2 opv[GI][4];
 #pragma unroll
       for (int i = 0; i < GI; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wr * 16 * MI + 16 * (i0 + i) + 4 * g + r;
-          bps[i][r] = EP == GEP_QKV ? qkv_row(p, m) : make_int2(0, 0);
-          opv[i][r] = gemm_operand<EP>(p, m, n, bps[i][r].y, Cd);
+          opv[i][r] = gemm_operand<EP>(p, m, n, qrow[EP == GEP_QKV ? i0 + i : 0][r], qc);
         }
 #pragma unroll
       for (int i = 0; i < GI; ++i) {
@@ -605,7 +626,7 @@ __global__ __launch_bounds__(2 * BM) void gemm_kernel(GemmParams p) {
             y = (float)iacc[i0 + i][j][r] * (sa * szn.x * (1.f / (127.f * 127.f)));
             y = (float)(_Float16)((float)(_Float16)y + sacc[i0 + i][j][r]);
           }
-          gemm_store_elem<EP>(p, y, m, n, nblk, live, row, Cd, opv[i][r], bps[i][r]);
+          gemm_store_elem<EP>(p, y, m, n, live, row, Cd, opv[i][r], qrow[EP == GEP_QKV ? i0 + i : 0][r], qc);
         }
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the next group's operand loads out of this one's live range
@@ -655,6 +676,24 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
 #endif
 #ifndef LLJ_GLDS_PRE
 #define LLJ_GLDS_PRE 1  // 256 x 128 tiles: read both MFMA steps' fragments of a chunk before its MFMAs (bf16 window 35.9 -> 35.4 ms)
+#endif
+#ifndef LLJ_W4Z_PRIO
+#define LLJ_W4Z_PRIO 0  // convert-once int4: s_setprio around the MFMA clusters (1; 0: none, so the conversion interleaves with them)
+#endif
+#ifndef LLJ_W4Z_WAVES
+#define LLJ_W4Z_WAVES 8  // convert-once int4: waves converting a chunk's codes (8 or 4)
+#endif
+#ifndef LLJ_W4Z_SPLIT
+#define LLJ_W4Z_SPLIT 1  // convert-once int4, 8 converting waves: codes read before the fragment reads (A/B)
+#endif
+#ifndef LLJ_W4Z_IGLP
+#define LLJ_W4Z_IGLP 1  // convert-once int4: sched_group_barrier interleave of the conversion with the MFMAs
+#endif
+#ifndef LLJ_W4Z_VPM
+#define LLJ_W4Z_VPM 3  // VALU instructions per MFMA in that interleave
+#endif
+#ifndef LLJ_W4Z_AFTER
+#define LLJ_W4Z_AFTER 0  // convert-once int4: the converting waves convert after their MFMAs (A/B)
 #endif
 #ifndef LLJ_GLDS_COST128
 #define LLJ_GLDS_COST128 55  // time of a 256 x 128 tile in % of a 256 x 256 one (tile-shape choice)
@@ -798,31 +837,76 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
         }
       }
     }
-    __builtin_amdgcn_s_setprio(1);
+    if (!CVT || LLJ_W4Z_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
+    if (!CVT || LLJ_W4Z_PRIO) __builtin_amdgcn_s_setprio(0);
   };
-  // convert-once int4: wave w converts tile w's codes of a chunk (lane: word pair gp of W4P lane L =
-  // 16 s + column) into 16-B segments 4 s + 2 gp, 4 s + 2 gp + 1 of B row 16 w + column, in the bf16
-  // image's swizzle: bf16(128 + q) - (128 + z) in fp32 is q - z exactly (integral zeros), so the tile
-  // holds exact integers and the scale is applied in the epilogue
+  // convert-once int4: the chunk's codes are converted into 16-B segments 4 s + g of B row
+  // 16 tile + column (W4P lane L = 16 s + column of the tile), in the bf16 image's swizzle:
+  // bf16(128 + q) - (128 + z) in fp32 is q - z exactly (integral zeros), so the tile holds exact
+  // integers and the scale is applied in the epilogue. LLJ_W4Z_WAVES 8: every wave converts its
+  // own tile w, word pair (lane & 1) of W4P lane lane >> 1, branch-free after its MFMAs (the
+  // scheduler may interleave the VALU with them); 4: waves 0-3 convert tiles 2 w, 2 w + 1 (all four
+  // words of lane L = lane & 31 of tile 2 w + (lane >> 5)), before (LLJ_W4Z_AFTER 0) or after their MFMAs
+  constexpr int CW = LLJ_W4Z_WAVES;
   const unsigned char* bf_lds = smem + NST * G::STAGE;
+  const int ctile = CW == 8 ? w : 2 * w + (lane >> 5), cl = CW == 8 ? lane >> 1 : lane & 31, ccol = cl & 15,
+            cs = cl >> 4, cg = CW == 8 ? 2 * (lane & 1) : 0;
   float zoff = 0.f;  // 128 + zero of this lane's column
-  if constexpr (CVT) zoff = p.sz[n0 + 16 * w + ((lane >> 1) & 15)].y;
+  if constexpr (CVT) {
+    if (CW == 8 || w < 4) zoff = p.sz[n0 + 16 * ctile + ccol].y;
+  }
+  // CW 8, split: the codes read issued before the chunk's fragment reads (asm, no wait; LDS reads
+  // complete in order, so the compiler's own lgkmcnt waits for the later fragment reads cover it, and
+  // the explicit wait below ties the value to it), the conversion after them, in the MFMAs' block
+  auto cread = [&](int buf) {
+    const uint32_t ra = (uint32_t)(uintptr_t)(lds_void_t*)(smem + (size_t)buf * G::STAGE + G::SA + 512 * ctile + 16 * cl +
+                                                           4 * cg);
+    uint2 t;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(t) : "v"(ra) : "memory");
+    return t;
+  };
+  auto cfinish = [&](uint2 t, int slot) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t));
+    const uint32_t da = (uint32_t)(uintptr_t)(lds_void_t*)(bf_lds + (size_t)slot * BN * 128 + (16 * ctile + ccol) * 128);
+#pragma unroll
+    for (int g4 = 0; g4 < 2; ++g4) {
+      const uint32_t wv = g4 ? t.y : t.x;
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t d = and_or(wv >> (4 * e), msk, mag);
+        const float lo = __uint_as_float(d << 16) - zoff, hi = __uint_as_float(d & 0xFFFF0000u) - zoff;
+        o[e] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xFFFF0000u);
+      }
+      const u32x4 ov = {o[0], o[1], o[2], o[3]};
+      asm volatile("ds_write_b128 %0, %1" ::"v"(da + (((4 * cs + cg + g4) ^ ((ccol >> 1) & 7)) * 16)), "v"(ov) : "memory");
+    }
+  };
   auto convert = [&](int buf, int slot) {
-    const int L = lane >> 1, gp = lane & 1, col = L & 15, s = L >> 4, cr = 16 * w + col;
     // the read in asm, with its own wait: read as a plain LDS load, hipcc waits vmcnt(0) for every
     // LDS-DMA in flight first (the next chunks' too), de-pipelining the loop
-    const uint32_t ra = (uint32_t)(uintptr_t)(lds_void_t*)(smem + (size_t)buf * G::STAGE + G::SA + 512 * w + 16 * L + 8 * gp);
-    uint2 wv2;
-    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(wv2) : "v"(ra) : "memory");
-    const uint32_t da = (uint32_t)(uintptr_t)(lds_void_t*)(bf_lds + (size_t)slot * BN * 128 + cr * 128);
+    const uint32_t ra = (uint32_t)(uintptr_t)(lds_void_t*)(smem + (size_t)buf * G::STAGE + G::SA + 512 * ctile + 16 * cl +
+                                                           4 * cg);
+    constexpr int NWD = CW == 8 ? 2 : 4;  // words per lane
+    uint32_t wv4[NWD];
+    if constexpr (CW == 8) {
+      uint2 t;
+      asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(ra) : "memory");
+      wv4[0] = t.x;
+      wv4[1] = t.y;
+    } else {
+      u32x4 t;
+      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(ra) : "memory");
+      wv4[0] = t[0]; wv4[1] = t[1]; wv4[2] = t[2]; wv4[3] = t[3];
+    }
+    const uint32_t da = (uint32_t)(uintptr_t)(lds_void_t*)(bf_lds + (size_t)slot * BN * 128 + (16 * ctile + ccol) * 128);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t wv = h ? wv2.y : wv2.x;
+    for (int g4 = 0; g4 < NWD; ++g4) {
+      const uint32_t wv = wv4[g4];
       uint32_t o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -833,7 +917,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
       // (asm too: hipcc also waits vmcnt(0) before a plain LDS store while LDS-DMAs are in flight; the
       // loop's lgkmcnt(0) before its barrier retires it)
       const u32x4 ov = {o[0], o[1], o[2], o[3]};
-      asm volatile("ds_write_b128 %0, %1" ::"v"(da + (((4 * s + 2 * gp + h) ^ ((col >> 1) & 7)) * 16)), "v"(ov) : "memory");
+      asm volatile("ds_write_b128 %0, %1" ::"v"(da + (((4 * cs + cg + g4) ^ ((ccol >> 1) & 7)) * 16)), "v"(ov) : "memory");
     }
   };
   auto compute = [&](int buf, int slot) {
@@ -866,7 +950,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   if constexpr (CVT) {
     wait_vm<2 * G::NG>();  // chunk 0's codes (KC >= 2: both groups were issued)
     __builtin_amdgcn_s_barrier();
-    convert(0, 0);
+    if (CW == 8 || w < 4) convert(0, 0);
   }
   int cb = 0;  // buffer of chunk t
   for (int tc = 0; tc < KC; ++tc) {
@@ -878,10 +962,28 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads (and tile writes) of chunk t - 1 are done
     __builtin_amdgcn_s_barrier();  // chunk t landed for every wave (CVT: and chunk t + 1's codes); t - 1's buffers are free
     if (tc + NST - 1 < KC) stage(cb == 0 ? NST - 1 : cb - 1, tc + NST - 1);
-    if constexpr (CVT) {
-      if (tc + 1 < KC) convert(cb + 1 == NST ? 0 : cb + 1, (tc + 1) & 1);
+    if constexpr (CVT && CW == 4 && !LLJ_W4Z_AFTER) {
+      if (tc + 1 < KC && w < 4) convert(cb + 1 == NST ? 0 : cb + 1, (tc + 1) & 1);
     }
-    compute(cb, tc & 1);
+    if constexpr (CVT && CW == 8 && LLJ_W4Z_SPLIT) {
+      const uint2 ct = cread(cb + 1 == NST ? 0 : cb + 1);
+      compute(cb, tc & 1);
+      cfinish(ct, (tc + 1) & 1);
+      if constexpr (LLJ_W4Z_IGLP) {  // the conversion's VALU between the MFMAs: 1 MFMA, LLJ_W4Z_VPM VALU, ...
+#pragma unroll
+        for (int q = 0; q < 2 * MI * NJ; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, LLJ_W4Z_VPM, 0);
+        }
+      }
+    } else {
+      compute(cb, tc & 1);
+    }
+    if constexpr (CVT && CW == 4 && LLJ_W4Z_AFTER) {
+      if (tc + 1 < KC && w < 4) convert(cb + 1 == NST ? 0 : cb + 1, (tc + 1) & 1);
+    }
+    // branch-free: past the last chunk it converts the clamped codes into the unused slot
+    if constexpr (CVT && CW == 8 && !LLJ_W4Z_SPLIT) convert(cb + 1 == NST ? 0 : cb + 1, (tc + 1) & 1);
     cb = cb + 1 == NST ? 0 : cb + 1;
   }
 
@@ -898,24 +1000,36 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     __syncthreads();
   }
   const int Cd = p.n_head * p.head_size;
+  // QKV rows' (position, cache offset) once per tile where registers allow (MI <= 4; the 256 x 256
+  // tile recomputes them per row group)
+  constexpr bool QH = EP == GEP_QKV && MI <= 4;
+  QkvRow qrow[QH ? MI : 1][4] = {};
+  if constexpr (QH) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) qrow[i][r] = qkv_row(p, m0 + wr * 16 * MI + 16 * i + 4 * g + r);
+  }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int nblk = n0 + wc * 16 * NJ + 16 * j;
     const int n = nblk + row;
     float2 szn = make_float2(1.f, 0.f);
     if constexpr (NIB || CVT) szn = p.sz[n];
+    const QkvCol qc = EP == GEP_QKV ? qkv_col(p, nblk, n, Cd) : QkvCol{};
     constexpr int GI = (MI > 4 && EP == GEP_QKV) ? 1 : 4;  // row blocks whose operands are in flight together
 #pragma unroll
     for (int i0 = 0; i0 < MI; i0 += GI) {
-      int2 bps[GI][4];  // QKV: (sequence, position) per row
       float2 opv[GI][4];
+      QkvRow qg[GI][4] = {};
 #pragma unroll
       for (int i = 0; i < GI; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wr * 16 * MI + 16 * (i0 + i) + 4 * g + r;
-          bps[i][r] = EP == GEP_QKV ? qkv_row(p, m) : make_int2(0, 0);
-          opv[i][r] = gemm_operand<EP>(p, m, n, bps[i][r].y, Cd);
+          if constexpr (QH) qg[i][r] = qrow[i0 + i][r];
+          else if constexpr (EP == GEP_QKV) qg[i][r] = qkv_row(p, m);
+          opv[i][r] = gemm_operand<EP>(p, m, n, qg[i][r], qc);
         }
 #pragma unroll
       for (int i = 0; i < GI; ++i) {
@@ -926,7 +1040,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
           float y = acc[i0 + i][j][r];
           if constexpr (NIB) y = szn.x * (y - szn.y * rs_lds[ml]);
           if constexpr (CVT) y = szn.x * y;
-          gemm_store_elem<EP>(p, y, m, n, nblk, m < M, row, Cd, opv[i][r], bps[i][r]);
+          gemm_store_elem<EP>(p, y, m, n, m < M, row, Cd, opv[i][r], qg[i][r], qc);
         }
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the next group's operand loads out of this one's live range

@@ -15,4 +15,3 @@ cd /tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d /tmp/r06k_prof -o w4z -- python3 $GRAFT_REPO_ROOT/tools/prefill_bench.py --T 2048 --modes gptq.int4 --iters 2 > $GRAFT_REPO_ROOT/$O/prof.log 2>&1 || exit $?
 cd $GRAFT_REPO_ROOT
 python3 tools/kstats_db.py /tmp/r06k_prof > $O/w4z_kernel_stats.csv 2> $O/kstats.log
-ls -R /tmp/r06k_prof | head -20 >> $O/kstats.log
