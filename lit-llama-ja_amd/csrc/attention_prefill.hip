@@ -32,13 +32,19 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 #ifndef LLJ_FLASH_PAIR
 #define LLJ_FLASH_PAIR 1  // causal balance: one workgroup per (long, short) pair of query blocks (7B window -1.0 ms)
 #endif
+#ifndef LLJ_FLASH_FAST
+#define LLJ_FLASH_FAST 1  // softmax: mask only the diagonal tiles, raw-score max, v_exp_f32, rescale only when a max moved
+#endif
+#ifndef LLJ_FLASH_NWQ
+#define LLJ_FLASH_NWQ 4  // waves per workgroup (16 queries each) of the head-size-128 one-block form (8: 128 queries share a K / V tile)
+#endif
 #ifndef LLJ_FLASH_QB
 #define LLJ_FLASH_QB 1  // 16-query blocks per wave (2: every K / V fragment read feeds two MFMAs; with the pairing 1 is faster)
 #endif
 // QB 16-query blocks per wave: 64 QB queries per workgroup; a K fragment (S^T) and a V^T fragment
 // (O^T) read from LDS feed QB MFMAs, and the tile's staging and barriers are shared by 4 x 16 QB queries
-template <int HS, int QB, bool PAIR>
-__global__ __launch_bounds__(256, QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefill_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+template <int HS, int QB, bool PAIR, int NWQ = 4>
+__global__ __launch_bounds__(64 * NWQ, NWQ == 8 ? 1 : QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefill_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                             const int* __restrict__ pos, int T, int S, int nh,
                                                             float sl2) {
@@ -50,7 +56,8 @@ __global__ __launch_bounds__(256, QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefil
   __shared__ __attribute__((aligned(16))) bf16_t Vs[kFK * VP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, g = lane >> 4;
-  constexpr int kFQ = 64 * QB;  // queries per workgroup
+  constexpr int NT = 64 * NWQ;       // threads per workgroup
+  constexpr int kFQ = 16 * NWQ * QB;  // queries per workgroup
   auto run = [&](const int qb) {
     const int h = blockIdx.y, b = blockIdx.z;
     const int C = nh * HS;
@@ -72,13 +79,13 @@ __global__ __launch_bounds__(256, QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefil
     const int ntile = kmax / kFK + 1;
     const bf16_t* kbase = kc + ((size_t)(b * nh + h) * S) * HS;
     const bf16_t* vbase = vc + ((size_t)(b * nh + h) * S) * HS;
-    // staging map: 64 keys x HS/8 vectors = 64 * HS / 8 16-B pieces over 256 threads
-    constexpr int PV = kFK * HS / 8 / 256;
+    // staging map: 64 keys x HS/8 vectors = 64 * HS / 8 16-B pieces over NT threads
+    constexpr int PV = kFK * HS / 8 / NT;
     u32x4 kreg[PV], vreg[PV];
     auto load_tile = [&](int kt) {
   #pragma unroll
       for (int i = 0; i < PV; ++i) {
-        const int piece = tid + 256 * i;
+        const int piece = tid + NT * i;
         const int key = piece / (HS / 8), v8 = piece % (HS / 8);
         int slot = kt * kFK + key;
         slot = slot <= kmax ? slot : kmax;  // clamped: masked below
@@ -100,7 +107,7 @@ __global__ __launch_bounds__(256, QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefil
       __syncthreads();  // the previous tile's readers are done with Ks / Vt
   #pragma unroll
       for (int i = 0; i < PV; ++i) {
-        const int piece = tid + 256 * i;
+        const int piece = tid + NT * i;
         const int key = piece / (HS / 8), v8 = piece % (HS / 8);
         *reinterpret_cast<u32x4*>(Ks + key * KP + 8 * v8) = kreg[i];
         *reinterpret_cast<u32x4*>(Vs + key * VP + 8 * v8) = vreg[i];
@@ -121,19 +128,26 @@ __global__ __launch_bounds__(256, QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefil
         }
       }
       uint32_t pb[QB][4][2];  // bf16 P^T pairs per key block: (r0, r1), (r2, r3)
+      // only the tiles that reach past the wave's first query need the causal mask (wave-uniform)
+      const bool masked = kt * kFK + kFK - 1 > p0 + qb * kFQ + wave * 16 * QB;
   #pragma unroll
       for (int qi = 0; qi < QB; ++qi) {
-        // mask (key slot > query position) and scale into log2 units; per-query max
+        // mask (key slot > query position); per-query max of the raw scores (the scale sl2 > 0
+        // commutes with the max and is applied in the exponent's fma)
+        if (LLJ_FLASH_FAST == 0 || masked) {
+  #pragma unroll
+          for (int j = 0; j < 4; ++j)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int key = kt * kFK + 16 * j + 4 * g + r;
+              s[qi][j][r] = key <= qpos[qi] ? s[qi][j][r] : -INFINITY;
+            }
+        }
         float mx = -INFINITY;
   #pragma unroll
         for (int j = 0; j < 4; ++j)
   #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = kt * kFK + 16 * j + 4 * g + r;
-            const float v = key <= qpos[qi] ? s[qi][j][r] * sl2 : -INFINITY;
-            s[qi][j][r] = v;
-            mx = fmaxf(mx, v);
-          }
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[qi][j][r]);
         {  // max over the 4 lane groups holding this query's keys (lanes col, col+16, col+32, col+48)
           float lo, hi;
           lane_halves<false>(mx, lo, hi);
@@ -141,7 +155,9 @@ __global__ __launch_bounds__(256, QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefil
           lane_halves<true>(mx, lo, hi);
           mx = fmaxf(lo, hi);
         }
-        const float m_new = fmaxf(m_run[qi], mx);
+        // finite: key 0 of tile 0 is visible to every query, so no tile leaves m_new at -inf and
+        // exp2(-inf - m_new) = 0 needs no select
+        const float m_new = fmaxf(m_run[qi], mx * sl2);
         const float corr = m_run[qi] == -INFINITY ? 0.f : exp2f(m_run[qi] - m_new);
         float psum = 0.f;
   #pragma unroll
@@ -149,7 +165,11 @@ __global__ __launch_bounds__(256, QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefil
           float pr[4];
   #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            pr[r] = s[qi][j][r] == -INFINITY ? 0.f : exp2f(s[qi][j][r] - m_new);
+  #pragma clang fp contract(off)
+            // the scaled score rounded before the subtraction (no fma contraction): the same p as the
+            // scale-first form; v_exp_f32 directly (exp2f's denormal-range path only moves p < 2^-126)
+            const float sc = s[qi][j][r] * sl2;
+            pr[r] = LLJ_FLASH_FAST ? __builtin_amdgcn_exp2f(sc - m_new) : (s[qi][j][r] == -INFINITY ? 0.f : exp2f(sc - m_new));
             psum += pr[r];
           }
           pb[qi][j][0] = pack2bf(pr[0], pr[1]);
@@ -164,10 +184,12 @@ __global__ __launch_bounds__(256, QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefil
         }
         l_run[qi] = l_run[qi] * corr + psum;
         m_run[qi] = m_new;
+        if (LLJ_FLASH_FAST == 0 || __any(corr != 1.f)) {  // the running max moved for some query of the wave
   #pragma unroll
-        for (int d = 0; d < DB; ++d)
+          for (int d = 0; d < DB; ++d)
   #pragma unroll
-          for (int r = 0; r < 4; ++r) acc_o[qi][d][r] *= corr;
+            for (int r = 0; r < 4; ++r) acc_o[qi][d][r] *= corr;
+        }
       }
       // O^T += V^T . P^T, two 32-key steps
   #pragma unroll
@@ -220,15 +242,15 @@ __global__ __launch_bounds__(256, QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefil
   }
 }
 
-template <int HS, int QB>
+template <int HS, int QB, int NWQ = 4>
 static void flash_launch(const void* q, const void* kcache, const void* vcache, void* y, const int* pos, int B, int T,
                          int n_head, int S, float sl2, bool pair, hipStream_t st) {
-  const int nqb = (T + 64 * QB - 1) / (64 * QB);
+  const int nqb = (T + 16 * NWQ * QB - 1) / (16 * NWQ * QB);
   if (pair) {
-    hipLaunchKernelGGL((flash_prefill_kernel<HS, QB, true>), dim3((nqb + 1) / 2, n_head, B), dim3(256), 0, st,
+    hipLaunchKernelGGL((flash_prefill_kernel<HS, QB, true, NWQ>), dim3((nqb + 1) / 2, n_head, B), dim3(64 * NWQ), 0, st,
                        (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
   } else {
-    hipLaunchKernelGGL((flash_prefill_kernel<HS, QB, false>), dim3(nqb, n_head, B), dim3(256), 0, st,
+    hipLaunchKernelGGL((flash_prefill_kernel<HS, QB, false, NWQ>), dim3(nqb, n_head, B), dim3(64 * NWQ), 0, st,
                        (const bf16_t*)q, (const bf16_t*)kcache, (const bf16_t*)vcache, (bf16_t*)y, pos, T, S, n_head, sl2);
   }
 }
@@ -249,6 +271,7 @@ int llj_attention_prefill(const void* q, const void* kcache, const void* vcache,
   const bool pair = op >= 0 ? op != 0 : LLJ_FLASH_PAIR != 0;  // a long and a short query block per workgroup
   if (head_size == 128) {
     if (qbw == 2) flash_launch<128, 2>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, pair, st);
+    else if (LLJ_FLASH_NWQ == 8) flash_launch<128, 1, 8>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, pair, st);
     else flash_launch<128, 1>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, pair, st);
   } else if (head_size == 64) {
     if (qbw == 2) flash_launch<64, 2>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, pair, st);

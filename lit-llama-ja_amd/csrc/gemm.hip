@@ -690,7 +690,7 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
 #define LLJ_W4Z_IGLP 1  // convert-once int4: sched_group_barrier interleave of the conversion with the MFMAs
 #endif
 #ifndef LLJ_W4Z_VPM
-#define LLJ_W4Z_VPM 3  // VALU instructions per MFMA in that interleave
+#define LLJ_W4Z_VPM 2  // VALU instructions per MFMA in that interleave (3 with the conversion's packed form: +1 ms per 7B window)
 #endif
 #ifndef LLJ_W4Z_AFTER
 #define LLJ_W4Z_AFTER 0  // convert-once int4: the converting waves convert after their MFMAs (A/B)
@@ -699,6 +699,7 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
 #define LLJ_GLDS_COST128 55  // time of a 256 x 128 tile in % of a 256 x 256 one (tile-shape choice)
 #endif
 typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
 template <int WF, int BN>
 struct GldsGeo {
@@ -866,7 +867,8 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     const uint32_t ra = (uint32_t)(uintptr_t)(lds_void_t*)(smem + (size_t)buf * G::STAGE + G::SA + 512 * ctile + 16 * cl +
                                                            4 * cg);
     uint2 t;
-    asm volatile("ds_read_b64 %0, %1" : "=v"(t) : "v"(ra) : "memory");
+    // (s_nop: the destination may be a register an MFMA of the previous chunk read as an operand)
+    asm volatile("s_nop 4\n\tds_read_b64 %0, %1" : "=v"(t) : "v"(ra) : "memory");
     return t;
   };
   auto cfinish = [&](uint2 t, int slot) {
@@ -878,9 +880,10 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
       uint32_t o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const uint32_t d = and_or(wv >> (4 * e), msk, mag);
-        const float lo = __uint_as_float(d << 16) - zoff, hi = __uint_as_float(d & 0xFFFF0000u) - zoff;
-        o[e] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xFFFF0000u);
+        const uint32_t d = and_or(wv >> (4 * e), msk, mag);  // bf16 pair (128 + q_lo, 128 + q_hi)
+        // as fp32 (exact), minus 128 + z in one packed add, back to a bf16 pair in one convert (exact)
+        const f32x2 v = f32x2{__uint_as_float(d << 16), __uint_as_float(d & 0xFFFF0000u)} - f32x2{zoff, zoff};
+        o[e] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
       }
       const u32x4 ov = {o[0], o[1], o[2], o[3]};
       asm volatile("ds_write_b128 %0, %1" ::"v"(da + (((4 * cs + cg + g4) ^ ((ccol >> 1) & 7)) * 16)), "v"(ov) : "memory");
