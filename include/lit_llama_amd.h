@@ -197,6 +197,12 @@ int llj_gemm_resid(int wfmt, const void* A, int lda, const void* W, const void* 
  * pass (model.py:258; two passes instead of a dual-weight tile). */
 int llj_gemm_silu_mul(int wfmt, const void* A, int lda, const void* W, const void* sz, void* h, int ldh, int M, int N,
                       int K, void* stream);
+/* h[M, H] = bf16(silu(bf16(A . W1^T))) * bf16(A . W2^T) in ONE pass (model.py:258, c_fc1 and c_fc2 of
+ * the SwiGLU MLP): int4 with integral zeros only (wfmt 0 | LLJ_WF_ZINT), M >= 256, H % 64 == 0; each
+ * 256 x 64 tile stages one A tile for both weights. LLJ_EINVAL otherwise (then llj_gemm_linear +
+ * llj_gemm_silu_mul). */
+int llj_gemm_swiglu(int wfmt, const void* A, int lda, const void* W1, const void* sz1, const void* W2, const void* sz2,
+                    void* h, int ldh, int M, int H, int K, void* stream);
 /* c_attn + split + RoPE(q, k) + KV-cache write for B*T pre-normalized rows x (as llj_norm_qkv_rope
  * with norm_w NULL; model.py:204-228). */
 int llj_gemm_qkv_rope(int wfmt, const void* x, const void* W, const void* sz, void* q_out, void* kcache, void* vcache,

@@ -50,7 +50,9 @@ namespace llj {
 
 // GWF_W4Z: int4 W4P with integral zeros (LLJ_WF_ZINT) in the convert-once LDS-DMA GEMM (internal)
 enum : int { GWF_W4 = 0, GWF_BF16 = 1, GWF_I8 = 2, GWF_W8 = 3, GWF_W4G = 4, GWF_W4Z = 5 };
-enum : int { GEP_STORE = 0, GEP_RESID = 1, GEP_QKV = 2, GEP_SILU_MUL = 3 };
+// GEP_SWIGLU: h = bf16(silu(bf16(A . W1^T))) * bf16(A . W2^T) in one pass (convert-once int4: both weights'
+// codes staged per chunk, one A tile feeding both; W2 / sz2)
+enum : int { GEP_STORE = 0, GEP_RESID = 1, GEP_QKV = 2, GEP_SILU_MUL = 3, GEP_SWIGLU = 4 };
 
 struct GemmParams {
   const bf16_t* A;  // (M, K) rows with stride lda
@@ -76,6 +78,9 @@ struct GemmParams {
   const _Float16* ao16;
   const _Float16* w16;
   int kpad;
+  // GEP_SWIGLU: the second weight (c_fc2) and its (scale, 128 + zero) pairs
+  const void* W2;
+  const float2* sz2;
 };
 
 // Tile epilogues run in two phases per 16-column block: every element's operand is loaded first
@@ -730,6 +735,12 @@ template <int WF, int EP, int BN>
 __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   static_assert(WF == GWF_BF16 || WF == GWF_W4 || WF == GWF_W4Z, "LDS-DMA GEMM: bf16 and int4 W4P");
   static_assert(WF != GWF_W4Z || BN == 128, "convert-once int4: 256 x 128 tiles");
+  // the dual SwiGLU form: 64 output columns per tile, B rows 0-63 from W1 and 64-127 from W2 (the same
+  // columns), wave column group wc holding output columns 32 wc .. + 31 of BOTH (fragments j < NJ / 2
+  // from W1, j >= NJ / 2 from W2), so each lane has fc1 and fc2 of the same element
+  constexpr bool DUAL = EP == GEP_SWIGLU;
+  static_assert(!DUAL || WF == GWF_W4Z, "dual SwiGLU GEMM: convert-once int4");
+  constexpr int NOUT = DUAL ? BN / 2 : BN;  // output columns per tile
   using G = GldsGeo<WF, BN>;
   constexpr int MI = G::MI, NJ = G::NJ, WN = G::WN, NST = G::NST;
   constexpr bool NIB = WF == GWF_W4;  // per-fragment dequant (bf16 128 + q) + row sums
@@ -739,14 +750,14 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   const int wr = w / WN, wc = w % WN;
   const int row = lane & 15, g = lane >> 4;
   const int M = p.M, K = p.K, KC = K / 64, KC128 = K / 128;
-  const int mtiles = (M + 255) / 256, ntiles = p.N / BN, total = mtiles * ntiles;
+  const int mtiles = (M + 255) / 256, ntiles = p.N / NOUT, total = mtiles * ntiles;
   int t = blockIdx.x;
   {  // contiguous tile ranges per XCD (bijective for any total)
     const int q = total / 8, r = total % 8, x = t % 8;
     t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + t / 8;
   }
   const int nb = t / mtiles, mb = t % mtiles;  // m fastest: a weight panel's row tiles run together
-  const int m0 = mb * 256, n0 = nb * BN;
+  const int m0 = mb * 256, n0 = nb * NOUT;
   float* rs_lds = reinterpret_cast<float*>(smem + NST * G::STAGE);
 
   // ---- DMA sources: A rows q * 64 + 8 w + lane / 8 (q < 4), physical segment lane % 8 holds the
@@ -761,7 +772,10 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   const char* bsrc;
   if constexpr (NIB || CVT) {  // W4P: wave w stages tiles 2 w, 2 w + 1 (BN 128: waves 4-7 a copy of 0-3's)
     const int tl = (2 * w + (lane >> 5)) % (BN / 16);
-    bsrc = reinterpret_cast<const char*>(p.W) + (size_t)(n0 / 16 + tl) * KC128 * 1024 + 16 * (lane & 31);
+    if (DUAL)  // B tiles 0-3: W1's columns n0 .. + 63, tiles 4-7: W2's
+      bsrc = reinterpret_cast<const char*>(tl < 4 ? p.W : p.W2) + (size_t)(n0 / 16 + (tl & 3)) * KC128 * 1024 + 16 * (lane & 31);
+    else
+      bsrc = reinterpret_cast<const char*>(p.W) + (size_t)(n0 / 16 + tl) * KC128 * 1024 + 16 * (lane & 31);
   } else {
     bsrc = reinterpret_cast<const char*>(reinterpret_cast<const bf16_t*>(p.W) + (size_t)(n0 + drow) * K + 8 * dseg);
   }
@@ -794,6 +808,10 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   // step s reads logical segment 4 s + g at physical (4 s + g) ^ sw
   const int sw = (row >> 1) & 7;
   const int aoff0 = (wr * 16 * MI + row) * 128, boff0 = (wc * 16 * NJ + row) * 128;
+  // B row (tile column) of fragment j: DUAL -> W1 rows 32 wc + 16 j (j < NJ / 2), W2 rows 64 + 32 wc + 16 (j - NJ / 2)
+  auto brow_off = [&](int j) {
+    return DUAL ? ((j >= NJ / 2 ? 64 : 0) + wc * 16 * (NJ / 2) + 16 * (j % (NJ / 2)) + row) * 128 : boff0 + 16 * j * 128;
+  };
   uint32_t msk = 0x000F000Fu, mag = 0x43004300u;
   asm volatile("" : "+s"(msk));
   asm volatile("" : "+v"(mag));
@@ -822,7 +840,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
         bfr[j] = __builtin_bit_cast(bf16x8, make_uint4(and_or(wv, msk, mag), and_or(wv >> 4, msk, mag),
                                                        and_or(wv >> 8, msk, mag), and_or(wv >> 12, msk, mag)));
       } else {
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bb + boff0 + 16 * j * 128 + so);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bb + brow_off(j) + so);
       }
     }
   };
@@ -858,7 +876,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
             cs = cl >> 4, cg = CW == 8 ? 2 * (lane & 1) : 0;
   float zoff = 0.f;  // 128 + zero of this lane's column
   if constexpr (CVT) {
-    if (CW == 8 || w < 4) zoff = p.sz[n0 + 16 * ctile + ccol].y;
+    if (CW == 8 || w < 4) zoff = DUAL ? (ctile < 4 ? p.sz : p.sz2)[n0 + 16 * (ctile & 3) + ccol].y : p.sz[n0 + 16 * ctile + ccol].y;
   }
   // CW 8, split: the codes read issued before the chunk's fragment reads (asm, no wait; LDS reads
   // complete in order, so the compiler's own lgkmcnt waits for the later fragment reads cover it, and
@@ -991,6 +1009,25 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   }
 
   // ---- epilogue: lane holds rows m0 + wr * 16 MI + 16 i + 4 g + r, column n0 + wc * 16 NJ + 16 j + row
+  if constexpr (DUAL) {  // h = bf16(silu(bf16(fc1))) * bf16(fc2), fc1 in fragments j < NJ / 2, fc2 at j + NJ / 2
+#pragma unroll
+    for (int j = 0; j < NJ / 2; ++j) {
+      const int n = n0 + wc * 16 * (NJ / 2) + 16 * j + row;
+      const float s1 = p.sz[n].x, s2 = p.sz2[n].x;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wr * 16 * MI + 16 * i + 4 * g + r;
+          const float a1 = round_bf(s1 * acc[i][j][r]);  // bf16(c_fc1 x)
+          const float sl = round_bf(a1 / (1.f + __expf(-a1)));  // F.silu in bf16
+          const uint32_t ob = (uint32_t)f2bf(sl * round_bf(s2 * acc[i][j + NJ / 2][r]));
+          const uint32_t pr = lane_xor1(ob);
+          if (m < M && !(row & 1)) *reinterpret_cast<uint32_t*>(p.C + (size_t)m * p.ldc + n) = ob | (pr << 16);
+        }
+    }
+    return;
+  }
   if constexpr (NIB) {
 #pragma unroll
     for (int i = 0; i < MI; ++i) {  // two waves hold parts of each row: 0 + a + b is order-free
@@ -1061,7 +1098,7 @@ static int gemm_glds_launch(const GemmParams& p, hipStream_t s) {
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  const int tiles = ((p.M + 255) / 256) * (p.N / BN);
+  const int tiles = ((p.M + 255) / 256) * (p.N / (EP == GEP_SWIGLU ? BN / 2 : BN));
   hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), lds, s, p);
   LLJ_CHECK_LAUNCH();
   return 0;
@@ -1173,6 +1210,19 @@ int llj_gemm_silu_mul(int wfmt, const void* A, int lda, const void* W, const voi
   p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = W; p.sz = (const float2*)sz;
   p.C = (bf16_t*)h; p.ldc = ldh;
   return gemm_run<GEP_SILU_MUL>(wfmt, p, stream);
+}
+
+// h[M, H] = bf16(silu(bf16(A . W1^T))) * bf16(A . W2^T) in one pass: int4 W4P with integral zeros
+// (wfmt 0 | LLJ_WF_ZINT), M >= 256, H % 64 == 0 (the convert-once kernel with both weights' codes per chunk)
+int llj_gemm_swiglu(int wfmt, const void* A, int lda, const void* W1, const void* sz1, const void* W2, const void* sz2,
+                    void* h, int ldh, int M, int H, int K, void* stream) {
+  if (wfmt != (GWF_W4 | LLJ_WF_ZINT) || M < 256 || H % 64 || K % 128 || K < 128 || (lda & 7) || (ldh & 1) || !A ||
+      !W1 || !W2 || !sz1 || !sz2 || !h)
+    return LLJ_EINVAL;
+  GemmParams p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = H; p.K = K; p.W = W1; p.sz = (const float2*)sz1;
+  p.W2 = W2; p.sz2 = (const float2*)sz2; p.C = (bf16_t*)h; p.ldc = ldh;
+  return gemm_glds_launch<GWF_W4Z, GEP_SWIGLU, 128>(p, (hipStream_t)stream);
 }
 
 // LLM.int8() forms (wfmt 2): W = CB in the I8P tiling, sz = SCB (fp32), i8ws = llj_i8_stats of A

@@ -68,6 +68,7 @@ SIGNATURES = {
     "llj_gemm_linear": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_silu_mul": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
+    "llj_gemm_swiglu": [_I, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_qkv_rope": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_stream_read": [_P, ctypes.c_size_t, _P, _I, _P],
     "llj_g_embedding": [_P, _P, _P, _I, _I, _P, _I, _P],

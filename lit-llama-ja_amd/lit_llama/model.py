@@ -148,6 +148,9 @@ def _gemm_fmt(wfmt: int) -> bool:
 # codes converted once per workgroup into an exact bf16 (q - z) tile, the scale in the epilogue
 # (LLJ_WF_ZINT; csrc/gemm.hip, the convert-once LDS-DMA kernel at M >= 256)
 GEMM_ZINT = True
+# ... and c_fc1 / c_fc2 of such weights in one dual pass (llj_gemm_swiglu: one A tile for both, silu * mul
+# in the epilogue, no h round trip) at M >= 256
+GEMM_SWIGLU = True
 
 
 def _gz(wfmt: int, lin: nn.Module) -> int:
@@ -549,10 +552,15 @@ class LLaMA(nn.Module):
             else:
                 _hip.call("llj_rmsnorm_rows", w.x.data_ptr(), blk.rms_2.scale.data_ptr(), blk.rms_2.eps,
                           w.xn.data_ptr(), None, M, C, st)
-                _hip.call("llj_gemm_linear", _gz(f1, blk.mlp.c_fc1), w.xn.data_ptr(), C, w1.data_ptr(), P(s1),
-                          w.h.data_ptr(), H, M, H, C, st)
-                _hip.call("llj_gemm_silu_mul", _gz(f2, blk.mlp.c_fc2), w.xn.data_ptr(), C, w2.data_ptr(), P(s2),
-                          w.h.data_ptr(), H, M, H, C, st)
+                g1, g2 = _gz(f1, blk.mlp.c_fc1), _gz(f2, blk.mlp.c_fc2)
+                if GEMM_SWIGLU and g1 == g2 == _hip.WF_ZINT and M >= 256 and H % 64 == 0:  # both in one pass
+                    _hip.call("llj_gemm_swiglu", g1, w.xn.data_ptr(), C, w1.data_ptr(), P(s1), w2.data_ptr(), P(s2),
+                              w.h.data_ptr(), H, M, H, C, st)
+                else:
+                    _hip.call("llj_gemm_linear", g1, w.xn.data_ptr(), C, w1.data_ptr(), P(s1), w.h.data_ptr(), H, M,
+                              H, C, st)
+                    _hip.call("llj_gemm_silu_mul", g2, w.xn.data_ptr(), C, w2.data_ptr(), P(s2), w.h.data_ptr(), H,
+                              M, H, C, st)
             self._gemm_resid(_gz(fd, blk.mlp.c_proj), w.h, wd, sd, w.x, M, C, H, w, st)
 
     def _gemm_resid(self, f, A, W, sz, x, M, N, K, w, st):

@@ -1245,6 +1245,40 @@ def test_gemm_w4z_exact_on_integer_rows(hip):
     np.testing.assert_array_equal(out.float().cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("M,H,K", [(256, 2816, 1024), (300, 11008, 4096), (2048, 11008, 4096), (520, 4096, 11008)])
+def test_gemm_swiglu_dual_pass(hip, M, H, K):
+    """llj_gemm_swiglu (c_fc1 and c_fc2 of integral-zero int4 weights in one pass, one A tile for both,
+    silu * mul in the epilogue) against the oracle, and bitwise equal to the two-pass form
+    (llj_gemm_linear + llj_gemm_silu_mul with LLJ_WF_ZINT: the same per-element accumulation)."""
+    rng = np.random.default_rng(M + H + K)
+    W1, W1d, s1 = quant_operands(hip, rng, ZINT4, H, K)
+    W2, W2d, s2 = quant_operands(hip, rng, ZINT4, H, K)
+    x = bf16(rng.standard_normal((M, K)).astype(np.float32))
+    xd = T(x, torch.bfloat16)
+    h1 = torch.full((M + 1, H), 7.0, dtype=torch.bfloat16, device=dev)  # row M: canary
+    call(hip, "llj_gemm_swiglu", ZINT4, xd.data_ptr(), K, W1d.data_ptr(), s1.data_ptr(), W2d.data_ptr(), s2.data_ptr(),
+         h1.data_ptr(), H, M, H, K, st())
+    h2 = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+    call(hip, "llj_gemm_linear", ZINT4, xd.data_ptr(), K, W1d.data_ptr(), s1.data_ptr(), h2.data_ptr(), H, M, H, K, st())
+    call(hip, "llj_gemm_silu_mul", ZINT4, xd.data_ptr(), K, W2d.data_ptr(), s2.data_ptr(), h2.data_ptr(), H, M, H, K,
+         st())
+    torch.cuda.synchronize()
+    got = h1.float().cpu().numpy()
+    assert (got[M] == 7.0).all(), "wrote past row M"
+    np.testing.assert_array_equal(got[:M], h2.float().cpu().numpy())
+    hexp = bf16(bf16(O.silu(bf16(x @ W1.T))) * bf16(x @ W2.T))
+    assert_bf16_close(got[:M], hexp, f"gemm swiglu dual M={M}", rel=3e-2)
+
+
+def test_gemm_swiglu_dual_refuses(hip):
+    """The one-pass form takes only integral-zero int4 at M >= 256 and H % 64 == 0 (EINVAL otherwise)."""
+    L = hip
+    z = torch.zeros(16, dtype=torch.uint8, device=dev)
+    for wf, M, H in ((0, 256, 128), (ZINT4, 255, 128), (ZINT4, 256, 96), (1 | ZINT4, 256, 128)):
+        assert L.llj_gemm_swiglu(wf, z.data_ptr(), 128, z.data_ptr(), z.data_ptr(), z.data_ptr(), z.data_ptr(),
+                                 z.data_ptr(), H, M, H, 128, st()) == 1000
+
+
 @pytest.mark.parametrize("glds_tile", ["256x256", "256x128"], indirect=True)
 @pytest.mark.parametrize("wfmt", [0, 1, ZINT4])
 def test_gemm_glds_qkv_swiglu(hip, glds_tile, wfmt):

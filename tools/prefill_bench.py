@@ -34,9 +34,13 @@ def main():
     ap.add_argument("--model", default="7B")
     ap.add_argument("--ab-w4z", type=int, default=0,
                     help="rounds of an interleaved A/B of the convert-once int4 GEMM (LLJ_OPT_GEMM_W4Z 1 vs 0)")
+    ap.add_argument("--ab-flag", default=None,
+                    help="NAME:ROUNDS -- interleaved A/B of a lit_llama.model module flag (True vs False), int4")
     a = ap.parse_args()
     if a.ab_w4z:
         return ab_w4z(a)
+    if a.ab_flag:
+        return ab_flag(a)
     for mode in a.modes:
         model = bench.build_model(a.model, None if mode == "none" else mode)
         cfg = model.config
@@ -96,6 +100,37 @@ def ab_w4z(a):
                               "arm": "convert-once (q - z) tile" if arm else "default int4 kernel",
                               "ms_per_window_median": round(v[len(v) // 2], 3), "ms_min": round(v[0], 3),
                               "rounds": a.ab_w4z}), flush=True)
+
+
+def ab_flag(a):
+    """Interleaved A/B in one process of a module flag of lit_llama.model (e.g. GEMM_SWIGLU), int4 window."""
+    from lit_llama import model as MD
+    name, rounds = a.ab_flag.split(":")
+    model = bench.build_model(a.model, "gptq.int4")
+    cfg = model.config
+    for T in a.T:
+        idx = torch.randint(3, cfg.vocab_size, (1, T), generator=torch.Generator().manual_seed(T)).cuda()
+        res = {True: [], False: []}
+        with torch.no_grad():
+            for arm in (True, False):
+                setattr(MD, name, arm)
+                model(idx)
+            for _ in range(int(rounds)):
+                for arm in (True, False):
+                    setattr(MD, name, arm)
+                    torch.cuda.synchronize()
+                    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    ev0.record()
+                    for _ in range(a.iters):
+                        model(idx)
+                    ev1.record()
+                    torch.cuda.synchronize()
+                    res[arm].append(ev0.elapsed_time(ev1) / a.iters)
+        for arm in (True, False):
+            v = sorted(res[arm])
+            print(json.dumps({"mode": "gptq.int4", "model": a.model, "T": T, "flag": name, "arm": arm,
+                              "ms_per_window_median": round(v[len(v) // 2], 3), "ms_min": round(v[0], 3),
+                              "rounds": int(rounds)}), flush=True)
 
 
 if __name__ == "__main__":
