@@ -38,13 +38,16 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 #ifndef LLJ_FLASH_NWQ
 #define LLJ_FLASH_NWQ 4  // waves per workgroup (16 queries each) of the head-size-128 one-block form (8: 128 queries share a K / V tile)
 #endif
+#ifndef LLJ_FLASH_PF
+#define LLJ_FLASH_PF 1  // K / V tiles in flight in registers (2: two register sets; 7B window 32.03-32.06 ms at 1 vs 32.13-32.31 at 2)
+#endif
 #ifndef LLJ_FLASH_QB
 #define LLJ_FLASH_QB 1  // 16-query blocks per wave (2: every K / V fragment read feeds two MFMAs; with the pairing 1 is faster)
 #endif
 // QB 16-query blocks per wave: 64 QB queries per workgroup; a K fragment (S^T) and a V^T fragment
 // (O^T) read from LDS feed QB MFMAs, and the tile's staging and barriers are shared by 4 x 16 QB queries
 template <int HS, int QB, bool PAIR, int NWQ = 4>
-__global__ __launch_bounds__(64 * NWQ, NWQ == 8 ? 1 : QB == 1 ? LLJ_FLASH_OCC : 2) void flash_prefill_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+__global__ __launch_bounds__(64 * NWQ, NWQ == 8 ? 1 : QB == 1 && LLJ_FLASH_PF == 1 ? LLJ_FLASH_OCC : 2) void flash_prefill_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ y,
                                                             const int* __restrict__ pos, int T, int S, int nh,
                                                             float sl2) {
@@ -81,16 +84,18 @@ __global__ __launch_bounds__(64 * NWQ, NWQ == 8 ? 1 : QB == 1 ? LLJ_FLASH_OCC : 
     const bf16_t* vbase = vc + ((size_t)(b * nh + h) * S) * HS;
     // staging map: 64 keys x HS/8 vectors = 64 * HS / 8 16-B pieces over NT threads
     constexpr int PV = kFK * HS / 8 / NT;
-    u32x4 kreg[PV], vreg[PV];
-    auto load_tile = [&](int kt) {
+    // two register sets (LLJ_FLASH_PF 2): tile kt + 2's loads are issued while tile kt is multiplied,
+    // so each tile's K / V loads have two tiles of MFMA work to land in (one with LLJ_FLASH_PF 1)
+    u32x4 kA[PV], vA[PV], kB[PV], vB[PV];
+    auto load_into = [&](int kt, u32x4 (&kr)[PV], u32x4 (&vr)[PV]) {
   #pragma unroll
       for (int i = 0; i < PV; ++i) {
         const int piece = tid + NT * i;
         const int key = piece / (HS / 8), v8 = piece % (HS / 8);
         int slot = kt * kFK + key;
         slot = slot <= kmax ? slot : kmax;  // clamped: masked below
-        kreg[i] = *reinterpret_cast<const u32x4*>(kbase + (size_t)slot * HS + 8 * v8);
-        vreg[i] = *reinterpret_cast<const u32x4*>(vbase + (size_t)slot * HS + 8 * v8);
+        kr[i] = *reinterpret_cast<const u32x4*>(kbase + (size_t)slot * HS + 8 * v8);
+        vr[i] = *reinterpret_cast<const u32x4*>(vbase + (size_t)slot * HS + 8 * v8);
       }
     };
     float m_run[QB], l_run[QB];
@@ -102,18 +107,21 @@ __global__ __launch_bounds__(64 * NWQ, NWQ == 8 ? 1 : QB == 1 ? LLJ_FLASH_OCC : 
   #pragma unroll
       for (int d = 0; d < DB; ++d) acc_o[qi][d] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    load_tile(0);
-    for (int kt = 0; kt < ntile; ++kt) {
+    auto step = [&](int kt, u32x4 (&kr)[PV], u32x4 (&vr)[PV], u32x4 (&kn)[PV], u32x4 (&vn)[PV]) {
       __syncthreads();  // the previous tile's readers are done with Ks / Vt
   #pragma unroll
       for (int i = 0; i < PV; ++i) {
         const int piece = tid + NT * i;
         const int key = piece / (HS / 8), v8 = piece % (HS / 8);
-        *reinterpret_cast<u32x4*>(Ks + key * KP + 8 * v8) = kreg[i];
-        *reinterpret_cast<u32x4*>(Vs + key * VP + 8 * v8) = vreg[i];
+        *reinterpret_cast<u32x4*>(Ks + key * KP + 8 * v8) = kr[i];
+        *reinterpret_cast<u32x4*>(Vs + key * VP + 8 * v8) = vr[i];
       }
       __syncthreads();
-      if (kt + 1 < ntile) load_tile(kt + 1);  // in flight during this tile's MFMAs
+      if (LLJ_FLASH_PF == 2) {
+        if (kt + 2 < ntile) load_into(kt + 2, kr, vr);  // the set just staged is free
+      } else {
+        if (kt + 1 < ntile) load_into(kt + 1, kn, vn);  // in flight during this tile's MFMAs
+      }
       // S^T = K . Q^T for the tile's four 16-key blocks
       f32x4 s[QB][4];
   #pragma unroll
@@ -212,6 +220,19 @@ __global__ __launch_bounds__(64 * NWQ, NWQ == 8 ? 1 : QB == 1 ? LLJ_FLASH_OCC : 
   #pragma unroll
           for (int qi = 0; qi < QB; ++qi) acc_o[qi][d] = mfma_bf16(__builtin_bit_cast(bf16x8, aw), bfrag[qi], acc_o[qi][d]);
         }
+      }
+    };
+    load_into(0, kA, vA);
+    if (LLJ_FLASH_PF == 2) {
+      if (ntile > 1) load_into(1, kB, vB);
+      for (int kt = 0; kt < ntile; kt += 2) {
+        step(kt, kA, vA, kB, vB);
+        if (kt + 1 < ntile) step(kt + 1, kB, vB, kA, vA);
+      }
+    } else {
+      for (int kt = 0; kt < ntile; kt += 2) {
+        step(kt, kA, vA, kB, vB);
+        if (kt + 1 < ntile) step(kt + 1, kB, vB, kA, vA);
       }
     }
     // y[b*T + t][h*HS + d] = O / l; lane holds d = 16 db + 4 g + r of its query
