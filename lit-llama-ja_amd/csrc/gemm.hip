@@ -682,6 +682,9 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
 #ifndef LLJ_GLDS_PRE
 #define LLJ_GLDS_PRE 1  // 256 x 128 tiles: read both MFMA steps' fragments of a chunk before its MFMAs (bf16 window 35.9 -> 35.4 ms)
 #endif
+#ifndef LLJ_GLDS_FDB
+#define LLJ_GLDS_FDB 1  // LDS-DMA GEMM at 256 x 128: chunk t + 1's fragments read during chunk t's MFMAs (A/B)
+#endif
 #ifndef LLJ_W4Z_PRIO
 #define LLJ_W4Z_PRIO 0  // convert-once int4: s_setprio around the MFMA clusters (1; 0: none, so the conversion interleaves with them)
 #endif
@@ -745,6 +748,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   constexpr int MI = G::MI, NJ = G::NJ, WN = G::WN, NST = G::NST;
   constexpr bool NIB = WF == GWF_W4;  // per-fragment dequant (bf16 128 + q) + row sums
   constexpr bool CVT = G::CVT;        // W4P codes converted once per chunk into a bf16 (q - z) tile
+  constexpr bool FDB = LLJ_GLDS_FDB && BN == 128 && G::NST == 3 && (WF == GWF_BF16 || (CVT && LLJ_W4Z_WAVES == 8));
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w / WN, wc = w % WN;
@@ -960,6 +964,64 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     }
   };
 
+  // ---- K loop, fragment double buffering (LLJ_GLDS_FDB, bf16 and convert-once int4 at 256 x 128): the
+  // fragments of chunk t + 1 are read from LDS while chunk t's MFMAs run (two register sets), so the DMA
+  // runs three chunks ahead (every stage issued, past the end with a clamped chunk index: equal DMA
+  // counts per wave in every iteration) and each iteration waits for chunk t + 1 instead of t
+  if constexpr (FDB) {
+    struct Fr {
+      bf16x8 a0[MI], b0[NJ], a1[MI], b1[NJ];
+    };
+    auto rd = [&](int buf, int slot, Fr& f) {
+      const unsigned char* Ab = smem + (size_t)buf * G::STAGE;
+      const unsigned char* Bb = CVT ? bf_lds + (size_t)slot * BN * 128 : Ab + G::SA;
+      frags(Ab, Bb, 0, f.a0, f.b0);
+      frags(Ab, Bb, 1, f.a1, f.b1);
+    };
+    auto step = [&](int t, Fr& cur, Fr& nxt) {
+      wait_vm<G::NG>();  // chunk t + 1 (and the codes of t + 2) landed; t + 2 in flight
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of chunk t's fragments (and codes) are done
+      __builtin_amdgcn_s_barrier();
+      const int b0 = t % 3;
+      stage(b0, t + 3 < KC ? t + 3 : KC - 1);
+      uint2 ct = {0u, 0u};
+      if constexpr (CVT) ct = cread(b0 + 2 >= 3 ? b0 - 1 : b0 + 2);  // codes of chunk t + 2
+      if (t + 1 < KC) rd(b0 + 1 == 3 ? 0 : b0 + 1, (t + 1) & 1, nxt);
+      mma(0, cur.a0, cur.b0);
+      mma(1, cur.a1, cur.b1);
+      if constexpr (CVT) {
+        cfinish(ct, t & 1);  // chunk t + 2's tile into chunk t's slot (read in the previous iteration)
+        if constexpr (LLJ_W4Z_IGLP) {
+#pragma unroll
+          for (int q = 0; q < 2 * MI * NJ; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, LLJ_W4Z_VPM, 0);
+          }
+        }
+      }
+    };
+    // prologue: chunks 0 and 1 (CVT: and chunk 0's codes, then both tiles converted) before chunk 2 is
+    // staged -- chunk 2's group carries chunk 3's codes into stage buffer 0, over chunk 0's
+    if constexpr (CVT) stage_codes(0, 0);
+    stage(0, 0);
+    stage(1, 1 < KC ? 1 : KC - 1);
+    wait_vm<G::NG>();  // chunk 0 (CVT: the codes of chunks 0 and 1)
+    __builtin_amdgcn_s_barrier();
+    if constexpr (CVT) {
+      convert(0, 0);
+      convert(1, 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's code reads done, both tiles written
+    }
+    stage(2, 2 < KC ? 2 : KC - 1);
+    Fr F0, F1;
+    rd(0, 0, F0);
+    for (int t = 0; t < KC; t += 2) {
+      step(t, F0, F1);
+      if (t + 1 < KC) step(t + 1, F1, F0);
+    }
+    wait_vm<0>();  // the clamped stages past the end land before the workgroup's LDS is released
+  } else {
   // ---- K loop: NST - 1 chunks staged ahead
   if constexpr (CVT) {  // chunk 0's codes first, converted before the loop
     static_assert(NST == 3, "convert-once int4: three stages");
@@ -1006,6 +1068,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     // branch-free: past the last chunk it converts the clamped codes into the unused slot
     if constexpr (CVT && CW == 8 && !LLJ_W4Z_SPLIT) convert(cb + 1 == NST ? 0 : cb + 1, (tc + 1) & 1);
     cb = cb + 1 == NST ? 0 : cb + 1;
+  }
   }
 
   // ---- epilogue: lane holds rows m0 + wr * 16 MI + 16 i + 4 g + r, column n0 + wc * 16 NJ + 16 j + row
