@@ -685,6 +685,9 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
 #ifndef LLJ_GLDS_FDB
 #define LLJ_GLDS_FDB 1  // LDS-DMA GEMM at 256 x 128: chunk t + 1's fragments read during chunk t's MFMAs (A/B)
 #endif
+#ifndef LLJ_FDB_DSPM
+#define LLJ_FDB_DSPM 0  // fragment double buffering: LDS fragment reads per MFMA in the sched_group pattern (0: the scheduler's)
+#endif
 #ifndef LLJ_W4Z_PRIO
 #define LLJ_W4Z_PRIO 0  // convert-once int4: s_setprio around the MFMA clusters (1; 0: none, so the conversion interleaves with them)
 #endif
@@ -989,14 +992,15 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
       if (t + 1 < KC) rd(b0 + 1 == 3 ? 0 : b0 + 1, (t + 1) & 1, nxt);
       mma(0, cur.a0, cur.b0);
       mma(1, cur.a1, cur.b1);
-      if constexpr (CVT) {
-        cfinish(ct, t & 1);  // chunk t + 2's tile into chunk t's slot (read in the previous iteration)
-        if constexpr (LLJ_W4Z_IGLP) {
+      if constexpr (CVT) cfinish(ct, t & 1);  // chunk t + 2's tile into chunk t's slot (read in the previous iteration)
+      // the MFMAs interleaved with the next chunk's fragment reads (LLJ_FDB_DSPM per MFMA) and the
+      // conversion's VALU (LLJ_W4Z_VPM per MFMA)
+      if constexpr ((CVT && LLJ_W4Z_IGLP) || LLJ_FDB_DSPM > 0) {
 #pragma unroll
-          for (int q = 0; q < 2 * MI * NJ; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, LLJ_W4Z_VPM, 0);
-          }
+        for (int q = 0; q < 2 * MI * NJ; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if constexpr (LLJ_FDB_DSPM > 0) __builtin_amdgcn_sched_group_barrier(0x100, LLJ_FDB_DSPM, 0);
+          if constexpr (CVT && LLJ_W4Z_IGLP) __builtin_amdgcn_sched_group_barrier(0x002, LLJ_W4Z_VPM, 0);
         }
       }
     };
