@@ -701,7 +701,7 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
 #define LLJ_W4Z_IGLP 1  // convert-once int4: sched_group_barrier interleave of the conversion with the MFMAs
 #endif
 #ifndef LLJ_W4Z_VPM
-#define LLJ_W4Z_VPM 2  // VALU instructions per MFMA in that interleave (3 with the conversion's packed form: +1 ms per 7B window)
+#define LLJ_W4Z_VPM 1  // VALU instructions per MFMA in that interleave (with fragment double buffering: 1 vs 2 vs 3 = 29.4-29.5 vs 29.9-30.0 vs 31.1 ms per 7B window)
 #endif
 #ifndef LLJ_W4Z_AFTER
 #define LLJ_W4Z_AFTER 0  // convert-once int4: the converting waves convert after their MFMAs (A/B)
