@@ -1164,7 +1164,8 @@ def glds_tile(request, hip):
 
 @pytest.mark.parametrize("glds_tile", list(GLDS_TILES), indirect=True)
 @pytest.mark.parametrize("wfmt", [0, 1])
-@pytest.mark.parametrize("M,N,K", [(256, 512, 256), (300, 4096, 4096), (520, 11008, 4096), (257, 4096, 11008)])
+@pytest.mark.parametrize("M,N,K", [(256, 512, 256), (300, 4096, 4096), (520, 11008, 4096), (257, 4096, 11008),
+                                   (256, 256, 128), (384, 512, 384)])
 def test_gemm_glds_tiles(hip, glds_tile, wfmt, M, N, K):
     """The LDS-DMA prefill GEMM (global_load_lds staging, counted vmcnt, source-swizzled LDS image,
     int4 row sums from the A fragments) in both tile shapes and the register-staged kernel, int4
@@ -1193,7 +1194,7 @@ ZINT4 = _hip.WF_ZINT  # int4 with integral zeros: the convert-once LDS-DMA kerne
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 512, 256), (300, 4096, 4096), (520, 11008, 4096), (257, 4096, 11008),
-                                   (2048, 12288, 4096), (100, 384, 1024)])
+                                   (2048, 12288, 4096), (100, 384, 1024), (256, 256, 128), (512, 384, 384)])
 def test_gemm_w4z_convert_once(hip, M, N, K):
     """int4 prompt GEMM with LLJ_WF_ZINT (each chunk's codes converted once per workgroup into a bf16
     (q - z) tile, the scale in the epilogue; M < 256 takes the default int4 kernel) against the
@@ -1245,7 +1246,8 @@ def test_gemm_w4z_exact_on_integer_rows(hip):
     np.testing.assert_array_equal(out.float().cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("M,H,K", [(256, 2816, 1024), (300, 11008, 4096), (2048, 11008, 4096), (520, 4096, 11008)])
+@pytest.mark.parametrize("M,H,K", [(256, 2816, 1024), (300, 11008, 4096), (2048, 11008, 4096), (520, 4096, 11008),
+                                   (256, 128, 128)])
 def test_gemm_swiglu_dual_pass(hip, M, H, K):
     """llj_gemm_swiglu (c_fc1 and c_fc2 of integral-zero int4 weights in one pass, one A tile for both,
     silu * mul in the epilogue) against the oracle, and bitwise equal to the two-pass form
