@@ -1,5 +1,5 @@
 #!/bin/bash
-# MFMA busy of the prefill kernels (gemm_kernel, flash_prefill_kernel): one rocprofv3 --pmc pass
+# MFMA busy of the prefill kernels (gemm_kernel, gemm_glds_kernel, flash_prefill_kernel): one rocprofv3 --pmc pass
 # (SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, GRBM_GUI_ACTIVE) over one 7B 2048-token window per
 # mode, summarized per kernel on the box into gpurun_out/$1.json.
 #   mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)
@@ -20,7 +20,7 @@ cnt = collections.Counter()
 for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        if "gemm_kernel" not in n and "flash" not in n:
+        if "gemm_kernel" not in n and "gemm_glds_kernel" not in n and "flash" not in n:
             continue
         key = n.split("(")[0].replace("void ", "")
         agg[key][r["Counter_Name"]] += float(r["Counter_Value"])
