@@ -193,6 +193,14 @@ int llj_gemm_linear(int wfmt, const void* A, int lda, const void* W, const void*
 /* x[M, N] += A . W^T (bf16 residual add, model.py:172-173). */
 int llj_gemm_resid(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M, int N,
                    int K, void* stream);
+/* llj_gemm_resid for prompts whose 256-row x 128-column tiles fill at most half the CUs (256..1024
+ * rows at the 4096-wide residual GEMMs): the K range is split over up to 8 workgroups per tile, fp32
+ * partials go to `ws` (llj_gemm_resid_ws_bytes(wfmt, M, N, K) bytes; 0 = no split, and then this call is
+ * llj_gemm_resid), one reduce launch adds them in slice order and the residual. bf16 and integral-zero
+ * int4 (0 | LLJ_WF_ZINT) weights, M >= 256. */
+size_t llj_gemm_resid_ws_bytes(int wfmt, int M, int N, int K);
+int llj_gemm_resid_ws(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M, int N,
+                      int K, void* ws, size_t ws_bytes, void* stream);
 /* h[M, N] = bf16(silu(h)) * bf16(A . W^T), h holding bf16(rms_2(x) . W_fc1^T) from a llj_gemm_linear
  * pass (model.py:258; two passes instead of a dual-weight tile). */
 int llj_gemm_silu_mul(int wfmt, const void* A, int lda, const void* W, const void* sz, void* h, int ldh, int M, int N,

@@ -52,7 +52,9 @@ namespace llj {
 enum : int { GWF_W4 = 0, GWF_BF16 = 1, GWF_I8 = 2, GWF_W8 = 3, GWF_W4G = 4, GWF_W4Z = 5 };
 // GEP_SWIGLU: h = bf16(silu(bf16(A . W1^T))) * bf16(A . W2^T) in one pass (convert-once int4: both weights'
 // codes staged per chunk, one A tile feeding both; W2 / sz2)
-enum : int { GEP_STORE = 0, GEP_RESID = 1, GEP_QKV = 2, GEP_SILU_MUL = 3, GEP_SWIGLU = 4 };
+// GEP_PARTIAL: split-K slice of a residual GEMM -- fp32 partials y (scale applied) of K range slice
+// blockIdx.x % nsplit into ws[slice][M][N]; llj_gemm_resid_ws's reduce adds them and the residual
+enum : int { GEP_STORE = 0, GEP_RESID = 1, GEP_QKV = 2, GEP_SILU_MUL = 3, GEP_SWIGLU = 4, GEP_PARTIAL = 5 };
 
 struct GemmParams {
   const bf16_t* A;  // (M, K) rows with stride lda
@@ -81,6 +83,9 @@ struct GemmParams {
   // GEP_SWIGLU: the second weight (c_fc2) and its (scale, 128 + zero) pairs
   const void* W2;
   const float2* sz2;
+  // GEP_PARTIAL: nsplit K slices of kcs 64-deep chunks each (kcs even), fp32 partials [nsplit][M][N]
+  float* ws;
+  int nsplit, kcs;
 };
 
 // Tile epilogues run in two phases per 16-column block: every element's operand is loaded first
@@ -746,6 +751,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   // from W1, j >= NJ / 2 from W2), so each lane has fc1 and fc2 of the same element
   constexpr bool DUAL = EP == GEP_SWIGLU;
   static_assert(!DUAL || WF == GWF_W4Z, "dual SwiGLU GEMM: convert-once int4");
+  static_assert(EP != GEP_PARTIAL || ((WF == GWF_W4Z || WF == GWF_BF16) && BN == 128), "split-K slices: 256 x 128");
   constexpr int NOUT = DUAL ? BN / 2 : BN;  // output columns per tile
   using G = GldsGeo<WF, BN>;
   constexpr int MI = G::MI, NJ = G::NJ, WN = G::WN, NST = G::NST;
@@ -756,9 +762,13 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w / WN, wc = w % WN;
   const int row = lane & 15, g = lane >> 4;
-  const int M = p.M, K = p.K, KC = K / 64, KC128 = K / 128;
+  constexpr bool PART = EP == GEP_PARTIAL;  // split-K slice (kc0 .. kc0 + KC of the K chunks)
+  const int M = p.M, K = p.K, KC128 = K / 128;
+  const int split = PART ? (int)blockIdx.x % p.nsplit : 0;
+  const int kc0 = PART ? split * p.kcs : 0;  // even: the W4P chunk pairs stay aligned
+  const int KC = PART ? min(p.kcs, K / 64 - kc0) : K / 64;
   const int mtiles = (M + 255) / 256, ntiles = p.N / NOUT, total = mtiles * ntiles;
-  int t = blockIdx.x;
+  int t = PART ? (int)blockIdx.x / p.nsplit : (int)blockIdx.x;
   {  // contiguous tile ranges per XCD (bijective for any total)
     const int q = total / 8, r = total % 8, x = t % 8;
     t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + t / 8;
@@ -774,7 +784,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int m = m0 + 64 * q + drow;
-    asrc[q] = p.A + (size_t)(m < M ? m : M - 1) * p.lda + 8 * dseg;
+    asrc[q] = p.A + (size_t)(m < M ? m : M - 1) * p.lda + 8 * dseg + (size_t)kc0 * 64;
   }
   const char* bsrc;
   if constexpr (NIB || CVT) {  // W4P: wave w stages tiles 2 w, 2 w + 1 (BN 128: waves 4-7 a copy of 0-3's)
@@ -782,9 +792,11 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     if (DUAL)  // B tiles 0-3: W1's columns n0 .. + 63, tiles 4-7: W2's
       bsrc = reinterpret_cast<const char*>(tl < 4 ? p.W : p.W2) + (size_t)(n0 / 16 + (tl & 3)) * KC128 * 1024 + 16 * (lane & 31);
     else
-      bsrc = reinterpret_cast<const char*>(p.W) + (size_t)(n0 / 16 + tl) * KC128 * 1024 + 16 * (lane & 31);
+      bsrc = reinterpret_cast<const char*>(p.W) + (size_t)(n0 / 16 + tl) * KC128 * 1024 + 16 * (lane & 31) +
+             (size_t)(kc0 >> 1) * 1024;
   } else {
-    bsrc = reinterpret_cast<const char*>(reinterpret_cast<const bf16_t*>(p.W) + (size_t)(n0 + drow) * K + 8 * dseg);
+    bsrc = reinterpret_cast<const char*>(reinterpret_cast<const bf16_t*>(p.W) + (size_t)(n0 + drow) * K + 8 * dseg +
+                                         (size_t)kc0 * 64);
   }
   // convert-once int4: the codes run one chunk ahead of A (DMA group c = A(c) + the codes of chunk
   // c + 1, into the stage buffer of chunk c + 1), so a chunk's codes have landed one iteration before
@@ -1076,6 +1088,22 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   }
 
   // ---- epilogue: lane holds rows m0 + wr * 16 MI + 16 i + 4 g + r, column n0 + wc * 16 NJ + 16 j + row
+  if constexpr (PART) {  // the slice's fp32 partials, scale applied (summed over the slices by the reduce)
+    float* wsl = p.ws + (size_t)split * M * p.N;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wc * 16 * NJ + 16 * j + row;
+      const float sc = CVT ? p.sz[n].x : 1.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wr * 16 * MI + 16 * i + 4 * g + r;
+          if (m < M) wsl[(size_t)m * p.N + n] = sc * acc[i][j][r];
+        }
+    }
+    return;
+  }
   if constexpr (DUAL) {  // h = bf16(silu(bf16(fc1))) * bf16(fc2), fc1 in fragments j < NJ / 2, fc2 at j + NJ / 2
 #pragma unroll
     for (int j = 0; j < NJ / 2; ++j) {
@@ -1165,7 +1193,7 @@ static int gemm_glds_launch(const GemmParams& p, hipStream_t s) {
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  const int tiles = ((p.M + 255) / 256) * (p.N / (EP == GEP_SWIGLU ? BN / 2 : BN));
+  const int tiles = ((p.M + 255) / 256) * (p.N / (EP == GEP_SWIGLU ? BN / 2 : BN)) * (EP == GEP_PARTIAL ? p.nsplit : 1);
   hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), lds, s, p);
   LLJ_CHECK_LAUNCH();
   return 0;
@@ -1203,14 +1231,64 @@ static int gemm_glds_run(const GemmParams& p, hipStream_t s) {
   return gemm_glds_launch<WF, EP, 128>(p, s);
 }
 
+// split-K residual GEMM (few row tiles: a prompt of 256..1024 rows leaves the 4096-column GEMMs at
+// 64..128 workgroups): x = bf16(x + bf16(sum over the slices of their fp32 partials)), slices in order
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __restrict__ ws, int nsplit, int M, int N,
+                                                                 bf16_t* __restrict__ x, int ldx) {
+  const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;  // 4 consecutive columns (N % 4 == 0)
+  if (i >= (size_t)M * N) return;
+  const int m = (int)(i / N), n = (int)(i % N);
+  float4 y = *reinterpret_cast<const float4*>(ws + i);
+  for (int sp = 1; sp < nsplit; ++sp) {
+    const float4 v = *reinterpret_cast<const float4*>(ws + (size_t)sp * M * N + i);
+    y.x += v.x; y.y += v.y; y.z += v.z; y.w += v.w;
+  }
+  uint2* xp = reinterpret_cast<uint2*>(x + (size_t)m * ldx + n);
+  const uint2 xv = *xp;
+  const uint32_t lo = pack2bf(round_bf(bflo(xv.x) + round_bf(y.x)), round_bf(bfhi(xv.x) + round_bf(y.y)));
+  const uint32_t hi = pack2bf(round_bf(bflo(xv.y) + round_bf(y.z)), round_bf(bfhi(xv.y) + round_bf(y.w)));
+  *xp = make_uint2(lo, hi);
+}
+
+// K slices for a residual GEMM on the LDS-DMA kernels (0: none): when the row tiles x 128-column tiles
+// fill at most half the CUs, up to 8 slices of >= 8 64-deep chunks (an even count each)
+static int splitk_plan(int wfmt, int M, int N, int K, int* kcs_out);
+
 // option LLJ_OPT_GEMM_W4Z (LLJ_GEMM_W4Z) 1 / 0: int4 with integral zeros (LLJ_WF_ZINT) in the
 // convert-once LDS-DMA kernel / in the int4 default kernel
 #ifndef LLJ_GEMM_W4Z
 #define LLJ_GEMM_W4Z 1
 #endif
+#ifndef LLJ_GEMM_SPLITK
+#define LLJ_GEMM_SPLITK 1  // split-K residual GEMMs for few row tiles (llj_gemm_resid_ws)
+#endif
 static bool w4z_enabled() {
   const int o = opt(LLJ_OPT_GEMM_W4Z);
   return o >= 0 ? o != 0 : LLJ_GEMM_W4Z != 0;
+}
+
+static int splitk_plan(int wfmt, int M, int N, int K, int* kcs_out) {
+  const bool w4z = wfmt == (GWF_W4 | LLJ_WF_ZINT) && w4z_enabled();
+  const bool bf = wfmt == GWF_BF16 && glds_enabled(GWF_BF16);
+  if ((!w4z && !bf) || M < 256 || N % 128 || K % 128 || K < 1024 || !LLJ_GEMM_SPLITK) return 0;
+  int cus = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const long tiles = (long)((M + 255) / 256) * (N / 128);
+  if (2 * tiles > cus) return 0;
+  const int KC = K / 64;
+  int ns = (int)(cus / tiles);
+  ns = ns > 8 ? 8 : ns;
+  ns = ns > KC / 8 ? KC / 8 : ns;
+  if (ns < 2) return 0;
+  int kcs = (KC + ns - 1) / ns;
+  kcs += kcs & 1;
+  ns = (KC + kcs - 1) / kcs;
+  if (kcs_out) *kcs_out = kcs;
+  return ns < 2 ? 0 : ns;
 }
 
 template <int EP>
@@ -1277,6 +1355,37 @@ int llj_gemm_silu_mul(int wfmt, const void* A, int lda, const void* W, const voi
   p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = W; p.sz = (const float2*)sz;
   p.C = (bf16_t*)h; p.ldc = ldh;
   return gemm_run<GEP_SILU_MUL>(wfmt, p, stream);
+}
+
+// Workspace bytes llj_gemm_resid_ws needs for this residual GEMM (0: it would not split K -- call
+// llj_gemm_resid).
+size_t llj_gemm_resid_ws_bytes(int wfmt, int M, int N, int K) {
+  int kcs = 0;
+  const int ns = splitk_plan(wfmt, M, N, K, &kcs);
+  return ns ? (size_t)ns * M * N * sizeof(float) : 0;
+}
+
+// llj_gemm_resid with the K range split over workgroups (few row tiles): fp32 partials into ws
+// (llj_gemm_resid_ws_bytes), then one reduce launch adds them in slice order and the residual.
+int llj_gemm_resid_ws(int wfmt, const void* A, int lda, const void* W, const void* sz, void* x, int ldx, int M, int N,
+                      int K, void* ws, size_t ws_bytes, void* stream) {
+  int kcs = 0;
+  const int ns = splitk_plan(wfmt, M, N, K, &kcs);
+  if (!ns) return llj_gemm_resid(wfmt, A, lda, W, sz, x, ldx, M, N, K, stream);
+  if (!ws || ws_bytes < (size_t)ns * M * N * sizeof(float) || (lda & 7) || (ldx & 3) || !A || !W || !x) return LLJ_EINVAL;
+  if ((wfmt & ~LLJ_WF_ZINT) == GWF_W4 && !sz) return LLJ_EINVAL;
+  GemmParams p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = N; p.K = K; p.W = W; p.sz = (const float2*)sz;
+  p.ws = (float*)ws; p.nsplit = ns; p.kcs = kcs;
+  hipStream_t s = (hipStream_t)stream;
+  const int rc = wfmt == GWF_BF16 ? gemm_glds_launch<GWF_BF16, GEP_PARTIAL, 128>(p, s)
+                                  : gemm_glds_launch<GWF_W4Z, GEP_PARTIAL, 128>(p, s);
+  if (rc) return rc;
+  const size_t n4 = (size_t)M * N / 4;
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, (const float*)ws, ns,
+                     M, N, (bf16_t*)x, ldx);
+  LLJ_CHECK_LAUNCH();
+  return 0;
 }
 
 // h[M, H] = bf16(silu(bf16(A . W1^T))) * bf16(A . W2^T) in one pass: int4 W4P with integral zeros

@@ -571,8 +571,15 @@ class LLaMA(nn.Module):
             _hip.call("llj_gemm_i8_resid", A.data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz), _hip.ptr(w.i8ws),
                       _hip.ptr(ao), _hip.ptr(wg), kp, x.data_ptr(), x.stride(0), M, N, K, st)
         else:
-            _hip.call("llj_gemm_resid", f, A.data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz), x.data_ptr(),
-                      x.stride(0), M, N, K, st)
+            # few row tiles (256..1024 prompt rows): the K range split over workgroups (llj_gemm_resid_ws)
+            nb = _hip.lib().llj_gemm_resid_ws_bytes(f, M, N, K) if M >= 256 else 0
+            if nb:
+                ws = torch.empty(nb // 4, dtype=torch.float32, device=x.device)
+                _hip.call("llj_gemm_resid_ws", f, A.data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz), x.data_ptr(),
+                          x.stride(0), M, N, K, ws.data_ptr(), nb, st)
+            else:
+                _hip.call("llj_gemm_resid", f, A.data_ptr(), A.stride(0), W.data_ptr(), _hip.ptr(sz), x.data_ptr(),
+                          x.stride(0), M, N, K, st)
 
     @staticmethod
     def _glinear(spec, A, M, K, N, out, resid, st):

@@ -1272,6 +1272,44 @@ def test_gemm_swiglu_dual_pass(hip, M, H, K):
     assert_bf16_close(got[:M], hexp, f"gemm swiglu dual M={M}", rel=3e-2)
 
 
+@pytest.mark.parametrize("wfmt", [1, ZINT4])
+@pytest.mark.parametrize("M,N,K", [(256, 4096, 4096), (512, 4096, 11008), (300, 1024, 1024), (1024, 4096, 2048)])
+def test_gemm_resid_split_k(hip, wfmt, M, N, K):
+    """llj_gemm_resid_ws (K split over workgroups for few row tiles, fp32 partials reduced in slice order
+    with the residual) against the oracle and against the unsplit llj_gemm_resid (same inputs, within
+    bf16 rounding: the fp32 sums differ in order only); a workspace short by 4 bytes is refused."""
+    L = hip
+    nb = L.llj_gemm_resid_ws_bytes(wfmt, M, N, K)
+    assert nb > 0, "this shape is expected to split"
+    rng = np.random.default_rng(M + N + K + wfmt)
+    Wref, Wd, szd = quant_operands(hip, rng, wfmt, N, K)
+    x = bf16(rng.standard_normal((M, K)).astype(np.float32))
+    xd = T(x, torch.bfloat16)
+    x0 = bf16(rng.standard_normal((M, N)).astype(np.float32))
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    ws = torch.empty(nb // 4, dtype=torch.float32, device=dev)
+    assert L.llj_gemm_resid_ws(wfmt, xd.data_ptr(), K, Wd.data_ptr(), P(szd), T(x0, torch.bfloat16).data_ptr(), N, M, N,
+                               K, ws.data_ptr(), nb - 4, st()) == 1000
+    xr = T(x0, torch.bfloat16)
+    call(hip, "llj_gemm_resid_ws", wfmt, xd.data_ptr(), K, Wd.data_ptr(), P(szd), xr.data_ptr(), N, M, N, K, ws.data_ptr(),
+         nb, st())
+    xu = T(x0, torch.bfloat16)
+    call(hip, "llj_gemm_resid", wfmt, xd.data_ptr(), K, Wd.data_ptr(), P(szd), xu.data_ptr(), N, M, N, K, st())
+    torch.cuda.synchronize()
+    got = xr.float().cpu().numpy()
+    assert_bf16_close(got, x0 + bf16(x @ Wref.T), f"gemm resid split-K wfmt={wfmt} M={M}")
+    assert_bf16_close(got, xu.float().cpu().numpy(), f"gemm resid split-K vs unsplit wfmt={wfmt} M={M}")
+
+
+def test_gemm_resid_split_k_plan(hip):
+    """The split plan: none at 7B's 2048-row windows (256 tiles fill the CUs) or below 256 rows."""
+    L = hip
+    assert L.llj_gemm_resid_ws_bytes(ZINT4, 2048, 4096, 11008) == 0
+    assert L.llj_gemm_resid_ws_bytes(1, 128, 4096, 4096) == 0
+    assert L.llj_gemm_resid_ws_bytes(0, 512, 4096, 4096) == 0  # int4 without integral zeros: no LDS-DMA form
+    assert L.llj_gemm_resid_ws_bytes(ZINT4, 512, 4096, 4096) > 0
+
+
 def test_gemm_swiglu_dual_refuses(hip):
     """The one-pass form takes only integral-zero int4 at M >= 256 and H % 64 == 0 (EINVAL otherwise)."""
     L = hip
