@@ -41,6 +41,9 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 #ifndef LLJ_FLASH_PF
 #define LLJ_FLASH_PF 1  // K / V tiles in flight in registers (2: two register sets; 7B window 32.03-32.06 ms at 1 vs 32.13-32.31 at 2)
 #endif
+#ifndef LLJ_FLASH_QB2_MIN_T
+#define LLJ_FLASH_QB2_MIN_T 2048
+#endif
 #ifndef LLJ_FLASH_QB
 #define LLJ_FLASH_QB 1  // 16-query blocks per wave (2: every K / V fragment read feeds two MFMAs; with the pairing 1 is faster)
 #endif
@@ -288,7 +291,9 @@ int llj_attention_prefill(const void* q, const void* kcache, const void* vcache,
   const float sl2 = 1.4426950408889634f / sqrtf((float)head_size);
   hipStream_t st = (hipStream_t)stream;
   const int oq = opt(LLJ_OPT_FLASH_QB), op = opt(LLJ_OPT_FLASH_PAIR);  // A/B options (llj_set_option)
-  const int qbw = oq > 0 ? oq : LLJ_FLASH_QB;  // 1 or 2 query blocks per wave
+  // 1 or 2 query blocks per wave: 2 from LLJ_FLASH_QB2_MIN_T queries on (7B T = 2048: 29.28 / 29.43 vs
+  // 29.45 / 29.67 ms per window, profiles/r06aa_flash_qb.jsonl), where the grid still fills the CUs
+  const int qbw = oq > 0 ? oq : (T >= LLJ_FLASH_QB2_MIN_T ? 2 : LLJ_FLASH_QB);
   const bool pair = op >= 0 ? op != 0 : LLJ_FLASH_PAIR != 0;  // a long and a short query block per workgroup
   if (head_size == 128) {
     if (qbw == 2) flash_launch<128, 2>(q, kcache, vcache, y, pos, B, T, n_head, S, sl2, pair, st);
