@@ -93,6 +93,9 @@ struct GemmParams {
 // element is computed and stored (gemm_store_elem) -- one load latency per block instead of a
 // load -> store dependence per element (7B 2048-token window: the QKV and silu * mul GEMMs ran
 // 20-26 % slower than the plain store GEMM of the same shape with per-element loads).
+#ifndef LLJ_QKV_ABL
+#define LLJ_QKV_ABL 0  // prompt QKV epilogue timing ablations (profiling only): 1 no RoPE operand loads, 2 no stores
+#endif
 // QKV rows: sequence b, position ps and KV-cache ring slot of (clamped) row m, computed once per row
 // and tile (the divisions by T and S stay out of the per-element path)
 struct QkvRow {
@@ -125,6 +128,7 @@ __device__ __forceinline__ float2 gemm_operand(const GemmParams& p, int m, int n
     const int mm = m < p.M ? m : p.M - 1;  // rows past M: a clamped copy, never stored
     return make_float2(bf2f(p.C[(size_t)mm * p.ldc + n]), 0.f);
   } else if constexpr (EP == GEP_QKV) {
+    if (LLJ_QKV_ABL & 1) return make_float2(1.f, 0.f);  // timing ablation: no RoPE operand loads (results wrong)
     if (qc.region < 2) return *reinterpret_cast<const float2*>(p.rope + ((size_t)qr.ps * (p.head_size >> 1) + (qc.dd >> 1)) * 2);
     return make_float2(1.f, 0.f);
   } else {
@@ -149,7 +153,7 @@ __device__ __forceinline__ void gemm_store_elem(const GemmParams& p, float y, in
     if (qc.region < 2) out = (dd & 1) ? (v * op.x + partner * op.y) : (v * op.x - partner * op.y);
     const uint32_t ob = (uint32_t)f2bf(out);
     const uint32_t pr = lane_xor1(ob);
-    if (live && !(dd & 1)) {
+    if (live && !(dd & 1) && !(LLJ_QKV_ABL & 2)) {  // (LLJ_QKV_ABL & 2: timing ablation, no q / k / v stores)
       bf16_t* dst;
       size_t ei;
       if (qc.region == 0) {
