@@ -691,6 +691,12 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
 #ifndef LLJ_GLDS_PRE
 #define LLJ_GLDS_PRE 1  // 256 x 128 tiles: read both MFMA steps' fragments of a chunk before its MFMAs (bf16 window 35.9 -> 35.4 ms)
 #endif
+#ifndef LLJ_GLDS_NFAST_W4Z
+#define LLJ_GLDS_NFAST_W4Z 1  // convert-once int4 LDS-DMA GEMM: n-fastest tile order (A/B)
+#endif
+#ifndef LLJ_GLDS_NFAST_BF16
+#define LLJ_GLDS_NFAST_BF16 0  // bf16 LDS-DMA GEMM: n-fastest tile order (A/B)
+#endif
 #ifndef LLJ_GLDS_FDB
 #define LLJ_GLDS_FDB 1  // LDS-DMA GEMM at 256 x 128: chunk t + 1's fragments read during chunk t's MFMAs (A/B)
 #endif
@@ -777,7 +783,12 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     const int q = total / 8, r = total % 8, x = t % 8;
     t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + t / 8;
   }
-  const int nb = t / mtiles, mb = t % mtiles;  // m fastest: a weight panel's row tiles run together
+  // tile order inside an XCD's contiguous range: m fastest (a weight panel's row tiles run together and
+  // share it through the XCD's L2) or n fastest (an A row panel stays in L2 while the XCD sweeps the
+  // weight columns: the A re-reads go from one per column tile to one per XCD -- the int4 weights are a
+  // quarter of the bf16 bytes, so re-reading them per row panel is the cheaper side)
+  constexpr bool NFAST = CVT ? LLJ_GLDS_NFAST_W4Z != 0 : LLJ_GLDS_NFAST_BF16 != 0;
+  const int nb = NFAST ? t % ntiles : t / mtiles, mb = NFAST ? t / ntiles : t % mtiles;
   const int m0 = mb * 256, n0 = nb * NOUT;
   float* rs_lds = reinterpret_cast<float*>(smem + NST * G::STAGE);
 
