@@ -691,6 +691,9 @@ static int gemm_launch(const GemmParams& p, hipStream_t s) {
 #ifndef LLJ_GLDS_PRE
 #define LLJ_GLDS_PRE 1  // 256 x 128 tiles: read both MFMA steps' fragments of a chunk before its MFMAs (bf16 window 35.9 -> 35.4 ms)
 #endif
+#ifndef LLJ_GLDS_GROUPM
+#define LLJ_GLDS_GROUPM 0  // A/B only: grouped tile order (row tiles per group); 0 = the m- / n-fastest orders below
+#endif
 #ifndef LLJ_GLDS_NFAST_W4Z
 #define LLJ_GLDS_NFAST_W4Z 1  // convert-once int4 LDS-DMA GEMM: n-fastest tile order (A/B)
 #endif
@@ -788,7 +791,15 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   // weight columns: the A re-reads go from one per column tile to one per XCD -- the int4 weights are a
   // quarter of the bf16 bytes, so re-reading them per row panel is the cheaper side)
   constexpr bool NFAST = CVT ? LLJ_GLDS_NFAST_W4Z != 0 : LLJ_GLDS_NFAST_BF16 != 0;
-  const int nb = NFAST ? t % ntiles : t / mtiles, mb = NFAST ? t / ntiles : t % mtiles;
+  // (LLJ_GLDS_GROUPM > 0, A/B: groups of that many row tiles sweep the columns together, m fastest inside)
+  int nb = NFAST ? t % ntiles : t / mtiles, mb = NFAST ? t / ntiles : t % mtiles;
+  if constexpr (LLJ_GLDS_GROUPM > 0) {
+    const int gm = LLJ_GLDS_GROUPM, grp = t / (gm * ntiles), first = grp * gm;
+    const int rows = mtiles - first < gm ? mtiles - first : gm;
+    const int in = t - grp * gm * ntiles;
+    mb = first + in % rows;
+    nb = in / rows;
+  }
   const int m0 = mb * 256, n0 = nb * NOUT;
   float* rs_lds = reinterpret_cast<float*>(smem + NST * G::STAGE);
 
