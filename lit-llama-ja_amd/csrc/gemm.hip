@@ -93,6 +93,9 @@ struct GemmParams {
 // element is computed and stored (gemm_store_elem) -- one load latency per block instead of a
 // load -> store dependence per element (7B 2048-token window: the QKV and silu * mul GEMMs ran
 // 20-26 % slower than the plain store GEMM of the same shape with per-element loads).
+#ifndef LLJ_QKV_GI
+#define LLJ_QKV_GI 4  // LDS-DMA GEMM QKV epilogue: 16-row blocks whose RoPE operands are loaded together (A/B)
+#endif
 #ifndef LLJ_QKV_ABL
 #define LLJ_QKV_ABL 0  // prompt QKV epilogue timing ablations (profiling only): 1 no RoPE operand loads, 2 no stores
 #endif
@@ -1178,7 +1181,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     float2 szn = make_float2(1.f, 0.f);
     if constexpr (NIB || CVT) szn = p.sz[n];
     const QkvCol qc = EP == GEP_QKV ? qkv_col(p, nblk, n, Cd) : QkvCol{};
-    constexpr int GI = (MI > 4 && EP == GEP_QKV) ? 1 : 4;  // row blocks whose operands are in flight together
+    constexpr int GI = EP == GEP_QKV ? (MI > 4 ? 1 : LLJ_QKV_GI) : 4;  // row blocks whose operands are in flight together
 #pragma unroll
     for (int i0 = 0; i0 < MI; i0 += GI) {
       float2 opv[GI][4];

@@ -1,0 +1,63 @@
+"""Prompt-GEMM epilogue probe: the 7B QKV GEMM (M = 2048, N = 12288, K = 4096, integral-zero int4) timed as
+llj_gemm_qkv_rope (RoPE + q / KV-cache stores) and as llj_gemm_linear (plain bf16 store) on the same weights,
+interleaved; prints one JSON line. Timing only (random codes, scales, zeros 8)."""
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "lit-llama-ja_amd"))
+from lit_llama import _hip  # noqa: E402
+
+
+def main():
+    L = _hip.lib()
+    dev = "cuda"
+    M, C, nh, S = 2048, 4096, 32, 2048
+    N, K = 3 * C, C
+    g = torch.Generator(device=dev).manual_seed(5)
+    qw = torch.randint(0, 256, (K // 2, N), dtype=torch.uint8, device=dev, generator=g)
+    Wp = torch.empty_like(qw)
+    _hip.call("llj_w4_repack", qw.data_ptr(), Wp.data_ptr(), N, K, 0)
+    sc = torch.full((N,), 0.002, dtype=torch.float32, device=dev)
+    zr = torch.full((N,), 8.0, dtype=torch.float32, device=dev)
+    sz = torch.empty(N, 2, dtype=torch.float32, device=dev)
+    _hip.call("llj_w4_scale_zero", sc.data_ptr(), zr.data_ptr(), 0, sz.data_ptr(), N, 0)
+    x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    q = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    kc = torch.empty(1, nh, S, C // nh, dtype=torch.bfloat16, device=dev)
+    vc = torch.empty_like(kc)
+    rope = torch.randn(S, C // nh // 2, 2, device=dev, generator=g)
+    pos = torch.arange(M, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    wf = _hip.WF_ZINT
+    runs = {
+        "qkv_rope": lambda: _hip.call("llj_gemm_qkv_rope", wf, x.data_ptr(), Wp.data_ptr(), sz.data_ptr(), q.data_ptr(),
+                                      kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), 1, M, C, nh, S, st),
+        "store": lambda: _hip.call("llj_gemm_linear", wf, x.data_ptr(), K, Wp.data_ptr(), sz.data_ptr(), out.data_ptr(), N,
+                                   M, N, K, st),
+    }
+    res = {k: [] for k in runs}
+    for f in runs.values():
+        f()
+    torch.cuda.synchronize()
+    for _ in range(5):
+        for k, f in runs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                f()
+            e1.record()
+            torch.cuda.synchronize()
+            res[k].append(e0.elapsed_time(e1) / 10 * 1e3)
+    print(json.dumps({k: round(sorted(v)[2], 1) for k, v in res.items()} | {"unit": "us per launch (median of 5 x 10)",
+                                                                              "shape": [M, N, K]}))
+
+
+if __name__ == "__main__":
+    main()
