@@ -93,6 +93,9 @@ struct GemmParams {
 // element is computed and stored (gemm_store_elem) -- one load latency per block instead of a
 // load -> store dependence per element (7B 2048-token window: the QKV and silu * mul GEMMs ran
 // 20-26 % slower than the plain store GEMM of the same shape with per-element loads).
+#ifndef LLJ_QKV_LDS
+#define LLJ_QKV_LDS 1  // LDS-DMA GEMM at 256 x 128 (bf16, convert-once int4): QKV epilogue through LDS, 16-byte row stores
+#endif
 #ifndef LLJ_QKV_GI
 #define LLJ_QKV_GI 4  // LDS-DMA GEMM QKV epilogue: 16-row blocks whose RoPE operands are loaded together (A/B)
 #endif
@@ -1117,6 +1120,54 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   }
 
   // ---- epilogue: lane holds rows m0 + wr * 16 MI + 16 i + 4 g + r, column n0 + wc * 16 NJ + 16 j + row
+  if constexpr (EP == GEP_QKV && LLJ_QKV_LDS && !NIB && BN == 128 && MI <= 4) if ((p.head_size & 7) == 0) {
+    // QKV through LDS: the tile's bf16 c_attn outputs (model.py:204) go to LDS in the accumulator layout,
+    // then every thread takes 8 consecutive columns (4 RoPE pairs: no lane exchange) of one row and
+    // stores them as one 16-byte vector -- a tile row is 256 contiguous bytes of q, or of one K / V cache
+    // row (the head dimension), instead of 4-byte pairs from every other lane
+    constexpr int TP = BN + 8;  // row pitch (elements): 16-B aligned rows on shifted banks
+    bf16_t* Ts = reinterpret_cast<bf16_t*>(smem);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is past its last fragment read of the K loop
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int nl = wc * 16 * NJ + 16 * j + row;
+      const float sc = CVT ? p.sz[n0 + nl].x : 1.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ts[(wr * 16 * MI + 16 * i + 4 * g + r) * TP + nl] = f2bf(sc * acc[i][j][r]);
+    }
+    __syncthreads();
+    const int Cd = p.n_head * p.head_size, seg = tid & 15;
+    const int nc0 = n0 + 8 * seg, region = nc0 / Cd, nc = nc0 - region * Cd;
+    const int h = nc / p.head_size, dd = nc - h * p.head_size;  // 8 | head_size: the 8 columns share a head
+#pragma unroll 2
+    for (int k = 0; k < 8; ++k) {
+      const int rl = (tid >> 4) + 32 * k, m = m0 + rl;
+      if (m >= M) continue;
+      const uint4 v = *reinterpret_cast<const uint4*>(Ts + rl * TP + 8 * seg);
+      const QkvRow qr = qkv_row(p, m);
+      uint4 o = v;
+      if (region < 2) {
+        const float4* rp = reinterpret_cast<const float4*>(p.rope + ((size_t)qr.ps * (p.head_size >> 1) + (dd >> 1)) * 2);
+        const float4 c01 = rp[0], c23 = rp[1];  // (cos, sin) of pairs dd / 2 .. + 3
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        const float cs[8] = {c01.x, c01.y, c01.z, c01.w, c23.x, c23.y, c23.z, c23.w};
+        uint32_t ow[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float e0 = bflo(w[q]), e1 = bfhi(w[q]), c = cs[2 * q], sn = cs[2 * q + 1];
+          ow[q] = pack2bf(e0 * c - e1 * sn, e1 * c + e0 * sn);
+        }
+        o = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+      }
+      bf16_t* dst = region == 0 ? p.q_out + (size_t)m * Cd + nc
+                                : (region == 1 ? p.kcache : p.vcache) + (size_t)qr.kvrow + (size_t)h * p.S * p.head_size + dd;
+      *reinterpret_cast<uint4*>(dst) = o;
+    }
+    return;
+  }
   if constexpr (PART) {  // the slice's fp32 partials, scale applied (summed over the slices by the reduce)
     float* wsl = p.ws + (size_t)split * M * p.N;
 #pragma unroll

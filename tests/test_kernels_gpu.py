@@ -1359,6 +1359,38 @@ def test_gemm_glds_qkv_swiglu(hip, glds_tile, wfmt):
     assert_bf16_close(h.float().cpu().numpy(), hexp, f"gemm swiglu {glds_tile}", rel=3e-2)
 
 
+@pytest.mark.parametrize("wfmt", [1, ZINT4])
+@pytest.mark.parametrize("B,T_,nh,hs,S,p0", [(2, 150, 4, 64, 256, 200), (1, 257, 8, 128, 512, 0), (3, 100, 2, 128, 128, 60)])
+def test_gemm_glds_qkv_lds_epilogue(hip, wfmt, B, T_, nh, hs, S, p0):
+    """The 256 x 128 LDS-DMA GEMM's QKV epilogue through LDS (8 columns = 4 RoPE pairs per thread, one
+    16-byte store): head sizes 64 / 128, ring slots wrapping past S, ragged last tile, several sequences;
+    cache slots the prompt does not cover stay untouched."""
+    rng = np.random.default_rng(7 * T_ + hs + p0 + (wfmt & 1))
+    C, M = nh * hs, B * T_
+    x = bf16(rng.standard_normal((M, C)).astype(np.float32))
+    rope = O.build_rope_cache(p0 + T_ + 8, hs)
+    pos = np.arange(p0, p0 + T_, dtype=np.int32)
+    Wref, Wd, szd = quant_operands(hip, rng, wfmt, 3 * C, C)
+    q = torch.zeros(M, C, dtype=torch.bfloat16, device=dev)
+    kc = torch.zeros(B, nh, S, hs, dtype=torch.bfloat16, device=dev)
+    vc = torch.zeros_like(kc)
+    xd, rd, pd = T(x, torch.bfloat16), T(rope), T(pos)
+    call(hip, "llj_gemm_qkv_rope", wfmt, xd.data_ptr(), Wd.data_ptr(), None if szd is None else szd.data_ptr(),
+         q.data_ptr(), kc.data_ptr(), vc.data_ptr(), rd.data_ptr(), pd.data_ptr(), B, T_, C, nh, S, st())
+    torch.cuda.synchronize()
+    qkv = bf16(x @ Wref.T)
+    qe = O.apply_rope(qkv[:, :C].reshape(B, T_, nh, hs), rope[pos]).reshape(M, C)
+    ke = O.apply_rope(qkv[:, C:2 * C].reshape(B, T_, nh, hs), rope[pos])
+    ve = qkv[:, 2 * C:].reshape(B, T_, nh, hs)
+    assert_bf16_close(q.float().cpu().numpy(), qe, "gemm q (LDS epilogue)")
+    kcn, vcn = kc.float().cpu().numpy(), vc.float().cpu().numpy()
+    slots = pos % S
+    assert_bf16_close(kcn[:, :, slots].transpose(0, 2, 1, 3), ke, "gemm k cache (LDS epilogue)")
+    assert_bf16_close(vcn[:, :, slots].transpose(0, 2, 1, 3), ve, "gemm v cache (LDS epilogue)")
+    rest = np.setdiff1d(np.arange(S), slots)
+    assert not kcn[:, :, rest].any() and not vcn[:, :, rest].any()
+
+
 def _i8_operands(hip, W):
     """CB / SCB of an LLM.int8 weight (llj_i8_quant_weight, checked against the oracle's rule) and
     CB re-tiled into I8P (what Linear8bitLt holds on the device)."""
