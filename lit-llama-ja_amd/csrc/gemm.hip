@@ -96,6 +96,9 @@ struct GemmParams {
 #ifndef LLJ_QKV_LDS
 #define LLJ_QKV_LDS 1  // LDS-DMA GEMM at 256 x 128 (bf16, convert-once int4): QKV epilogue through LDS, 16-byte row stores
 #endif
+#ifndef LLJ_GLDS_LDS_EPI
+#define LLJ_GLDS_LDS_EPI 1  // LDS-DMA GEMM at 256 x 128: store / residual / SwiGLU epilogues through LDS, 16-byte rows
+#endif
 #ifndef LLJ_QKV_GI
 #define LLJ_QKV_GI 4  // LDS-DMA GEMM QKV epilogue: 16-row blocks whose RoPE operands are loaded together (A/B)
 #endif
@@ -1168,6 +1171,66 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
     }
     return;
   }
+  if constexpr (LLJ_GLDS_LDS_EPI && !NIB && !PART && BN == 128 && MI <= 4 &&
+                (EP == GEP_STORE || EP == GEP_RESID || EP == GEP_SILU_MUL || EP == GEP_SWIGLU))
+    if ((p.ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(p.C) & 15) == 0) {
+      // the other bf16 epilogues through LDS as well: the tile's bf16 values (y, or the whole SwiGLU product) to
+      // LDS in the accumulator layout, then 16-byte row segments (8 columns) per thread, the residual / c_fc1
+      // operand read the same way -- rows of 256 (SwiGLU: 128) contiguous bytes instead of 4-byte pairs
+      constexpr int TW = DUAL ? BN / 2 : BN, TP = TW + 8, SEGS = TW / 8, RPP = 512 / SEGS;
+      bf16_t* Ts = reinterpret_cast<bf16_t*>(smem);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __syncthreads();  // every wave is past its last fragment read of the K loop
+#pragma unroll
+      for (int j = 0; j < (DUAL ? NJ / 2 : NJ); ++j) {
+        const int nl = wc * 16 * (DUAL ? NJ / 2 : NJ) + 16 * j + row;
+        const float s1 = CVT ? p.sz[n0 + nl].x : 1.f;
+        float s2 = 1.f;
+        if constexpr (DUAL) s2 = p.sz2[n0 + nl].x;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float o;
+            if constexpr (DUAL) {  // h = bf16(silu(bf16(fc1))) * bf16(fc2)
+              const float a1 = round_bf(s1 * acc[i][j][r]);
+              const float sl = round_bf(a1 / (1.f + __expf(-a1)));
+              o = sl * round_bf(s2 * acc[i][j + NJ / 2][r]);
+            } else {
+              o = s1 * acc[i][j][r];
+            }
+            Ts[(wr * 16 * MI + 16 * i + 4 * g + r) * TP + nl] = f2bf(o);
+          }
+      }
+      __syncthreads();
+      const int seg = tid % SEGS;
+#pragma unroll 2
+      for (int k = 0; k < 256 / RPP; ++k) {
+        const int rl = tid / SEGS + RPP * k, m = m0 + rl;
+        if (m >= M) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(Ts + rl * TP + 8 * seg);
+        uint4* cp = reinterpret_cast<uint4*>(p.C + (size_t)m * p.ldc + n0 + 8 * seg);
+        uint4 o = v;
+        if constexpr (EP == GEP_RESID || EP == GEP_SILU_MUL) {
+          const uint4 c = *cp;
+          const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, cw[4] = {c.x, c.y, c.z, c.w};
+          uint32_t ow[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float y0 = bflo(vw[q]), y1 = bfhi(vw[q]), c0 = bflo(cw[q]), c1 = bfhi(cw[q]);
+            if constexpr (EP == GEP_RESID) {
+              ow[q] = pack2bf(c0 + y0, c1 + y1);  // x + y in bf16 (model.py:172-173)
+            } else {
+              const float l0 = round_bf(c0 / (1.f + __expf(-c0))), l1 = round_bf(c1 / (1.f + __expf(-c1)));
+              ow[q] = pack2bf(l0 * y0, l1 * y1);  // silu(bf16(c_fc1 x)) * bf16(c_fc2 x)
+            }
+          }
+          o = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        }
+        *cp = o;
+      }
+      return;
+    }
   if constexpr (PART) {  // the slice's fp32 partials, scale applied (summed over the slices by the reduce)
     float* wsl = p.ws + (size_t)split * M * p.N;
 #pragma unroll
