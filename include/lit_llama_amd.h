@@ -211,6 +211,13 @@ int llj_gemm_silu_mul(int wfmt, const void* A, int lda, const void* W, const voi
  * llj_gemm_silu_mul). */
 int llj_gemm_swiglu(int wfmt, const void* A, int lda, const void* W1, const void* sz1, const void* W2, const void* sz2,
                     void* h, int ldh, int M, int H, int K, void* stream);
+/* llj_gemm_swiglu whose tiles leave a partial last wave over the CUs (7B: 2,048 or 512 rows x 11,008): that
+ * wave's column tiles (the right end of h) run as two K halves into a caller-owned fp32 workspace and one
+ * more launch finishes them; the rest is llj_gemm_swiglu on whole waves. 0 bytes = no split (then
+ * llj_gemm_swiglu_ws is llj_gemm_swiglu). Same arguments as llj_gemm_swiglu + the workspace. */
+size_t llj_gemm_swiglu_ws_bytes(int wfmt, int M, int H, int K);
+int llj_gemm_swiglu_ws(int wfmt, const void* A, int lda, const void* W1, const void* sz1, const void* W2,
+                       const void* sz2, void* h, int ldh, int M, int H, int K, void* ws, size_t ws_bytes, void* stream);
 /* c_attn + split + RoPE(q, k) + KV-cache write for B*T pre-normalized rows x (as llj_norm_qkv_rope
  * with norm_w NULL; model.py:204-228). */
 int llj_gemm_qkv_rope(int wfmt, const void* x, const void* W, const void* sz, void* q_out, void* kcache, void* vcache,

@@ -54,7 +54,9 @@ enum : int { GWF_W4 = 0, GWF_BF16 = 1, GWF_I8 = 2, GWF_W8 = 3, GWF_W4G = 4, GWF_
 // codes staged per chunk, one A tile feeding both; W2 / sz2)
 // GEP_PARTIAL: split-K slice of a residual GEMM -- fp32 partials y (scale applied) of K range slice
 // blockIdx.x % nsplit into ws[slice][M][N]; llj_gemm_resid_ws's reduce adds them and the residual
-enum : int { GEP_STORE = 0, GEP_RESID = 1, GEP_QKV = 2, GEP_SILU_MUL = 3, GEP_SWIGLU = 4, GEP_PARTIAL = 5 };
+// GEP_SWIGLU_PART: split-K slice of the dual SwiGLU pass (its last partial wave of tiles) -- fp32 partials of
+// c_fc1 and c_fc2 (scales applied) into ws[slice][2][M][N]; llj_gemm_swiglu_ws's reduce finishes h
+enum : int { GEP_STORE = 0, GEP_RESID = 1, GEP_QKV = 2, GEP_SILU_MUL = 3, GEP_SWIGLU = 4, GEP_PARTIAL = 5, GEP_SWIGLU_PART = 6 };
 
 struct GemmParams {
   const bf16_t* A;  // (M, K) rows with stride lda
@@ -771,7 +773,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   // the dual SwiGLU form: 64 output columns per tile, B rows 0-63 from W1 and 64-127 from W2 (the same
   // columns), wave column group wc holding output columns 32 wc .. + 31 of BOTH (fragments j < NJ / 2
   // from W1, j >= NJ / 2 from W2), so each lane has fc1 and fc2 of the same element
-  constexpr bool DUAL = EP == GEP_SWIGLU;
+  constexpr bool DUAL = EP == GEP_SWIGLU || EP == GEP_SWIGLU_PART;
   static_assert(!DUAL || WF == GWF_W4Z, "dual SwiGLU GEMM: convert-once int4");
   static_assert(EP != GEP_PARTIAL || ((WF == GWF_W4Z || WF == GWF_BF16) && BN == 128), "split-K slices: 256 x 128");
   constexpr int NOUT = DUAL ? BN / 2 : BN;  // output columns per tile
@@ -784,7 +786,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w / WN, wc = w % WN;
   const int row = lane & 15, g = lane >> 4;
-  constexpr bool PART = EP == GEP_PARTIAL;  // split-K slice (kc0 .. kc0 + KC of the K chunks)
+  constexpr bool PART = EP == GEP_PARTIAL || EP == GEP_SWIGLU_PART;  // split-K slice (kc0 .. kc0 + KC of the K chunks)
   const int M = p.M, K = p.K, KC128 = K / 128;
   const int split = PART ? (int)blockIdx.x % p.nsplit : 0;
   const int kc0 = PART ? split * p.kcs : 0;  // even: the W4P chunk pairs stay aligned
@@ -825,7 +827,8 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
   if constexpr (NIB || CVT) {  // W4P: wave w stages tiles 2 w, 2 w + 1 (BN 128: waves 4-7 a copy of 0-3's)
     const int tl = (2 * w + (lane >> 5)) % (BN / 16);
     if (DUAL)  // B tiles 0-3: W1's columns n0 .. + 63, tiles 4-7: W2's
-      bsrc = reinterpret_cast<const char*>(tl < 4 ? p.W : p.W2) + (size_t)(n0 / 16 + (tl & 3)) * KC128 * 1024 + 16 * (lane & 31);
+      bsrc = reinterpret_cast<const char*>(tl < 4 ? p.W : p.W2) + (size_t)(n0 / 16 + (tl & 3)) * KC128 * 1024 + 16 * (lane & 31) +
+             (size_t)(kc0 >> 1) * 1024;
     else
       bsrc = reinterpret_cast<const char*>(p.W) + (size_t)(n0 / 16 + tl) * KC128 * 1024 + 16 * (lane & 31) +
              (size_t)(kc0 >> 1) * 1024;
@@ -1231,6 +1234,25 @@ __global__ __launch_bounds__(512, 1) void gemm_glds_kernel(GemmParams p) {
       }
       return;
     }
+  if constexpr (PART && DUAL) {  // the slice's c_fc1 / c_fc2 fp32 partials, scales applied, two planes
+    float* wsl = p.ws + (size_t)split * 2 * M * p.N;
+#pragma unroll
+    for (int j = 0; j < NJ / 2; ++j) {
+      const int n = n0 + wc * 16 * (NJ / 2) + 16 * j + row;
+      const float s1 = p.sz[n].x, s2 = p.sz2[n].x;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wr * 16 * MI + 16 * i + 4 * g + r;
+          if (m < M) {
+            wsl[(size_t)m * p.N + n] = s1 * acc[i][j][r];
+            wsl[(size_t)(M + m) * p.N + n] = s2 * acc[i][j + NJ / 2][r];
+          }
+        }
+    }
+    return;
+  }
   if constexpr (PART) {  // the slice's fp32 partials, scale applied (summed over the slices by the reduce)
     float* wsl = p.ws + (size_t)split * M * p.N;
 #pragma unroll
@@ -1336,7 +1358,9 @@ static int gemm_glds_launch(const GemmParams& p, hipStream_t s) {
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  const int tiles = ((p.M + 255) / 256) * (p.N / (EP == GEP_SWIGLU ? BN / 2 : BN)) * (EP == GEP_PARTIAL ? p.nsplit : 1);
+  constexpr bool DUAL = EP == GEP_SWIGLU || EP == GEP_SWIGLU_PART;
+  const int tiles = ((p.M + 255) / 256) * (p.N / (DUAL ? BN / 2 : BN)) *
+                    (EP == GEP_PARTIAL || EP == GEP_SWIGLU_PART ? p.nsplit : 1);
   hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), lds, s, p);
   LLJ_CHECK_LAUNCH();
   return 0;
@@ -1531,6 +1555,58 @@ int llj_gemm_resid_ws(int wfmt, const void* A, int lda, const void* W, const voi
   return 0;
 }
 
+// the dual SwiGLU pass's tail: h[m, n] = bf16(silu(bf16(a))) * bf16(b), a / b the c_fc1 / c_fc2 partials of the
+// slices summed in slice order (4 consecutive columns per thread, N % 4 == 0)
+__global__ __launch_bounds__(256) void gemm_swiglu_reduce_kernel(const float* __restrict__ ws, int nsplit, int M, int N,
+                                                                 bf16_t* __restrict__ h, int ldh) {
+  const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const size_t MN = (size_t)M * N;
+  if (i >= MN) return;
+  const int m = (int)(i / N), n = (int)(i % N);
+  float4 a = *reinterpret_cast<const float4*>(ws + i), b = *reinterpret_cast<const float4*>(ws + MN + i);
+  for (int sp = 1; sp < nsplit; ++sp) {
+    const float4 u = *reinterpret_cast<const float4*>(ws + 2 * sp * MN + i);
+    const float4 v = *reinterpret_cast<const float4*>(ws + (2 * sp + 1) * MN + i);
+    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+  }
+  const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+  float o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float a1 = round_bf(av[q]);
+    const float sl = round_bf(a1 / (1.f + __expf(-a1)));  // F.silu in bf16
+    o[q] = sl * round_bf(bv[q]);
+  }
+  *reinterpret_cast<uint2*>(h + (size_t)m * ldh + n) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+}
+
+#ifndef LLJ_GEMM_SWIGLU_TAIL
+#define LLJ_GEMM_SWIGLU_TAIL 1  // the dual SwiGLU pass's partial last wave of tiles as split-K halves
+#endif
+// The dual SwiGLU pass over (row tiles) x (H / 64 column tiles): when the tiles leave a partial last wave
+// over the CUs, its column tiles (tc of them, at the right end) run as two K halves -- twice the
+// workgroups at half the length, fitting one wave -- and the full-K launch keeps only whole waves.
+// Returns the tail's column tiles (0: no split), kcs = its 64-deep chunks per half.
+static int swiglu_tail_plan(int M, int H, int K, int* kcs_out) {
+  if (!LLJ_GEMM_SWIGLU_TAIL || M < 256 || H % 64 || K % 128 || K / 64 < 16) return 0;
+  int cus = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const long mt = (M + 255) / 256, ntn = H / 64, tiles = mt * ntn;
+  const long full = tiles / cus * cus;
+  if (full == tiles || full == 0) return 0;
+  const long tc = ntn - full / mt;  // the full-K launch keeps (ntn - tc) column tiles: at most the whole waves
+  if (tc <= 0 || tc >= ntn || 2 * mt * tc > cus) return 0;
+  int kcs = (K / 64 + 1) / 2;
+  kcs += kcs & 1;
+  if (kcs_out) *kcs_out = kcs;
+  return (int)tc;
+}
+
 // h[M, H] = bf16(silu(bf16(A . W1^T))) * bf16(A . W2^T) in one pass: int4 W4P with integral zeros
 // (wfmt 0 | LLJ_WF_ZINT), M >= 256, H % 64 == 0 (the convert-once kernel with both weights' codes per chunk)
 int llj_gemm_swiglu(int wfmt, const void* A, int lda, const void* W1, const void* sz1, const void* W2, const void* sz2,
@@ -1542,6 +1618,43 @@ int llj_gemm_swiglu(int wfmt, const void* A, int lda, const void* W1, const void
   p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = H; p.K = K; p.W = W1; p.sz = (const float2*)sz1;
   p.W2 = W2; p.sz2 = (const float2*)sz2; p.C = (bf16_t*)h; p.ldc = ldh;
   return gemm_glds_launch<GWF_W4Z, GEP_SWIGLU, 128>(p, (hipStream_t)stream);
+}
+
+// Workspace bytes llj_gemm_swiglu_ws needs (0: no partial last wave to split -- call llj_gemm_swiglu).
+size_t llj_gemm_swiglu_ws_bytes(int wfmt, int M, int H, int K) {
+  if (wfmt != (GWF_W4 | LLJ_WF_ZINT) || !w4z_enabled()) return 0;
+  int kcs = 0;
+  const int tc = swiglu_tail_plan(M, H, K, &kcs);
+  return tc ? (size_t)2 * 2 * M * (64 * tc) * sizeof(float) : 0;
+}
+
+// llj_gemm_swiglu with the partial last wave of column tiles split into two K halves (fp32 partials of both
+// weights into ws, llj_gemm_swiglu_ws_bytes), one reduce launch finishing those columns of h
+int llj_gemm_swiglu_ws(int wfmt, const void* A, int lda, const void* W1, const void* sz1, const void* W2, const void* sz2,
+                       void* h, int ldh, int M, int H, int K, void* ws, size_t ws_bytes, void* stream) {
+  int kcs = 0;
+  const int tc = (wfmt == (GWF_W4 | LLJ_WF_ZINT) && w4z_enabled()) ? swiglu_tail_plan(M, H, K, &kcs) : 0;
+  if (!tc) return llj_gemm_swiglu(wfmt, A, lda, W1, sz1, W2, sz2, h, ldh, M, H, K, stream);
+  const int Ht = 64 * tc, Hc = H - Ht;
+  if ((lda & 7) || (ldh & 3) || !A || !W1 || !W2 || !sz1 || !sz2 || !h || !ws ||
+      ws_bytes < (size_t)2 * 2 * M * Ht * sizeof(float))
+    return LLJ_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  int rc = llj_gemm_swiglu(wfmt, A, lda, W1, sz1, W2, sz2, h, ldh, M, Hc, K, stream);  // whole waves, full K
+  if (rc) return rc;
+  GemmParams p{};  // the tail's columns Hc .. H - 1: W4P column tiles are K-contiguous, so pointer offsets
+  const size_t woff = (size_t)Hc * K / 2;
+  p.A = (const bf16_t*)A; p.lda = lda; p.M = M; p.N = Ht; p.K = K;
+  p.W = (const char*)W1 + woff; p.sz = (const float2*)sz1 + Hc;
+  p.W2 = (const char*)W2 + woff; p.sz2 = (const float2*)sz2 + Hc;
+  p.ws = (float*)ws; p.nsplit = 2; p.kcs = kcs;
+  rc = gemm_glds_launch<GWF_W4Z, GEP_SWIGLU_PART, 128>(p, s);
+  if (rc) return rc;
+  const size_t n4 = (size_t)M * Ht / 4;
+  hipLaunchKernelGGL(gemm_swiglu_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, (const float*)ws, 2, M,
+                     Ht, (bf16_t*)h + Hc, ldh);
+  LLJ_CHECK_LAUNCH();
+  return 0;
 }
 
 // LLM.int8() forms (wfmt 2): W = CB in the I8P tiling, sz = SCB (fp32), i8ws = llj_i8_stats of A

@@ -69,6 +69,7 @@ SIGNATURES = {
     "llj_gemm_resid": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_silu_mul": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P],
     "llj_gemm_swiglu": [_I, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "llj_gemm_swiglu_ws": [_I, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, ctypes.c_size_t, _P],
     "llj_gemm_resid_ws": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, ctypes.c_size_t, _P],
     "llj_gemm_qkv_rope": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "llj_stream_read": [_P, ctypes.c_size_t, _P, _I, _P],
@@ -119,6 +120,8 @@ def lib() -> ctypes.CDLL:
         L.llj_i8_rowstats_bytes.restype = ctypes.c_size_t
         L.llj_gemm_resid_ws_bytes.argtypes = [_I, _I, _I, _I]
         L.llj_gemm_resid_ws_bytes.restype = ctypes.c_size_t
+        L.llj_gemm_swiglu_ws_bytes.argtypes = [_I, _I, _I, _I]
+        L.llj_gemm_swiglu_ws_bytes.restype = ctypes.c_size_t
         _lib = L
     return _lib
 

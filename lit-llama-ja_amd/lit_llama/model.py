@@ -554,8 +554,15 @@ class LLaMA(nn.Module):
                           w.xn.data_ptr(), None, M, C, st)
                 g1, g2 = _gz(f1, blk.mlp.c_fc1), _gz(f2, blk.mlp.c_fc2)
                 if GEMM_SWIGLU and g1 == g2 == _hip.WF_ZINT and M >= 256 and H % 64 == 0:  # both in one pass
-                    _hip.call("llj_gemm_swiglu", g1, w.xn.data_ptr(), C, w1.data_ptr(), P(s1), w2.data_ptr(), P(s2),
-                              w.h.data_ptr(), H, M, H, C, st)
+                    # (a partial last wave of tiles: its columns as two K halves, llj_gemm_swiglu_ws)
+                    nb = _hip.lib().llj_gemm_swiglu_ws_bytes(g1, M, H, C)
+                    if nb:
+                        ws = torch.empty(nb // 4, dtype=torch.float32, device=w.h.device)
+                        _hip.call("llj_gemm_swiglu_ws", g1, w.xn.data_ptr(), C, w1.data_ptr(), P(s1), w2.data_ptr(),
+                                  P(s2), w.h.data_ptr(), H, M, H, C, ws.data_ptr(), nb, st)
+                    else:
+                        _hip.call("llj_gemm_swiglu", g1, w.xn.data_ptr(), C, w1.data_ptr(), P(s1), w2.data_ptr(),
+                                  P(s2), w.h.data_ptr(), H, M, H, C, st)
                 else:
                     _hip.call("llj_gemm_linear", g1, w.xn.data_ptr(), C, w1.data_ptr(), P(s1), w.h.data_ptr(), H, M,
                               H, C, st)

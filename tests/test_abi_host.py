@@ -113,7 +113,7 @@ def test_ctypes_table_matches_header():
         assert [kind[a] for a in argt] == kinds, name
     assert set(decls) - set(_hip.SIGNATURES) == {"llj_i8_ws_bytes", "llj_attention_ws_bytes",
                                                    "llj_g_i8_ws_bytes", "llj_i8_rowstats_bytes",
-                                                   "llj_gemm_resid_ws_bytes"}
+                                                   "llj_gemm_resid_ws_bytes", "llj_gemm_swiglu_ws_bytes"}
 
 
 def test_library_holds_gfx950_code():

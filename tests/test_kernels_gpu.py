@@ -1272,6 +1272,43 @@ def test_gemm_swiglu_dual_pass(hip, M, H, K):
     assert_bf16_close(got[:M], hexp, f"gemm swiglu dual M={M}", rel=3e-2)
 
 
+@pytest.mark.parametrize("M,H,K,tail", [(2048, 11008, 4096, 12), (512, 11008, 4096, 44), (300, 11008, 1024, 44),
+                                        (768, 5632, 2048, 3), (1024, 11008, 4096, 0), (256, 2816, 1024, 0)])
+def test_gemm_swiglu_tail_split(hip, M, H, K, tail):
+    """llj_gemm_swiglu_ws: the dual pass's partial last wave of column tiles (the right `tail` x 64 columns of
+    h at 256 CUs) as two K halves + a reduce, the rest on whole waves. Against the oracle; the whole-wave
+    columns bitwise equal to llj_gemm_swiglu, the tail's within bf16 rounding of it (two fp32 partials);
+    no split (0 bytes) where the tail would not fit one wave or there is none."""
+    L = hip
+    nb = L.llj_gemm_swiglu_ws_bytes(ZINT4, M, H, K)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    if cus == 256:
+        assert nb == 16 * M * 64 * tail
+    assert L.llj_gemm_swiglu_ws_bytes(0, M, H, K) == 0  # int4 without integral zeros: no dual pass
+    rng = np.random.default_rng(M + H + K + 1)
+    W1, W1d, s1 = quant_operands(hip, rng, ZINT4, H, K)
+    W2, W2d, s2 = quant_operands(hip, rng, ZINT4, H, K)
+    x = bf16(rng.standard_normal((M, K)).astype(np.float32))
+    xd = T(x, torch.bfloat16)
+    ws = torch.full((max(nb, 4) // 4,), float("nan"), dtype=torch.float32, device=dev)
+    h1 = torch.full((M + 1, H), 7.0, dtype=torch.bfloat16, device=dev)  # row M: canary
+    call(hip, "llj_gemm_swiglu_ws", ZINT4, xd.data_ptr(), K, W1d.data_ptr(), s1.data_ptr(), W2d.data_ptr(),
+         s2.data_ptr(), h1.data_ptr(), H, M, H, K, ws.data_ptr(), nb, st())
+    h2 = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+    call(hip, "llj_gemm_swiglu", ZINT4, xd.data_ptr(), K, W1d.data_ptr(), s1.data_ptr(), W2d.data_ptr(), s2.data_ptr(),
+         h2.data_ptr(), H, M, H, K, st())
+    torch.cuda.synchronize()
+    got, one = h1.float().cpu().numpy(), h2.float().cpu().numpy()
+    assert (got[M] == 7.0).all(), "wrote past row M"
+    got = got[:M]
+    Hc = H - 64 * (nb // (16 * M * 64) if nb else 0)
+    np.testing.assert_array_equal(got[:, :Hc], one[:, :Hc])
+    if Hc < H:
+        assert_bf16_close(got[:, Hc:], one[:, Hc:], f"swiglu tail vs one pass M={M}", rel=3e-2)
+    hexp = bf16(bf16(O.silu(bf16(x @ W1.T))) * bf16(x @ W2.T))
+    assert_bf16_close(got, hexp, f"gemm swiglu tail split M={M}", rel=3e-2)
+
+
 @pytest.mark.parametrize("wfmt", [1, ZINT4])
 @pytest.mark.parametrize("M,N,K", [(256, 4096, 4096), (512, 4096, 11008), (300, 1024, 1024), (1024, 4096, 2048)])
 def test_gemm_resid_split_k(hip, wfmt, M, N, K):

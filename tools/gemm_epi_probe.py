@@ -54,6 +54,8 @@ def main():
     hx = torch.randn(M, H, device=dev, generator=g).to(torch.bfloat16)
     xr = torch.randn(M, C, device=dev, generator=g).to(torch.bfloat16)
     hh = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+    nb = L.llj_gemm_swiglu_ws_bytes(wf, M, H, K)
+    ws = torch.empty(max(nb, 4) // 4, dtype=torch.float32, device=dev)
     runs = {
         "qkv_rope": lambda: _hip.call("llj_gemm_qkv_rope", wf, x.data_ptr(), Wp.data_ptr(), sz.data_ptr(), q.data_ptr(),
                                       kc.data_ptr(), vc.data_ptr(), rope.data_ptr(), pos.data_ptr(), 1, M, C, nh, S, st),
@@ -63,6 +65,8 @@ def main():
                                           xr.data_ptr(), C, M, C, H, st),
         "swiglu": lambda: _hip.call("llj_gemm_swiglu", wf, x.data_ptr(), K, W1.data_ptr(), s1.data_ptr(), W2.data_ptr(),
                                     s2.data_ptr(), hh.data_ptr(), H, M, H, K, st),
+        "swiglu_ws": lambda: _hip.call("llj_gemm_swiglu_ws", wf, x.data_ptr(), K, W1.data_ptr(), s1.data_ptr(),
+                                       W2.data_ptr(), s2.data_ptr(), hh.data_ptr(), H, M, H, K, ws.data_ptr(), nb, st),
     }
     res = {k: [] for k in runs}
     for f in runs.values():
